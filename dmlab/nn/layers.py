@@ -1,0 +1,230 @@
+"""Layers of the dmlab engine.
+
+Every layer has a PyTorch reference forward (``torch_forward``; backward via
+local autograd) and a native path in :mod:`dmlab.ops` (explicit HIP kernels).
+Parameter names and shapes follow ``torch.nn`` (``Conv2d.weight`` is OIHW,
+``Linear.weight`` is [out, in]) so state dicts interchange with the reference
+models; the native path packs its own bf16 layouts from the fp32 master.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .program import Ctx, Layer
+
+
+def _kaiming_uniform_(w, fan_in):
+    # torch.nn default init for Conv2d/Linear (kaiming_uniform, a=sqrt(5))
+    bound = 1.0 / math.sqrt(fan_in) if fan_in > 0 else 0
+    gain_bound = math.sqrt(6.0 / ((1 + 5.0) * fan_in)) if fan_in > 0 else 0
+    with torch.no_grad():
+        w.uniform_(-gain_bound * math.sqrt(3.0) / math.sqrt(3.0), gain_bound)
+    return bound
+
+
+class Conv2d(Layer):
+    """Conv2d (+ optional fused ReLU and 2×2 max-pool epilogue).
+
+    ``pool=2`` fuses ``max_pool2d(relu(conv(x)), 2)`` — the LeNet stage
+    (task1/pytorch/model.py:27-28) — into one native kernel that also stores a
+    2-bit argmax per pooled element for backward."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, bias=True, relu=False, pool=1):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride, self.padding = cin, cout, k, stride, padding
+        self.relu, self.pool = relu, pool
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        self.bias = nn.Parameter(torch.empty(cout)) if bias else None
+        fan_in = cin * k * k
+        b = _kaiming_uniform_(self.weight, fan_in)
+        if self.bias is not None:
+            with torch.no_grad():
+                self.bias.uniform_(-b, b)
+
+    def torch_forward(self, x):
+        y = F.conv2d(x, self.weight, self.bias, self.stride, self.padding)
+        if self.relu:
+            y = F.relu(y)
+        if self.pool > 1:
+            y = F.max_pool2d(y, self.pool)
+        return y
+
+    def native_fwd(self, x, ctx, train):
+        from dmlab.ops import conv as C
+
+        return C.conv_fwd(self, x, ctx, train)
+
+    def native_bwd(self, dy, ctx, need_dx):
+        from dmlab.ops import conv as C
+
+        return C.conv_bwd(self, dy, ctx, need_dx)
+
+
+class Linear(Layer):
+    """Linear (+ optional fused ReLU) on MFMA GEMM kernels."""
+
+    def __init__(self, fin, fout, bias=True, relu=False):
+        super().__init__()
+        self.fin, self.fout, self.relu = fin, fout, relu
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.bias = nn.Parameter(torch.empty(fout)) if bias else None
+        b = _kaiming_uniform_(self.weight, fin)
+        if self.bias is not None:
+            with torch.no_grad():
+                self.bias.uniform_(-b, b)
+
+    def torch_forward(self, x):
+        y = F.linear(x.flatten(1) if x.dim() > 2 else x, self.weight, self.bias)
+        return F.relu(y) if self.relu else y
+
+    def native_fwd(self, x, ctx, train):
+        from dmlab.ops import linear as L
+
+        return L.linear_fwd(self, x, ctx, train)
+
+    def native_bwd(self, dy, ctx, need_dx):
+        from dmlab.ops import linear as L
+
+        return L.linear_bwd(self, dy, ctx, need_dx)
+
+
+class Flatten(Layer):
+    def torch_forward(self, x):
+        return x.flatten(1)
+
+    def native_fwd(self, x, ctx, train):
+        ctx["shape"] = x.shape
+        return x.reshape(x.shape[0], -1)
+
+    def native_bwd(self, dy, ctx, need_dx):
+        return dy.reshape(ctx["shape"]) if need_dx else None
+
+
+class Softmax(Layer):
+    """Softmax over classes — only for the MindSpore-notebook compat mode (B10)."""
+
+    def torch_forward(self, x):
+        return F.softmax(x, dim=1)
+
+    def native_fwd(self, x, ctx, train):
+        y = torch.softmax(x.float(), dim=1)
+        ctx["y"] = y
+        return y
+
+    def native_bwd(self, dy, ctx, need_dx):
+        y = ctx["y"]
+        return y * (dy - (dy * y).sum(1, keepdim=True))
+
+
+class ConvBN(Layer):
+    """conv (no bias) → BatchNorm2d (train: batch stats) → [+residual] → [ReLU].
+
+    Native path: NHWC bf16 implicit-GEMM conv on MFMA with the BN statistics
+    reduced in the conv epilogue, then one fused BN-apply/residual/ReLU pass
+    (SURVEY §2.5 'Extensions required by BASELINE.json')."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, relu=True, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride, self.padding = cin, cout, k, stride, padding
+        self.relu = relu
+        self.eps, self.momentum = eps, momentum
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        nn.init.kaiming_normal_(self.weight, mode="fan_out", nonlinearity="relu")
+        self.bn_weight = nn.Parameter(torch.ones(cout))
+        self.bn_bias = nn.Parameter(torch.zeros(cout))
+        self.register_buffer("running_mean", torch.zeros(cout))
+        self.register_buffer("running_var", torch.ones(cout))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def torch_forward(self, x, residual=None):
+        y = F.conv2d(x, self.weight, None, self.stride, self.padding)
+        if self.training:
+            self.num_batches_tracked.add_(1)
+        y = F.batch_norm(y, self.running_mean, self.running_var, self.bn_weight, self.bn_bias,
+                         self.training, self.momentum, self.eps)
+        if residual is not None:
+            y = y + residual
+        return F.relu(y) if self.relu else y
+
+    def native_fwd(self, x, ctx, train, residual=None):
+        from dmlab.ops import convbn as CB
+
+        return CB.convbn_fwd(self, x, ctx, train, residual)
+
+    def native_bwd(self, dy, ctx, need_dx):
+        from dmlab.ops import convbn as CB
+
+        return CB.convbn_bwd(self, dy, ctx, need_dx)
+
+
+class BasicBlock(Layer):
+    """ResNet BasicBlock: relu(bn2(conv2(relu(bn1(conv1 x)))) + shortcut(x))."""
+
+    def __init__(self, cin, cout, stride):
+        super().__init__()
+        self.c1 = ConvBN(cin, cout, 3, stride, 1, relu=True)
+        self.c2 = ConvBN(cout, cout, 3, 1, 1, relu=True)  # relu after the residual add
+        self.down = ConvBN(cin, cout, 1, stride, 0, relu=False) if (stride != 1 or cin != cout) else None
+
+    def torch_forward(self, x):
+        idt = x if self.down is None else self.down.torch_forward(x)
+        y = self.c1.torch_forward(x)
+        return self.c2.torch_forward(y, residual=idt)
+
+    def native_fwd(self, x, ctx, train):
+        c1, c2, cd = Ctx(), Ctx(), Ctx()
+        idt = x if self.down is None else self.down.native_fwd(x, cd, train)
+        y = self.c1.native_fwd(x, c1, train)
+        out = self.c2.native_fwd(y, c2, train, residual=idt)
+        ctx.update(c1=c1, c2=c2, cd=cd)
+        return out
+
+    def native_bwd(self, dy, ctx, need_dx):
+        # c2's backward returns (d_input_of_c2, d_residual); d_residual == ReLU/BN-masked dy
+        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True)
+        dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
+        if self.down is not None:
+            dd = self.down.native_bwd(dres, ctx["cd"], need_dx)
+            if need_dx:
+                dx = dx + dd if dx is not None else dd
+        elif need_dx:
+            dx = dx + dres
+        return dx
+
+
+class MaxPool(Layer):
+    def __init__(self, k=3, stride=2, padding=1):
+        super().__init__()
+        self.k, self.stride, self.padding = k, stride, padding
+
+    def torch_forward(self, x):
+        return F.max_pool2d(x, self.k, self.stride, self.padding)
+
+    def native_fwd(self, x, ctx, train):
+        from dmlab.ops import pool as P
+
+        return P.maxpool_fwd(self, x, ctx, train)
+
+    def native_bwd(self, dy, ctx, need_dx):
+        from dmlab.ops import pool as P
+
+        return P.maxpool_bwd(self, dy, ctx, need_dx)
+
+
+class GlobalAvgPool(Layer):
+    def torch_forward(self, x):
+        return F.adaptive_avg_pool2d(x, 1).flatten(1)
+
+    def native_fwd(self, x, ctx, train):
+        from dmlab.ops import pool as P
+
+        return P.avgpool_fwd(self, x, ctx, train)
+
+    def native_bwd(self, dy, ctx, need_dx):
+        from dmlab.ops import pool as P
+
+        return P.avgpool_bwd(self, dy, ctx, need_dx)

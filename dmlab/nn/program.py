@@ -1,0 +1,254 @@
+"""Explicit forward/backward programs (the dmlab execution engine).
+
+A :class:`Program` is an ``nn.Module`` whose layers each implement an explicit
+``fwd``/``bwd`` pair.  The whole program runs as ONE autograd node
+(:class:`_ProgramFn`): its backward walks the layers in reverse, writes weight
+gradients *directly* into the flat gradient buffer (no AccumulateGrad copies),
+and notifies a gradient hook after every layer so a data-parallel reducer can
+launch bucket all-reduces while the remaining layers are still computing.
+
+Each layer has two interchangeable implementations selected per call:
+
+* ``native`` — hand-written HIP kernels (``dmlab._C``), used for every HIP
+  device tensor.  If the extension is missing this raises; there is no silent
+  fallback.
+* ``torch``  — plain PyTorch ops through local autograd; the numerical
+  reference and the CPU execution path (BASELINE config 1 is CPU-only).
+
+Reference mapping: the reference models are plain ``nn.Module``s trained by
+autograd (task1/pytorch/model.py:12-35, task4/model.py:18-47); a Program keeps
+that user-facing contract (``out = model(x); loss.backward(); opt.step()``)
+while replacing the per-op autograd graph with an explicit schedule.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.nn as nn
+
+from .flat import FlatParams
+
+
+class Ctx(dict):
+    """Per-call saved state of one layer (activations, masks, stats)."""
+
+
+class Layer(nn.Module):
+    """Base class: subclasses define parameters in ``__init__`` and implement
+    ``torch_forward`` (reference) and optionally ``native_fwd``/``native_bwd``."""
+
+    native_ok = True  # False: layer has no native kernels yet (torch path on GPU is an error)
+
+    def __init__(self):
+        super().__init__()
+        self._prog: Optional["Program"] = None
+        self._pidx: dict[str, int] = {}
+
+    # ---------------------------------------------------------------- helpers
+    def grad_slot(self, name: str) -> torch.Tensor:
+        return self._prog.flat.grad_view(self._pidx[name])
+
+    def write_grad(self, name: str, g: torch.Tensor):
+        slot = self.grad_slot(name)
+        if self._prog._accumulate:
+            slot.add_(g.reshape(slot.shape).to(slot.dtype))
+        else:
+            slot.copy_(g.reshape(slot.shape))
+
+    @property
+    def accumulate(self) -> bool:
+        return self._prog._accumulate
+
+    # ---------------------------------------------------------------- torch reference path
+    def torch_forward(self, x: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def t_fwd(self, x, ctx: Ctx, train: bool):
+        if not train:
+            with torch.no_grad():
+                return self.torch_forward(x)
+        xi = x.detach().requires_grad_(x.is_floating_point())
+        with torch.enable_grad():
+            y = self.torch_forward(xi)
+        ctx["x"], ctx["y"] = xi, y
+        return y.detach()
+
+    def t_bwd(self, dy, ctx: Ctx, need_dx: bool):
+        xi, y = ctx["x"], ctx["y"]
+        names = [n for n, p in self.named_parameters(recurse=True) if p.requires_grad]
+        params = [self.get_parameter(n) for n in names]
+        inputs = ([xi] if need_dx and xi.requires_grad else []) + params
+        if not inputs:
+            return None
+        grads = torch.autograd.grad(y, inputs, dy, allow_unused=True)
+        dx = grads[0] if (need_dx and xi.requires_grad) else None
+        pg = grads[1:] if dx is not None else grads
+        for n, g in zip(names, pg):
+            if g is not None:
+                self._prog._write_grad_by_param(self.get_parameter(n), g)
+        return dx
+
+    # ---------------------------------------------------------------- dispatch
+    def fwd(self, x, ctx: Ctx, train: bool):
+        if self._prog._use_native(x):
+            return self.native_fwd(x, ctx, train)
+        return self.t_fwd(x, ctx, train)
+
+    def bwd(self, dy, ctx: Ctx, need_dx: bool):
+        if self._prog._use_native(dy):
+            return self.native_bwd(dy, ctx, need_dx)
+        return self.t_bwd(dy, ctx, need_dx)
+
+    def native_fwd(self, x, ctx, train):  # pragma: no cover - overridden
+        raise NotImplementedError(f"{type(self).__name__} has no native forward")
+
+    def native_bwd(self, dy, ctx, need_dx):  # pragma: no cover - overridden
+        raise NotImplementedError(f"{type(self).__name__} has no native backward")
+
+    def forward(self, x):  # standalone use (e.g. inside a plain nn.Module)
+        return self.torch_forward(x)
+
+
+class _ProgramFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, prog):
+        ctxs = []
+        h = x
+        for layer in prog.layers:
+            c = Ctx()
+            h = layer.fwd(h, c, True)
+            ctxs.append(c)
+        ctx.prog = prog
+        ctx.ctxs = ctxs
+        ctx.need_dx = x.requires_grad
+        return h
+
+    @staticmethod
+    def backward(ctx, dy):
+        prog = ctx.prog
+        prog._accumulate = prog.flat.prepare_backward()
+        dy = dy.contiguous() if not prog._native_active else dy
+        n = len(prog.layers)
+        for i in range(n - 1, -1, -1):
+            layer = prog.layers[i]
+            need_dx = i > 0 or ctx.need_dx
+            dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
+            ctx.ctxs[i] = None  # free saved activations as soon as possible
+            for hook in prog._grad_hooks:
+                hook(prog, i)
+        prog.flat.grad_valid = True
+        for hook in prog._post_backward_hooks:
+            hook(prog)
+        return (dy if ctx.need_dx else None), None, None
+
+
+class Program(nn.Module):
+    """A sequence of :class:`Layer` objects with flat parameters.
+
+    Subclasses build their layers and call :meth:`build` with the execution
+    order.  ``backend``: ``"auto"`` (native on HIP tensors, torch on CPU),
+    ``"torch"`` (reference ops everywhere, used for parity tests and for the
+    stock-PyTorch comparison) or ``"native"`` (error on CPU).
+    """
+
+    def __init__(self):
+        super().__init__()
+        self.layers: list[Layer] = []
+        self.flat: Optional[FlatParams] = None
+        self.backend = "auto"
+        self.compute_dtype = torch.float32
+        self._accumulate = False
+        self._native_active = False
+        self._grad_hooks: list[Callable] = []
+        self._post_backward_hooks: list[Callable] = []
+        self._anchor = torch.zeros(1, requires_grad=True)
+
+    # ---------------------------------------------------------------- construction
+    def build(self, layers):
+        object.__setattr__(self, "layers", list(layers))  # order list (modules are attrs)
+        for layer in self.layers:
+            for m in layer.modules():
+                if isinstance(m, Layer):
+                    m._prog = self
+        self._flatten()
+        return self
+
+    def _flatten(self):
+        # reverse execution order: the first bucket to become ready in backward
+        # (last layer's grads) is at offset 0.
+        named = []
+        seen = set()
+        for layer in reversed(self.layers):
+            for n, p in layer.named_parameters():
+                if id(p) not in seen:
+                    seen.add(id(p))
+                    named.append((n, p))
+        device = named[0][1].device if named else torch.device("cpu")
+        self.flat = FlatParams(named, device)
+        index = {id(p): i for i, (_, p) in enumerate(named)}
+        for layer in self.layers:
+            for m in layer.modules():
+                if isinstance(m, Layer):
+                    m._pidx = {n: index[id(p)] for n, p in m.named_parameters(recurse=False)}
+        self._param_index = index
+
+    def _write_grad_by_param(self, p, g):
+        slot = self.flat.grad_view(self._param_index[id(p)])
+        if self._accumulate:
+            slot.add_(g.reshape(slot.shape))
+        else:
+            slot.copy_(g.reshape(slot.shape))
+
+    def _apply(self, fn, *args, **kwargs):
+        super()._apply(fn, *args, **kwargs)
+        if self.flat is not None:
+            self._flatten()  # re-flatten after .to()/.cuda()
+        self._anchor = self._anchor.detach().to(self.flat.device if self.flat else "cpu")
+        self._anchor.requires_grad_(True)
+        return self
+
+    def set_backend(self, backend: str):
+        assert backend in ("auto", "torch", "native")
+        self.backend = backend
+        return self
+
+    def set_dtype(self, dtype):
+        """Compute dtype of the native path (fp32 master weights are kept)."""
+        self.compute_dtype = dtype
+        return self
+
+    def _use_native(self, t: torch.Tensor) -> bool:
+        if self.backend == "torch":
+            return False
+        if t.is_cuda:
+            return True
+        if self.backend == "native":
+            raise RuntimeError("native backend requested for a CPU tensor")
+        return False
+
+    # ---------------------------------------------------------------- hooks
+    def register_grad_hook(self, fn):
+        """fn(program, layer_index) after layer i wrote its weight gradients."""
+        self._grad_hooks.append(fn)
+
+    def register_post_backward_hook(self, fn):
+        self._post_backward_hooks.append(fn)
+
+    def layer_params(self, i):
+        return [self._param_index[id(p)] for p in self.layers[i].parameters()]
+
+    # ---------------------------------------------------------------- execution
+    def forward(self, x):
+        self._native_active = self._use_native(x)
+        if self._native_active:
+            self.prepare_native(x)
+        if self.training and torch.is_grad_enabled():
+            return _ProgramFn.apply(x, self._anchor, self)
+        h = x
+        for layer in self.layers:
+            h = layer.fwd(h, Ctx(), False)
+        return h
+
+    def prepare_native(self, x):
+        """Hook for subclasses: convert input layout / refresh packed weights."""
