@@ -91,6 +91,131 @@ void scale_inplace(at::Tensor x, double s) {
   dm::scale_inplace(x.data_ptr<float>(), x.numel(), (float)s, cur_stream());
 }
 
+// ------------------------------------------------------------------ small conv (LeNet)
+inline bool is_bf16(const at::Tensor& t) { return t.scalar_type() == at::kBFloat16; }
+inline void check_act(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda(), n, " must be a HIP tensor");
+  TORCH_CHECK(t.is_contiguous(), n, " must be contiguous");
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, n,
+              " must be fp32/bf16");
+}
+inline const void* optp(const c10::optional<at::Tensor>& t) {
+  return (t.has_value() && t->defined()) ? t->data_ptr() : nullptr;
+}
+
+void conv_small_fwd(at::Tensor x, at::Tensor w, c10::optional<at::Tensor> bias, at::Tensor y,
+                    c10::optional<at::Tensor> mask, int64_t pad, int64_t pool, bool relu) {
+  check_act(x, "x"); check_act(y, "y"); CHECK_F32(w); CHECK_CONTIG(w);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(1) == x.size(1) && w.size(2) == w.size(3));
+  TORCH_CHECK(is_bf16(x) == is_bf16(y), "x/y dtype mismatch");
+  const int B = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int Cout = w.size(0), K = w.size(2);
+  TORCH_CHECK(K == 3 || K == 5, "conv_small supports K in {3,5}");
+  TORCH_CHECK(pool == 1 || pool == 2, "pool must be 1 or 2");
+  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
+  TORCH_CHECK(y.size(0) == B && y.size(1) == Cout && y.size(2) == OH / pool && y.size(3) == OW / pool,
+              "y shape mismatch");
+  if (pool > 1) TORCH_CHECK(mask.has_value() && mask->numel() == y.numel(), "mask required");
+  const DeviceGuard guard(x.device());
+  dm::conv_small_fwd(x.data_ptr(), w.data_ptr<float>(),
+                     bias.has_value() ? bias->data_ptr<float>() : nullptr, y.data_ptr(),
+                     pool > 1 ? (uint8_t*)mask->data_ptr() : nullptr, B, Cin, H, W, Cout, K,
+                     (int)pad, (int)pool, relu ? 1 : 0, is_bf16(x), cur_stream());
+}
+
+void conv_small_bwd(at::Tensor x, at::Tensor w, at::Tensor dp, at::Tensor yp,
+                    c10::optional<at::Tensor> mask, c10::optional<at::Tensor> dx, at::Tensor dw,
+                    c10::optional<at::Tensor> db, at::Tensor work, int64_t pad, int64_t pool,
+                    bool relu, double beta, int64_t bs) {
+  check_act(x, "x"); check_act(dp, "dp"); check_act(yp, "yp");
+  CHECK_F32(w); CHECK_F32(dw); CHECK_F32(work);
+  const int B = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3);
+  const int Cout = w.size(0), K = w.size(2);
+  const int OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
+  const long long total = (long long)B * Cout * OH * OW;
+  const int S = (B + bs - 1) / bs;
+  const long long need = (total + 63) / 64 * 64 + (long long)S * (Cout * Cin * K * K + Cout);
+  TORCH_CHECK(work.numel() >= need, "workspace too small");
+  TORCH_CHECK(dw.numel() == w.numel(), "dw size");
+  if (dx.has_value()) { check_act(*dx, "dx"); TORCH_CHECK(dx->numel() == x.numel()); }
+  if (pool > 1) TORCH_CHECK(mask.has_value() && mask->numel() == dp.numel(), "mask required");
+  const DeviceGuard guard(x.device());
+  dm::conv_small_bwd(x.data_ptr(), w.data_ptr<float>(), dp.data_ptr(), yp.data_ptr(),
+                     pool > 1 ? (const uint8_t*)mask->data_ptr() : nullptr,
+                     dx.has_value() ? dx->data_ptr() : nullptr, dw.data_ptr<float>(),
+                     db.has_value() ? db->data_ptr<float>() : nullptr, work.data_ptr<float>(), B,
+                     Cin, H, W, Cout, K, (int)pad, (int)pool, relu ? 1 : 0, (float)beta, (int)bs,
+                     is_bf16(x), cur_stream());
+}
+
+int64_t conv_small_workspace(int64_t B, int64_t Cin, int64_t H, int64_t W, int64_t Cout,
+                             int64_t K, int64_t pad, int64_t bs) {
+  const long long OH = H + 2 * pad - K + 1, OW = W + 2 * pad - K + 1;
+  const long long total = B * Cout * OH * OW;
+  const long long S = (B + bs - 1) / bs;
+  return (total + 63) / 64 * 64 + S * (Cout * Cin * K * K + Cout);
+}
+
+// ------------------------------------------------------------------ strided GEMM
+// C[m,n] = alpha * sum_k A(m,k) B(k,n) + beta*C + bias ; strides in elements.
+void gemm(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor B, c10::optional<at::Tensor> C,
+          c10::optional<at::Tensor> C32, c10::optional<at::Tensor> bias, int64_t M, int64_t N,
+          int64_t K, int64_t sam, int64_t sak, int64_t sbk, int64_t sbn, int64_t scm,
+          double alpha, double beta, bool relu) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda());
+  auto span_ok = [](const at::Tensor& t, int64_t r, int64_t c, int64_t sr, int64_t sc) {
+    return (r - 1) * sr + (c - 1) * sc < t.numel();
+  };
+  TORCH_CHECK(span_ok(A, M, K, sam, sak), "A too small for M,K,strides");
+  TORCH_CHECK(span_ok(B, K, N, sbk, sbn), "B too small for K,N,strides");
+  if (Amask.has_value()) TORCH_CHECK(Amask->scalar_type() == A.scalar_type() && Amask->numel() >= A.numel());
+  void* cp = nullptr;
+  int cbf = 0;
+  if (C.has_value()) { cp = C->data_ptr(); cbf = is_bf16(*C); TORCH_CHECK(span_ok(*C, M, N, scm, 1)); }
+  float* c32 = nullptr;
+  if (C32.has_value()) { CHECK_F32(*C32); c32 = C32->data_ptr<float>(); TORCH_CHECK(span_ok(*C32, M, N, scm, 1)); }
+  TORCH_CHECK(cp || c32, "an output is required");
+  if (bias.has_value()) { CHECK_F32(*bias); TORCH_CHECK(bias->numel() >= N); }
+  const DeviceGuard guard(A.device());
+  dm::gemm_strided(A.data_ptr(), optp(Amask), is_bf16(A), B.data_ptr(), is_bf16(B), cp, cbf, c32,
+                   bias.has_value() ? bias->data_ptr<float>() : nullptr, M, N, K, sam, sak, sbk,
+                   sbn, scm, (float)alpha, (float)beta, relu ? 1 : 0, cur_stream());
+}
+
+void colsum(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor out, double beta) {
+  TORCH_CHECK(A.is_cuda() && A.dim() == 2 && A.is_contiguous());
+  CHECK_F32(out);
+  TORCH_CHECK(out.numel() == A.size(1));
+  const DeviceGuard guard(A.device());
+  dm::colsum(A.data_ptr(), optp(Amask), is_bf16(A), out.data_ptr<float>(), A.size(0), A.size(1),
+             (float)beta, cur_stream());
+}
+
+// ------------------------------------------------------------------ loss / eval / spin
+void cross_entropy(at::Tensor logits, at::Tensor labels, at::Tensor rowloss, at::Tensor loss,
+                   c10::optional<at::Tensor> dlogits, double scale) {
+  check_act(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && labels.scalar_type() == at::kLong && labels.numel() == logits.size(0));
+  CHECK_F32(rowloss); CHECK_F32(loss);
+  TORCH_CHECK(rowloss.numel() >= logits.size(0));
+  if (dlogits.has_value()) { check_act(*dlogits, "dlogits"); TORCH_CHECK(dlogits->sizes() == logits.sizes() && is_bf16(*dlogits) == is_bf16(logits)); }
+  const DeviceGuard guard(logits.device());
+  dm::cross_entropy(logits.data_ptr(), (const long long*)labels.data_ptr(), rowloss.data_ptr<float>(),
+                    loss.data_ptr<float>(), dlogits.has_value() ? dlogits->data_ptr() : nullptr,
+                    logits.size(0), logits.size(1), (float)scale, -100, is_bf16(logits),
+                    cur_stream());
+}
+
+void argmax_count(at::Tensor logits, at::Tensor labels, at::Tensor correct) {
+  check_act(logits, "logits");
+  TORCH_CHECK(correct.scalar_type() == at::kLong && labels.scalar_type() == at::kLong);
+  const DeviceGuard guard(logits.device());
+  dm::argmax_count(logits.data_ptr(), (const long long*)labels.data_ptr(), logits.size(0), logits.size(1),
+                   (unsigned long long*)correct.data_ptr(), is_bf16(logits), cur_stream());
+}
+
+void spin_us(double us) { dm::spin_us(us, cur_stream()); }
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -100,5 +225,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cast_f32_bf16", &cast_f32_bf16, "fp32 -> bf16 cast");
   m.def("rows_mean", &rows_mean, "[rows,N] -> [N] scaled row sum");
   m.def("scale_inplace", &scale_inplace, "x *= s");
+  m.def("conv_small_fwd", &conv_small_fwd);
+  m.def("conv_small_bwd", &conv_small_bwd);
+  m.def("conv_small_workspace", &conv_small_workspace);
+  m.def("gemm", &gemm);
+  m.def("colsum", &colsum);
+  m.def("cross_entropy", &cross_entropy);
+  m.def("argmax_count", &argmax_count);
+  m.def("spin_us", &spin_us);
   m.attr("arch") = "gfx950";
 }

@@ -1,0 +1,171 @@
+// Strided GEMM on the fp32-input MFMA (v_mfma_f32_16x16x4_f32) for Linear layers.
+//
+//   C[m,n] = alpha * sum_k A(m,k) * B(k,n)  (+ beta*C)  (+ bias[n])  (ReLU)
+//   A(m,k) = A[m*sam + k*sak] (optionally masked by Amask(m,k) > 0: ReLU backward
+//            fused into the operand load), B(k,n) = B[k*sbk + n*sbn]
+//
+// One kernel serves all three Linear GEMMs:
+//   fwd   Y  = X  · Wᵀ     A=X[M,K] (sam=K,sak=1)   B=Wᵀ (sbk=1, sbn=K)
+//   dgrad dX = dY · W      A=dY (masked)           B=W  (sbk=K_in... row-major)
+//   wgrad dW = dYᵀ · X     A=dYᵀ (sam=1, sak=N)     B=X
+// The operands are tiny (LeNet fc 400→120, MLP ≤784×512, ResNet fc 512→1000), so
+// the kernel is latency-oriented: 64×64 tile, 4 waves each owning a 32×32
+// quadrant as 2×2 MFMA 16×16 blocks, BK=16 staged through padded LDS.  Inputs may
+// be fp32 or bf16 (converted on the LDS store; exact fp32 MFMA math either way).
+// Exact f32 numerics: the MFMA is a k-ordered fmaf chain (guide §3).
+#include "common.h"
+
+namespace dm {
+
+template <typename T> __device__ __forceinline__ float ldx(const T* p, long long i);
+template <> __device__ __forceinline__ float ldx<float>(const float* p, long long i) { return p[i]; }
+template <> __device__ __forceinline__ float ldx<bf16_t>(const bf16_t* p, long long i) {
+  return bf2f(p[i]);
+}
+
+constexpr int GBM = 64, GBN = 64, GBK = 16;
+
+template <typename TA, typename TB, typename TC>
+__global__ void __launch_bounds__(256) gemm_f32mfma_kernel(
+    const TA* __restrict__ A, const TA* __restrict__ Amask, const TB* __restrict__ B,
+    TC* __restrict__ C, float* __restrict__ C32, const float* __restrict__ bias, int M, int N,
+    int K, long long sam, long long sak, long long sbk, long long sbn, long long scm,
+    float alpha, float beta, int relu) {
+  __shared__ float As[GBK][GBM + 4];
+  __shared__ float Bs[GBK][GBN + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 < K; k0 += GBK) {
+    // stage A tile [GBK][GBM]: 1024 elems / 256 threads = 4 each
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = tid + r * 256;
+      int mm, kk;
+      if (sak == 1) { mm = e / GBK; kk = e % GBK; }   // k contiguous: walk k fastest
+      else { kk = e / GBM; mm = e % GBM; }            // m contiguous
+      const int gm = m0 + mm, gk = k0 + kk;
+      float v = 0.f;
+      if (gm < M && gk < K) {
+        const long long o = (long long)gm * sam + (long long)gk * sak;
+        v = ldx(A, o);
+        if (Amask && !(ldx(Amask, o) > 0.f)) v = 0.f;
+      }
+      As[kk][mm] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = tid + r * 256;
+      int nn, kk;
+      if (sbk == 1) { nn = e / GBK; kk = e % GBK; }
+      else { kk = e / GBN; nn = e % GBN; }
+      const int gn = n0 + nn, gk = k0 + kk;
+      Bs[kk][nn] = (gn < N && gk < K) ? ldx(B, (long long)gk * sbk + (long long)gn * sbn) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < GBK; ks += 4) {
+      const int kk = ks + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const float a = As[kk][wm + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float b = Bs[kk][wn + j * 16 + (lane & 15)];
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        const int gn = n0 + wn + j * 16 + (lane & 15);
+        if (gm < M && gn < N) {
+          float v = alpha * acc[i][j][r];
+          const long long o = (long long)gm * scm + gn;
+          if (beta != 0.f) v += beta * (C32 ? C32[o] : ldx(C, o));
+          if (bias) v += bias[gn];
+          if (relu) v = fmaxf(v, 0.f);
+          if (C32) C32[o] = v;
+          if (C) {
+            if constexpr (sizeof(TC) == 4) C[o] = v;
+            else C[o] = f2bf(v);
+          }
+        }
+      }
+}
+
+// db[n] = beta*db[n] + sum_m A(m,n) [masked by Amask(m,n) > 0]   (bias gradient)
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ A,
+                                                     const T* __restrict__ Amask,
+                                                     float* __restrict__ out, int M, int N,
+                                                     float beta) {
+  // block = 256 threads: 64 columns x 4 row-groups
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < N)
+    for (int m = rg; m < M; m += 4) {
+      const long long o = (long long)m * N + c;
+      float v = ldx(A, o);
+      if (Amask && !(ldx(Amask, o) > 0.f)) v = 0.f;
+      s += v;
+    }
+  red[rg][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    const float t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                    red[3][threadIdx.x];
+    out[c] = beta * out[c] + t;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+// dtype codes: 0 = fp32, 1 = bf16
+void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, int b_bf16,
+                  void* C, int c_bf16, float* C32, const float* bias, int M, int N, int K,
+                  long long sam, long long sak, long long sbk, long long sbn, long long scm,
+                  float alpha, float beta, int relu, hipStream_t st) {
+  dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+#define DM_GEMM(TA, TB, TC)                                                                  \
+  gemm_f32mfma_kernel<TA, TB, TC><<<grid, 256, 0, st>>>(                                     \
+      (const TA*)A, (const TA*)Amask, (const TB*)B, (TC*)C, C32, bias, M, N, K, sam, sak, sbk, \
+      sbn, scm, alpha, beta, relu)
+  if (!a_bf16 && !b_bf16 && !c_bf16) DM_GEMM(float, float, float);
+  else if (!a_bf16 && !b_bf16 && c_bf16) DM_GEMM(float, float, bf16_t);
+  else if (a_bf16 && !b_bf16 && !c_bf16) DM_GEMM(bf16_t, float, float);
+  else if (a_bf16 && !b_bf16 && c_bf16) DM_GEMM(bf16_t, float, bf16_t);
+  else if (a_bf16 && b_bf16 && !c_bf16) DM_GEMM(bf16_t, bf16_t, float);
+  else if (a_bf16 && b_bf16 && c_bf16) DM_GEMM(bf16_t, bf16_t, bf16_t);
+  else if (!a_bf16 && b_bf16 && !c_bf16) DM_GEMM(float, bf16_t, float);
+  else DM_GEMM(float, bf16_t, bf16_t);
+#undef DM_GEMM
+}
+
+void colsum(const void* A, const void* Amask, int bf16, float* out, int M, int N, float beta,
+            hipStream_t st) {
+  dim3 grid((N + 63) / 64);
+  if (bf16)
+    colsum_kernel<bf16_t><<<grid, 256, 0, st>>>((const bf16_t*)A, (const bf16_t*)Amask, out, M,
+                                                N, beta);
+  else
+    colsum_kernel<float><<<grid, 256, 0, st>>>((const float*)A, (const float*)Amask, out, M, N,
+                                               beta);
+}
+
+}  // namespace dm

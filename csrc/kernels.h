@@ -20,3 +20,28 @@ void rows_mean(const float* x, float* out, int rows, long long n, float scale,
 void scale_inplace(float* x, long long n, float s, hipStream_t st);
 
 }  // namespace dm
+
+namespace dm {
+// conv_small.hip  (NCHW, tiny channel counts; x/y/dx fp32 or bf16, weights fp32)
+void conv_small_fwd(const void* x, const float* w, const float* bias, void* y, uint8_t* mask,
+                    int B, int Cin, int H, int W, int Cout, int K, int pad, int pool, int relu,
+                    bool bf16, hipStream_t st);
+void conv_small_bwd(const void* x, const float* w, const void* dp, const void* yp,
+                    const uint8_t* mask, void* dx, float* dw, float* db, float* work, int B,
+                    int Cin, int H, int W, int Cout, int K, int pad, int pool, int relu,
+                    float beta, int bs, bool bf16, hipStream_t st);
+// gemm.hip
+void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, int b_bf16,
+                  void* C, int c_bf16, float* C32, const float* bias, int M, int N, int K,
+                  long long sam, long long sak, long long sbk, long long sbn, long long scm,
+                  float alpha, float beta, int relu, hipStream_t st);
+void colsum(const void* A, const void* Amask, int bf16, float* out, int M, int N, float beta,
+            hipStream_t st);
+// loss.hip
+void cross_entropy(const void* logits, const long long* labels, float* rowloss, float* loss,
+                   void* dlogits, int B, int C, float scale, int ignore_index, bool bf16,
+                   hipStream_t st);
+void argmax_count(const void* logits, const long long* labels, int B, int C,
+                  unsigned long long* correct, bool bf16, hipStream_t st);
+void spin_us(double us, hipStream_t st);
+}  // namespace dm

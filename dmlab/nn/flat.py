@@ -49,6 +49,7 @@ class FlatParams:
                 v = self.data[o:o + p.numel()].view_as(p)
                 v.copy_(p.data)
                 p.data = v
+                p._dm_flat = self
         self.attach_grads()
 
     # ------------------------------------------------------------ views

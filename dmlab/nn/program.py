@@ -170,7 +170,7 @@ class Program(nn.Module):
         for layer in self.layers:
             for m in layer.modules():
                 if isinstance(m, Layer):
-                    m._prog = self
+                    object.__setattr__(m, "_prog", self)
         self._flatten()
         return self
 

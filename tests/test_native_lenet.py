@@ -1,0 +1,110 @@
+"""Native HIP LeNet / MLP / loss vs the PyTorch fp32 reference of the same ops."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dmlab.models import ForwardNN, Net
+from dmlab.nn import count_correct, cross_entropy
+from dmlab.ops._native import lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(cls, dev, **kw):
+    torch.manual_seed(0)
+    a = cls(**kw).to(dev)
+    b = copy.deepcopy(a).set_backend("torch")
+    b._flatten()
+    return a, b
+
+
+def _grads(m):
+    return {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("B", [1, 32, 257])
+def test_lenet_fwd_bwd_matches_torch(dev, B):
+    lib()  # fail loudly if the extension is missing
+    a, b = _pair(Net, dev)
+    x = torch.rand(B, 1, 28, 28, device=dev)
+    y = torch.randint(0, 10, (B,), device=dev)
+    la = cross_entropy(a(x), y)
+    lb = F.cross_entropy(b(x), y)
+    la.backward()
+    lb.backward()
+    torch.testing.assert_close(la, lb, rtol=1e-4, atol=1e-5)
+    ga, gb = _grads(a), _grads(b)
+    for n in ga:
+        torch.testing.assert_close(ga[n], gb[n], rtol=2e-3, atol=2e-5, msg=n)
+
+
+def test_lenet_grad_accumulation_semantics(dev):
+    a, b = _pair(Net, dev)
+    x = torch.rand(16, 1, 28, 28, device=dev)
+    y = torch.randint(0, 10, (16,), device=dev)
+    for m in (a, b):
+        for _ in range(2):  # no zero_grad in between -> grads accumulate
+            F.cross_entropy(m(x), y).backward()
+    ga, gb = _grads(a), _grads(b)
+    for n in ga:
+        torch.testing.assert_close(ga[n], gb[n], rtol=2e-3, atol=4e-5, msg=n)
+
+
+def test_lenet_input_grad(dev):
+    a, b = _pair(Net, dev)
+    x1 = torch.rand(8, 1, 28, 28, device=dev, requires_grad=True)
+    x2 = x1.detach().clone().requires_grad_(True)
+    a(x1).square().sum().backward()
+    b(x2).square().sum().backward()
+    torch.testing.assert_close(x1.grad, x2.grad, rtol=2e-3, atol=1e-5)
+
+
+def test_mlp_matches_torch(dev):
+    a, b = _pair(ForwardNN, dev)
+    x = torch.rand(64, 1, 28, 28, device=dev)
+    y = torch.randint(0, 10, (64,), device=dev)
+    la = cross_entropy(a(x), y)
+    lb = F.cross_entropy(b(x), y)
+    la.backward()
+    lb.backward()
+    torch.testing.assert_close(la, lb, rtol=1e-4, atol=1e-5)
+    ga, gb = _grads(a), _grads(b)
+    for n in ga:
+        torch.testing.assert_close(ga[n], gb[n], rtol=2e-3, atol=2e-5, msg=n)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_cross_entropy_kernel(dev, dtype):
+    x = (torch.randn(300, 1000, device=dev) * 3).to(dtype).requires_grad_(True)
+    y = torch.randint(0, 1000, (300,), device=dev)
+    l1 = cross_entropy(x, y)
+    l1.backward(torch.tensor(2.0, device=dev))
+    xr = x.detach().float().requires_grad_(True)
+    l2 = F.cross_entropy(xr, y)
+    (2 * l2).backward()
+    torch.testing.assert_close(l1, l2, rtol=1e-4, atol=1e-4)
+    tol = 1e-6 if dtype == torch.float32 else 2e-3
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol, atol=tol)
+
+
+def test_argmax_count(dev):
+    x = torch.randn(1000, 10, device=dev)
+    y = torch.randint(0, 10, (1000,), device=dev)
+    c = count_correct(x, y)
+    assert int(c) == int((x.argmax(1) == y).sum())
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (33, 70, 129), (256, 1000, 512)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_gemm_strided(dev, M, N, K, relu):
+    A = torch.randn(M, K, device=dev)
+    W = torch.randn(N, K, device=dev)
+    bias = torch.randn(N, device=dev)
+    C = torch.empty(M, N, device=dev)
+    lib().gemm(A, None, W, C, None, bias, M, N, K, K, 1, 1, K, N, 1.0, 0.0, relu)
+    ref = A @ W.T + bias
+    if relu:
+        ref = ref.relu()
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-4 * K ** 0.5)
