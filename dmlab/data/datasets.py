@@ -57,7 +57,10 @@ def _prototypes(num_classes, shape, gen):
     return proto
 
 
-def synthetic_classification(n, shape, num_classes, seed, noise=0.35):
+def synthetic_classification(n, shape, num_classes, seed, noise=0.35, sparse=True):
+    """Learnable synthetic data: each class is a smooth random prototype; a sample
+    is its prototype with per-pixel noise.  ``sparse=True`` thresholds the field
+    into MNIST-like strokes on a zero background (mean intensity ~0.1)."""
     gen = torch.Generator().manual_seed(seed)
     proto_gen = torch.Generator().manual_seed(1234)  # prototypes shared by train/test
     proto = _prototypes(num_classes, shape, proto_gen)
@@ -67,7 +70,10 @@ def synthetic_classification(n, shape, num_classes, seed, noise=0.35):
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         nz = torch.rand((e - s,) + tuple(shape), generator=gen)
-        out[s:e] = (1 - noise) * proto[labels[s:e]] + noise * nz
+        f = (1 - noise) * proto[labels[s:e]] + noise * nz
+        if sparse:
+            f = ((f - 0.55) * 4.0).clamp_(0, 1)
+        out[s:e] = f
     return TensorDataset(out.clamp_(0, 1), labels)
 
 

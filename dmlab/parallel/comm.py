@@ -47,11 +47,30 @@ def _is_nccl():
     return env.is_initialized() and dist.get_backend() == "nccl"
 
 
+_AVG_OK = None
+
+
+def avg_supported() -> bool:
+    """Whether the backend implements ReduceOp.AVG (RCCL: ncclAvg).  Probed once
+    with a 1-element collective; gloo never does."""
+    global _AVG_OK
+    if _AVG_OK is None:
+        _AVG_OK = False
+        if _is_nccl():
+            try:
+                t = torch.ones(1, device=env.device())
+                dist.all_reduce(t, op=dist.ReduceOp.AVG)
+                _AVG_OK = abs(t.item() - 1.0) < 1e-6
+            except Exception:
+                _AVG_OK = False
+    return _AVG_OK
+
+
 def all_reduce_mean_(t: torch.Tensor, async_op=False):
     ws = env.get_world_size()
     if ws == 1:
         return None
-    if _is_nccl():
+    if avg_supported():
         return dist.all_reduce(t, op=dist.ReduceOp.AVG, async_op=async_op)
     w = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=async_op)
     if async_op:
@@ -167,15 +186,24 @@ def allgather_average_gradients(model, granularity: str = "flat"):
     if flat is not None and flat.attached():
         src = flat.grad
         gathered = torch.empty((ws, src.numel()), device=src.device, dtype=src.dtype)
-        dist.all_gather_into_tensor(gathered, src)
+        _all_gather_rows(gathered, src)
         _rows_mean(gathered, src)
         return
     gs = _grads(model)
     f = _flatten(gs)
     gathered = torch.empty((ws, f.numel()), device=f.device, dtype=f.dtype)
-    dist.all_gather_into_tensor(gathered, f)
+    _all_gather_rows(gathered, f)
     _rows_mean(gathered, f)
     _unflatten_into(f, gs)
+
+
+def _all_gather_rows(gathered, src):
+    """[ws, N] <- every rank's src; one RCCL all_gather_into_tensor (gloo: list form
+    into row views, still one collective)."""
+    if _is_nccl():
+        dist.all_gather_into_tensor(gathered, src)
+    else:
+        dist.all_gather(list(gathered.unbind(0)), src)
 
 
 def _rows_mean(gathered, out):

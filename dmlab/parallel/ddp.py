@@ -32,7 +32,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from . import env
-from .comm import init_parameters
+from .comm import avg_supported, init_parameters
 
 
 class _Bucket:
@@ -45,15 +45,6 @@ class _Bucket:
         self.comm_buf = None
 
 
-def _probe_avg_supported():
-    if not env.is_initialized() or dist.get_backend() != "nccl":
-        return False
-    try:
-        t = torch.ones(1, device=env.device())
-        dist.all_reduce(t, op=dist.ReduceOp.AVG)
-        return abs(t.item() - 1.0) < 1e-6
-    except Exception:
-        return False
 
 
 class DistributedDataParallel(nn.Module):
@@ -66,7 +57,7 @@ class DistributedDataParallel(nn.Module):
         self.pg = process_group
         self.comm_dtype = comm_dtype
         self.average = average
-        self._use_avg = _probe_avg_supported() if self.ws > 1 else False
+        self._use_avg = avg_supported() if self.ws > 1 else False
         self._fold = False  # 1/ws folded into the optimiser
         self.program = module if hasattr(module, "register_grad_hook") else None
         if broadcast_init and self.ws > 1:

@@ -88,6 +88,9 @@ def init(world_size: int | None = None, rank: int | None = None, master_addr: st
         torch.cuda.set_device(_DEVICE)
     else:
         _DEVICE = torch.device("cpu")
+        # CPU ranks share the host: split the cores instead of oversubscribing
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", ws))
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(lws, 1)))
     backend = backend or default_backend(_DEVICE)
     if ws > 1 or backend is not None:
         if not is_initialized():

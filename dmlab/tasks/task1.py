@@ -1,0 +1,87 @@
+"""Lab 1 — single-node optimisers (GD / SGD / Adam) on MNIST-shaped data.
+
+Reference: codes/task1/pytorch/model.py (LeNet ``Net``, batch 200, 1 epoch,
+``lr = 5e-4·√bs``, ``AdamOptimizer(b1=.9, b2=.999)``, TensorBoard 'Train Loss')
+and the MindSpore MLP notebook (codes/task1/mindspore/model.ipynb: ForwardNN,
+lr 0.1, momentum 0.9, batch 32, 10 epochs).  BASELINE.json config 1 runs this on
+the CPU (``--device cpu``); on a HIP device every op is a native kernel.
+
+    python -m dmlab.tasks.task1 --optimizer adam --model lenet --device cpu
+"""
+from __future__ import annotations
+
+import argparse
+import math
+
+import torch
+
+from dmlab.data import DeviceLoader, load_mnist
+from dmlab.models import ForwardNN, Net
+from dmlab.nn import CrossEntropyLoss
+from dmlab.optim import SGD, AdamOptimizer, GdOptimizer
+from dmlab.tasks.common import test, train
+from dmlab.utils import getSummaryWriter
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    p.add_argument("--model", default="lenet", choices=["lenet", "mlp"])
+    p.add_argument("--optimizer", default="adam", choices=["adam", "gd", "sgd"])
+    p.add_argument("--device", default="cuda" if torch.cuda.is_available() else "cpu")
+    p.add_argument("--batch-size", "--batch_size", type=int, default=None)
+    p.add_argument("--epochs", type=int, default=None)
+    p.add_argument("--lr", type=float, default=None)
+    p.add_argument("--momentum", type=float, default=0.9)
+    p.add_argument("--bias-correction", action="store_true", help="textbook Adam (reference has none)")
+    p.add_argument("--data", default="./data")
+    p.add_argument("--synthetic", action="store_true", help="force synthetic MNIST")
+    p.add_argument("--train-samples", type=int, default=None)
+    p.add_argument("--max-steps", type=int, default=None)
+    p.add_argument("--logdir", default="./logs/")
+    p.add_argument("--del-logs", action="store_true")
+    p.add_argument("--no-tb", action="store_true")
+    p.add_argument("--reference-compat", action="store_true",
+                   help="MLP: softmax before the loss, as the MindSpore notebook")
+    p.add_argument("--seed", type=int, default=0)
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    a = parse_args(argv)
+    torch.manual_seed(a.seed)
+    dev = torch.device(a.device)
+    if a.model == "lenet":
+        bs = a.batch_size or 200            # task1/pytorch/model.py:96
+        epochs = a.epochs or 1              # :97
+        model = Net(1, 10)
+    else:
+        bs = a.batch_size or 32             # model.ipynb create_dataset batch 32
+        epochs = a.epochs or 10             # model.ipynb: 10 epochs
+        model = ForwardNN(reference_compat=a.reference_compat)
+    model = model.to(dev)
+    train_set = load_mnist(a.data, True, synthetic=True if a.synthetic else None, n=a.train_samples)
+    test_set = load_mnist(a.data, False, synthetic=True if a.synthetic else None)
+    train_loader = DeviceLoader(train_set.to(dev), bs, shuffle=True, seed=a.seed)
+    test_loader = DeviceLoader(test_set.to(dev), 32)
+    if a.optimizer == "adam":
+        lr = a.lr if a.lr is not None else 5e-4 * math.sqrt(bs)   # :98
+        opt = AdamOptimizer(model.parameters(), lr=lr, b1=0.9, b2=0.999,
+                            bias_correction=a.bias_correction)
+    elif a.optimizer == "gd":
+        lr = a.lr if a.lr is not None else 5e-4 * math.sqrt(bs)
+        opt = GdOptimizer(model.parameters(), lr=lr)
+    else:
+        lr = a.lr if a.lr is not None else (0.1 if a.model == "mlp" else 0.01)
+        opt = SGD(model.parameters(), lr=lr, momentum=a.momentum)
+    writer = None if a.no_tb else getSummaryWriter(epochs, a.del_logs, a.logdir)
+    stats = train(model, train_loader, CrossEntropyLoss(), opt, epochs, writer=writer,
+                  batch_size=bs, max_steps=a.max_steps, task1_format=True)
+    if writer is not None:
+        writer.close()
+    acc = test(model, test_loader)
+    stats["accuracy"] = acc
+    return stats
+
+
+if __name__ == "__main__":
+    main()
