@@ -1,0 +1,155 @@
+"""Headline benchmark: task3 DDP CNN training throughput on 1..8 MI355X.
+
+Metric (BASELINE.json): "samples/sec (whole node) for task3 DDP CNN at 1/2/4/8
+MI355X"; the scaling-curve headline config is the ResNet-18-shaped CNN, DDP, bf16.
+Each rank trains on its own synthetic ImageNet-shaped batch (random-init weights,
+data resident on the GPU; BASELINE: synthetic data), so per-GPU work is fixed as N
+grows ("weak" scaling).  One timed step = forward + backward (with bucketed RCCL
+all-reduce overlapped) + fused SGD-momentum update of all 11.7 M parameters.
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8 ...
+
+``--model lenet`` benchmarks the reference LeNet at the reference batch (32/rank).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "samples/sec (whole node) for task3 DDP CNN at 1/2/4/8 MI355X"
+# stock PyTorch-ROCm 2.10 (MIOpen/hipBLASLt, channels_last bf16 autocast, SGD) on one
+# MI355X, measured by tools/probe_stock.py (profiles/stock_pytorch_rocm_r1.jsonl)
+STOCK_PER_GPU = {"resnet18": 16912.7, "lenet": 47836.5}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="resnet18", choices=["resnet18", "lenet"])
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
+    ap.add_argument("--res", type=int, default=224)
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--backend", default="native", choices=["native", "torch"])
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    from dmlab.models import Net, ResNet18
+    from dmlab.nn import cross_entropy
+    from dmlab.optim import SGD
+    from dmlab.parallel import DDP, env
+
+    ws_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws_env > 1:
+        dev = env.init()
+    else:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+    rank, ws = env.get_rank(), env.get_world_size()
+    if a.gpus != ws:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
+
+    torch.manual_seed(0)
+    if a.model == "resnet18":
+        bs = a.batch or 256
+        model = ResNet18(num_classes=1000).to(dev)
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        pool = [torch.rand(bs, 3, a.res, a.res, device=dev, generator=g)
+                .contiguous(memory_format=torch.channels_last) for _ in range(2)]
+        labels = [torch.randint(0, 1000, (bs,), device=dev, generator=g) for _ in range(2)]
+        lr = 0.1
+    else:
+        bs = a.batch or 32
+        model = Net().to(dev)
+        g = torch.Generator(device=dev).manual_seed(1000 + rank)
+        pool = [torch.rand(bs, 1, 28, 28, device=dev, generator=g) for _ in range(2)]
+        labels = [torch.randint(0, 10, (bs,), device=dev, generator=g) for _ in range(2)]
+        lr = 0.001
+    if a.backend == "torch":
+        model.set_backend("torch")
+    opt = SGD(model.parameters(), lr=lr, momentum=0.9)
+    net = DDP(model, bucket_cap_mb=a.bucket_mb,
+              comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None)
+    net.fold_average_into(opt)
+
+    def step(i):
+        x, y = pool[i % 2], labels[i % 2]
+        if a.backend == "torch":
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.model == "resnet18"):
+                out = net(x)
+            loss = torch.nn.functional.cross_entropy(out.float(), y)
+        else:
+            loss = cross_entropy(net(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(a.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    env.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    env.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    final_loss = float(loss)
+    ms = dt / a.steps * 1e3
+    value = bs * ws * a.steps / dt
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "samples/s",
+            "n_gpus": ws,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "vs_stock_pytorch_rocm": round(value / (STOCK_PER_GPU[a.model] * ws), 3),
+            "dtype": "bf16" if a.model == "resnet18" else "fp32",
+            "data": "synthetic (device-resident random images, random-init weights)",
+            "config": {
+                "model": a.model,
+                "global_batch": bs * ws,
+                "per_gpu_batch": bs,
+                "seq_len": None,
+                "image_size": a.res if a.model == "resnet18" else 28,
+                "parallelism": f"dp{ws}",
+                "optimizer": "SGD(momentum=0.9), fused flat",
+                "ddp": f"bucketed all-reduce overlapped with backward, bucket {a.bucket_mb} MB, comm {a.comm_dtype}",
+                "backend": a.backend,
+            },
+            "final_loss": round(final_loss, 4),
+        }
+        print(json.dumps(res), flush=True)
+    env.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,300 @@
+// Bindings for the NHWC bf16 ResNet kernels: implicit-GEMM conv (fwd / dgrad /
+// wgrad), BatchNorm, pooling, input/weight packing.  Geometry (ConvGeom) is built
+// here on the host from plain conv parameters, so Python never sees kernel structs.
+#include <torch/extension.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+
+#include "conv_geom.h"
+#include "kernels.h"
+
+namespace {
+
+inline hipStream_t cur_stream() {
+  return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream();
+}
+using DeviceGuard = c10::hip::HIPGuardMasqueradingAsCUDA;
+using bf = dm::bf16_t;
+
+inline bf* bp(const at::Tensor& t) { return reinterpret_cast<bf*>(t.data_ptr()); }
+inline float* fp(const at::Tensor& t) { return t.data_ptr<float>(); }
+
+void need_bf16_nhwc(const at::Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.dim() == 4,
+              n, " must be a contiguous 4-D bf16 HIP tensor [N,H,W,C]");
+  TORCH_CHECK(t.size(3) % 8 == 0, n, ": channels must be a multiple of 8");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, n, " must be 16-B aligned");
+}
+void need_f32(const at::Tensor& t, const char* n, int64_t numel = -1) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous(), n,
+              " must be a contiguous fp32 HIP tensor");
+  if (numel >= 0) TORCH_CHECK(t.numel() >= numel, n, " too small");
+}
+int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  TORCH_CHECK((1 << l) == v, "C/8 must be a power of two");
+  return l;
+}
+
+dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride, int pad, int OH,
+                      int OW) {
+  dm::ConvGeom g{};
+  g.N = x.size(0); g.H = x.size(1); g.W = x.size(2); g.C = x.size(3);
+  g.lgC8 = ilog2(g.C / 8);
+  g.Hg = OH; g.Wg = OW; g.isy = stride; g.isx = stride;
+  g.OH = OH; g.OW = OW; g.OC = Cout; g.osy = 1; g.osx = 1; g.oy0 = 0; g.ox0 = 0;
+  g.nth = KH; g.ntw = KW; g.dy0 = -pad; g.dys = 1; g.dx0 = -pad; g.dxs = 1;
+  g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1; g.KW = KW;
+  g.Ncols = Cout; g.wK = KH * KW * g.C;
+  g.M = (long long)g.N * OH * OW;
+  g.K = KH * KW * g.C;
+  TORCH_CHECK(KH * KW <= dm::MAXTAPS, "too many taps");
+  return g;
+}
+
+// y = conv(x, w)  (+add) ; stats [T][2][Cout] optional
+void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Tensor> stats,
+              c10::optional<at::Tensor> add, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+              int64_t cfg) {
+  need_bf16_nhwc(x, "x");
+  need_bf16_nhwc(y, "y");
+  const int Cout = y.size(3), OH = y.size(1), OW = y.size(2);
+  TORCH_CHECK(OH == (x.size(1) + 2 * pad - KH) / stride + 1 && OW == (x.size(2) + 2 * pad - KW) / stride + 1,
+              "output spatial size mismatch");
+  TORCH_CHECK(wpack.scalar_type() == at::kBFloat16 && wpack.numel() == (int64_t)Cout * KH * KW * x.size(3),
+              "wpack must be bf16 [Cout][KH][KW][C]");
+  auto g = fwd_geom(x, Cout, KH, KW, stride, pad, OH, OW);
+  float* sp = nullptr;
+  if (stats.has_value()) {
+    const int bm = dm::igemm_fwd_rowtile(cfg);
+    need_f32(*stats, "stats", ((g.M + bm - 1) / bm) * 2 * Cout);
+    sp = fp(*stats);
+  }
+  const bf* ap = nullptr;
+  if (add.has_value()) { need_bf16_nhwc(*add, "add"); TORCH_CHECK(add->sizes() == y.sizes()); ap = bp(*add); }
+  const DeviceGuard guard(x.device());
+  dm::igemm_fwd(bp(x), bp(wpack), bp(y), ap, sp, g, cfg, cur_stream());
+}
+
+int64_t conv_stats_rows(int64_t M, int64_t cfg) {
+  const int bm = dm::igemm_fwd_rowtile(cfg);
+  return (M + bm - 1) / bm;
+}
+
+// dx = conv_transpose(dy, w) for stride 1 or 2; accumulate => dx += ...
+void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
+                int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg) {
+  // add: tensor added to the result (may alias dx for in-place accumulation)
+  need_bf16_nhwc(dy, "dy");
+  need_bf16_nhwc(dx, "dx");
+  const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), Cout = dy.size(3);
+  const int H = dx.size(1), W = dx.size(2), Cin = dx.size(3);
+  TORCH_CHECK(dx.size(0) == N);
+  TORCH_CHECK(OH == (H + 2 * pad - KH) / stride + 1 && OW == (W + 2 * pad - KW) / stride + 1,
+              "dgrad shape mismatch");
+  TORCH_CHECK(wd.scalar_type() == at::kBFloat16 && wd.numel() == (int64_t)Cin * KH * KW * Cout,
+              "wd must be bf16 [Cin][KH][KW][Cout]");
+  TORCH_CHECK(stride == 1 || stride == 2, "stride must be 1 or 2");
+  const bf* addp = nullptr;
+  if (add.has_value()) { need_bf16_nhwc(*add, "add"); TORCH_CHECK(add->sizes() == dx.sizes()); addp = bp(*add); }
+  const bool accumulate = addp != nullptr;
+  TORCH_CHECK(stride == 1 || !accumulate || addp == bp(dx),
+              "stride-2 dgrad accumulates only in place (add must alias dx)");
+  const DeviceGuard guard(dy.device());
+  auto st = cur_stream();
+  dm::ConvGeom base{};
+  base.N = N; base.H = OH; base.W = OW; base.C = Cout; base.lgC8 = ilog2(Cout / 8);
+  base.OH = H; base.OW = W; base.OC = Cin;
+  base.KW = KW; base.Ncols = Cin; base.wK = KH * KW * Cout;
+  if (stride == 1) {
+    auto g = base;
+    g.Hg = H; g.Wg = W; g.isy = 1; g.isx = 1; g.osy = 1; g.osx = 1; g.oy0 = 0; g.ox0 = 0;
+    g.nth = KH; g.ntw = KW; g.dy0 = pad; g.dys = -1; g.dx0 = pad; g.dxs = -1;
+    g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
+    g.M = (long long)N * H * W; g.K = KH * KW * Cout;
+    dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
+    return;
+  }
+  // parity classes write disjoint output pixels; a class with no taps (e.g. the odd
+  // pixels of a 1x1/s2 conv) is exactly zero, so zero-fill once up front when needed
+  bool any_empty = false;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      const int kh0 = (a + pad) & 1, kw0 = (b + pad) & 1;
+      if ((KH - kh0 + 1) / 2 <= 0 || (KW - kw0 + 1) / 2 <= 0) any_empty = true;
+    }
+  if (any_empty && !accumulate)
+    TORCH_CHECK(hipMemsetAsync(dx.data_ptr(), 0, dx.numel() * 2, st) == hipSuccess);
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      auto g = base;
+      g.Hg = (H - a + 1) / 2; g.Wg = (W - b + 1) / 2;
+      if (g.Hg <= 0 || g.Wg <= 0) continue;
+      const int kh0 = (a + pad) & 1, kw0 = (b + pad) & 1;
+      const int nth = (KH - kh0 + 1) / 2, ntw = (KW - kw0 + 1) / 2;
+      if (nth <= 0 || ntw <= 0) continue;
+      g.isy = 1; g.isx = 1; g.osy = 2; g.osx = 2; g.oy0 = a; g.ox0 = b;
+      g.nth = nth; g.ntw = ntw;
+      g.dy0 = (a + pad - kh0) / 2; g.dys = -1; g.dx0 = (b + pad - kw0) / 2; g.dxs = -1;
+      g.kh0 = kh0; g.khs = 2; g.kw0 = kw0; g.kws = 2;
+      g.M = (long long)N * g.Hg * g.Wg; g.K = nth * ntw * Cout;
+      dm::igemm_fwd(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr, g, cfg, st);
+    }
+}
+
+// dw (fp32 OIHW [Cout][Cin][KH][KW]) = beta*dw + Σ_m dy ⊗ im2col(x)
+void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int64_t Cin,
+                int64_t KH, int64_t KW, int64_t stride, int64_t pad, double beta, int64_t S,
+                int64_t cfg) {
+  need_bf16_nhwc(x, "x");
+  need_bf16_nhwc(dy, "dy");
+  const int Cout = dy.size(3);
+  need_f32(dw, "dw", (int64_t)Cout * Cin * KH * KW);
+  auto g = fwd_geom(x, Cout, KH, KW, stride, pad, dy.size(1), dy.size(2));
+  TORCH_CHECK(dy.size(0) == x.size(0));
+  need_f32(slab, "slab", (int64_t)S * Cout * g.K);
+  const long long steps = (g.M + 31) / 32;
+  const long long mchunk = ((steps + S - 1) / S) * 32;
+  const DeviceGuard guard(x.device());
+  auto st = cur_stream();
+  dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
+  dm::wgrad_reduce(fp(slab), (int)S, Cout, g.C, (int)Cin, KH, KW, fp(dw), (float)beta, st);
+}
+
+void pack_weights(at::Tensor w, at::Tensor wf, c10::optional<at::Tensor> wd, int64_t Cpad) {
+  need_f32(w, "w");
+  TORCH_CHECK(w.dim() == 4);
+  const int Cout = w.size(0), Cin = w.size(1), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(wf.scalar_type() == at::kBFloat16 && wf.numel() == (int64_t)Cout * KH * KW * Cpad);
+  bf* wdp = nullptr;
+  if (wd.has_value()) {
+    TORCH_CHECK(wd->scalar_type() == at::kBFloat16 && wd->numel() == (int64_t)Cin * KH * KW * Cout);
+    wdp = bp(*wd);
+  }
+  const DeviceGuard guard(w.device());
+  dm::pack_weights(fp(w), bp(wf), wdp, Cout, Cin, Cpad, KH, KW, cur_stream());
+}
+
+// ------------------------------------------------------------------ BN
+void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gamma, at::Tensor beta,
+                       c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
+                       double momentum, double eps, at::Tensor scale, at::Tensor shift,
+                       at::Tensor mean, at::Tensor invstd, at::Tensor work) {
+  const int C = gamma.numel();
+  need_f32(stats, "stats", T * 2 * C);
+  need_f32(work, "work", 64 * 2 * C);
+  for (auto* t : {&gamma, &beta, &scale, &shift, &mean, &invstd}) need_f32(*t, "bn vec", C);
+  const DeviceGuard guard(stats.device());
+  dm::bn_stats_finalize(fp(stats), T, C, count, fp(gamma), fp(beta),
+                        rmean.has_value() ? fp(*rmean) : nullptr, rvar.has_value() ? fp(*rvar) : nullptr,
+                        momentum, eps, fp(scale), fp(shift), fp(mean), fp(invstd), fp(work),
+                        cur_stream());
+}
+
+void bn_eval_coeffs(at::Tensor gamma, at::Tensor beta, at::Tensor rmean, at::Tensor rvar, double eps,
+                    at::Tensor scale, at::Tensor shift) {
+  const int C = gamma.numel();
+  const DeviceGuard guard(gamma.device());
+  dm::bn_eval_coeffs(fp(gamma), fp(beta), fp(rmean), fp(rvar), eps, C, fp(scale), fp(shift),
+                     cur_stream());
+}
+
+void bn_apply(at::Tensor y, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift,
+              at::Tensor out, bool relu) {
+  need_bf16_nhwc(y, "y");
+  need_bf16_nhwc(out, "out");
+  const int C = y.size(3);
+  need_f32(scale, "scale", C);
+  need_f32(shift, "shift", C);
+  const bf* rp = nullptr;
+  if (res.has_value()) { need_bf16_nhwc(*res, "res"); TORCH_CHECK(res->sizes() == y.sizes()); rp = bp(*res); }
+  TORCH_CHECK(out.sizes() == y.sizes());
+  const DeviceGuard guard(y.device());
+  dm::bn_apply(bp(y), rp, fp(scale), fp(shift), bp(out), y.numel(), C, relu, cur_stream());
+}
+
+int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C; }
+
+void bn_backward(at::Tensor dout, at::Tensor out, at::Tensor y, at::Tensor mean, at::Tensor invstd,
+                 at::Tensor gamma, at::Tensor dgamma, at::Tensor dbeta, double gbeta, bool relu,
+                 at::Tensor dy, c10::optional<at::Tensor> dres, at::Tensor work) {
+  need_bf16_nhwc(dout, "dout");
+  need_bf16_nhwc(out, "out");
+  need_bf16_nhwc(y, "y");
+  need_bf16_nhwc(dy, "dy");
+  TORCH_CHECK(dout.sizes() == y.sizes() && out.sizes() == y.sizes() && dy.sizes() == y.sizes());
+  const int C = y.size(3);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "bn_backward: C/8 must divide 256");
+  const long long M = y.numel() / C;
+  need_f32(work, "work", bn_bwd_work(M, C));
+  bf* drp = nullptr;
+  if (dres.has_value()) { need_bf16_nhwc(*dres, "dres"); drp = bp(*dres); }
+  const DeviceGuard guard(y.device());
+  dm::bn_backward(bp(dout), bp(out), bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
+                  (float)gbeta, M, C, relu, bp(dy), drp, fp(work), cur_stream());
+}
+
+// ------------------------------------------------------------------ pooling / packing
+void maxpool_fwd(at::Tensor x, at::Tensor y, at::Tensor idx, int64_t K, int64_t S, int64_t P) {
+  need_bf16_nhwc(x, "x");
+  need_bf16_nhwc(y, "y");
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == y.numel());
+  const DeviceGuard guard(x.device());
+  dm::maxpool_fwd(bp(x), bp(y), (uint8_t*)idx.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3),
+                  y.size(1), y.size(2), K, S, P, cur_stream());
+}
+
+void maxpool_bwd(at::Tensor dy, at::Tensor idx, at::Tensor dx, int64_t K, int64_t S, int64_t P) {
+  need_bf16_nhwc(dy, "dy");
+  need_bf16_nhwc(dx, "dx");
+  const DeviceGuard guard(dy.device());
+  dm::maxpool_bwd(bp(dy), (const uint8_t*)idx.data_ptr(), bp(dx), dx.size(0), dx.size(1), dx.size(2),
+                  dx.size(3), dy.size(1), dy.size(2), K, S, P, cur_stream());
+}
+
+void avgpool_fwd(at::Tensor x, at::Tensor y) {
+  need_bf16_nhwc(x, "x");
+  TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.numel() == x.size(0) * x.size(3));
+  const DeviceGuard guard(x.device());
+  dm::avgpool_fwd(bp(x), bp(y), x.size(0), x.size(1) * x.size(2), x.size(3), cur_stream());
+}
+
+void avgpool_bwd(at::Tensor dy, at::Tensor dx) {
+  need_bf16_nhwc(dx, "dx");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.is_contiguous() && dy.numel() == dx.size(0) * dx.size(3));
+  const DeviceGuard guard(dx.device());
+  dm::avgpool_bwd(bp(dy), bp(dx), dx.size(0), dx.size(1) * dx.size(2), dx.size(3), cur_stream());
+}
+
+void pack_input(at::Tensor x, at::Tensor y) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4);
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16);
+  need_bf16_nhwc(y, "y");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) == x.size(2) && y.size(2) == x.size(3) &&
+              y.size(3) >= x.size(1));
+  const DeviceGuard guard(x.device());
+  dm::pack_input(x.data_ptr(), x.scalar_type() == at::kBFloat16, bp(y), x.size(0), x.size(1),
+                 x.size(2), x.size(3), y.size(3), x.stride(0), x.stride(1), x.stride(2), x.stride(3),
+                 cur_stream());
+}
+
+}  // namespace
+
+void register_resnet(pybind11::module_& m) {
+  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_stats_rows", &conv_stats_rows);
+  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("pack_weights", &pack_weights);
+  m.def("bn_stats_finalize", &bn_stats_finalize);
+  m.def("bn_eval_coeffs", &bn_eval_coeffs);
+  m.def("bn_apply", &bn_apply);
+  m.def("bn_bwd_work", &bn_bwd_work);
+  m.def("bn_backward", &bn_backward);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("pack_input", &pack_input);
+}

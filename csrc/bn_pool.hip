@@ -1,0 +1,485 @@
+// BatchNorm (train-mode batch statistics), fused BN-apply/residual/ReLU, BN backward,
+// max/avg pooling and input packing — NHWC bf16, 16-B vectorised (8 channels/lane).
+//
+// Forward BN statistics are produced by the conv epilogue (conv_igemm.hip) as
+// per-row-tile slabs [T][2][C]; here they are reduced in two fixed-order passes
+// (deterministic) and turned into per-channel scale/shift plus the running-stat
+// update (PyTorch semantics: unbiased variance for running_var, momentum 0.1).
+// BN backward is two memory passes: a reduction of Σdz and Σdz·x̂ (dz = ReLU-masked
+// upstream grad) and an apply pass dy = a·dz + b·y + c that also emits the residual
+// branch gradient dz when the block has a skip connection.
+#include "common.h"
+
+namespace dm {
+
+__device__ __forceinline__ void unpack8(const uint4& v, float f[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f[2 * q] = bf2f((bf16_t)(w[q] & 0xffff));
+    f[2 * q + 1] = bf2f((bf16_t)(w[q] >> 16));
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float f[8]) {
+  return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]),
+                    pack_bf2(f[6], f[7]));
+}
+
+// ------------------------------------------------------------------ slab column reduce
+// in: [T][W] fp32 (W = 2C) ; out: [G][W] partial sums over row groups (fixed order).
+__global__ void __launch_bounds__(256) slab_colsum_kernel(const float* __restrict__ in, int T,
+                                                          int W, float* __restrict__ out) {
+  const int G = gridDim.y, gi = blockIdx.y;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;  // 4 row lanes
+  __shared__ float red[4][64];
+  float s = 0.f;
+  if (col < W)
+    for (int t = gi * 4 + rl; t < T; t += 4 * G) s += in[(long long)t * W + col];
+  red[rl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (rl == 0 && col < W)
+    out[(long long)gi * W + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                   red[3][threadIdx.x];
+}
+
+// stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
+__global__ void __launch_bounds__(256) bn_finalize_kernel(
+    const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
+    float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift,
+    float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s += part[(long long)g * 2 * C + c];
+    q += part[(long long)g * 2 * C + C + c];
+  }
+  const double mean = s / count;
+  double var = q / count - mean * mean;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + eps));
+  const float sc = gamma[c] * invstd;
+  scale[c] = sc;
+  shift[c] = beta[c] - (float)mean * sc;
+  mean_out[c] = (float)mean;
+  invstd_out[c] = invstd;
+  if (rmean) {
+    const double unbiased = count > 1 ? var * count / (count - 1) : var;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+  }
+}
+
+// eval mode: scale/shift from running stats
+__global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
+                                      const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                      float eps, int C, float* __restrict__ scale,
+                                      float* __restrict__ shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = rsqrtf(rvar[c] + eps);
+  scale[c] = gamma[c] * inv;
+  shift[c] = beta[c] - rmean[c] * gamma[c] * inv;
+}
+
+// out = [relu](y*scale + shift [+ res])
+template <bool RES, bool RELU>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ y,
+                                                       const bf16_t* __restrict__ res,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift,
+                                                       bf16_t* __restrict__ out, long long n8,
+                                                       int C) {
+  extern __shared__ float sc_sh[];  // [2][C]
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    sc_sh[i] = scale[i];
+    sc_sh[C + i] = shift[i];
+  }
+  __syncthreads();
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int C8 = C >> 3;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)(i % C8) * 8;
+    float f[8];
+    unpack8(reinterpret_cast<const uint4*>(y)[i], f);
+    float r[8];
+    if (RES) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] * sc_sh[c0 + j] + sc_sh[C + c0 + j];
+      if (RES) v += r[j];
+      if (RELU) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(f);
+  }
+}
+
+// BN backward reduction: per channel Σdz, Σdz·x̂ over rows [M][C]; dz = dout·[out>0]
+// grid: (G); block 256; each thread owns 8 channels (chunk) of rows r ≡ tid/C8 (mod 256/C8)
+template <bool RELU>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ invstd, long long M, int C,
+    float* __restrict__ part) {
+  extern __shared__ float red[];  // [256][16] partials
+  const int C8 = C >> 3;
+  const int chunk = threadIdx.x % C8;
+  const int rl = threadIdx.x / C8;
+  const int RL = blockDim.x / C8;  // row lanes per block (C8 divides 256)
+  const int c0 = chunk * 8;
+  float mu[8], is[8], s[8], q[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = mean[c0 + j];
+    is[j] = invstd[c0 + j];
+    s[j] = 0.f;
+    q[j] = 0.f;
+  }
+  for (long long r = (long long)blockIdx.x * RL + rl; r < M; r += (long long)gridDim.x * RL) {
+    const long long i = r * C8 + chunk;
+    float d[8], yv[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+    if (RELU) {
+      float o[8];
+      unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      s[j] += d[j];
+      q[j] += d[j] * (yv[j] - mu[j]) * is[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x * 16 + j] = s[j];
+    red[threadIdx.x * 16 + 8 + j] = q[j];
+  }
+  __syncthreads();
+  // combine row lanes: thread t < C8*16 handles (chunk, j)
+  for (int e = threadIdx.x; e < C8 * 16; e += blockDim.x) {
+    const int ch = e / 16, j = e % 16;
+    float acc = 0.f;
+    for (int l = 0; l < RL; ++l) acc += red[(l * C8 + ch) * 16 + j];
+    const int c = ch * 8 + (j & 7);
+    part[(long long)blockIdx.x * 2 * C + (j < 8 ? 0 : C) + c] = acc;
+  }
+}
+
+// finalize: Σ over G partials -> dgamma, dbeta (written with beta-accumulate into grad
+// slots) and the affine dy coefficients a, b, c.
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
+    const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dgamma,
+    float* __restrict__ dbeta, float gbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0, q = 0.0;
+  for (int g = 0; g < G; ++g) {
+    s += part[(long long)g * 2 * C + c];
+    q += part[(long long)g * 2 * C + C + c];
+  }
+  dbeta[c] = (gbeta != 0.f ? gbeta * dbeta[c] : 0.f) + (float)s;
+  dgamma[c] = (gbeta != 0.f ? gbeta * dgamma[c] : 0.f) + (float)q;
+  const float a = gamma[c] * invstd[c];
+  const float inv_m = (float)(1.0 / count);
+  const float b = -a * invstd[c] * (float)q * inv_m;
+  const float cc = -a * (float)s * inv_m - b * mean[c];
+  coef[c] = a;
+  coef[C + c] = b;
+  coef[2 * C + c] = cc;
+}
+
+// dy = a·dz + b·y + c ; optional dres = dz
+template <bool RELU, bool DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
+    const float* __restrict__ coef, bf16_t* __restrict__ dy, bf16_t* __restrict__ dres,
+    long long n8, int C) {
+  extern __shared__ float cf[];  // [3][C]
+  for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
+  __syncthreads();
+  const int C8 = C >> 3;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    const int c0 = (int)(i % C8) * 8;
+    float d[8], yv[8];
+    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+    if (RELU) {
+      float o[8];
+      unpack8(reinterpret_cast<const uint4*>(out)[i], o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+    }
+    if (DRES) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
+    reinterpret_cast<uint4*>(dy)[i] = pack8(r);
+  }
+}
+
+// ------------------------------------------------------------------ max pool (NHWC)
+// out[n,oh,ow,c] = max window; idx = argmax position in window (0..K*K-1), first max wins
+__global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, int N, int H,
+                                                          int W, int C, int OH, int OW, int K,
+                                                          int S, int P) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * OH * OW * C8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c8 = i % C8;
+    long long t = i / C8;
+    const int ow = t % OW;
+    t /= OW;
+    const int oh = t % OH;
+    const int n = t / OH;
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * S - P + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = ow * S - P + kw;
+        if (iw < 0 || iw >= W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(x + (((long long)n * H + ih) * W + iw) * C + c8 * 8), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (f[j] > best[j]) { best[j] = f[j]; arg[j] = kh * K + kw; }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    a.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+    reinterpret_cast<uint2*>(idx)[i] = a;
+  }
+}
+
+// dx[n,ih,iw,c] = Σ_{windows (oh,ow) containing (ih,iw) whose argmax is (ih,iw)} dy
+__global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx,
+                                                          bf16_t* __restrict__ dx, int N, int H,
+                                                          int W, int C, int OH, int OW, int K,
+                                                          int S, int P) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * H * W * C8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c8 = i % C8;
+    long long t = i / C8;
+    const int iw = t % W;
+    t /= W;
+    const int ih = t % H;
+    const int n = t / H;
+    float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // output windows covering ih: oh in [ceil((ih+P-K+1)/S), floor((ih+P)/S)]
+    const int oh_lo = max(0, (ih + P - K + S) / S), oh_hi = min(OH - 1, (ih + P) / S);
+    const int ow_lo = max(0, (iw + P - K + S) / S), ow_hi = min(OW - 1, (iw + P) / S);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh)
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const int code = (ih - (oh * S - P)) * K + (iw - (ow * S - P));
+        const long long o = (((long long)n * OH + oh) * OW + ow) * C8 + c8;
+        const uint2 a = reinterpret_cast<const uint2*>(idx)[o];
+        float d[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+        const uint32_t aw[2] = {a.x, a.y};
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == (uint32_t)code) g[j] += d[j];
+      }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(g);
+  }
+}
+
+// ------------------------------------------------------------------ global average pool
+// x [N][HW][C] -> y [N][C] (bf16), fp32 accumulation; one block per (n, 8-channel group)
+__global__ void __launch_bounds__(256) avgpool_fwd_kernel(const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y, int HW, int C) {
+  const int n = blockIdx.y;
+  const int c = blockIdx.x * 8;
+  __shared__ float red[256][8];
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    float f[8];
+    unpack8(*reinterpret_cast<const uint4*>(x + ((long long)n * HW + p) * C + c), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] += f[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = s[j];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[threadIdx.x][j] += red[threadIdx.x + o][j];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float f[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = red[0][j] / HW;
+    *reinterpret_cast<uint4*>(y + (long long)n * C + c) = pack8(f);
+  }
+}
+
+__global__ void __launch_bounds__(256) avgpool_bwd_kernel(const bf16_t* __restrict__ dy,
+                                                          bf16_t* __restrict__ dx, int N, int HW,
+                                                          int C) {
+  const int C8 = C >> 3;
+  const long long total = (long long)N * HW * C8;
+  const float inv = 1.f / HW;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c8 = i % C8;
+    const int n = (i / C8) / HW;
+    float d[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[(long long)n * C8 + c8], d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] *= inv;
+    reinterpret_cast<uint4*>(dx)[i] = pack8(d);
+  }
+}
+
+// ------------------------------------------------------------------ input packing
+// x: fp32 or bf16 with arbitrary NCHW strides (sn, sc, sh, sw in elements) -> NHWC bf16,
+// channels zero-padded to Cp (multiple of 8)
+template <typename T>
+__global__ void __launch_bounds__(256) pack_input_kernel(const T* __restrict__ x,
+                                                         bf16_t* __restrict__ y, int N, int C,
+                                                         int H, int W, int Cp, long long sn,
+                                                         long long sc, long long sh, long long sw) {
+  const long long total = (long long)N * H * W;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int w = i % W;
+    long long t = i / W;
+    const int h = t % H;
+    const int n = t / H;
+    const T* src = x + n * sn + h * sh + w * sw;
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        if (c < C) {
+          if constexpr (sizeof(T) == 4) f[j] = src[c * sc];
+          else f[j] = bf2f(src[c * sc]);
+        } else {
+          f[j] = 0.f;
+        }
+      }
+      *reinterpret_cast<uint4*>(y + i * Cp + c0) = pack8(f);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
+                       const float* beta, float* rmean, float* rvar, float momentum, float eps,
+                       float* scale, float* shift, float* mean, float* invstd, float* work,
+                       hipStream_t st) {
+  const int W = 2 * C;
+  const int G = min(64, max(1, T / 16));
+  slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
+  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(work, G, C, count, gamma, beta, rmean, rvar,
+                                                      momentum, eps, scale, shift, mean, invstd);
+}
+
+void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                    float eps, int C, float* scale, float* shift, hipStream_t st) {
+  bn_eval_coeffs_kernel<<<(C + 255) / 256, 256, 0, st>>>(gamma, beta, rmean, rvar, eps, C, scale,
+                                                         shift);
+}
+
+void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
+              bf16_t* out, long long n, int C, bool relu, hipStream_t st) {
+  const long long n8 = n / 8;
+  const int grid = grid_for(n8, 256, 4096);
+  const size_t sh = sizeof(float) * 2 * C;
+  if (res) {
+    if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
+    else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
+  } else {
+    if (relu) bn_apply_kernel<false, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
+    else bn_apply_kernel<false, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
+  }
+}
+
+int bn_bwd_groups(long long M, int C) {
+  const int RL = 256 / (C / 8);
+  long long g = (M + RL * 64 - 1) / (RL * 64);  // >= 64 rows per row lane
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* mean,
+                 const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                 float gbeta, long long M, int C, bool relu, bf16_t* dy, bf16_t* dres,
+                 float* work, hipStream_t st) {
+  // work: [G][2C] partials + [3C] coefficients
+  const int G = bn_bwd_groups(M, C);
+  float* part = work;
+  float* coef = work + (long long)G * 2 * C;
+  const size_t shr = sizeof(float) * 256 * 16;
+  if (relu) bn_bwd_reduce_kernel<true><<<G, 256, shr, st>>>(dout, out, y, mean, invstd, M, C, part);
+  else bn_bwd_reduce_kernel<false><<<G, 256, shr, st>>>(dout, out, y, mean, invstd, M, C, part);
+  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(part, G, C, (double)M, gamma, mean,
+                                                          invstd, dgamma, dbeta, gbeta, coef);
+  const long long n8 = M * C / 8;
+  const int grid = grid_for(n8, 256, 4096);
+  const size_t sh = sizeof(float) * 3 * C;
+#define DM_BNB(R, D) bn_bwd_apply_kernel<R, D><<<grid, 256, sh, st>>>(dout, out, y, coef, dy, dres, n8, C)
+  if (relu && dres) DM_BNB(true, true);
+  else if (relu) DM_BNB(true, false);
+  else if (dres) DM_BNB(false, true);
+  else DM_BNB(false, false);
+#undef DM_BNB
+}
+
+void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
+                 int OW, int K, int S, int P, hipStream_t st) {
+  const long long total = (long long)N * OH * OW * (C / 8);
+  maxpool_fwd_kernel<<<grid_for(total, 256, 8192), 256, 0, st>>>(x, y, idx, N, H, W, C, OH, OW, K, S, P);
+}
+
+void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
+                 int OH, int OW, int K, int S, int P, hipStream_t st) {
+  const long long total = (long long)N * H * W * (C / 8);
+  maxpool_bwd_kernel<<<grid_for(total, 256, 8192), 256, 0, st>>>(dy, idx, dx, N, H, W, C, OH, OW, K, S, P);
+}
+
+void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st) {
+  avgpool_fwd_kernel<<<dim3(C / 8, N), 256, 0, st>>>(x, y, HW, C);
+}
+
+void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st) {
+  const long long total = (long long)N * HW * (C / 8);
+  avgpool_bwd_kernel<<<grid_for(total, 256, 8192), 256, 0, st>>>(dy, dx, N, HW, C);
+}
+
+void pack_input(const void* x, bool bf16, bf16_t* y, int N, int C, int H, int W, int Cp,
+                long long sn, long long sc, long long sh, long long sw, hipStream_t st) {
+  const long long total = (long long)N * H * W;
+  if (bf16)
+    pack_input_kernel<bf16_t><<<grid_for(total, 256, 8192), 256, 0, st>>>(
+        (const bf16_t*)x, y, N, C, H, W, Cp, sn, sc, sh, sw);
+  else
+    pack_input_kernel<float><<<grid_for(total, 256, 8192), 256, 0, st>>>(
+        (const float*)x, y, N, C, H, W, Cp, sn, sc, sh, sw);
+}
+
+}  // namespace dm

@@ -1,0 +1,25 @@
+// Geometry of one implicit-GEMM convolution launch (shared by host and device code).
+#pragma once
+
+namespace dm {
+
+constexpr int MAXTAPS = 64;
+
+struct ConvGeom {
+  int N, H, W, C;            // input tensor NHWC; C % 8 == 0 and C/8 a power of two
+  int lgC8;                  // log2(C / 8)
+  int Hg, Wg;                // GEMM rows: m = (n*Hg + y)*Wg + x
+  int isy, isx;              // input coordinate = (y*isy + dy_t, x*isx + dx_t)
+  int OH, OW, OC;            // output tensor (NHWC, channel count OC)
+  int osy, osx, oy0, ox0;    // output coordinate = (y*osy + oy0, x*osx + ox0)
+  // tap grid: t = th*ntw + tw, th < nth, tw < ntw
+  int nth, ntw;
+  int dy0, dys, dx0, dxs;    // dy_t = dy0 + th*dys, dx_t = dx0 + tw*dxs
+  int kh0, khs, kw0, kws, KW;// packed-weight tap = (kh0 + th*khs)*KW + (kw0 + tw*kws)
+  int Ncols;                 // output channels of the GEMM
+  int wK;                    // packed weight row length (elements) = KH*KW*C
+  long long M;               // N*Hg*Wg
+  int K;                     // ntaps*C
+};
+
+}  // namespace dm

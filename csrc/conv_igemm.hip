@@ -1,0 +1,516 @@
+// NHWC bf16 implicit-GEMM convolution on MFMA (v_mfma_f32_16x16x32_bf16), gfx950.
+//
+// One forward-style kernel covers every conv GEMM that writes activations:
+//   * forward        Y[m, co]  = Σ_{tap, ci} X[n, y*s + dy_t, x*s + dx_t, ci] · W[co, tap, ci]
+//   * dgrad stride 1 dX[m, ci] = Σ_{tap, co} dY[n, y + dy_t, x + dx_t, co] · Wt[ci, tap, co]
+//                    (tap offsets dy_t = p − kh encode the 180° kernel flip)
+//   * dgrad stride 2 one launch per output parity class (a, b): rows m = (n, y, x) are the
+//                    output pixels (2y+a, 2x+b); only the taps with kh ≡ a+p (mod 2) are
+//                    visited, so no MFMA work is spent on the 3/4 structural zeros.
+// The per-launch geometry is an arithmetic tap grid (ConvGeom) expanded into an LDS
+// table once per block.
+//
+// Tiling (CDNA4, wave64): BM×BN block tile, BK = 64 (one 128-B row per tile row),
+// 4 waves each owning a (BM/WM)×(BN/WN) sub-tile as 16×16 MFMA blocks; the LDS image
+// is row-major with the 16-B chunk XOR-swizzle  chunk ^ ((row >> 1) & 7), which makes
+// every ds_read_b128 fragment read of the 16x16x32 operand map and every 8-lane
+// ds_write_b128 group conflict-free (see docs/KERNELS.md for the derivation).
+// Global→LDS staging is register-double-buffered: tile k+1 is loaded into VGPRs
+// before the MFMAs of tile k and written to the other LDS buffer after them, so one
+// barrier per K-tile suffices.  The epilogue stages the fp32 tile through LDS to emit
+// fully coalesced 16-B bf16 stores, optionally adds a residual/accumulate tensor, and
+// reduces per-channel Σy and Σy² (BatchNorm batch statistics) from the fp32
+// accumulators into a per-row-tile slab — BN statistics cost no extra pass over Y.
+//
+// Weight gradient (igemm_wgrad): dW[co, tap, ci] = Σ_m dY[m, co] · X_im2col[m, (tap, ci)]
+// reduces over m, which is the row index of both operands in memory, so both tiles
+// are staged [m][cols] and read with the CDNA4 transpose read ds_read_b64_tr_b16.
+// The reduction is split over blocks into fp32 slabs and combined by a fixed-order
+// reduce that also permutes to the OIHW fp32 gradient layout and applies beta.
+#include "common.h"
+#include "conv_geom.h"
+
+namespace dm {
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// ------------------------------------------------------------------ forward / dgrad
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
+    const bf16_t* ADD /* may alias Y (in-place accumulate) */, float* __restrict__ stats,
+    ConvGeom g) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;     // wave tile
+  constexpr int RM = TM / 16, RN = TN / 16;     // MFMA blocks per wave
+  constexpr int AR = BM / 32, BR = BN / 32;     // rows per thread to stage (8 chunks per row)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                 // [2][BM][BK]
+  bf16_t* Bs = As + 2 * BM * BK;                                 // [2][BN][BK]
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);        // [MAXTAPS] {dy, dx, wcol, 0}
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ntaps = g.nth * g.ntw;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs,
+                          ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C, 0);
+  }
+  // rows this thread stages: r = tid/8 + 32*i, chunk = tid%8
+  const int chunk = tid & 7;
+  int a_iy[AR], a_ix[AR];
+  long long a_nb[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const long long m = m0 + (tid >> 3) + 32 * i;
+    if (m < g.M) {
+      const int x = (int)(m % g.Wg);
+      const long long t = m / g.Wg;
+      const int y = (int)(t % g.Hg);
+      const int n = (int)(t / g.Hg);
+      a_iy[i] = y * g.isy;
+      a_ix[i] = x * g.isx;
+      a_nb[i] = (long long)n * g.H * g.W;
+    } else {
+      a_iy[i] = -(1 << 28);  // never in range
+      a_ix[i] = 0;
+      a_nb[i] = 0;
+    }
+  }
+  __syncthreads();
+
+  uint4 ra[AR], rb[BR];
+  const int nk = (g.K + BK - 1) / BK;
+
+  auto load = [&](int kt) {
+    const int kc = kt * (BK / 8) + chunk;           // global 8-element chunk index
+    const int tap = kc >> g.lgC8;
+    const int c0 = (kc & ((1 << g.lgC8) - 1)) * 8;
+    const bool kval = tap < ntaps;
+    int4 tp = make_int4(0, 0, 0, 0);
+    if (kval) tp = taps[tap];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kval && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+        v = *reinterpret_cast<const uint4*>(X + ((a_nb[i] + (long long)iy * g.W + ix) * g.C + c0));
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kval && n < g.Ncols)
+        v = *reinterpret_cast<const uint4*>(Wp + (long long)n * g.wK + tp.z + c0);
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    bf16_t* as = As + buf * BM * BK;
+    bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);
+    const bf16_t* as = As + buf * BM * BK;
+    const bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int r = wm * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int r = wn * TN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue 1: BN batch statistics (Σ, Σ²) per output channel
+  float* red = reinterpret_cast<float*>(smem);  // reuse LDS (main loop finished)
+  if (stats) {
+    // red layout: [WM][BN][2]
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = acc[i][j][r];
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        const int c = wn * TN + j * 16 + lane;
+        red[(wm * BN + c) * 2 + 0] = s;
+        red[(wm * BN + c) * 2 + 1] = q;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += 256) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s += red[(w * BN + c) * 2 + 0];
+        q += red[(w * BN + c) * 2 + 1];
+      }
+      if (n0 + c < g.Ncols) {
+        stats[((long long)blockIdx.x * 2 + 0) * g.Ncols + n0 + c] = s;
+        stats[((long long)blockIdx.x * 2 + 1) * g.Ncols + n0 + c] = q;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue 2: fp32 tile -> LDS -> coalesced 16-B bf16 stores
+  constexpr int LDC = BN + 4;
+  float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC] fp32 (BM*LDC*4 <= LDS budget)
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int col = wn * TN + j * 16 + (lane & 15);
+        cs[row * LDC + col] = acc[i][j][r];
+      }
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-wide chunks per row
+  for (int e = tid; e < BM * CPR; e += 256) {
+    const int row = e / CPR, cc = e % CPR;
+    const long long m = m0 + row;
+    const int col = n0 + cc * 8;
+    if (m >= g.M || col >= g.Ncols) continue;
+    const int x = (int)(m % g.Wg);
+    const long long t = m / g.Wg;
+    const int y = (int)(t % g.Hg);
+    const int n = (int)(t / g.Hg);
+    const long long o =
+        (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+    const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
+    const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
+    float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    if (ADD) {
+      const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
+      const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
+        v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+      }
+    }
+    *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                                  pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+  }
+}
+
+// ------------------------------------------------------------------ weight gradient
+// grid: (ceil(Ncols/BM), ceil(K/BN), S).  Block reduces m in [s*mchunk, min(M,(s+1)*mchunk)).
+// A = dY (rows m, cols co), B = im2col(X) (rows m, cols k); LDS images [m][cols+PAD].
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) igemm_wgrad_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
+    ConvGeom g, long long mchunk) {
+  constexpr int BKM = 32;                  // m rows per K-step (one MFMA k=32)
+  constexpr int PAD = 16;                  // row stride ≡ 32 B (mod 256 B): tr reads conflict-free
+  constexpr int LA = BM + PAD, LB = BN + PAD;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int RM = TM / 16, RN = TN / 16;
+  constexpr int ACH = BM / 8, BCH = BN / 8;               // 16-B chunks per row
+  constexpr int AIT = (BKM * ACH + 255) / 256, BIT = (BKM * BCH + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);           // [2][BKM][LA]
+  bf16_t* Bs = As + 2 * BKM * LA;                         // [2][BKM][LB]
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BKM * LB);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int co0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
+  const long long mb = (long long)blockIdx.z * mchunk;
+  const long long me = min(g.M, mb + mchunk);
+  const int ntaps = g.nth * g.ntw;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs, 0, 0);
+  }
+  __syncthreads();
+
+  uint4 ra[AIT], rb[BIT];
+  auto load = [&](long long mt) {
+#pragma unroll
+    for (int it = 0; it < AIT; ++it) {
+      const int e = tid + it * 256;
+      const int r = e / ACH, c = e % ACH;
+      const long long m = mt + r;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < BKM * ACH && m < me && co0 + c * 8 < g.Ncols)
+        v = *reinterpret_cast<const uint4*>(DY + m * g.Ncols + co0 + c * 8);
+      ra[it] = v;
+    }
+#pragma unroll
+    for (int it = 0; it < BIT; ++it) {
+      const int e = tid + it * 256;
+      const int r = e / BCH, c = e % BCH;
+      const long long m = mt + r;
+      const int kc = (k0 >> 3) + c;
+      const int tap = kc >> g.lgC8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < BKM * BCH && m < me && tap < ntaps) {
+        const int c0 = (kc & ((1 << g.lgC8) - 1)) * 8;
+        const int x = (int)(m % g.Wg);
+        const long long t = m / g.Wg;
+        const int y = (int)(t % g.Hg);
+        const int n = (int)(t / g.Hg);
+        const int4 tp = taps[tap];
+        const int iy = y * g.isy + tp.x, ix = x * g.isx + tp.y;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          v = *reinterpret_cast<const uint4*>(
+              X + (((long long)n * g.H + iy) * g.W + ix) * g.C + c0);
+      }
+      rb[it] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    bf16_t* as = As + buf * BKM * LA;
+    bf16_t* bs = Bs + buf * BKM * LB;
+#pragma unroll
+    for (int it = 0; it < AIT; ++it) {
+      const int e = tid + it * 256;
+      if (e < BKM * ACH) {
+        const int r = e / ACH, c = e % ACH;
+        *reinterpret_cast<uint4*>(as + r * LA + c * 8) = ra[it];
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < BIT; ++it) {
+      const int e = tid + it * 256;
+      if (e < BKM * BCH) {
+        const int r = e / BCH, c = e % BCH;
+        *reinterpret_cast<uint4*>(bs + r * LB + c * 8) = rb[it];
+      }
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // transpose-read addressing: lane = 16*grp + 4*q + p ; block rows grp*4 + q (+16),
+  // columns col0 + 4p.  Element e<4 of the fragment = m-row 4*grp+e, e>=4: 16+4*grp+e-4
+  // (a k-permutation applied identically to A and B, so the MFMA sum is unchanged).
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int nsteps = (int)((me - mb + BKM - 1) / BKM);
+  if (nsteps > 0) {
+    load(mb);
+    store(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) load(mb + (long long)(st + 1) * BKM);
+    const bf16_t* as = As + buf * BKM * LA;
+    const bf16_t* bs = Bs + buf * BKM * LB;
+    bf16x8 af[RM], bfr[RN];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const int col = wm * TM + i * 16 + 4 * p;
+      typedef short s4 __attribute__((ext_vector_type(4)));
+      const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4*)(as + (grp * 4 + q) * LA + col));
+      const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4*)(as + (16 + grp * 4 + q) * LA + col));
+      af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      const int col = wn * TN + j * 16 + 4 * p;
+      typedef short s4 __attribute__((ext_vector_type(4)));
+      const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4*)(bs + (grp * 4 + q) * LB + col));
+      const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s4*)(bs + (16 + grp * 4 + q) * LB + col));
+      bfr[j] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < RM; ++i)
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    if (st + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+  // slab[s][co][k] (row length K, fp32)
+  float* out = slab + (long long)blockIdx.z * g.Ncols * g.K;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wn * TN + j * 16 + (lane & 15);
+        if (co < g.Ncols && k < g.K) out[(long long)co * g.K + k] = acc[i][j][r];
+      }
+}
+
+// dw[co][ci][kh][kw] = beta*dw + Σ_s slab[s][co][(kh*KW+kw)*C + ci]   (ci < Cin)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                           int S, int Cout, int C, int Cin,
+                                                           int KH, int KW,
+                                                           float* __restrict__ dw, float beta) {
+  const long long total = (long long)Cout * Cin * KH * KW;
+  const long long K = (long long)KH * KW * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int kw = o % KW;
+    long long t = o / KW;
+    const int kh = t % KH;
+    t /= KH;
+    const int ci = t % Cin;
+    const int co = t / Cin;
+    const long long src = (long long)co * K + (kh * KW + kw) * C + ci;
+    float s = 0.f;
+    for (int i = 0; i < S; ++i) s += slab[(long long)i * Cout * K + src];
+    dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + s;
+  }
+}
+
+// ------------------------------------------------------------------ weight packing
+// fp32 OIHW -> bf16 [Cout][KH][KW][Cpad] (forward) and optionally
+// bf16 [Cin][KH][KW][Cout] (dgrad; transpose only — the flip is in the tap offsets).
+__global__ void __launch_bounds__(256) pack_weights_kernel(const float* __restrict__ w,
+                                                           bf16_t* __restrict__ wf,
+                                                           bf16_t* __restrict__ wd, int Cout,
+                                                           int Cin, int Cpad, int KH, int KW) {
+  const long long total = (long long)Cout * KH * KW * Cpad;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int ci = o % Cpad;
+    long long t = o / Cpad;
+    const int kw = t % KW;
+    t /= KW;
+    const int kh = t % KH;
+    const int co = t / KH;
+    const float v = ci < Cin ? w[(((long long)co * Cin + ci) * KH + kh) * KW + kw] : 0.f;
+    const bf16_t b = f2bf(v);
+    wf[o] = b;
+    if (wd && ci < Cin) wd[(((long long)ci * KH + kh) * KW + kw) * Cout + co] = b;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+static size_t fwd_smem(int BM, int BN) {
+  const size_t main = (size_t)2 * (BM + BN) * 64 * 2 + MAXTAPS * 16;
+  const size_t epi = (size_t)BM * (BN + 4) * 4;
+  return main > epi ? main : epi;
+}
+
+template <typename K>
+static void set_smem_attr(K kernel, size_t bytes) {
+  // dynamic LDS above 64 KiB must be opted into per kernel
+  static bool done = false;
+  if (!done) {
+    DM_CHECK(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)bytes));
+    done = true;
+  }
+}
+
+void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+               const ConvGeom& g, int cfg, hipStream_t st) {
+  // cfg 0: 128x128 (2x2 waves, 64x64 per wave), 1: 128x64 (2x2), 2: 64x64 (2x2)
+  if (cfg == 0) {
+    auto k = igemm_fwd_kernel<128, 128, 2, 2>;
+    const size_t sm = fwd_smem(128, 128);
+    set_smem_attr(k, sm);
+    dim3 grid((unsigned)((g.M + 127) / 128), (g.Ncols + 127) / 128);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g);
+  } else if (cfg == 1) {
+    auto k = igemm_fwd_kernel<128, 64, 2, 2>;
+    const size_t sm = fwd_smem(128, 64);
+    set_smem_attr(k, sm);
+    dim3 grid((unsigned)((g.M + 127) / 128), (g.Ncols + 63) / 64);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g);
+  } else {
+    auto k = igemm_fwd_kernel<64, 64, 2, 2>;
+    const size_t sm = fwd_smem(64, 64);
+    set_smem_attr(k, sm);
+    dim3 grid((unsigned)((g.M + 63) / 64), (g.Ncols + 63) / 64);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g);
+  }
+}
+
+int igemm_fwd_rowtile(int cfg) { return cfg == 2 ? 64 : 128; }
+
+static size_t wgrad_smem(int BM, int BN) {
+  return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;
+}
+
+void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                 long long mchunk, int cfg, hipStream_t st) {
+  if (cfg == 0) {
+    dim3 grid((g.Ncols + 127) / 128, (g.K + 127) / 128, S);
+    igemm_wgrad_kernel<128, 128, 2, 2><<<grid, 256, wgrad_smem(128, 128), st>>>(X, DY, slab, g, mchunk);
+  } else {
+    dim3 grid((g.Ncols + 63) / 64, (g.K + 127) / 128, S);
+    igemm_wgrad_kernel<64, 128, 2, 2><<<grid, 256, wgrad_smem(64, 128), st>>>(X, DY, slab, g, mchunk);
+  }
+}
+
+void wgrad_reduce(const float* slab, int S, int Cout, int C, int Cin, int KH, int KW, float* dw,
+                  float beta, hipStream_t st) {
+  const long long total = (long long)Cout * Cin * KH * KW;
+  wgrad_reduce_kernel<<<grid_for(total, 256), 256, 0, st>>>(slab, S, Cout, C, Cin, KH, KW, dw, beta);
+}
+
+void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int Cpad, int KH,
+                  int KW, hipStream_t st) {
+  const long long total = (long long)Cout * KH * KW * Cpad;
+  pack_weights_kernel<<<grid_for(total, 256), 256, 0, st>>>(w, wf, wd, Cout, Cin, Cpad, KH, KW);
+}
+
+}  // namespace dm

@@ -45,3 +45,39 @@ void argmax_count(const void* logits, const long long* labels, int B, int C,
                   unsigned long long* correct, bool bf16, hipStream_t st);
 void spin_us(double us, hipStream_t st);
 }  // namespace dm
+
+namespace dm {
+// conv_igemm.hip
+struct ConvGeom;
+void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+               const ConvGeom& g, int cfg, hipStream_t st);
+int igemm_fwd_rowtile(int cfg);
+void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                 long long mchunk, int cfg, hipStream_t st);
+void wgrad_reduce(const float* slab, int S, int Cout, int C, int Cin, int KH, int KW, float* dw,
+                  float beta, hipStream_t st);
+void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int Cpad, int KH,
+                  int KW, hipStream_t st);
+// bn_pool.hip
+void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
+                       const float* beta, float* rmean, float* rvar, float momentum, float eps,
+                       float* scale, float* shift, float* mean, float* invstd, float* work,
+                       hipStream_t st);
+void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                    float eps, int C, float* scale, float* shift, hipStream_t st);
+void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
+              bf16_t* out, long long n, int C, bool relu, hipStream_t st);
+int bn_bwd_groups(long long M, int C);
+void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* mean,
+                 const float* invstd, const float* gamma, float* dgamma, float* dbeta,
+                 float gbeta, long long M, int C, bool relu, bf16_t* dy, bf16_t* dres,
+                 float* work, hipStream_t st);
+void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
+                 int OW, int K, int S, int P, hipStream_t st);
+void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,
+                 int OH, int OW, int K, int S, int P, hipStream_t st);
+void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t st);
+void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
+void pack_input(const void* x, bool bf16, bf16_t* y, int N, int C, int H, int W, int Cp,
+                long long sn, long long sc, long long sh, long long sw, hipStream_t st);
+}  // namespace dm

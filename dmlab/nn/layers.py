@@ -155,10 +155,10 @@ class ConvBN(Layer):
 
         return CB.convbn_fwd(self, x, ctx, train, residual)
 
-    def native_bwd(self, dy, ctx, need_dx):
+    def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None):
         from dmlab.ops import convbn as CB
 
-        return CB.convbn_bwd(self, dy, ctx, need_dx)
+        return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into)
 
 
 class BasicBlock(Layer):
@@ -184,15 +184,14 @@ class BasicBlock(Layer):
         return out
 
     def native_bwd(self, dy, ctx, need_dx):
-        # c2's backward returns (d_input_of_c2, d_residual); d_residual == ReLU/BN-masked dy
+        # c2's backward returns (d_input_of_c2, d_residual); d_residual = ReLU-masked dy
         dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True)
+        if self.down is None:
+            # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass)
+            return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None)
         dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
-        if self.down is not None:
-            dd = self.down.native_bwd(dres, ctx["cd"], need_dx)
-            if need_dx:
-                dx = dx + dd if dx is not None else dd
-        elif need_dx:
-            dx = dx + dres
+        # projection skip: its dgrad accumulates in place into dx
+        self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx)
         return dx
 
 

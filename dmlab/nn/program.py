@@ -163,6 +163,7 @@ class Program(nn.Module):
         self._grad_hooks: list[Callable] = []
         self._post_backward_hooks: list[Callable] = []
         self._anchor = torch.zeros(1, requires_grad=True)
+        self._wver = None
 
     # ---------------------------------------------------------------- construction
     def build(self, layers):
@@ -242,6 +243,7 @@ class Program(nn.Module):
     def forward(self, x):
         self._native_active = self._use_native(x)
         if self._native_active:
+            self._wver = self.flat.version()  # packed-weight caches key on this
             self.prepare_native(x)
         if self.training and torch.is_grad_enabled():
             return _ProgramFn.apply(x, self._anchor, self)

@@ -1,0 +1,161 @@
+"""Native path of :class:`dmlab.nn.layers.ConvBN` (NHWC bf16, ResNet family).
+
+Forward : implicit-GEMM MFMA conv whose epilogue also emits per-tile Σy/Σy² →
+          BN statistics finalize (+ running-stat update) → fused BN-apply
+          [+ residual] [+ ReLU].
+Backward: BN backward (reduce + apply, also emitting the residual-branch grad) →
+          weight-gradient implicit GEMM (split-M fp32 slabs, fixed-order reduce into
+          the OIHW fp32 grad slot) → data-gradient implicit GEMM (parity-class
+          decomposition for stride 2), optionally fused with the skip-connection
+          add.
+
+Activations are plain contiguous ``[N, H, W, C]`` bf16 tensors.  Packed bf16
+weights ([Cout][KH][KW][Cpad] for forward, [Cin][KH][KW][Cout] for dgrad) are
+cached per layer and refreshed when the fp32 master changes.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._native import lib
+
+
+def _cpad(c):
+    return max(8, (c + 7) // 8 * 8)
+
+
+def pick_cfg(M, ncols):
+    """Block tile for the forward-style kernel: 0=128x128, 1=128x64, 2=64x64."""
+    if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 480:
+        return 0
+    if math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
+        return 1
+    return 2
+
+
+def _wgrad_plan(M, cout, K):
+    cfg = 0 if cout % 128 == 0 else 1
+    bm = 128 if cfg == 0 else 64
+    tiles = math.ceil(cout / bm) * math.ceil(K / 128)
+    max_split = max(1, M // 512)  # >= 16 K-steps of 32 rows per split
+    S = max(1, min(max_split, math.ceil(1024 / tiles)))
+    return cfg, S
+
+
+def as_nhwc(x, cpad=None):
+    """Accept [N,H,W,C] bf16 (internal layout) or a user NCHW / channels_last tensor."""
+    if x.dim() == 4 and x.dtype == torch.bfloat16 and x.is_contiguous() and getattr(x, "_dm_nhwc", False):
+        return x
+    N, C, H, W = x.shape
+    cp = cpad or _cpad(C)
+    y = torch.empty((N, H, W, cp), device=x.device, dtype=torch.bfloat16)
+    lib().pack_input(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), y)
+    return _mark(y)
+
+
+def _mark(t):
+    t._dm_nhwc = True
+    return t
+
+
+def empty_nhwc(N, H, W, C, like):
+    return _mark(torch.empty((N, H, W, C), device=like.device, dtype=torch.bfloat16))
+
+
+def packed_weights(layer, need_wd=True):
+    prog = layer._prog
+    ver = prog._wver
+    cache = getattr(layer, "_wcache", None)
+    cp = _cpad(layer.cin)
+    if cache is None or cache[0] != ver or (need_wd and cache[2] is None):
+        w = layer.weight.detach()
+        k = layer.k
+        wf = torch.empty((layer.cout, k, k, cp), device=w.device, dtype=torch.bfloat16)
+        wd = (torch.empty((layer.cin, k, k, layer.cout), device=w.device, dtype=torch.bfloat16)
+              if need_wd else None)
+        lib().pack_weights(w, wf, wd, cp)
+        cache = (ver, wf, wd)
+        object.__setattr__(layer, "_wcache", cache)
+    return cache[1], cache[2]
+
+
+def convbn_fwd(layer, x, ctx, train, residual=None):
+    L = lib()
+    first = not (x.dim() == 4 and getattr(x, "_dm_nhwc", False))
+    x = as_nhwc(x, _cpad(layer.cin)) if first else x
+    N, H, W, C = x.shape
+    k, s, p = layer.k, layer.stride, layer.padding
+    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    M = N * OH * OW
+    cout = layer.cout
+    wf, _ = packed_weights(layer, need_wd=train and not first)
+    y = empty_nhwc(N, OH, OW, cout, x)
+    cfg = pick_cfg(M, cout)
+    f32 = dict(device=x.device, dtype=torch.float32)
+    scale = torch.empty(cout, **f32)
+    shift = torch.empty(cout, **f32)
+    use_batch = layer.training
+    if use_batch:
+        T = L.conv_stats_rows(M, cfg)
+        stats = torch.empty(T * 2 * cout, **f32)
+        L.conv_fwd(x, wf, y, stats, None, k, k, s, p, cfg)
+        mean = torch.empty(cout, **f32)
+        invstd = torch.empty(cout, **f32)
+        work = torch.empty(64 * 2 * cout, **f32)
+        L.bn_stats_finalize(stats, T, float(M), layer.bn_weight.detach(), layer.bn_bias.detach(),
+                            layer.running_mean, layer.running_var, layer.momentum, layer.eps,
+                            scale, shift, mean, invstd, work)
+        layer.num_batches_tracked.add_(1)
+    else:
+        L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg)
+        L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
+                         layer.running_var, layer.eps, scale, shift)
+        mean = invstd = None
+    out = empty_nhwc(N, OH, OW, cout, x)
+    L.bn_apply(y, residual, scale, shift, out, layer.relu)
+    if train:
+        ctx.update(x=x, y=y, out=out, mean=mean, invstd=invstd, has_res=residual is not None,
+                   first=first)
+    return out
+
+
+def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
+    """Returns dx (or (dx, dres) when the forward had a residual input).
+
+    ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient)
+    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)."""
+    L = lib()
+    x, y, out = ctx["x"], ctx["y"], ctx["out"]
+    N, OH, OW, cout = y.shape
+    M = N * OH * OW
+    k, s, p = layer.k, layer.stride, layer.padding
+    acc = 1.0 if layer.accumulate else 0.0
+    dout = dout.contiguous()
+    dy = empty_nhwc(N, OH, OW, cout, y)
+    dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
+    work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
+    L.bn_backward(dout, out, y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
+                  layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc, layer.relu, dy,
+                  dres, work)
+    # weight gradient
+    C = x.shape[3]
+    K = k * k * C
+    wcfg, S = _wgrad_plan(M, cout, K)
+    slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
+    L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg)
+    dx = None
+    if need_dx and not ctx["first"]:
+        _, wd = packed_weights(layer, need_wd=True)
+        N_, H, W, Cin = x.shape
+        cfg = pick_cfg(N_ * H * W, Cin)
+        if dx_into is not None:
+            L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
+            dx = dx_into
+        else:
+            dx = empty_nhwc(N_, H, W, Cin, x)
+            L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)
+    if ctx["has_res"]:
+        return dx, dres
+    return dx

@@ -1,0 +1,181 @@
+"""NHWC bf16 ResNet kernels (implicit-GEMM conv fwd/dgrad/wgrad, BN, pooling) vs
+PyTorch fp32 references computed on the same bf16-rounded inputs."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dmlab.ops._native import lib
+from dmlab.ops.convbn import _cpad, pick_cfg
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [  # (N, H, Cin, Cout, k, stride, pad)
+    (2, 8, 64, 64, 3, 1, 1),
+    (2, 9, 64, 128, 3, 2, 1),
+    (2, 8, 64, 128, 1, 2, 0),
+    (3, 7, 256, 512, 3, 1, 1),
+    (2, 14, 128, 256, 3, 2, 1),
+    (2, 16, 3, 64, 7, 2, 3),  # stem (channels padded to 8)
+]
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def _nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def _setup(dev, N, H, Cin, Cout, k, s, p, seed=0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.randn(N, Cin, H, H, device=dev, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k))
+    cp = _cpad(Cin)
+    xn = torch.empty(N, H, H, cp, device=dev, dtype=torch.bfloat16)
+    lib().pack_input(x, xn)
+    wf = torch.empty(Cout, k, k, cp, device=dev, dtype=torch.bfloat16)
+    wd = torch.empty(Cin, k, k, Cout, device=dev, dtype=torch.bfloat16)
+    lib().pack_weights(w.contiguous(), wf, wd, cp)
+    return x, w, xn, wf, wd
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+@pytest.mark.parametrize("cfg", [0, 1, 2])
+def test_conv_fwd_and_stats(dev, geom, cfg):
+    N, H, Cin, Cout, k, s, p = geom
+    if cfg == 0 and Cout % 128:
+        pytest.skip("128-wide tile needs Cout % 128 == 0")
+    x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
+    ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
+    OH = ref.shape[2]
+    y = torch.empty(N, OH, OH, Cout, device=dev, dtype=torch.bfloat16)
+    M = N * OH * OH
+    T = lib().conv_stats_rows(M, cfg)
+    stats = torch.empty(T * 2 * Cout, device=dev)
+    lib().conv_fwd(xn, wf, y, stats, None, k, k, s, p, cfg)
+    assert _rel(_nchw(y), ref) < 6e-3
+    st = stats.view(T, 2, Cout).sum(0)
+    torch.testing.assert_close(st[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
+    torch.testing.assert_close(st[1], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
+
+
+def test_conv_fwd_add(dev):
+    N, H, Cin, Cout, k, s, p = GEOMS[0]
+    x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
+    ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
+    add = torch.randn(N, H, H, Cout, device=dev).bfloat16()
+    y = torch.empty_like(add)
+    lib().conv_fwd(xn, wf, y, None, add, k, k, s, p, pick_cfg(N * H * H, Cout))
+    assert _rel(_nchw(y), ref + _nchw(add).float()) < 6e-3
+
+
+@pytest.mark.parametrize("geom", GEOMS[:5])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_dgrad(dev, geom, accumulate):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    wb = w.bfloat16().float()
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wb, dy.float(), s, p)
+    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    base = dx.clone()
+    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None,
+                     pick_cfg(N * H * H, Cin))
+    if accumulate:
+        ref = ref + _nchw(base).float()
+    assert _rel(_nchw(dx), ref) < 6e-3
+
+
+@pytest.mark.parametrize("geom", GEOMS)
+def test_conv_wgrad(dev, geom):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, p)
+    M = N * OH * OH
+    for beta in (0.0, 1.0):
+        dw = torch.randn_like(w) if beta else torch.empty_like(w)
+        base = dw.clone()
+        for S, cfg in ((1, 0 if Cout % 128 == 0 else 1), (3, 1)):
+            K = k * k * _cpad(Cin)
+            slab = torch.empty(S * Cout * K, device=dev)
+            d = dw.clone()
+            lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, beta, S, cfg)
+            exp = ref + (base if beta else 0)
+            assert _rel(d, exp) < 2e-3, (S, cfg, beta)
+    assert M > 0
+
+
+@pytest.mark.parametrize("C,M", [(64, 4096), (512, 98), (128, 1000)])
+@pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
+def test_bn_forward_backward(dev, C, M, relu, res):
+    torch.manual_seed(0)
+    y = (torch.randn(M, C, device=dev) * 2 + 0.5).bfloat16()
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev)
+    r = torch.randn(M, C, device=dev).bfloat16() if res else None
+    # reference
+    yr = y.float().requires_grad_(True)
+    g_ = gamma.clone().requires_grad_(True)
+    b_ = beta.clone().requires_grad_(True)
+    rm_ref, rv_ref = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    z = F.batch_norm(yr.t().unsqueeze(0), rm_ref, rv_ref, g_, b_, True, 0.1, 1e-5).squeeze(0).t()
+    if res:
+        z = z + r.float()
+    out_ref = F.relu(z) if relu else z
+    dout = torch.randn(M, C, device=dev).bfloat16()
+    out_ref.backward(dout.float())
+    # native: stats from a [T][2][C] slab (T=1)
+    stats = torch.stack([y.float().sum(0), (y.float() ** 2).sum(0)]).reshape(-1).contiguous()
+    f = dict(device=dev, dtype=torch.float32)
+    scale, shift, mean, invstd = (torch.empty(C, **f) for _ in range(4))
+    rm, rv = torch.zeros(C, **f), torch.ones(C, **f)
+    lib().bn_stats_finalize(stats, 1, float(M), gamma, beta, rm, rv, 0.1, 1e-5, scale, shift, mean,
+                            invstd, torch.empty(128 * C, **f))
+    torch.testing.assert_close(rm, rm_ref, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-3)
+    y4, out = y.view(1, 1, M, C), torch.empty(1, 1, M, C, device=dev, dtype=torch.bfloat16)
+    lib().bn_apply(y4, r.view(1, 1, M, C) if res else None, scale, shift, out, relu)
+    assert _rel(out.view(M, C), out_ref.detach()) < 5e-3
+    dy = torch.empty_like(out)
+    dres = torch.empty_like(out) if res else None
+    dg, db = torch.zeros(C, **f), torch.zeros(C, **f)
+    work = torch.empty(lib().bn_bwd_work(M, C), **f)
+    lib().bn_backward(dout.view(1, 1, M, C), out, y4, mean, invstd, gamma, dg, db, 0.0, relu, dy,
+                      dres, work)
+    assert _rel(dy.view(M, C), yr.grad) < 1e-2
+    assert _rel(dg, g_.grad) < 1e-2
+    assert _rel(db, b_.grad) < 1e-2
+
+
+def test_maxpool_avgpool(dev):
+    x = torch.randn(2, 64, 17, 17, device=dev).bfloat16()
+    xn = _nhwc(x)
+    y = torch.empty(2, 9, 9, 64, device=dev, dtype=torch.bfloat16)
+    idx = torch.empty(2, 9, 9, 64, device=dev, dtype=torch.uint8)
+    lib().maxpool_fwd(xn, y, idx, 3, 2, 1)
+    xr = x.float().requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    torch.testing.assert_close(_nchw(y).float(), yr, rtol=0, atol=0)
+    dy = torch.randn_like(yr).bfloat16()
+    yr.backward(dy.float())
+    dx = torch.empty_like(xn)
+    lib().maxpool_bwd(_nhwc(dy), idx, dx, 3, 2, 1)
+    assert _rel(_nchw(dx), xr.grad) < 5e-3
+    a = torch.empty(2, 64, device=dev, dtype=torch.bfloat16)
+    lib().avgpool_fwd(xn, a)
+    assert _rel(a, x.float().mean((2, 3))) < 5e-3
+    g = torch.randn(2, 64, device=dev).bfloat16()
+    dxa = torch.empty_like(xn)
+    lib().avgpool_bwd(g, dxa)
+    ref = (g.float() / (17 * 17))[:, None, None, :].expand(2, 17, 17, 64)
+    assert _rel(dxa, ref) < 5e-3

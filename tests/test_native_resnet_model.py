@@ -1,0 +1,71 @@
+"""End-to-end native ResNet-18 (bf16 NHWC HIP kernels) vs the same Program on the
+PyTorch fp32 reference path."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dmlab.models import ResNet18
+from dmlab.nn import cross_entropy
+from dmlab.ops._native import lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+def test_resnet18_native_matches_reference(dev):
+    """bf16 vs fp32 differences compound through 20 BN layers of a random-init net
+    (early-layer grads differ by ~40% for ANY bf16 implementation), so the native
+    path is held to the error level of PyTorch's own bf16 autocast on the same
+    model and data: native error <= 1.5 x autocast error + 0.05, per parameter."""
+    lib()
+    torch.manual_seed(0)
+    a = ResNet18(num_classes=10).to(dev)
+    b = copy.deepcopy(a).set_backend("torch")
+    b._flatten()
+    c = copy.deepcopy(b)
+    c._flatten()
+    x = torch.rand(16, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (16,), device=dev)
+    la = cross_entropy(a(x), y)
+    lb = F.cross_entropy(b(x), y)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        oc = c(x)
+    lc = F.cross_entropy(oc.float(), y)
+    for l in (la, lb, lc):
+        l.backward()
+    assert abs(la.item() - lb.item()) < 5e-2 * max(1.0, abs(lb.item()))
+    bad = []
+    for (n, pa), (_, pb), (_, pc) in zip(a.named_parameters(), b.named_parameters(),
+                                         c.named_parameters()):
+        rn, rc = _rel(pa.grad, pb.grad), _rel(pc.grad, pb.grad)
+        if rn > 1.5 * rc + 0.05:
+            bad.append((n, rn, rc))
+    assert not bad, bad
+    # running statistics were updated like torch's
+    torch.testing.assert_close(a.stem.running_mean, b.stem.running_mean, rtol=2e-2, atol=2e-3)
+
+
+def test_resnet18_eval_mode(dev):
+    """Eval mode uses running statistics; error held to the torch-autocast level."""
+    torch.manual_seed(1)
+    a = ResNet18(num_classes=10).to(dev)
+    b = copy.deepcopy(a).set_backend("torch")
+    b._flatten()
+    x = torch.rand(8, 3, 32, 32, device=dev)
+    for m in (a, b):
+        m.train()
+        for _ in range(3):
+            m(x)  # populate running stats
+        m.eval()
+    torch.testing.assert_close(a.layer2_0.c1.running_var, b.layer2_0.c1.running_var,
+                               rtol=5e-2, atol=1e-2)
+    with torch.no_grad():
+        ref = b(x)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            auto = b(x)
+        assert _rel(a(x), ref) < 1.5 * _rel(auto, ref) + 0.02
