@@ -214,7 +214,7 @@ void bn_apply(at::Tensor y, c10::optional<at::Tensor> res, at::Tensor scale, at:
   dm::bn_apply(bp(y), rp, fp(scale), fp(shift), bp(out), y.numel(), C, relu, cur_stream());
 }
 
-int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C; }
+int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C + 32 * 2 * C; }
 
 void bn_backward(at::Tensor dout, at::Tensor out, at::Tensor y, at::Tensor mean, at::Tensor invstd,
                  at::Tensor gamma, at::Tensor dgamma, at::Tensor dbeta, double gbeta, bool relu,

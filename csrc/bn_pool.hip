@@ -392,9 +392,9 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
                        float* scale, float* shift, float* mean, float* invstd, float* work,
                        hipStream_t st) {
   const int W = 2 * C;
-  const int G = min(64, max(1, T / 16));
+  const int G = min(32, max(1, T / 16));
   slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
-  bn_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(work, G, C, count, gamma, beta, rmean, rvar,
+  bn_finalize_kernel<<<(C + 63) / 64, 64, 0, st>>>(work, G, C, count, gamma, beta, rmean, rvar,
                                                       momentum, eps, scale, shift, mean, invstd);
 }
 
@@ -418,6 +418,7 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
   }
 }
 
+int bn_bwd_groups(long long M, int C);
 int bn_bwd_groups(long long M, int C) {
   const int RL = 256 / (C / 8);
   long long g = (M + RL * 64 - 1) / (RL * 64);  // >= 64 rows per row lane
@@ -434,11 +435,19 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   const int G = bn_bwd_groups(M, C);
   float* part = work;
   float* coef = work + (long long)G * 2 * C;
+  float* part2 = coef + 3 * C;  // [<=32][2C] second-level partials
   const size_t shr = sizeof(float) * 256 * 16;
   if (relu) bn_bwd_reduce_kernel<true><<<G, 256, shr, st>>>(dout, out, y, mean, invstd, M, C, part);
   else bn_bwd_reduce_kernel<false><<<G, 256, shr, st>>>(dout, out, y, mean, invstd, M, C, part);
-  bn_bwd_finalize_kernel<<<(C + 255) / 256, 256, 0, st>>>(part, G, C, (double)M, gamma, mean,
-                                                          invstd, dgamma, dbeta, gbeta, coef);
+  int Gf = G;
+  const float* fin = part;
+  if (G > 32) {  // parallel fixed-order pre-reduction so the finalize loop stays short
+    Gf = 32;
+    slab_colsum_kernel<<<dim3((2 * C + 63) / 64, Gf), 256, 0, st>>>(part, G, 2 * C, part2);
+    fin = part2;
+  }
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, 64, 0, st>>>(fin, Gf, C, (double)M, gamma, mean,
+                                                       invstd, dgamma, dbeta, gbeta, coef);
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 3 * C;

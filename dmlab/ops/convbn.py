@@ -39,8 +39,10 @@ def _wgrad_plan(M, cout, K):
     cfg = 0 if cout % 128 == 0 else 1
     bm = 128 if cfg == 0 else 64
     tiles = math.ceil(cout / bm) * math.ceil(K / 128)
-    max_split = max(1, M // 512)  # >= 16 K-steps of 32 rows per split
-    S = max(1, min(max_split, math.ceil(1024 / tiles)))
+    max_split = max(1, M // 2048)  # >= 64 K-steps of 32 rows per split
+    # ~2 blocks per CU: enough to fill 256 CUs while keeping the fp32 slab traffic
+    # of the fixed-order reduce small (S * Cout * K * 4 bytes)
+    S = max(1, min(max_split, math.ceil(512 / tiles)))
     return cfg, S
 
 

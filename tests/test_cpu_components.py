@@ -1,0 +1,240 @@
+"""CPU tests: samplers, TB event writer, optimisers, Program engine parity."""
+import math
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dmlab.data import (DeviceLoader, MySampler, PartitionSampler, RandomSampleSampler,
+                        SyntheticMNIST, load_mnist)
+from dmlab.models import ForwardNN, Net, ResNet18, SubNetConv, SubNetFC
+from dmlab.models.reference import TorchLeNet, TorchMLP
+from dmlab.optim import SGD, AdamOptimizer, GdOptimizer
+from dmlab.utils import getSummaryWriter, read_events
+
+# ---------------------------------------------------------------- samplers
+
+
+@pytest.mark.parametrize("n,ws", [(100, 3), (60000, 8), (7, 4)])
+def test_partition_sampler_disjoint_cover(n, ws):
+    ds = list(range(n))
+    shards = [PartitionSampler(ds, ws, r, seed=3).indices() for r in range(ws)]
+    assert all(len(s) == math.ceil(n / ws) for s in shards)
+    allidx = torch.cat(shards)
+    assert set(allidx.tolist()) == set(range(n))        # covers the dataset
+    if n % ws == 0:
+        assert len(set(allidx.tolist())) == n           # disjoint when no padding
+
+
+def test_partition_sampler_epochs_and_determinism():
+    ds = list(range(1000))
+    a = PartitionSampler(ds, 4, 1, seed=0)
+    b = PartitionSampler(ds, 4, 1, seed=0)
+    assert torch.equal(a.indices(), b.indices())
+    e0 = a.indices()
+    a.set_epoch(1)
+    assert not torch.equal(e0, a.indices())              # reshuffled per epoch (B3)
+
+
+def test_random_sample_sampler():
+    ds = list(range(1000))
+    s0 = RandomSampleSampler(ds, 4, 0, seed=0)
+    s1 = RandomSampleSampler(ds, 4, 1, seed=0)
+    i0, i1 = s0.indices(), s1.indices()
+    assert len(i0) == 250 and len(set(i0.tolist())) == 250  # no duplicates within a rank
+    assert not torch.equal(i0, i1)                           # ranks draw independently
+    s0.set_epoch(2)
+    assert not torch.equal(i0, s0.indices())
+    boot = RandomSampleSampler(ds, 4, 0, seed=0, replacement=True).indices()
+    assert boot.max() < 1000 and len(boot) == 250
+
+
+def test_mysampler_reference_api():
+    ds = list(range(10))
+    s = MySampler(ds, 2, 1, shuffle=True, seed=1)
+    assert len(s) == 5 and len(list(iter(s))) == 5          # reference skeleton raised here (B2)
+    s.set_epoch(3)
+    assert MySampler(ds, 2, 0, mode="division").mode == "partition"
+    with pytest.raises(ValueError):
+        MySampler(ds, 2, 0, mode="bogus")
+
+
+def test_device_loader_batches():
+    ds = SyntheticMNIST(train=False, n=100)
+    ld = DeviceLoader(ds, 32, sampler=PartitionSampler(ds, 2, 0))
+    sizes = [x.shape[0] for x, _ in ld]
+    assert sizes == [32, 18] and len(ld) == 2
+
+
+def test_synthetic_mnist_shape_and_range():
+    ds = load_mnist("/nonexistent", train=True, n=256)
+    assert ds.images.shape == (256, 1, 28, 28)
+    assert ds.images.min() >= 0 and ds.images.max() <= 1
+    assert ds.labels.min() >= 0 and ds.labels.max() <= 9
+
+
+# ---------------------------------------------------------------- TB writer
+
+
+def test_summary_writer_roundtrip(tmp_path):
+    w = getSummaryWriter(3, del_dir=False, root=str(tmp_path) + "/")
+    for i in range(5):
+        w.add_scalar("Train Loss", 2.0 - 0.1 * i, i * 20)
+    w.close()
+    files = list(tmp_path.rglob("events.out.tfevents.*"))
+    assert len(files) == 1
+    assert files[0].parent.name.endswith("-epoch3")          # ./logs/<date>/<time>-epoch<N>/
+    ev = read_events(files[0])
+    assert ev[0]["file_version"] == "brain.Event:2"
+    sc = [e for e in ev if "tag" in e]
+    assert [e["step"] for e in sc] == [0, 20, 40, 60, 80]
+    assert sc[-1]["tag"] == "Train Loss" and abs(sc[-1]["value"] - 1.6) < 1e-6
+    # del_dir wipes the log root
+    w2 = getSummaryWriter(1, del_dir=True, root=str(tmp_path) + "/")
+    w2.close()
+    assert len(list(tmp_path.rglob("events.out.tfevents.*"))) == 1
+
+
+def test_crc32c_known_vector():
+    from dmlab.utils.summary import crc32c
+
+    assert crc32c(b"123456789") == 0xE3069283  # standard CRC-32C check value
+
+
+# ---------------------------------------------------------------- optimisers
+
+
+def _lenet_pair():
+    torch.manual_seed(0)
+    a = Net()
+    b = TorchLeNet()
+    b.load_state_dict(a.state_dict())
+    return a, b
+
+
+def _loss(m, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(16, 1, 28, 28, generator=g)
+    y = torch.randint(0, 10, (16,), generator=g)
+    return F.cross_entropy(m(x), y)
+
+
+def test_adam_reference_formula_flat_and_per_tensor():
+    a, b = _lenet_pair()
+    oa = AdamOptimizer(a.parameters(), lr=0.01)   # flat path (Program)
+    ob = AdamOptimizer(b.parameters(), lr=0.01)   # per-tensor path (plain module)
+    assert oa.flat is not None and ob.flat is None
+    for s in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            _loss(m, s).backward()
+            o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+
+
+def test_sgd_matches_torch_optim():
+    a, b = _lenet_pair()
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    ob = torch.optim.SGD(b.parameters(), lr=0.05, momentum=0.9, weight_decay=1e-4, nesterov=True)
+    for s in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad()
+            _loss(m, s).backward()
+            o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+
+
+def test_gd_is_plain_gradient_step():
+    a, b = _lenet_pair()
+    before = [p.detach().clone() for p in a.parameters()]
+    o = GdOptimizer(a.parameters(), lr=0.1)
+    o.zero_grad()
+    _loss(a).backward()
+    grads = [p.grad.clone() for p in a.parameters()]
+    o.step()
+    for p, p0, g in zip(a.parameters(), before, grads):
+        torch.testing.assert_close(p, p0 - 0.1 * g)
+
+
+def test_torch_optimizer_on_program_with_set_to_none():
+    """torch.optim + zero_grad(set_to_none=True) re-attaches flat grad views."""
+    a, b = _lenet_pair()
+    oa = torch.optim.SGD(a.parameters(), lr=0.05, momentum=0.9)
+    ob = torch.optim.SGD(b.parameters(), lr=0.05, momentum=0.9)
+    for s in range(3):
+        for m, o in ((a, oa), (b, ob)):
+            o.zero_grad(set_to_none=True)
+            _loss(m, s).backward()
+            o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6)
+    assert a.flat.attached()
+
+
+# ---------------------------------------------------------------- program engine
+
+
+def test_mlp_param_count_and_parity():
+    torch.manual_seed(0)
+    a = ForwardNN()
+    b = TorchMLP()
+    b.load_state_dict(_mlp_sd(a))
+    assert sum(p.numel() for p in a.parameters()) == 576_810
+    x = torch.rand(8, 1, 28, 28)
+    torch.testing.assert_close(a(x), b(x))
+
+
+def _mlp_sd(a):
+    sd = {}
+    for k, v in a.state_dict().items():
+        i = int(k[2:k.index(".")]) - 1
+        sd[f"layers.{i}.{k.split('.')[1]}"] = v
+    return sd
+
+
+def test_reference_compat_softmax():
+    m = ForwardNN(reference_compat=True)
+    out = m(torch.rand(4, 1, 28, 28))
+    torch.testing.assert_close(out.sum(1), torch.ones(4))
+
+
+def test_pipeline_halves_compose_to_lenet():
+    torch.manual_seed(0)
+    full = Net()
+    a, b = SubNetConv(), SubNetFC()
+    a.load_state_dict({k: v for k, v in full.state_dict().items() if k.startswith("conv")})
+    b.load_state_dict({k: v for k, v in full.state_dict().items() if k.startswith("fc")})
+    x = torch.rand(5, 1, 28, 28)
+    torch.testing.assert_close(b(a(x)), full(x))
+    xr = x.clone().requires_grad_(True)
+    b(a(xr)).sum().backward()                                # grad flows across programs
+    assert xr.grad is not None and a.conv1.weight.grad.abs().sum() > 0
+
+
+def test_resnet18_cpu_forward_backward():
+    torch.manual_seed(0)
+    m = ResNet18(num_classes=10)
+    assert sum(p.numel() for p in m.parameters()) == 11_181_642
+    out = m(torch.rand(2, 3, 32, 32))
+    assert out.shape == (2, 10)
+    F.cross_entropy(out, torch.tensor([1, 2])).backward()
+    assert all(p.grad is not None for p in m.parameters())
+    assert int(m.stem.num_batches_tracked) == 1
+
+
+def test_program_grad_hooks_fire_in_reverse_order():
+    m = Net()
+    seen = []
+    m.register_grad_hook(lambda prog, i: seen.append(i))
+    _loss(m).backward()
+    assert seen == list(range(len(m.layers) - 1, -1, -1))
+
+
+def test_program_to_refits_flat_buffer():
+    m = Net().to(torch.device("cpu"))
+    assert m.flat.attached()
+    for p in m.parameters():
+        assert p._dm_flat is m.flat

@@ -1,0 +1,179 @@
+"""Multi-process (gloo, CPU) tests of the lab-2/3 communication layer and DDP."""
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from dist_helpers import run_dist
+
+pytestmark = pytest.mark.slow
+
+
+def _make(seed):
+    from dmlab.models import Net
+
+    torch.manual_seed(seed)
+    return Net()
+
+
+def _aggregation_equivalence(rank, ws, out):
+    from dmlab.parallel import comm
+
+    torch.manual_seed(100 + rank)
+    m1 = _make(rank)  # different weights per rank ...
+    comm.init_parameters(m1)  # ... until broadcast
+    m2 = _make(0)
+    comm.init_parameters(m2)
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+    x = torch.rand(8, 1, 28, 28)
+    y = torch.randint(0, 10, (8,))
+    for m in (m1, m2):
+        F.cross_entropy(m(x), y).backward()
+    local = [p.grad.clone() for p in m1.parameters()]
+    comm.allreduce_average_gradients(m1)
+    comm.allgather_average_gradients(m2)
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+    # the mean really is the mean of the per-rank gradients
+    gathered = [torch.zeros_like(local[0]) for _ in range(ws)]
+    dist.all_gather(gathered, local[0])
+    torch.testing.assert_close(m1.conv1.weight.grad, torch.stack(gathered).mean(0),
+                               rtol=1e-5, atol=1e-7)
+    # per-parameter (reference call pattern) gives the same answer
+    m3 = _make(0)
+    F.cross_entropy(m3(x), y).backward()
+    comm.allreduce_average_gradients(m3, granularity="per_param")
+    for a, b in zip(m1.parameters(), m3.parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_allreduce_equals_allgather(ws):
+    run_dist(_aggregation_equivalence, ws, None)
+
+
+def _reference_bug(rank, ws, out):
+    from dmlab.parallel import comm
+
+    m = _make(0)
+    x = torch.rand(4, 1, 28, 28) + rank
+    F.cross_entropy(m(x), torch.zeros(4, dtype=torch.long)).backward()
+    mine = m.fc2.bias.grad.clone()
+    last = mine.clone()
+    dist.broadcast(last, ws - 1)
+    comm.allgather_average_gradients_reference_compat(m)
+    # every rank ends up with the LAST rank's gradient, not the mean
+    torch.testing.assert_close(m.fc2.bias.grad, last)
+
+
+def test_reference_allgather_bug_reproduced():
+    run_dist(_reference_bug, 2, None)
+
+
+def _ddp_equivalence(rank, ws, path):
+    """DDP on ws ranks with batch b each == one process on the concatenated batch."""
+    from dmlab.models import Net
+    from dmlab.optim import SGD
+    from dmlab.parallel import DDP
+
+    torch.manual_seed(0)
+    model = Net()
+    ref = Net()
+    ref.load_state_dict(model.state_dict())
+    g = torch.Generator().manual_seed(7)
+    X = torch.rand(ws * 6, 1, 28, 28, generator=g)
+    Y = torch.randint(0, 10, (ws * 6,), generator=g)
+    ddp = DDP(model, bucket_cap_mb=0.05, first_bucket_mb=0.01)  # several buckets
+    assert len(ddp.buckets) >= 2
+    opt = SGD(model.parameters(), lr=0.1, momentum=0.9)
+    ddp.fold_average_into(opt)
+    opt_ref = SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    for step in range(3):
+        xs, ys = X[rank * 6:(rank + 1) * 6], Y[rank * 6:(rank + 1) * 6]
+        loss = F.cross_entropy(ddp(xs), ys)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        lr = F.cross_entropy(ref(X), Y)
+        opt_ref.zero_grad()
+        lr.backward()
+        opt_ref.step()
+    for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5, msg=n)
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_ddp_matches_single_process_big_batch(ws):
+    run_dist(_ddp_equivalence, ws, None)
+
+
+def _ddp_generic_module(rank, ws, path):
+    """The hook-based reducer on a plain nn.Module (no Program)."""
+    from dmlab.models.reference import TorchLeNet
+    from dmlab.parallel import DDP
+
+    torch.manual_seed(0)
+    model = TorchLeNet()
+    ref = TorchLeNet()
+    ref.load_state_dict(model.state_dict())
+    ddp = DDP(model, bucket_cap_mb=0.05, first_bucket_mb=0.01)
+    g = torch.Generator().manual_seed(3)
+    X = torch.rand(ws * 4, 1, 28, 28, generator=g)
+    Y = torch.randint(0, 10, (ws * 4,), generator=g)
+    F.cross_entropy(ddp(X[rank * 4:(rank + 1) * 4]), Y[rank * 4:(rank + 1) * 4]).backward()
+    F.cross_entropy(ref(X), Y).backward()
+    for (n, a), (_, b) in zip(model.named_parameters(), ref.named_parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-6, msg=n)
+
+
+def test_ddp_generic_module():
+    run_dist(_ddp_generic_module, 2, None)
+
+
+def _no_sync(rank, ws, path):
+    from dmlab.models import Net
+    from dmlab.parallel import DDP
+
+    torch.manual_seed(0)
+    model = Net()
+    ref = Net()
+    ref.load_state_dict(model.state_dict())
+    ddp = DDP(model)
+    xs = [torch.rand(4, 1, 28, 28) + rank for _ in range(2)]
+    y = torch.zeros(4, dtype=torch.long)
+    with ddp.no_sync():
+        F.cross_entropy(ddp(xs[0]), y).backward()
+    F.cross_entropy(ddp(xs[1]), y).backward()  # accumulates, then reduces
+    for x in xs:
+        for r in range(ws):
+            F.cross_entropy(ref(x - rank + r), y).backward()
+    for a, b in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(a.grad, b.grad / ws, rtol=1e-4, atol=1e-6)
+
+
+def test_ddp_no_sync_accumulation():
+    run_dist(_no_sync, 2, None)
+
+
+def _straggler(rank, ws, path):
+    from dmlab.parallel import GradAggregator, Straggler
+
+    m = _make(0)
+    F.cross_entropy(m(torch.rand(2, 1, 28, 28)), torch.zeros(2, dtype=torch.long)).backward()
+    agg = GradAggregator(m)
+    s = Straggler(rank=1, delay_ms=150)
+    for _ in range(3):
+        agg()
+        s()
+    if rank == 0:
+        # rank 0 waits for the straggler inside the next collective
+        assert agg.comm_time > 0.2, agg.comm_time
+    else:
+        assert s.injected_ms == 450
+
+
+def test_straggler_slows_the_other_rank():
+    run_dist(_straggler, 2, None)

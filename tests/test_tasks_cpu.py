@@ -1,0 +1,64 @@
+"""Integration: the task entrypoints run on the CPU with tiny settings and print the
+reference console formats."""
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+from dist_helpers import free_port
+
+ROOT = Path(__file__).resolve().parent.parent
+pytestmark = pytest.mark.slow
+
+
+def _run(args, tmp_path, timeout=300, env_extra=None):
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2")
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable] + args, cwd=tmp_path, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def _losses(out):
+    return [float(x) for x in re.findall(r"loss: (\d+\.\d+)", out)]
+
+
+def test_task1_cpu_adam(tmp_path):
+    out = _run(["-m", "dmlab.tasks.task1", "--device", "cpu", "--synthetic", "--train-samples",
+                "12000", "--logdir", str(tmp_path / "logs") + "/"], tmp_path)
+    assert re.search(r"epoch: 1, iters:    20, loss: \d\.\d{3}", out)
+    assert "Finished epoch:   1 /   1" in out and "Training Finished!" in out
+    assert re.search(r"Test set: Accuracy: \d+/10000 \(\d+\.\d{2}%\)", out)
+    ls = _losses(out)
+    assert ls[-1] < ls[0]
+    assert list((tmp_path / "logs").rglob("events.out.tfevents.*"))
+
+
+def test_task1_cpu_mlp_sgd(tmp_path):
+    out = _run(["-m", "dmlab.tasks.task1", "--device", "cpu", "--synthetic", "--model", "mlp",
+                "--optimizer", "sgd", "--epochs", "1", "--train-samples", "3200", "--no-tb"],
+               tmp_path)
+    ls = _losses(out)
+    assert ls[-1] < ls[0]
+
+
+def test_task2_spawn_allgather_straggler(tmp_path):
+    out = _run(["-m", "dmlab.tasks.task2", "--n_devices", "2", "--spawn", "--device", "cpu",
+                "--synthetic", "--train-samples", "2560", "--epochs", "1", "--master_port",
+                str(free_port()), "--aggregation", "allgather", "--straggler-rank", "1",
+                "--straggler-delay-ms", "2"], tmp_path)
+    assert "Device 0 starts training ..." in out and "Device 1 starts training ..." in out
+    assert re.search(r"Device: 1 epoch: 1, iters:    20, loss: \d\.\d{3}", out)
+    assert "Total communication time:" in out and "Training time:" in out
+
+
+def test_task3_torchrun_random_sampler(tmp_path):
+    out = _run(["-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                "127.0.0.1", "--master-port", str(free_port()), "-m", "dmlab.tasks.task3",
+                "--device", "cpu", "--synthetic", "--train-samples", "2560", "--epochs", "1",
+                "--sampler", "random", "--lr", "0.01"], tmp_path)
+    assert "Device: 0 epoch: 1" in out and "Test set: Accuracy" in out
