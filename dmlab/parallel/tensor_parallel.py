@@ -1,0 +1,124 @@
+"""Intra-layer ("horizontal") model parallelism — the optional lab-4 split.
+
+Reference: requirement only — "将模型横向划分" (sections/checking.tex:14) and
+"（可选）实现横向划分" (sections/task4.tex:21); no code exists.
+
+Megatron-style pair for an MLP head:
+* :class:`ColumnParallelLinear` — W split by output features; forward needs no
+  communication (each rank produces its slice of the features, ReLU is local);
+  backward all-reduces the input gradient.
+* :class:`RowParallelLinear` — W split by input features; forward all-reduces
+  the partial products (then adds the replicated bias); backward needs none.
+One all-reduce per direction for the whole fc1→ReLU→fc2 head, on RCCL/xGMI
+(gloo on CPU).  :class:`TPLeNet` replicates the conv trunk and splits the head.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from dmlab.nn.layers import Conv2d, Flatten, Linear
+from dmlab.nn.program import Program
+
+from . import env
+
+
+def _tp():
+    return env.get_world_size(), env.get_rank()
+
+
+def _all_reduce(t, group=None):
+    if env.get_world_size() > 1:
+        dist.all_reduce(t, group=group)
+    return t
+
+
+class ColumnParallelLinear(Linear):
+    def __init__(self, fin, fout, bias=True, relu=False, group=None):
+        ws, _ = _tp()
+        assert fout % ws == 0, "output features must divide the TP degree"
+        super().__init__(fin, fout // ws, bias=bias, relu=relu)
+        self.full_out = fout
+        self.group = group
+
+    def load_from_full(self, w, b=None):
+        ws, r = _tp()
+        n = self.fout
+        with torch.no_grad():
+            self.weight.copy_(w[r * n:(r + 1) * n])
+            if b is not None and self.bias is not None:
+                self.bias.copy_(b[r * n:(r + 1) * n])
+
+    def bwd(self, dy, ctx, need_dx):
+        dx = super().bwd(dy, ctx, need_dx)
+        if need_dx and dx is not None:
+            dx = _all_reduce(dx.contiguous(), self.group)
+        return dx
+
+
+class RowParallelLinear(Linear):
+    """Input features are sharded; the bias is replicated and added after the sum."""
+
+    def __init__(self, fin, fout, bias=True, relu=False, group=None):
+        ws, _ = _tp()
+        assert fin % ws == 0, "input features must divide the TP degree"
+        super().__init__(fin // ws, fout, bias=False, relu=False)
+        self.full_in = fin
+        self.post_relu = relu
+        self.group = group
+        self.rbias = nn.Parameter(torch.zeros(fout)) if bias else None
+
+    def load_from_full(self, w, b=None):
+        ws, r = _tp()
+        n = self.fin
+        with torch.no_grad():
+            self.weight.copy_(w[:, r * n:(r + 1) * n])
+            if b is not None and self.rbias is not None:
+                self.rbias.copy_(b)
+
+    def fwd(self, x, ctx, train):
+        y = super().fwd(x, ctx, train)
+        y = _all_reduce(y.float().contiguous(), self.group)
+        if self.rbias is not None:
+            y = y + self.rbias.detach()
+        if self.post_relu:
+            y = torch.relu(y)
+        if train:
+            ctx["tp_y"] = y
+        return y.to(x.dtype) if x.dtype != torch.float32 else y
+
+    def bwd(self, dy, ctx, need_dx):
+        if self.post_relu:
+            dy = dy * (ctx["tp_y"] > 0)
+        if self.rbias is not None:
+            self._prog._write_grad_by_param(self.rbias, dy.float().sum(0))
+        dy = dy.to(ctx["y"].dtype if "y" in ctx else dy.dtype)
+        return super().bwd(dy, ctx, need_dx)
+
+    def t_bwd(self, dy, ctx, need_dx):  # reference path: local linear without the bias
+        return Linear.t_bwd(self, dy, ctx, need_dx)
+
+
+class TPLeNet(Program):
+    """LeNet with the fc head split across the tensor-parallel group."""
+
+    def __init__(self, in_channels=1, num_classes=10, group=None):
+        super().__init__()
+        self.conv1 = Conv2d(in_channels, 6, 5, 1, 2, bias=True, relu=True, pool=2)
+        self.conv2 = Conv2d(6, 16, 5, 1, 0, bias=True, relu=True, pool=2)
+        self.flatten = Flatten()
+        self.fc1 = ColumnParallelLinear(400, 120, relu=True, group=group)
+        self.fc2 = RowParallelLinear(120, num_classes, group=group)
+        self.build([self.conv1, self.conv2, self.flatten, self.fc1, self.fc2])
+
+    @torch.no_grad()
+    def load_from_full(self, net):
+        """Copy a full (single-device) ``Net``'s weights, sharding the head."""
+        self.conv1.weight.copy_(net.conv1.weight)
+        self.conv1.bias.copy_(net.conv1.bias)
+        self.conv2.weight.copy_(net.conv2.weight)
+        self.conv2.bias.copy_(net.conv2.bias)
+        self.fc1.load_from_full(net.fc1.weight, net.fc1.bias)
+        self.fc2.load_from_full(net.fc2.weight, net.fc2.bias)
+        return self

@@ -1,0 +1,109 @@
+"""Lab-4 model parallelism on CPU/gloo: P2P pipeline (GPipe, 1F1B), tensor-parallel
+head, and the reference RPC/RRef programming model."""
+import os
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dist_helpers import free_port, run_dist
+
+ROOT = Path(__file__).resolve().parent.parent
+pytestmark = pytest.mark.slow
+
+
+def _full_reference(steps, X, Y, lr, momentum=0.0):
+    from dmlab.models import Net
+    from dmlab.optim import SGD
+
+    torch.manual_seed(0)
+    net = Net()
+    opt = SGD(net.parameters(), lr=lr, momentum=momentum)
+    for _ in range(steps):
+        opt.zero_grad()
+        F.cross_entropy(net(X), Y).backward()
+        opt.step()
+    return net
+
+
+def _pipeline(rank, ws, schedule):
+    from dmlab.models import Net, SubNetConv, SubNetFC
+    from dmlab.nn import CrossEntropyLoss
+    from dmlab.optim import SGD
+    from dmlab.parallel.pipeline import PipelineStage
+
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand(16, 1, 28, 28, generator=g)
+    Y = torch.randint(0, 10, (16,), generator=g)
+    torch.manual_seed(0)
+    full0 = Net()
+    mod = SubNetConv() if rank == 0 else SubNetFC()
+    sd = {k: v for k, v in full0.state_dict().items() if k.startswith("conv" if rank == 0 else "fc")}
+    mod.load_state_dict(sd)
+    stage = PipelineStage(mod, SGD(mod.parameters(), lr=0.1), CrossEntropyLoss(),
+                          schedule=schedule, device=torch.device("cpu"))
+    losses = []
+    for _ in range(2):
+        loss = stage.train_step(X if rank == 0 else None, Y if rank == 0 else None, n_micro=4)
+        if loss is not None:
+            losses.append(float(loss))
+    ref = _full_reference(2, X, Y, 0.1)
+    for n, p in mod.named_parameters():
+        torch.testing.assert_close(p, ref.get_parameter(n), rtol=1e-4, atol=1e-6, msg=n)
+    if rank == 1:
+        assert len(losses) == 2
+
+
+@pytest.mark.parametrize("schedule", ["gpipe", "1f1b"])
+def test_pipeline_matches_single_process(schedule):
+    run_dist(_pipeline, 2, schedule)
+
+
+def _tp(rank, ws, _):
+    from dmlab.models import Net
+    from dmlab.optim import SGD
+    from dmlab.parallel.tensor_parallel import TPLeNet
+
+    g = torch.Generator().manual_seed(9)
+    X = torch.rand(8, 1, 28, 28, generator=g)
+    Y = torch.randint(0, 10, (8,), generator=g)
+    torch.manual_seed(0)
+    full = Net()
+    tp = TPLeNet().load_from_full(full)
+    ref = Net()
+    ref.load_state_dict(full.state_dict())
+    torch.testing.assert_close(tp(X), ref(X), rtol=1e-5, atol=1e-6)
+    o1, o2 = SGD(tp.parameters(), lr=0.1, momentum=0.9), SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    for _ in range(2):
+        for m, o in ((tp, o1), (ref, o2)):
+            o.zero_grad()
+            F.cross_entropy(m(X), Y).backward()
+            o.step()
+    n = 120 // ws
+    torch.testing.assert_close(tp.fc1.weight, ref.fc1.weight[rank * n:(rank + 1) * n], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(tp.fc2.weight, ref.fc2.weight[:, rank * n:(rank + 1) * n], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(tp.fc2.rbias, ref.fc2.bias, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(tp.conv1.weight, ref.conv1.weight, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_tensor_parallel_head_matches_full_model(ws):
+    run_dist(_tp, ws, None)
+
+
+def test_rpc_reference_model_trains(tmp_path):
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+                        "dmlab.tasks.task4", "--mode", "rpc", "--synthetic", "--train-samples",
+                        "3200", "--epochs", "1", "--lr", "0.05"], cwd=tmp_path, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Training on the worker1..." in r.stdout and "Training on the worker2..." in r.stdout
+    ls = [float(x) for x in re.findall(r"loss: (\d+\.\d+)", r.stdout)]
+    assert len(ls) == 5 and ls[-1] < ls[0]
+    assert "Test set: Accuracy" in r.stdout
