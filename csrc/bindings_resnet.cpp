@@ -50,6 +50,7 @@ dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride,
   g.M = (long long)g.N * OH * OW;
   g.K = KH * KW * g.C;
   TORCH_CHECK(KH * KW <= dm::MAXTAPS, "too many taps");
+  dm::geom_finalize(g);
   return g;
 }
 
@@ -113,6 +114,7 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     g.nth = KH; g.ntw = KW; g.dy0 = pad; g.dys = -1; g.dx0 = pad; g.dxs = -1;
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
+    dm::geom_finalize(g);
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
     return;
   }
@@ -139,6 +141,7 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       g.dy0 = (a + pad - kh0) / 2; g.dys = -1; g.dx0 = (b + pad - kw0) / 2; g.dxs = -1;
       g.kh0 = kh0; g.khs = 2; g.kw0 = kw0; g.kws = 2;
       g.M = (long long)N * g.Hg * g.Wg; g.K = nth * ntw * Cout;
+      dm::geom_finalize(g);
       dm::igemm_fwd(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr, g, cfg, st);
     }
 }
@@ -154,8 +157,8 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   auto g = fwd_geom(x, Cout, KH, KW, stride, pad, dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(0) == x.size(0));
   need_f32(slab, "slab", (int64_t)S * Cout * g.K);
-  const long long steps = (g.M + 31) / 32;
-  const long long mchunk = ((steps + S - 1) / S) * 32;
+  const long long steps = (g.M + 63) / 64;
+  const long long mchunk = ((steps + S - 1) / S) * 64;  // multiple of both kernels' row step
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
   dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);

@@ -20,6 +20,19 @@ struct ConvGeom {
   int wK;                    // packed weight row length (elements) = KH*KW*C
   long long M;               // N*Hg*Wg
   int K;                     // ntaps*C
+  // magic-number division by Wg and Hg (m < 2^31): q = (umulhi(n, mul) + n) >> shr
+  unsigned wg_mul, wg_shr, hg_mul, hg_shr;
 };
+
+inline void fastdiv_init(unsigned d, unsigned& mul, unsigned& shr) {
+  unsigned l = 0;
+  while ((1u << l) < d) ++l;
+  mul = (unsigned)((((unsigned long long)1 << 32) * ((1ull << l) - d)) / d + 1);
+  shr = l;
+}
+inline void geom_finalize(ConvGeom& g) {
+  fastdiv_init((unsigned)g.Wg, g.wg_mul, g.wg_shr);
+  fastdiv_init((unsigned)g.Hg, g.hg_mul, g.hg_shr);
+}
 
 }  // namespace dm

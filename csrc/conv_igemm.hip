@@ -32,136 +32,26 @@
 
 namespace dm {
 
+template <typename K>
+static void set_smem_attr(K kernel, size_t bytes) {
+  // dynamic LDS above 64 KiB must be opted into per kernel (idempotent, cheap)
+  if (bytes > 65536)
+    DM_CHECK(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)bytes));
+}
+
+
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-// ------------------------------------------------------------------ forward / dgrad
+// ------------------------------------------------------------------ shared epilogue
 template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
-    const bf16_t* ADD /* may alias Y (in-place accumulate) */, float* __restrict__ stats,
-    ConvGeom g) {
-  constexpr int BK = 64;
-  constexpr int TM = BM / WM, TN = BN / WN;     // wave tile
-  constexpr int RM = TM / 16, RN = TN / 16;     // MFMA blocks per wave
-  constexpr int AR = BM / 32, BR = BN / 32;     // rows per thread to stage (8 chunks per row)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                 // [2][BM][BK]
-  bf16_t* Bs = As + 2 * BM * BK;                                 // [2][BN][BK]
-  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);        // [MAXTAPS] {dy, dx, wcol, 0}
-
+__device__ __forceinline__ void igemm_epilogue(
+    f32x4 (&acc)[BM / WM / 16][BN / WN / 16], unsigned char* smem, bf16_t* Y, const bf16_t* ADD,
+    float* __restrict__ stats, const ConvGeom& g, long long m0, int n0) {
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int RM = TM / 16, RN = TN / 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int ntaps = g.nth * g.ntw;
-  if (tid < ntaps) {
-    const int th = tid / g.ntw, tw = tid % g.ntw;
-    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs,
-                          ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C, 0);
-  }
-  // rows this thread stages: r = tid/8 + 32*i, chunk = tid%8
-  const int chunk = tid & 7;
-  int a_iy[AR], a_ix[AR];
-  long long a_nb[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const long long m = m0 + (tid >> 3) + 32 * i;
-    if (m < g.M) {
-      const int x = (int)(m % g.Wg);
-      const long long t = m / g.Wg;
-      const int y = (int)(t % g.Hg);
-      const int n = (int)(t / g.Hg);
-      a_iy[i] = y * g.isy;
-      a_ix[i] = x * g.isx;
-      a_nb[i] = (long long)n * g.H * g.W;
-    } else {
-      a_iy[i] = -(1 << 28);  // never in range
-      a_ix[i] = 0;
-      a_nb[i] = 0;
-    }
-  }
-  __syncthreads();
-
-  uint4 ra[AR], rb[BR];
-  const int nk = (g.K + BK - 1) / BK;
-
-  auto load = [&](int kt) {
-    const int kc = kt * (BK / 8) + chunk;           // global 8-element chunk index
-    const int tap = kc >> g.lgC8;
-    const int c0 = (kc & ((1 << g.lgC8) - 1)) * 8;
-    const bool kval = tap < ntaps;
-    int4 tp = make_int4(0, 0, 0, 0);
-    if (kval) tp = taps[tap];
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kval && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-        v = *reinterpret_cast<const uint4*>(X + ((a_nb[i] + (long long)iy * g.W + ix) * g.C + c0));
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kval && n < g.Ncols)
-        v = *reinterpret_cast<const uint4*>(Wp + (long long)n * g.wK + tp.z + c0);
-      rb[i] = v;
-    }
-  };
-  auto store = [&](int buf) {
-    bf16_t* as = As + buf * BM * BK;
-    bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[i];
-    }
-  };
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load(kt + 1);
-    const bf16_t* as = As + buf * BM * BK;
-    const bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[RM], bfr[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int r = wm * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int r = wn * TN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) store(buf ^ 1);
-    __syncthreads();
-  }
-
   // ---------------- epilogue 1: BN batch statistics (Σ, Σ²) per output channel
   float* red = reinterpret_cast<float*>(smem);  // reuse LDS (main loop finished)
   if (stats) {
@@ -244,6 +134,306 @@ __global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
     *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
                                                   pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
   }
+}
+
+// ------------------------------------------------------------------ forward / dgrad
+template <int BM, int BN, int WM, int WN, bool BUF>
+__global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
+    const bf16_t* ADD /* may alias Y (in-place accumulate) */, float* __restrict__ stats,
+    ConvGeom g, unsigned xbytes, unsigned wbytes) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;     // wave tile
+  constexpr int RM = TM / 16, RN = TN / 16;     // MFMA blocks per wave
+  constexpr int AR = BM / 32, BR = BN / 32;     // rows per thread to stage (8 chunks per row)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                 // [2][BM][BK]
+  bf16_t* Bs = As + 2 * BM * BK;                                 // [2][BN][BK]
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);        // [MAXTAPS] {dy, dx, wcol, 0}
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ntaps = g.nth * g.ntw;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs,
+                          ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C, 0);
+  }
+  // rows this thread stages: r = tid/8 + 32*i, chunk = tid%8
+  const int chunk = tid & 7;
+  int a_iy[AR], a_ix[AR];
+  long long a_nb[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const long long m = m0 + (tid >> 3) + 32 * i;
+    if (m < g.M) {
+      const int x = (int)(m % g.Wg);
+      const long long t = m / g.Wg;
+      const int y = (int)(t % g.Hg);
+      const int n = (int)(t / g.Hg);
+      a_iy[i] = y * g.isy;
+      a_ix[i] = x * g.isx;
+      a_nb[i] = (long long)n * g.H * g.W;
+    } else {
+      a_iy[i] = -(1 << 28);  // never in range
+      a_ix[i] = 0;
+      a_nb[i] = 0;
+    }
+  }
+  __syncthreads();
+
+  uint4 ra[AR], rb[BR];
+  const int nk = (g.K + BK - 1) / BK;
+
+  // BUF: branch-free buffer loads (32-bit offsets; out-of-range chunks read as zero
+  // through the descriptor's range check) instead of predicated 64-bit global loads
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
+  unsigned b_off[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : 0x80000000u;
+  }
+  auto load = [&](int kt) {
+    const int kc = kt * (BK / 8) + chunk;           // global 8-element chunk index
+    const int tap = kc >> g.lgC8;
+    const int c0 = (kc & ((1 << g.lgC8) - 1)) * 8;
+    const bool kval = tap < ntaps;
+    int4 tp = make_int4(0, 0, 0, 0);
+    if (kval) tp = taps[tap];
+    if constexpr (BUF) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
+        const bool ok = kval && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+        const unsigned off =
+            ok ? (((unsigned)a_nb[i] + (unsigned)(iy * g.W + ix)) * (unsigned)g.C + (unsigned)c0) * 2u
+               : 0x80000000u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+        ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+#pragma unroll
+      for (int i = 0; i < BR; ++i) {
+        const unsigned off = (kval && b_off[i] != 0x80000000u)
+                                 ? b_off[i] + (unsigned)(tp.z + c0) * 2u : 0x80000000u;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0);
+        rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kval && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+        v = *reinterpret_cast<const uint4*>(X + ((a_nb[i] + (long long)iy * g.W + ix) * g.C + c0));
+      ra[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + (tid >> 3) + 32 * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (kval && n < g.Ncols)
+        v = *reinterpret_cast<const uint4*>(Wp + (long long)n * g.wK + tp.z + c0);
+      rb[i] = v;
+    }
+  };
+  auto store = [&](int buf) {
+    bf16_t* as = As + buf * BM * BK;
+    bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[i];
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);
+    const bf16_t* as = As + buf * BM * BK;
+    const bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int r = wm * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int r = wn * TN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  igemm_epilogue<BM, BN, WM, WN>(acc, smem, Y, ADD, stats, g, m0, n0);
+}
+
+// ------------------------------------------------------------------ forward / dgrad, LDS-DMA
+// Same GEMM as igemm_fwd_kernel, but both operand tiles are staged with
+// buffer_load_dwordx4 ... lds (LDS-DMA: global -> LDS with no VGPR round trip).
+// Zero padding of the implicit im2col comes for free from the buffer range check:
+// an out-of-image (or K-tail) chunk gets a voffset beyond num_records and the
+// hardware returns zeros.  The LDS image is lane-linear per wave instruction
+// (8 rows x 128 B), so the chunk swizzle is applied to the SOURCE address.
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) igemm_fwd_dma_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
+    const bf16_t* ADD, float* __restrict__ stats, ConvGeom g, unsigned xbytes,
+    unsigned wbytes) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int RM = TM / 16, RN = TN / 16;
+  constexpr int AR = BM / 32, BR = BN / 32;     // wave-instructions per wave per tile
+  constexpr unsigned OOB = 0x80000000u;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                 // [2][BM][BK]
+  bf16_t* Bs = As + 2 * BM * BK;                                 // [2][BN][BK]
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ntaps = g.nth * g.ntw;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs,
+                          ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C, 0);
+  }
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
+  const int pc = lane & 7;                       // physical 16-B chunk this lane fills
+  int a_iy[AR], a_ix[AR], a_lc[AR];
+  unsigned a_nb[AR];                             // (n*H*W) pixel base
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int r = (i * 4 + wid) * 8 + (lane >> 3);
+    a_lc[i] = pc ^ ((r >> 1) & 7);
+    const long long m = m0 + r;
+    if (m < g.M) {
+      const int x = (int)(m % g.Wg);
+      const long long t = m / g.Wg;
+      const int y = (int)(t % g.Hg);
+      const int n = (int)(t / g.Hg);
+      a_iy[i] = y * g.isy;
+      a_ix[i] = x * g.isx;
+      a_nb[i] = (unsigned)n * (unsigned)(g.H * g.W);
+    } else {
+      a_iy[i] = -(1 << 28);
+      a_ix[i] = 0;
+      a_nb[i] = 0;
+    }
+  }
+  int b_lc[BR];
+  unsigned b_row[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int r = (i * 4 + wid) * 8 + (lane >> 3);
+    b_lc[i] = pc ^ ((r >> 1) & 7);
+    const int n = n0 + r;
+    b_row[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
+  }
+  __syncthreads();
+  const int nk = (g.K + BK - 1) / BK;
+  const int cmask = (1 << g.lgC8) - 1;
+
+  auto issue = [&](int kt, int buf) {
+    bf16_t* as = As + buf * BM * BK;
+    bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int kc = kt * 8 + a_lc[i];
+      const int tap = kc >> g.lgC8;
+      unsigned off = OOB;
+      if (tap < ntaps) {
+        const int4 tp = taps[tap];
+        const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          off = ((a_nb[i] + (unsigned)(iy * g.W + ix)) * (unsigned)g.C + (unsigned)((kc & cmask) * 8)) * 2u;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsx, (__attribute__((address_space(3))) void*)(as + (i * 4 + wid) * 8 * BK), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int kc = kt * 8 + b_lc[i];
+      const int tap = kc >> g.lgC8;
+      unsigned off = OOB;
+      if (tap < ntaps && b_row[i] != OOB)
+        off = b_row[i] + (unsigned)(taps[tap].z + (kc & cmask) * 8) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsw, (__attribute__((address_space(3))) void*)(bs + (i * 4 + wid) * 8 * BK), 16, off, 0, 0, 0);
+    }
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+    const bf16_t* as = As + buf * BM * BK;
+    const bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      const int ch = ks * 4 + (lane >> 4);
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int r = wm * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int r = wn * TN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  igemm_epilogue<BM, BN, WM, WN>(acc, smem, Y, ADD, stats, g, m0, n0);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -397,6 +587,153 @@ __global__ void __launch_bounds__(256, 2) igemm_wgrad_kernel(
       }
 }
 
+__device__ __forceinline__ unsigned fdiv(unsigned n, unsigned mul, unsigned shr) {
+  return (__umulhi(n, mul) + n) >> shr;
+}
+
+// Weight gradient, v2: 64 m-rows per barrier (two MFMA k-steps), branch-free buffer
+// loads with range-check zero fill, magic-number row decomposition.
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(256, 2) igemm_wgrad2_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
+    ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes) {
+  constexpr int BKM = 64;
+  constexpr int PAD = 16;
+  constexpr int LA = BM + PAD, LB = BN + PAD;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int RM = TM / 16, RN = TN / 16;
+  constexpr int ACH = BM / 8, BCH = BN / 8;
+  constexpr int AIT = BKM * ACH / 256, BIT = BKM * BCH / 256;
+  constexpr unsigned OOB = 0x80000000u;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);           // [2][BKM][LA]
+  bf16_t* Bs = As + 2 * BKM * LA;                         // [2][BKM][LB]
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BKM * LB);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int co0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
+  const unsigned mb = (unsigned)((long long)blockIdx.z * mchunk);
+  const unsigned me = (unsigned)min(g.M, (long long)mb + mchunk);
+  const int ntaps = g.nth * g.ntw;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs, 0, 0);
+  }
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsd = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, (int)dybytes, 0x00020000);
+  // per-thread fixed column chunks (the row varies with the step)
+  const int acol = tid % ACH, arow0 = tid / ACH;          // A: rows arow0 + it*(256/ACH)
+  const int bcol = tid % BCH, brow0 = tid / BCH;
+  const bool a_colok = co0 + acol * 8 < g.Ncols;
+  const int kc = (k0 >> 3) + bcol;
+  const int btap = kc >> g.lgC8;
+  const unsigned bc0 = (unsigned)((kc & ((1 << g.lgC8) - 1)) * 8);
+  __syncthreads();
+  const bool b_ok = btap < ntaps;
+  int4 btp = make_int4(0, 0, 0, 0);
+  if (b_ok) btp = taps[btap];
+
+  uint4 ra[AIT], rb[BIT];
+  auto load = [&](unsigned mt) {
+#pragma unroll
+    for (int it = 0; it < AIT; ++it) {
+      const unsigned m = mt + arow0 + it * (256 / ACH);
+      const unsigned off = (m < me && a_colok) ? (m * (unsigned)g.Ncols + co0 + acol * 8) * 2u : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsd, off, 0, 0);
+      ra[it] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int it = 0; it < BIT; ++it) {
+      const unsigned m = mt + brow0 + it * (256 / BCH);
+      unsigned off = OOB;
+      if (m < me && b_ok) {
+        const unsigned t = fdiv(m, g.wg_mul, g.wg_shr);
+        const int x = (int)(m - t * (unsigned)g.Wg);
+        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+        const int y = (int)(t - n * (unsigned)g.Hg);
+        const int iy = y * g.isy + btp.x, ix = x * g.isx + btp.y;
+        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          off = (((n * (unsigned)g.H + (unsigned)iy) * (unsigned)g.W + (unsigned)ix) * (unsigned)g.C + bc0) * 2u;
+      }
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      rb[it] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store = [&](int buf) {
+    bf16_t* as = As + buf * BKM * LA;
+    bf16_t* bs = Bs + buf * BKM * LB;
+#pragma unroll
+    for (int it = 0; it < AIT; ++it)
+      *reinterpret_cast<uint4*>(as + (arow0 + it * (256 / ACH)) * LA + acol * 8) = ra[it];
+#pragma unroll
+    for (int it = 0; it < BIT; ++it)
+      *reinterpret_cast<uint4*>(bs + (brow0 + it * (256 / BCH)) * LB + bcol * 8) = rb[it];
+  };
+
+  f32x4 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int nsteps = me > mb ? (int)((me - mb + BKM - 1) / BKM) : 0;
+  if (nsteps > 0) {
+    load(mb);
+    store(0);
+  }
+  __syncthreads();
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) load(mb + (unsigned)(st + 1) * BKM);
+    const bf16_t* as = As + buf * BKM * LA;
+    const bf16_t* bs = Bs + buf * BKM * LB;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int r0 = ks * 32 + grp * 4 + q;
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i) {
+        const int col = wm * TM + i * 16 + 4 * p;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(as + r0 * LA + col));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(as + (r0 + 16) * LA + col));
+        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int col = wn * TN + j * 16 + 4 * p;
+        const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(bs + r0 * LB + col));
+        const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s4*)(bs + (r0 + 16) * LB + col));
+        bfr[j] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (st + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = slab + (long long)blockIdx.z * g.Ncols * g.K;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wn * TN + j * 16 + (lane & 15);
+        if (co < g.Ncols && k < g.K) out[(long long)co * g.K + k] = acc[i][j][r];
+      }
+}
+
 // dw[co][ci][kh][kw] = beta*dw + Σ_s slab[s][co][(kh*KW+kw)*C + ci]   (ci < Cin)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            int S, int Cout, int C, int Cin,
@@ -449,42 +786,43 @@ static size_t fwd_smem(int BM, int BN) {
   return main > epi ? main : epi;
 }
 
-template <typename K>
-static void set_smem_attr(K kernel, size_t bytes) {
-  // dynamic LDS above 64 KiB must be opted into per kernel
-  static bool done = false;
-  if (!done) {
-    DM_CHECK(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)bytes));
-    done = true;
+
+template <int BM, int BN, int WM, int WN>
+static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                       float* stats, const ConvGeom& g, bool dma, bool buf, hipStream_t st) {
+  const size_t sm = fwd_smem(BM, BN);
+  dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
+  if (dma) {
+    auto k = igemm_fwd_dma_kernel<BM, BN, WM, WN>;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+  } else if (buf) {
+    auto k = igemm_fwd_kernel<BM, BN, WM, WN, true>;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+  } else {
+    auto k = igemm_fwd_kernel<BM, BN, WM, WN, false>;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
   }
 }
 
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st) {
-  // cfg 0: 128x128 (2x2 waves, 64x64 per wave), 1: 128x64 (2x2), 2: 64x64 (2x2)
-  if (cfg == 0) {
-    auto k = igemm_fwd_kernel<128, 128, 2, 2>;
-    const size_t sm = fwd_smem(128, 128);
-    set_smem_attr(k, sm);
-    dim3 grid((unsigned)((g.M + 127) / 128), (g.Ncols + 127) / 128);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g);
-  } else if (cfg == 1) {
-    auto k = igemm_fwd_kernel<128, 64, 2, 2>;
-    const size_t sm = fwd_smem(128, 64);
-    set_smem_attr(k, sm);
-    dim3 grid((unsigned)((g.M + 127) / 128), (g.Ncols + 63) / 64);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g);
-  } else {
-    auto k = igemm_fwd_kernel<64, 64, 2, 2>;
-    const size_t sm = fwd_smem(64, 64);
-    set_smem_attr(k, sm);
-    dim3 grid((unsigned)((g.M + 63) / 64), (g.Ncols + 63) / 64);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g);
+  // cfg % 3: 0 = 128x128 (2x2 waves, 64x64 per wave), 1 = 128x64, 2 = 64x64
+  // cfg / 3: 0 = register-staged global loads, 1 = LDS-DMA (buffer_load ... lds),
+  //          2 = register-staged buffer loads (branch-free zero fill)
+  const bool dma = cfg / 3 == 1, buf = cfg / 3 == 2;
+  switch (cfg % 3) {
+    case 0: launch_fwd<128, 128, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, st); break;
+    case 1: launch_fwd<128, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, st); break;
+    default: launch_fwd<64, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, st); break;
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return cfg == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;
@@ -492,12 +830,26 @@ static size_t wgrad_smem(int BM, int BN) {
 
 void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                  long long mchunk, int cfg, hipStream_t st) {
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned db = (unsigned)(g.M * g.Ncols * 2);
   if (cfg == 0) {
     dim3 grid((g.Ncols + 127) / 128, (g.K + 127) / 128, S);
     igemm_wgrad_kernel<128, 128, 2, 2><<<grid, 256, wgrad_smem(128, 128), st>>>(X, DY, slab, g, mchunk);
-  } else {
+  } else if (cfg == 1) {
     dim3 grid((g.Ncols + 63) / 64, (g.K + 127) / 128, S);
     igemm_wgrad_kernel<64, 128, 2, 2><<<grid, 256, wgrad_smem(64, 128), st>>>(X, DY, slab, g, mchunk);
+  } else if (cfg == 2) {
+    dim3 grid((g.Ncols + 127) / 128, (g.K + 127) / 128, S);
+    auto k = igemm_wgrad2_kernel<128, 128, 2, 2>;
+    const size_t sm = 2 * 64 * ((128 + 16) + (128 + 16)) * 2 + MAXTAPS * 16;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db);
+  } else {
+    dim3 grid((g.Ncols + 63) / 64, (g.K + 127) / 128, S);
+    auto k = igemm_wgrad2_kernel<64, 128, 2, 2>;
+    const size_t sm = 2 * 64 * ((64 + 16) + (128 + 16)) * 2 + MAXTAPS * 16;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db);
   }
 }
 

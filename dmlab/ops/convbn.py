@@ -26,18 +26,29 @@ def _cpad(c):
     return max(8, (c + 7) // 8 * 8)
 
 
+# forward-style kernel configs (csrc/conv_igemm.hip igemm_fwd): tile = cfg % 3
+# (0: 128x128, 1: 128x64, 2: 64x64); loader = cfg // 3 (0: predicated global loads,
+# 1: LDS-DMA, 2: branch-free buffer loads).  Measured on MI355X (tools/bench_conv.py,
+# profiles/conv_kernels_r1.jsonl) the buffer-load loader is fastest on every shape.
+LOADER = 2
+
+
 def pick_cfg(M, ncols):
-    """Block tile for the forward-style kernel: 0=128x128, 1=128x64, 2=64x64."""
+    """Block tile for the forward-style kernel (see LOADER)."""
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 480:
-        return 0
-    if math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
-        return 1
-    return 2
+        t = 0
+    elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
+        t = 1
+    else:
+        t = 2
+    return t + 3 * LOADER
 
 
 def _wgrad_plan(M, cout, K):
-    cfg = 0 if cout % 128 == 0 else 1
-    bm = 128 if cfg == 0 else 64
+    # cfg 2/3: v2 weight-gradient kernel (64 rows per barrier, buffer loads), tile
+    # 128x128 / 64x128; cfg 0/1 are the v1 kernels kept for A/B measurements.
+    cfg = 2 if cout % 128 == 0 else 3
+    bm = 128 if cfg == 2 else 64
     tiles = math.ceil(cout / bm) * math.ceil(K / 128)
     max_split = max(1, M // 2048)  # >= 64 K-steps of 32 rows per split
     # ~2 blocks per CU: enough to fill 256 CUs while keeping the fp32 slab traffic

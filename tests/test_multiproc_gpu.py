@@ -1,0 +1,97 @@
+"""Two ranks sharing the box's single GPU (gloo group; device tensors staged
+through the host where gloo needs it): the DDP reducer and the P2P pipeline
+driving the NATIVE HIP kernels, checked against a single-process run."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dist_helpers import free_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _entry(rank, ws, port, kind, q):
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(ws), LOCAL_RANK="0")
+    import torch.distributed as dist
+
+    from dmlab.models import Net, SubNetConv, SubNetFC
+    from dmlab.nn import cross_entropy, CrossEntropyLoss
+    from dmlab.optim import SGD
+
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        g = torch.Generator().manual_seed(5)
+        X = torch.rand(16, 1, 28, 28, generator=g).to(dev)
+        Y = torch.randint(0, 10, (16,), generator=g).to(dev)
+        torch.manual_seed(0)
+        ref = Net().to(dev)
+        ropt = SGD(ref.parameters(), lr=0.1, momentum=0.9)
+        if kind == "ddp":
+            from dmlab.parallel import DDP
+
+            torch.manual_seed(0)
+            model = Net().to(dev)
+            ddp = DDP(model)
+            opt = SGD(model.parameters(), lr=0.1, momentum=0.9)
+            ddp.fold_average_into(opt)
+            for _ in range(2):
+                opt.zero_grad()
+                cross_entropy(ddp(X[rank * 8:(rank + 1) * 8]), Y[rank * 8:(rank + 1) * 8]).backward()
+                opt.step()
+                ropt.zero_grad()
+                cross_entropy(ref(X), Y).backward()
+                ropt.step()
+            err = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
+        else:
+            from dmlab.parallel.pipeline import PipelineStage
+
+            mod = (SubNetConv() if rank == 0 else SubNetFC()).to(dev)
+            sd = {k: v for k, v in ref.state_dict().items()
+                  if k.startswith("conv" if rank == 0 else "fc")}
+            mod.load_state_dict(sd)
+            st = PipelineStage(mod, SGD(mod.parameters(), lr=0.1, momentum=0.9), CrossEntropyLoss(),
+                               device=dev)
+            for _ in range(2):
+                st.train_step(X if rank == 0 else None, Y if rank == 0 else None, n_micro=4)
+                ropt.zero_grad()
+                cross_entropy(ref(X), Y).backward()
+                ropt.step()
+            err = max((p - ref.get_parameter(n)).abs().max().item()
+                      for n, p in mod.named_parameters())
+        q.put((rank, err, None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("kind", ["ddp", "pipeline"])
+def test_two_ranks_one_gpu(kind):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = free_port()
+    ps = [ctx.Process(target=_entry, args=(r, 2, port, kind, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    res = [q.get() for _ in range(2) if not q.empty()]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert len(res) == 2, res
+    for rank, err, tb in res:
+        assert tb is None, tb
+        assert err < 2e-4, (rank, err)

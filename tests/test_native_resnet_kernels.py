@@ -47,10 +47,10 @@ def _setup(dev, N, H, Cin, Cout, k, s, p, seed=0):
 
 
 @pytest.mark.parametrize("geom", GEOMS)
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", list(range(9)))
 def test_conv_fwd_and_stats(dev, geom, cfg):
     N, H, Cin, Cout, k, s, p = geom
-    if cfg == 0 and Cout % 128:
+    if cfg % 3 == 0 and Cout % 128:
         pytest.skip("128-wide tile needs Cout % 128 == 0")
     x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
     ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
@@ -78,7 +78,8 @@ def test_conv_fwd_add(dev):
 
 @pytest.mark.parametrize("geom", GEOMS[:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-def test_conv_dgrad(dev, geom, accumulate):
+@pytest.mark.parametrize("variant", [0, 2])
+def test_conv_dgrad(dev, geom, accumulate, variant):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
     wb = w.bfloat16().float()
@@ -88,7 +89,7 @@ def test_conv_dgrad(dev, geom, accumulate):
     dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
     base = dx.clone()
     lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None,
-                     pick_cfg(N * H * H, Cin))
+                     pick_cfg(N * H * H, Cin) % 3 + 3 * variant)
     if accumulate:
         ref = ref + _nchw(base).float()
     assert _rel(_nchw(dx), ref) < 6e-3
@@ -105,7 +106,8 @@ def test_conv_wgrad(dev, geom):
     for beta in (0.0, 1.0):
         dw = torch.randn_like(w) if beta else torch.empty_like(w)
         base = dw.clone()
-        for S, cfg in ((1, 0 if Cout % 128 == 0 else 1), (3, 1)):
+        big = 0 if Cout % 128 == 0 else 1
+        for S, cfg in ((1, big), (3, 1), (1, big + 2), (3, 3)):
             K = k * k * _cpad(Cin)
             slab = torch.empty(S * Cout * K, device=dev)
             d = dw.clone()

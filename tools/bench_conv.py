@@ -1,0 +1,116 @@
+"""Micro-benchmark of the implicit-GEMM conv kernels on every ResNet-18 layer shape.
+
+Interleaves variants in one process (methodology: cdna guide §5.4 rule 24) and
+prints TFLOP/s per (shape, pass, variant); checks that variants agree numerically.
+
+    python tools/bench_conv.py [--batch 256] [--iters 20]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+import torch  # noqa: E402
+
+from dmlab.ops._native import lib  # noqa: E402
+
+# (name, H_in, Cin, Cout, k, stride, pad)
+SHAPES = [
+    ("stem7x7", 224, 8, 64, 7, 2, 3),
+    ("l1_3x3", 56, 64, 64, 3, 1, 1),
+    ("l2_3x3s2", 56, 64, 128, 3, 2, 1),
+    ("l2_3x3", 28, 128, 128, 3, 1, 1),
+    ("l2_down", 56, 64, 128, 1, 2, 0),
+    ("l3_3x3s2", 28, 128, 256, 3, 2, 1),
+    ("l3_3x3", 14, 256, 256, 3, 1, 1),
+    ("l4_3x3s2", 14, 256, 512, 3, 2, 1),
+    ("l4_3x3", 7, 512, 512, 3, 1, 1),
+]
+
+
+def timeit(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cfgs", default="0,1,2,6,7,8")
+    ap.add_argument("--wcfgs", default="v1,v2")
+    ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    a = ap.parse_args()
+    L = lib()
+    dev = torch.device("cuda")
+    N = a.batch
+    cfgs = [int(c) for c in a.cfgs.split(",")]
+    out = []
+    for name, H, C, Co, k, s, p in SHAPES:
+        OH = (H + 2 * p - k) // s + 1
+        flops = 2.0 * N * OH * OH * Co * k * k * C
+        x = torch.randn(N, H, H, C, device=dev).bfloat16()
+        wf = (torch.randn(Co, k, k, C, device=dev) * 0.05).bfloat16()
+        wd = (torch.randn(C, k, k, Co, device=dev) * 0.05).bfloat16()
+        y = torch.empty(N, OH, OH, Co, device=dev, dtype=torch.bfloat16)
+        dy = torch.randn(N, OH, OH, Co, device=dev).bfloat16()
+        dx = torch.empty(N, H, H, C, device=dev, dtype=torch.bfloat16)
+        row = {"shape": name, "gflop": round(flops / 1e9, 1)}
+        if "fwd" in a.passes:
+            ref = None
+            for cfg in cfgs:
+                if cfg % 3 == 0 and Co % 128:
+                    continue
+                M = N * OH * OH
+                T = L.conv_stats_rows(M, cfg)
+                st = torch.empty(T * 2 * Co, device=dev)
+                t = timeit(lambda: L.conv_fwd(x, wf, y, st, None, k, k, s, p, cfg), a.iters)
+                row[f"fwd_c{cfg}_TF"] = round(flops / t / 1e12, 1)
+                if ref is None:
+                    ref = y.clone()
+                else:
+                    row[f"fwd_c{cfg}_maxdiff"] = float((y.float() - ref.float()).abs().max())
+        if "dgrad" in a.passes and name != "stem7x7":
+            ref = None
+            for cfg in cfgs:
+                if cfg % 3 == 0 and C % 128:
+                    continue
+                t = timeit(lambda: L.conv_dgrad(dy, wd, dx, k, k, s, p, None, cfg), a.iters)
+                row[f"dgrad_c{cfg}_TF"] = round(flops / t / 1e12, 1)
+                if ref is None:
+                    ref = dx.clone()
+                else:
+                    row[f"dgrad_c{cfg}_maxdiff"] = float((dx.float() - ref.float()).abs().max())
+        if "wgrad" in a.passes:
+            from dmlab.ops.convbn import _wgrad_plan
+
+            M = N * OH * OH
+            K = k * k * C
+            wcfg, S = _wgrad_plan(M, Co, K)
+            wcfg = (wcfg - 2) % 2
+            slab = torch.empty(S * Co * K, device=dev)
+            dw = torch.empty(Co, C, k, k, device=dev)
+            ref = None
+            for v in a.wcfgs.split(","):
+                c = wcfg + (2 if v == "v2" else 0)
+                t = timeit(lambda: L.conv_wgrad(x, dy, dw, slab, C, k, k, s, p, 0.0, S, c), a.iters)
+                row[f"wgrad_{v}_TF"] = round(flops / t / 1e12, 1)
+                if ref is None:
+                    ref = dw.clone()
+                else:
+                    row[f"wgrad_{v}_reldiff"] = float((dw - ref).norm() / ref.norm())
+            row["wgrad_S"] = S
+        out.append(row)
+        print(json.dumps(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
