@@ -61,7 +61,9 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
   need_bf16_nhwc(x, "x");
   need_bf16_nhwc(y, "y");
   const int Cout = y.size(3), OH = y.size(1), OW = y.size(2);
-  TORCH_CHECK(OH == (x.size(1) + 2 * pad - KH) / stride + 1 && OW == (x.size(2) + 2 * pad - KW) / stride + 1,
+  // pad is the top/left padding; the output size (taken from y) may imply a smaller
+  // bottom/right padding (space-to-depth stem), never a larger one
+  TORCH_CHECK(OH <= (x.size(1) + 2 * pad - KH) / stride + 1 && OW <= (x.size(2) + 2 * pad - KW) / stride + 1,
               "output spatial size mismatch");
   TORCH_CHECK(wpack.scalar_type() == at::kBFloat16 && wpack.numel() == (int64_t)Cout * KH * KW * x.size(3),
               "wpack must be bf16 [Cout][KH][KW][C]");
@@ -149,11 +151,13 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
 // dw (fp32 OIHW [Cout][Cin][KH][KW]) = beta*dw + Σ_m dy ⊗ im2col(x)
 void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int64_t Cin,
                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, double beta, int64_t S,
-                int64_t cfg) {
+                int64_t cfg, bool s2d) {
+  // s2d: x/dy are the space-to-depth stem operands (4x4/s1 conv over 4*Cin channels);
+  // dw is the original [Cout][Cin][7][7] gradient
   need_bf16_nhwc(x, "x");
   need_bf16_nhwc(dy, "dy");
   const int Cout = dy.size(3);
-  need_f32(dw, "dw", (int64_t)Cout * Cin * KH * KW);
+  need_f32(dw, "dw", s2d ? (int64_t)Cout * Cin * 49 : (int64_t)Cout * Cin * KH * KW);
   auto g = fwd_geom(x, Cout, KH, KW, stride, pad, dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(0) == x.size(0));
   need_f32(slab, "slab", (int64_t)S * Cout * g.K);
@@ -162,7 +166,34 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
   dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
-  dm::wgrad_reduce(fp(slab), (int)S, Cout, g.C, (int)Cin, KH, KW, fp(dw), (float)beta, st);
+  if (s2d)
+    dm::wgrad_reduce_s2d(fp(slab), (int)S, Cout, (int)Cin, g.C, fp(dw), (float)beta, st);
+  else
+    dm::wgrad_reduce(fp(slab), (int)S, Cout, g.C, (int)Cin, KH, KW, fp(dw), (float)beta, st);
+}
+
+void pack_weights_s2d(at::Tensor w, at::Tensor wf) {
+  need_f32(w, "w");
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == 7 && w.size(3) == 7, "s2d stem needs a 7x7 kernel");
+  const int Cout = w.size(0), C = w.size(1);
+  TORCH_CHECK(wf.scalar_type() == at::kBFloat16 && wf.numel() % (Cout * 16) == 0);
+  const int Cp = wf.numel() / (Cout * 16);
+  TORCH_CHECK(Cp % 8 == 0 && Cp >= 4 * C);
+  const DeviceGuard guard(w.device());
+  dm::pack_weights_s2d(fp(w), bp(wf), Cout, C, Cp, cur_stream());
+}
+
+void pack_input_s2d(at::Tensor x, at::Tensor y) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4);
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16);
+  need_bf16_nhwc(y, "y");
+  TORCH_CHECK(x.size(2) % 2 == 0 && x.size(3) % 2 == 0, "s2d needs even H, W");
+  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) * 2 == x.size(2) && y.size(2) * 2 == x.size(3) &&
+              y.size(3) >= 4 * x.size(1));
+  const DeviceGuard guard(x.device());
+  dm::pack_input_s2d(x.data_ptr(), x.scalar_type() == at::kBFloat16, bp(y), x.size(0), x.size(1),
+                     y.size(1), y.size(2), y.size(3), x.stride(0), x.stride(1), x.stride(2),
+                     x.stride(3), cur_stream());
 }
 
 void pack_weights(at::Tensor w, at::Tensor wf, c10::optional<at::Tensor> wd, int64_t Cpad) {
@@ -300,4 +331,6 @@ void register_resnet(pybind11::module_& m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("pack_input", &pack_input);
+  m.def("pack_input_s2d", &pack_input_s2d);
+  m.def("pack_weights_s2d", &pack_weights_s2d);
 }

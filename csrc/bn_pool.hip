@@ -386,7 +386,55 @@ __global__ void __launch_bounds__(256) pack_input_kernel(const T* __restrict__ x
   }
 }
 
+// Space-to-depth input packing for the 7x7/s2 stem: (N,C,H,W) -> (N,H/2,W/2,Cp) with
+// channel (dy*2+dx)*C + c holding x[n, c, 2i+dy, 2j+dx]; the stem then runs as a
+// 4x4/s1 conv over 4C (<= Cp) channels: K = 16*16 = 256 instead of 49*8 = 392
+// (padded to 448), and every tap is one contiguous 32-B channel vector.
+template <typename T>
+__global__ void __launch_bounds__(256) pack_input_s2d_kernel(const T* __restrict__ x,
+                                                             bf16_t* __restrict__ y, int N, int C,
+                                                             int H2, int W2, int Cp, long long sn,
+                                                             long long sc, long long sh,
+                                                             long long sw) {
+  const long long total = (long long)N * H2 * W2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int j = i % W2;
+    long long t = i / W2;
+    const int r = t % H2;
+    const int n = t / H2;
+    for (int c0 = 0; c0 < Cp; c0 += 8) {
+      float f[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int ch = c0 + q;
+        const int sub = ch / C, c = ch % C;
+        if (sub < 4) {
+          const int dy = sub >> 1, dx = sub & 1;
+          const T v = x[n * sn + c * sc + (2 * r + dy) * sh + (2 * j + dx) * sw];
+          if constexpr (sizeof(T) == 4) f[q] = v;
+          else f[q] = bf2f(v);
+        } else {
+          f[q] = 0.f;
+        }
+      }
+      *reinterpret_cast<uint4*>(y + i * Cp + c0) = pack8(f);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ launchers
+void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, int W2, int Cp,
+                    long long sn, long long sc, long long sh, long long sw, hipStream_t st) {
+  const long long total = (long long)N * H2 * W2;
+  if (bf16)
+    pack_input_s2d_kernel<bf16_t><<<grid_for(total, 256, 8192), 256, 0, st>>>(
+        (const bf16_t*)x, y, N, C, H2, W2, Cp, sn, sc, sh, sw);
+  else
+    pack_input_s2d_kernel<float><<<grid_for(total, 256, 8192), 256, 0, st>>>(
+        (const float*)x, y, N, C, H2, W2, Cp, sn, sc, sh, sw);
+}
+
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
                        float* scale, float* shift, float* mean, float* invstd, float* work,

@@ -779,6 +779,59 @@ __global__ void __launch_bounds__(256) pack_weights_kernel(const float* __restri
   }
 }
 
+// Space-to-depth stem weights: W[co][c][7][7] -> W'[co][4][4][Cp] with
+// W'[co][u][v][(dy*2+dx)*C + c] = W[co][c][2u+dy-1][2v+dx-1] (0 outside the 7x7 window)
+__global__ void __launch_bounds__(256) pack_weights_s2d_kernel(const float* __restrict__ w,
+                                                               bf16_t* __restrict__ wf, int Cout,
+                                                               int C, int Cp) {
+  const long long total = (long long)Cout * 16 * Cp;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int ch = o % Cp;
+    const int uv = (o / Cp) % 16;
+    const int co = o / (Cp * 16);
+    const int u = uv / 4, v = uv % 4;
+    const int sub = ch / C, c = ch % C;
+    float val = 0.f;
+    if (sub < 4) {
+      const int kh = 2 * u + (sub >> 1) - 1, kw = 2 * v + (sub & 1) - 1;
+      if (kh >= 0 && kh < 7 && kw >= 0 && kw < 7) val = w[(((long long)co * C + c) * 7 + kh) * 7 + kw];
+    }
+    wf[o] = f2bf(val);
+  }
+}
+
+// dw[co][c][kh][kw] = beta*dw + Σ_s slab[s][co][(u*4+v)*Cp + (dy*2+dx)*C + c]
+__global__ void __launch_bounds__(256) wgrad_reduce_s2d_kernel(const float* __restrict__ slab,
+                                                               int S, int Cout, int C, int Cp,
+                                                               float* __restrict__ dw, float beta) {
+  const long long total = (long long)Cout * C * 49;
+  const long long K = 16LL * Cp;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int kw = o % 7;
+    const int kh = (o / 7) % 7;
+    const int c = (o / 49) % C;
+    const int co = o / (49 * C);
+    const int u = (kh + 1) >> 1, dy = (kh + 1) & 1, v = (kw + 1) >> 1, dx = (kw + 1) & 1;
+    const long long src = (long long)co * K + (u * 4 + v) * Cp + (dy * 2 + dx) * C + c;
+    float sacc = 0.f;
+    for (int i = 0; i < S; ++i) sacc += slab[(long long)i * Cout * K + src];
+    dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + sacc;
+  }
+}
+
+void pack_weights_s2d(const float* w, bf16_t* wf, int Cout, int C, int Cp, hipStream_t st) {
+  const long long total = (long long)Cout * 16 * Cp;
+  pack_weights_s2d_kernel<<<grid_for(total, 256), 256, 0, st>>>(w, wf, Cout, C, Cp);
+}
+
+void wgrad_reduce_s2d(const float* slab, int S, int Cout, int C, int Cp, float* dw, float beta,
+                      hipStream_t st) {
+  const long long total = (long long)Cout * C * 49;
+  wgrad_reduce_s2d_kernel<<<grid_for(total, 256), 256, 0, st>>>(slab, S, Cout, C, Cp, dw, beta);
+}
+
 // ------------------------------------------------------------------ launchers
 static size_t fwd_smem(int BM, int BN) {
   const size_t main = (size_t)2 * (BM + BN) * 64 * 2 + MAXTAPS * 16;

@@ -80,4 +80,9 @@ void avgpool_fwd(const bf16_t* x, bf16_t* y, int N, int HW, int C, hipStream_t s
 void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t st);
 void pack_input(const void* x, bool bf16, bf16_t* y, int N, int C, int H, int W, int Cp,
                 long long sn, long long sc, long long sh, long long sw, hipStream_t st);
+void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, int W2, int Cp,
+                    long long sn, long long sc, long long sh, long long sw, hipStream_t st);
+void pack_weights_s2d(const float* w, bf16_t* wf, int Cout, int C, int Cp, hipStream_t st);
+void wgrad_reduce_s2d(const float* slab, int S, int Cout, int C, int Cp, float* dw, float beta,
+                      hipStream_t st);
 }  // namespace dm

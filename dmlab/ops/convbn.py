@@ -35,8 +35,8 @@ LOADER = 2
 
 def pick_cfg(M, ncols):
     """Block tile for the forward-style kernel (see LOADER)."""
-    if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 480:
-        t = 0
+    if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
+        t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
     elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
         t = 1
     else:
@@ -77,6 +77,25 @@ def empty_nhwc(N, H, W, C, like):
     return _mark(torch.empty((N, H, W, C), device=like.device, dtype=torch.bfloat16))
 
 
+def use_s2d(layer, x):
+    """7x7/s2 stem on a small-channel input with even H, W -> space-to-depth 4x4/s1."""
+    return (layer.k == 7 and layer.stride == 2 and layer.padding == 3 and layer.cin <= 4
+            and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
+
+
+def packed_weights_s2d(layer):
+    prog = layer._prog
+    cache = getattr(layer, "_wcache_s2d", None)
+    if cache is None or cache[0] != prog._wver:
+        w = layer.weight.detach()
+        wf = torch.empty((layer.cout, 4, 4, _cpad(4 * layer.cin)), device=w.device,
+                         dtype=torch.bfloat16)
+        lib().pack_weights_s2d(w, wf)
+        cache = (prog._wver, wf)
+        object.__setattr__(layer, "_wcache_s2d", cache)
+    return cache[1]
+
+
 def packed_weights(layer, need_wd=True):
     prog = layer._prog
     ver = prog._wver
@@ -97,13 +116,27 @@ def packed_weights(layer, need_wd=True):
 def convbn_fwd(layer, x, ctx, train, residual=None):
     L = lib()
     first = not (x.dim() == 4 and getattr(x, "_dm_nhwc", False))
-    x = as_nhwc(x, _cpad(layer.cin)) if first else x
+    s2d = first and use_s2d(layer, x)
+    if s2d:
+        # stem as a 4x4/s1 conv over the space-to-depth input (pad 2 top/left, 1 bottom/right)
+        Nn, Cc, Hh, Ww = x.shape
+        xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
+        L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
+        x = xs
+        k, s, p = 4, 1, 2
+        OH, OW = Hh // 2, Ww // 2
+        wf = packed_weights_s2d(layer)
+    else:
+        x = as_nhwc(x, _cpad(layer.cin)) if first else x
+        k, s, p = layer.k, layer.stride, layer.padding
+        wf = None
     N, H, W, C = x.shape
-    k, s, p = layer.k, layer.stride, layer.padding
-    OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    if not s2d:
+        OH, OW = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
     M = N * OH * OW
     cout = layer.cout
-    wf, _ = packed_weights(layer, need_wd=train and not first)
+    if wf is None:
+        wf, _ = packed_weights(layer, need_wd=train and not first)
     y = empty_nhwc(N, OH, OW, cout, x)
     cfg = pick_cfg(M, cout)
     f32 = dict(device=x.device, dtype=torch.float32)
@@ -130,7 +163,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
     L.bn_apply(y, residual, scale, shift, out, layer.relu)
     if train:
         ctx.update(x=x, y=y, out=out, mean=mean, invstd=invstd, has_res=residual is not None,
-                   first=first)
+                   first=first, s2d=s2d)
     return out
 
 
@@ -143,7 +176,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     x, y, out = ctx["x"], ctx["y"], ctx["out"]
     N, OH, OW, cout = y.shape
     M = N * OH * OW
-    k, s, p = layer.k, layer.stride, layer.padding
+    s2d = ctx.get("s2d", False)
+    k, s, p = (4, 1, 2) if s2d else (layer.k, layer.stride, layer.padding)
     acc = 1.0 if layer.accumulate else 0.0
     dout = dout.contiguous()
     dy = empty_nhwc(N, OH, OW, cout, y)
@@ -157,7 +191,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     K = k * k * C
     wcfg, S = _wgrad_plan(M, cout, K)
     slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
-    L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg)
+    L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg, s2d)
     dx = None
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)

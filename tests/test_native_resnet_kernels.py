@@ -111,7 +111,7 @@ def test_conv_wgrad(dev, geom):
             K = k * k * _cpad(Cin)
             slab = torch.empty(S * Cout * K, device=dev)
             d = dw.clone()
-            lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, beta, S, cfg)
+            lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, beta, S, cfg, False)
             exp = ref + (base if beta else 0)
             assert _rel(d, exp) < 2e-3, (S, cfg, beta)
     assert M > 0
@@ -181,3 +181,27 @@ def test_maxpool_avgpool(dev):
     lib().avgpool_bwd(g, dxa)
     ref = (g.float() / (17 * 17))[:, None, None, :].expand(2, 17, 17, 64)
     assert _rel(dxa, ref) < 5e-3
+
+
+@pytest.mark.parametrize("H", [32, 224])
+def test_stem_space_to_depth(dev, H):
+    """7x7/s2/p3 stem == 4x4/s1 conv over the space-to-depth packed input."""
+    N, C, Co = 2, 3, 64
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(N, C, H, H, device=dev, generator=g).bfloat16()
+    w = torch.randn(Co, C, 7, 7, device=dev, generator=g) / math.sqrt(C * 49)
+    xs = torch.empty(N, H // 2, H // 2, 16, device=dev, dtype=torch.bfloat16)
+    lib().pack_input_s2d(x, xs)
+    wf = torch.empty(Co, 4, 4, 16, device=dev, dtype=torch.bfloat16)
+    lib().pack_weights_s2d(w.contiguous(), wf)
+    ref = F.conv2d(x.float(), w.bfloat16().float(), None, 2, 3)
+    y = torch.empty(N, H // 2, H // 2, Co, device=dev, dtype=torch.bfloat16)
+    lib().conv_fwd(xs, wf, y, None, None, 4, 4, 1, 2, pick_cfg(N * (H // 2) ** 2, Co))
+    assert _rel(_nchw(y), ref) < 6e-3
+    dy = torch.randn_like(ref).bfloat16()
+    dref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), 2, 3)
+    for S, cfg in ((1, 3), (4, 3)):
+        slab = torch.empty(S * Co * 256, device=dev)
+        dw = torch.empty_like(w)
+        lib().conv_wgrad(xs, _nhwc(dy), dw, slab, C, 4, 4, 1, 2, 0.0, S, cfg, True)
+        assert _rel(dw, dref) < 2e-3

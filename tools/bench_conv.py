@@ -101,7 +101,7 @@ def main():
             ref = None
             for v in a.wcfgs.split(","):
                 c = wcfg + (2 if v == "v2" else 0)
-                t = timeit(lambda: L.conv_wgrad(x, dy, dw, slab, C, k, k, s, p, 0.0, S, c), a.iters)
+                t = timeit(lambda: L.conv_wgrad(x, dy, dw, slab, C, k, k, s, p, 0.0, S, c, False), a.iters)
                 row[f"wgrad_{v}_TF"] = round(flops / t / 1e12, 1)
                 if ref is None:
                     ref = dw.clone()
