@@ -43,7 +43,10 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
-    ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the whole step (fwd+bwd+all-reduce+opt) in a hipGraph; "
+                         "-1 = auto (on for one GPU; off for multi-GPU, where the step is "
+                         "GPU-bound and eager RCCL keeps the launch path simplest)")
     return ap.parse_args()
 
 
@@ -87,8 +90,7 @@ def main():
               comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None)
     net.fold_average_into(opt)
 
-    def step(i):
-        x, y = pool[i % 2], labels[i % 2]
+    def train_step(x, y):
         if a.backend == "torch":
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.model == "resnet18"):
                 out = net(x)
@@ -98,7 +100,20 @@ def main():
         opt.zero_grad()
         loss.backward()
         opt.step()
-        return loss
+        return loss.detach()
+
+    if a.graph < 0:
+        a.graph = 1 if ws == 1 else 0
+    if a.graph and a.backend == "native":
+        from dmlab.utils.graph import CapturedStep
+
+        captured = CapturedStep(train_step, [pool[0], labels[0]], warmup=3)
+
+        def step(i):
+            return captured(pool[i % 2], labels[i % 2])
+    else:
+        def step(i):
+            return train_step(pool[i % 2], labels[i % 2])
 
     for i in range(a.warmup):
         loss = step(i)
@@ -144,6 +159,7 @@ def main():
                 "optimizer": "SGD(momentum=0.9), fused flat",
                 "ddp": f"bucketed all-reduce overlapped with backward, bucket {a.bucket_mb} MB, comm {a.comm_dtype}",
                 "backend": a.backend,
+                "hip_graph": bool(a.graph and a.backend == "native"),
             },
             "final_loss": round(final_loss, 4),
         }
