@@ -41,6 +41,29 @@ def available() -> bool:
     return _mod is not None
 
 
+class _SyncDebug:
+    """DMLAB_SYNC_DEBUG=1: synchronise after every native launch so a faulting kernel
+    is reported at its own call site (stream-ordering / race debugging aid)."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        f = getattr(self._mod, name)
+        if not callable(f):
+            return f
+
+        def wrapped(*a, **kw):
+            out = f(*a, **kw)
+            try:
+                torch.cuda.synchronize()
+            except Exception as e:  # pragma: no cover - only on a faulting kernel
+                raise RuntimeError(f"dmlab native op {name} failed: {e}") from e
+            return out
+
+        return wrapped
+
+
 def lib():
     """Return the native module or raise (never silently fall back)."""
     _load()
@@ -49,4 +72,6 @@ def lib():
             "dmlab native extension (dmlab/_C*.so) is not built: run "
             "`python -m dmlab._build` (hipcc --offload-arch=gfx950). "
             f"Import error: {_err!r}")
+    if os.environ.get("DMLAB_SYNC_DEBUG", "0") == "1":
+        return _SyncDebug(_mod)
     return _mod

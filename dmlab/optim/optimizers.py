@@ -76,12 +76,23 @@ class BaseOptimizer:
     def _native(self):
         return self.flat is not None and self.flat.device.type == "cuda"
 
+    def _state_tensors(self):
+        return {}
+
     def state_dict(self):
-        return {"lr": self.lr, "step_count": self.step_count}
+        sd = {"lr": self.lr, "step_count": self.step_count, "grad_scale": self.grad_scale}
+        sd.update({k: v.detach().clone() for k, v in self._state_tensors().items()
+                   if v is not None})
+        return sd
 
     def load_state_dict(self, sd):
         self.lr = sd["lr"]
         self.step_count = sd.get("step_count", 0)
+        self.grad_scale = sd.get("grad_scale", self.grad_scale)
+        for k, t in self._state_tensors().items():
+            if t is not None and k in sd:
+                with torch.no_grad():
+                    t.copy_(sd[k])
 
 
 class GdOptimizer(BaseOptimizer):
@@ -124,6 +135,13 @@ class AdamOptimizer(BaseOptimizer):
         else:
             self.momentums = [torch.zeros_like(p) for p in self.params]
             self.velocities = [torch.zeros_like(p) for p in self.params]
+
+    def _state_tensors(self):
+        if self.flat is not None:
+            return {"m": self.m, "v": self.v}
+        d = {f"m{i}": t for i, t in enumerate(self.momentums)}
+        d.update({f"v{i}": t for i, t in enumerate(self.velocities)})
+        return d
 
     def _bc(self):
         t = self.step_count
@@ -170,6 +188,18 @@ class SGD(BaseOptimizer):
             self.buf = torch.zeros_like(self.flat.data) if momentum else None
         else:
             self.bufs = [None] * len(self.params)
+
+    def _state_tensors(self):
+        if self.flat is not None:
+            return {"buf": self.buf}
+        return {f"buf{i}": b for i, b in enumerate(self.bufs)}
+
+    def load_state_dict(self, sd):
+        if self.flat is None:  # per-tensor buffers are created lazily: materialise them
+            for i, p in enumerate(self.params):
+                if f"buf{i}" in sd and self.bufs[i] is None:
+                    self.bufs[i] = torch.zeros_like(p)
+        super().load_state_dict(sd)
 
     def step(self):
         self.step_count += 1

@@ -52,6 +52,8 @@ def parse_args(argv=None):
     p.add_argument("--max-steps", type=int, default=None)
     p.add_argument("--no-test", action="store_true")
     p.add_argument("--json", default=None)
+    p.add_argument("--save", default=None, help="checkpoint path written after training")
+    p.add_argument("--resume", default=None, help="checkpoint to load before training")
     return p.parse_args(argv)
 
 
@@ -79,6 +81,10 @@ def main(argv=None):
     sampler = MySampler(train_set, ws, rank, shuffle=True, seed=seed, mode=a.sampler)
     loader = DeviceLoader(train_set.to(dev), a.batch_size, sampler=sampler)
     opt = SGD(model.parameters(), lr=a.lr, momentum=a.momentum)
+    if a.resume:
+        from dmlab.utils import checkpoint
+
+        checkpoint.load(a.resume, model, opt)
     if a.dp == "ddp":
         net = DDP(model, bucket_cap_mb=a.bucket_mb)  # broadcasts rank-0 params
         net.fold_average_into(opt)
@@ -90,6 +96,10 @@ def main(argv=None):
     stats = train(net, loader, CrossEntropyLoss(), opt, a.epochs, rank=rank, aggregate=agg,
                   batch_size=a.batch_size, max_steps=a.max_steps)
     print("Training time: {}".format(stats["train_time"]))
+    if a.save:
+        from dmlab.utils import checkpoint
+
+        checkpoint.save(a.save, model, opt, epochs=a.epochs)
     if not a.no_test and rank == 0:
         stats["accuracy"] = test(model, DeviceLoader(test_set.to(dev), 32))
     stats.update(rank=rank, world_size=ws, sampler=a.sampler, dp=a.dp,

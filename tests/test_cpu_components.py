@@ -238,3 +238,29 @@ def test_program_to_refits_flat_buffer():
     assert m.flat.attached()
     for p in m.parameters():
         assert p._dm_flat is m.flat
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    from dmlab.utils import checkpoint
+
+    a, _ = _lenet_pair()
+    oa = SGD(a.parameters(), lr=0.05, momentum=0.9)
+    for s in range(2):
+        oa.zero_grad()
+        _loss(a, s).backward()
+        oa.step()
+    checkpoint.save(tmp_path / "ck.pt", a, oa, epoch=3)
+    torch.manual_seed(1)
+    b = Net()
+    ob = SGD(b.parameters(), lr=0.01, momentum=0.9)
+    extra = checkpoint.load(tmp_path / "ck.pt", b, ob)
+    assert extra == {"epoch": 3} and ob.lr == 0.05 and ob.step_count == 2
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb)
+    # one more identical step keeps them identical (momentum restored)
+    for m, o in ((a, oa), (b, ob)):
+        o.zero_grad()
+        _loss(m, 9).backward()
+        o.step()
+    for pa, pb in zip(a.parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb)
