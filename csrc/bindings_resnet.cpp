@@ -250,23 +250,78 @@ void bn_apply(at::Tensor y, c10::optional<at::Tensor> res, at::Tensor scale, at:
 
 int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C + 32 * 2 * C; }
 
-void bn_backward(at::Tensor dout, at::Tensor out, at::Tensor y, at::Tensor mean, at::Tensor invstd,
-                 at::Tensor gamma, at::Tensor dgamma, at::Tensor dbeta, double gbeta, bool relu,
-                 at::Tensor dy, c10::optional<at::Tensor> dres, at::Tensor work) {
-  need_bf16_nhwc(dout, "dout");
-  need_bf16_nhwc(out, "out");
+// mode: 0 no ReLU, 1 mask from `out`, 2 mask from y*scale+shift, 3 (stem) dz gathered
+// from the following max-pool's gradient (pdy, pidx; pool K/S/P) with mask from y.
+void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, at::Tensor y,
+                 at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
+                 at::Tensor dbeta, double gbeta, int64_t mode, c10::optional<at::Tensor> scale,
+                 c10::optional<at::Tensor> shift, c10::optional<at::Tensor> pdy,
+                 c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P, at::Tensor dy,
+                 c10::optional<at::Tensor> dres, at::Tensor work) {
   need_bf16_nhwc(y, "y");
   need_bf16_nhwc(dy, "dy");
-  TORCH_CHECK(dout.sizes() == y.sizes() && out.sizes() == y.sizes() && dy.sizes() == y.sizes());
+  TORCH_CHECK(dy.sizes() == y.sizes());
+  TORCH_CHECK(mode >= 0 && mode <= 3);
   const int C = y.size(3);
   TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "bn_backward: C/8 must divide 256");
   const long long M = y.numel() / C;
   need_f32(work, "work", bn_bwd_work(M, C));
+  const bf* doutp = nullptr;
+  if (mode < 3) {
+    TORCH_CHECK(dout.has_value());
+    need_bf16_nhwc(*dout, "dout");
+    TORCH_CHECK(dout->sizes() == y.sizes());
+    doutp = bp(*dout);
+  }
+  const bf* outp = nullptr;
+  if (mode == 1) {
+    TORCH_CHECK(out.has_value());
+    need_bf16_nhwc(*out, "out");
+    TORCH_CHECK(out->sizes() == y.sizes());
+    outp = bp(*out);
+  }
+  const float *scp = nullptr, *shp = nullptr;
+  if (mode >= 2) {
+    TORCH_CHECK(scale.has_value() && shift.has_value());
+    need_f32(*scale, "scale", C);
+    need_f32(*shift, "shift", C);
+    scp = fp(*scale);
+    shp = fp(*shift);
+  }
+  const bf* pdyp = nullptr;
+  const uint8_t* pidxp = nullptr;
+  int OH = 0, OW = 0;
+  if (mode == 3) {
+    TORCH_CHECK(pdy.has_value() && pidx.has_value());
+    need_bf16_nhwc(*pdy, "pdy");
+    TORCH_CHECK(pidx->scalar_type() == at::kByte && pidx->numel() == pdy->numel());
+    TORCH_CHECK(pdy->size(0) == y.size(0) && pdy->size(3) == C);
+    OH = pdy->size(1);
+    OW = pdy->size(2);
+    TORCH_CHECK(OH == (y.size(1) + 2 * P - K) / S + 1 && OW == (y.size(2) + 2 * P - K) / S + 1);
+    pdyp = bp(*pdy);
+    pidxp = (const uint8_t*)pidx->data_ptr();
+  }
   bf* drp = nullptr;
   if (dres.has_value()) { need_bf16_nhwc(*dres, "dres"); drp = bp(*dres); }
   const DeviceGuard guard(y.device());
-  dm::bn_backward(bp(dout), bp(out), bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
-                  (float)gbeta, M, C, relu, bp(dy), drp, fp(work), cur_stream());
+  dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
+                  (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
+                  OW, K, S, P, bp(dy), drp, fp(work), cur_stream());
+}
+
+void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,
+                     at::Tensor idx, int64_t K, int64_t S, int64_t P) {
+  need_bf16_nhwc(y, "y");
+  need_bf16_nhwc(out, "out");
+  const int C = y.size(3);
+  need_f32(scale, "scale", C);
+  need_f32(shift, "shift", C);
+  TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == out.numel());
+  TORCH_CHECK(out.size(1) == (y.size(1) + 2 * P - K) / S + 1 && out.size(2) == (y.size(2) + 2 * P - K) / S + 1);
+  const DeviceGuard guard(y.device());
+  dm::bn_relu_maxpool(bp(y), fp(scale), fp(shift), bp(out), (uint8_t*)idx.data_ptr(), y.size(0),
+                      y.size(1), y.size(2), C, out.size(1), out.size(2), K, S, P, cur_stream());
 }
 
 // ------------------------------------------------------------------ pooling / packing
@@ -326,6 +381,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_work", &bn_bwd_work);
   m.def("bn_backward", &bn_backward);
+  m.def("bn_relu_maxpool", &bn_relu_maxpool);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -117,38 +117,102 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
-// BN backward reduction: per channel Σdz, Σdz·x̂ over rows [M][C]; dz = dout·[out>0]
-// grid: (G); block 256; each thread owns 8 channels (chunk) of rows r ≡ tid/C8 (mod 256/C8)
-template <bool RELU>
-__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
-    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ invstd, long long M, int C,
-    float* __restrict__ part) {
-  extern __shared__ float red[];  // [256][16] partials
-  const int C8 = C >> 3;
+// ------------------------------------------------------------------ BN backward
+// dz = upstream grad with the ReLU mask; sources (template MODE):
+//   0  dout tensor, no ReLU
+//   1  dout tensor, mask from the saved output (out > 0)          -- residual layers
+//   2  dout tensor, mask recomputed from y (y*scale + shift > 0)   -- no `out` read
+//   3  gathered from a following 3x3/s2 max-pool's grads + argmax codes, mask from y
+//      (stem: neither `out` nor the unpooled gradient is ever materialised)
+struct BnBwdArgs {
+  const bf16_t* dout;
+  const bf16_t* out;
+  const bf16_t* y;
+  const float* mean;
+  const float* invstd;
+  const float* scale;   // forward BN scale/shift (modes 2, 3)
+  const float* shift;
+  const bf16_t* pdy;    // mode 3: pooled-output gradient [N][OH][OW][C]
+  const uint8_t* pidx;  //         argmax codes (kh*K + kw), same shape
+  int H, W, OH, OW, K, S, P;
+  long long M;
+  int C;
+};
+
+template <int MODE>
+__device__ __forceinline__ void load_dz(const BnBwdArgs& a, long long r, int chunk, int C8,
+                                        const float yv[8], const float* sc, const float* sh,
+                                        float d[8]) {
+  const long long i = r * C8 + chunk;
+  if (MODE == 3) {
+    const int iw = r % a.W;
+    const long long t = r / a.W;
+    const int ih = t % a.H;
+    const int n = t / a.H;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+    const int oh_lo = max(0, (ih + a.P - a.K + a.S) / a.S), oh_hi = min(a.OH - 1, (ih + a.P) / a.S);
+    const int ow_lo = max(0, (iw + a.P - a.K + a.S) / a.S), ow_hi = min(a.OW - 1, (iw + a.P) / a.S);
+    for (int oh = oh_lo; oh <= oh_hi; ++oh)
+      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+        const unsigned code = (ih - (oh * a.S - a.P)) * a.K + (iw - (ow * a.S - a.P));
+        const long long o = (((long long)n * a.OH + oh) * a.OW + ow) * C8 + chunk;
+        const uint2 ix = reinterpret_cast<const uint2*>(a.pidx)[o];
+        const uint32_t aw[2] = {ix.x, ix.y};
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) any |= ((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code;
+        if (!any) continue;
+        float g[8];
+        unpack8(reinterpret_cast<const uint4*>(a.pdy)[o], g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += g[j];
+      }
+  } else {
+    unpack8(reinterpret_cast<const uint4*>(a.dout)[i], d);
+  }
+  if (MODE == 1) {
+    float o[8];
+    unpack8(reinterpret_cast<const uint4*>(a.out)[i], o);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+  } else if (MODE >= 2) {
+    const int c0 = chunk * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = (yv[j] * sc[c0 + j] + sh[c0 + j]) > 0.f ? d[j] : 0.f;
+  }
+}
+
+// grid (G); block 256; each thread owns 8 channels of rows r ≡ tid/C8 (mod 256/C8)
+template <int MODE>
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* __restrict__ part) {
+  extern __shared__ float red[];  // [256][16] partials, then [2][C] scale/shift
+  const int C = a.C, C8 = C >> 3;
+  float* sc = red + 256 * 16;
+  float* sh = sc + C;
+  if (MODE >= 2)
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      sc[c] = a.scale[c];
+      sh[c] = a.shift[c];
+    }
+  __syncthreads();
   const int chunk = threadIdx.x % C8;
   const int rl = threadIdx.x / C8;
-  const int RL = blockDim.x / C8;  // row lanes per block (C8 divides 256)
+  const int RL = blockDim.x / C8;
   const int c0 = chunk * 8;
   float mu[8], is[8], s[8], q[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    mu[j] = mean[c0 + j];
-    is[j] = invstd[c0 + j];
+    mu[j] = a.mean[c0 + j];
+    is[j] = a.invstd[c0 + j];
     s[j] = 0.f;
     q[j] = 0.f;
   }
-  for (long long r = (long long)blockIdx.x * RL + rl; r < M; r += (long long)gridDim.x * RL) {
-    const long long i = r * C8 + chunk;
+  for (long long r = (long long)blockIdx.x * RL + rl; r < a.M; r += (long long)gridDim.x * RL) {
     float d[8], yv[8];
-    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
-    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
-    if (RELU) {
-      float o[8];
-      unpack8(reinterpret_cast<const uint4*>(out)[i], o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
-    }
+    unpack8(reinterpret_cast<const uint4*>(a.y)[r * C8 + chunk], yv);
+    load_dz<MODE>(a, r, chunk, C8, yv, sc, sh, d);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       s[j] += d[j];
@@ -161,7 +225,6 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     red[threadIdx.x * 16 + 8 + j] = q[j];
   }
   __syncthreads();
-  // combine row lanes: thread t < C8*16 handles (chunk, j)
   for (int e = threadIdx.x; e < C8 * 16; e += blockDim.x) {
     const int ch = e / 16, j = e % 16;
     float acc = 0.f;
@@ -196,33 +259,85 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
 }
 
 // dy = a·dz + b·y + c ; optional dres = dz
-template <bool RELU, bool DRES>
-__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
-    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out, const bf16_t* __restrict__ y,
-    const float* __restrict__ coef, bf16_t* __restrict__ dy, bf16_t* __restrict__ dres,
-    long long n8, int C) {
-  extern __shared__ float cf[];  // [3][C]
+template <int MODE, bool DRES>
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const float* __restrict__ coef,
+                                                           bf16_t* __restrict__ dy,
+                                                           bf16_t* __restrict__ dres) {
+  extern __shared__ float cf[];  // [3][C] coefficients, [2][C] forward scale/shift
+  const int C = a.C, C8 = C >> 3;
   for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
+  float* sc = cf + 3 * C;
+  float* sh = sc + C;
+  if (MODE >= 2)
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      sc[c] = a.scale[c];
+      sh[c] = a.shift[c];
+    }
   __syncthreads();
-  const int C8 = C >> 3;
+  const long long n8 = a.M * C8;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    const int c0 = (int)(i % C8) * 8;
+    const int chunk = (int)(i % C8);
+    const int c0 = chunk * 8;
     float d[8], yv[8];
-    unpack8(reinterpret_cast<const uint4*>(dout)[i], d);
-    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
-    if (RELU) {
-      float o[8];
-      unpack8(reinterpret_cast<const uint4*>(out)[i], o);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
-    }
+    unpack8(reinterpret_cast<const uint4*>(a.y)[i], yv);
+    load_dz<MODE>(a, i / C8, chunk, C8, yv, sc, sh, d);
     if (DRES) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
     float r[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
     reinterpret_cast<uint4*>(dy)[i] = pack8(r);
+  }
+}
+
+// Fused stem tail: pooled = maxpool_KxK/S(relu(y*scale + shift)) with argmax codes; the
+// BN output itself is never written.
+__global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
+    const bf16_t* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    bf16_t* __restrict__ out, uint8_t* __restrict__ idx, int N, int H, int W, int C, int OH,
+    int OW, int K, int S, int P) {
+  extern __shared__ float ss[];  // [2][C]
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    ss[c] = scale[c];
+    ss[C + c] = shift[c];
+  }
+  __syncthreads();
+  const int C8 = C >> 3;
+  const long long total = (long long)N * OH * OW * C8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c8 = i % C8;
+    long long t = i / C8;
+    const int ow = t % OW;
+    t /= OW;
+    const int oh = t % OH;
+    const int n = t / OH;
+    const int c0 = c8 * 8;
+    float best[8];
+    int arg[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+    for (int kh = 0; kh < K; ++kh) {
+      const int ih = oh * S - P + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < K; ++kw) {
+        const int iw = ow * S - P + kw;
+        if (iw < 0 || iw >= W) continue;
+        float f[8];
+        unpack8(*reinterpret_cast<const uint4*>(y + (((long long)n * H + ih) * W + iw) * C + c0), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = fmaxf(f[j] * ss[c0 + j] + ss[C + c0 + j], 0.f);
+          if (v > best[j]) { best[j] = v; arg[j] = kh * K + kw; }
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(out)[i] = pack8(best);
+    uint2 a2;
+    a2.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+    a2.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+    reinterpret_cast<uint2*>(idx)[i] = a2;
   }
 }
 
@@ -477,16 +592,23 @@ int bn_bwd_groups(long long M, int C) {
 
 void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* mean,
                  const float* invstd, const float* gamma, float* dgamma, float* dbeta,
-                 float gbeta, long long M, int C, bool relu, bf16_t* dy, bf16_t* dres,
-                 float* work, hipStream_t st) {
-  // work: [G][2C] partials + [3C] coefficients
+                 float gbeta, long long M, int C, int mode, const float* scale,
+                 const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
+                 int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
+                 hipStream_t st) {
+  // work: [G][2C] partials + [3C] coefficients + [32][2C] second-level partials
+  BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C};
   const int G = bn_bwd_groups(M, C);
   float* part = work;
   float* coef = work + (long long)G * 2 * C;
-  float* part2 = coef + 3 * C;  // [<=32][2C] second-level partials
-  const size_t shr = sizeof(float) * 256 * 16;
-  if (relu) bn_bwd_reduce_kernel<true><<<G, 256, shr, st>>>(dout, out, y, mean, invstd, M, C, part);
-  else bn_bwd_reduce_kernel<false><<<G, 256, shr, st>>>(dout, out, y, mean, invstd, M, C, part);
+  float* part2 = coef + 3 * C;
+  const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
+  switch (mode) {
+    case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
+    case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
+    case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
+    default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
+  }
   int Gf = G;
   const float* fin = part;
   if (G > 32) {  // parallel fixed-order pre-reduction so the finalize loop stays short
@@ -498,13 +620,27 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                                                        invstd, dgamma, dbeta, gbeta, coef);
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
-  const size_t sh = sizeof(float) * 3 * C;
-#define DM_BNB(R, D) bn_bwd_apply_kernel<R, D><<<grid, 256, sh, st>>>(dout, out, y, coef, dy, dres, n8, C)
-  if (relu && dres) DM_BNB(true, true);
-  else if (relu) DM_BNB(true, false);
-  else if (dres) DM_BNB(false, true);
-  else DM_BNB(false, false);
+  const size_t sh = sizeof(float) * 5 * C;
+#define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
+  switch (mode * 2 + (dres ? 1 : 0)) {
+    case 0: DM_BNB(0, false); break;
+    case 1: DM_BNB(0, true); break;
+    case 2: DM_BNB(1, false); break;
+    case 3: DM_BNB(1, true); break;
+    case 4: DM_BNB(2, false); break;
+    case 5: DM_BNB(2, true); break;
+    case 6: DM_BNB(3, false); break;
+    default: DM_BNB(3, true); break;
+  }
 #undef DM_BNB
+}
+
+void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
+                     uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
+                     int P, hipStream_t st) {
+  const long long total = (long long)N * OH * OW * (C / 8);
+  bn_relu_maxpool_kernel<<<grid_for(total, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
+      y, scale, shift, out, idx, N, H, W, C, OH, OW, K, S, P);
 }
 
 void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,

@@ -70,8 +70,13 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
 int bn_bwd_groups(long long M, int C);
 void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* mean,
                  const float* invstd, const float* gamma, float* dgamma, float* dbeta,
-                 float gbeta, long long M, int C, bool relu, bf16_t* dy, bf16_t* dres,
-                 float* work, hipStream_t st);
+                 float gbeta, long long M, int C, int mode, const float* scale,
+                 const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
+                 int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
+                 hipStream_t st);
+void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
+                     uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
+                     int P, hipStream_t st);
 void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                  int OW, int K, int S, int P, hipStream_t st);
 void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,

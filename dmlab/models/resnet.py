@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import torch
 
-from dmlab.nn.layers import BasicBlock, ConvBN, GlobalAvgPool, Linear, MaxPool
+from dmlab.nn.layers import BasicBlock, ConvBNPool, GlobalAvgPool, Linear
 from dmlab.nn.program import Program
 
 
@@ -23,9 +23,9 @@ class ResNet18(Program):
     def __init__(self, num_classes: int = 1000, in_channels: int = 3,
                  widths=(64, 128, 256, 512)):
         super().__init__()
-        self.stem = ConvBN(in_channels, widths[0], 7, 2, 3, relu=True)
-        self.pool = MaxPool(3, 2, 1)
-        layers = [self.stem, self.pool]
+        # stem = conv7x7/s2 + BN + ReLU + maxpool3x3/s2 (one fused layer)
+        self.stem = ConvBNPool(in_channels, widths[0], 7, 2, 3, pool_k=3, pool_s=2, pool_p=1)
+        layers = [self.stem]
         cin = widths[0]
         for i, w in enumerate(widths):
             b1 = BasicBlock(cin, w, 1 if i == 0 else 2)

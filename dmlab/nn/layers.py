@@ -161,6 +161,20 @@ class ConvBN(Layer):
         return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into)
 
 
+class ConvBNPool(ConvBN):
+    """ConvBN (+ReLU) followed by a max-pool: the ResNet stem.  The native path fuses
+    BN-apply, ReLU and the pool into one pass that never writes the BN output, and its
+    backward gathers the pooled gradient on the fly (no unpooled gradient tensor)."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0, pool_k=3, pool_s=2, pool_p=1):
+        super().__init__(cin, cout, k, stride, padding, relu=True)
+        self.pool_k, self.pool_s, self.pool_p = pool_k, pool_s, pool_p
+
+    def torch_forward(self, x, residual=None):
+        y = super().torch_forward(x)
+        return F.max_pool2d(y, self.pool_k, self.pool_s, self.pool_p)
+
+
 class BasicBlock(Layer):
     """ResNet BasicBlock: relu(bn2(conv2(relu(bn1(conv1 x)))) + shortcut(x))."""
 

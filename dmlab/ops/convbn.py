@@ -159,11 +159,24 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
         L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
                          layer.running_var, layer.eps, scale, shift)
         mean = invstd = None
+    if train:
+        ctx.update(x=x, y=y, mean=mean, invstd=invstd, has_res=residual is not None,
+                   first=first, s2d=s2d, scale=scale, shift=shift)
+    pool = getattr(layer, "pool_k", 0)
+    if pool:
+        # fused BN + ReLU + max-pool: the BN output is never materialised
+        pk, ps, pp = layer.pool_k, layer.pool_s, layer.pool_p
+        PH, PW = (OH + 2 * pp - pk) // ps + 1, (OW + 2 * pp - pk) // ps + 1
+        out = empty_nhwc(N, PH, PW, cout, x)
+        idx = torch.empty((N, PH, PW, cout), device=x.device, dtype=torch.uint8)
+        L.bn_relu_maxpool(y, scale, shift, out, idx, pk, ps, pp)
+        if train:
+            ctx["idx"] = idx
+        return out
     out = empty_nhwc(N, OH, OW, cout, x)
     L.bn_apply(y, residual, scale, shift, out, layer.relu)
-    if train:
-        ctx.update(x=x, y=y, out=out, mean=mean, invstd=invstd, has_res=residual is not None,
-                   first=first, s2d=s2d)
+    if train and residual is not None:
+        ctx["out"] = out  # ReLU mask source (the residual is not kept)
     return out
 
 
@@ -173,7 +186,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient)
     ``dx_into`` : accumulate dx in place into this tensor (downsample branch)."""
     L = lib()
-    x, y, out = ctx["x"], ctx["y"], ctx["out"]
+    x, y = ctx["x"], ctx["y"]
     N, OH, OW, cout = y.shape
     M = N * OH * OW
     s2d = ctx.get("s2d", False)
@@ -183,9 +196,21 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     dy = empty_nhwc(N, OH, OW, cout, y)
     dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
-    L.bn_backward(dout, out, y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
-                  layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc, layer.relu, dy,
-                  dres, work)
+    pool = getattr(layer, "pool_k", 0)
+    if pool:
+        mode = 3       # dz gathered from the max-pool gradient, ReLU mask from y
+    elif not layer.relu:
+        mode = 0
+    elif ctx["has_res"]:
+        mode = 1       # mask needs the residual: read the saved output
+    else:
+        mode = 2       # mask recomputed from y (no `out` read)
+    L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
+                  layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
+                  layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
+                  dout if pool else None, ctx.get("idx"),
+                  getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
+                  getattr(layer, "pool_p", 1), dy, dres, work)
     # weight gradient
     C = x.shape[3]
     K = k * k * C

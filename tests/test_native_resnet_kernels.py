@@ -148,15 +148,17 @@ def test_bn_forward_backward(dev, C, M, relu, res):
     y4, out = y.view(1, 1, M, C), torch.empty(1, 1, M, C, device=dev, dtype=torch.bfloat16)
     lib().bn_apply(y4, r.view(1, 1, M, C) if res else None, scale, shift, out, relu)
     assert _rel(out.view(M, C), out_ref.detach()) < 5e-3
-    dy = torch.empty_like(out)
-    dres = torch.empty_like(out) if res else None
-    dg, db = torch.zeros(C, **f), torch.zeros(C, **f)
-    work = torch.empty(lib().bn_bwd_work(M, C), **f)
-    lib().bn_backward(dout.view(1, 1, M, C), out, y4, mean, invstd, gamma, dg, db, 0.0, relu, dy,
-                      dres, work)
-    assert _rel(dy.view(M, C), yr.grad) < 1e-2
-    assert _rel(dg, g_.grad) < 1e-2
-    assert _rel(db, b_.grad) < 1e-2
+    modes = [0] if not relu else ([1] if res else [1, 2])  # 2: ReLU mask from y
+    for mode in modes:
+        dy = torch.empty_like(out)
+        dres = torch.empty_like(out) if res else None
+        dg, db = torch.zeros(C, **f), torch.zeros(C, **f)
+        work = torch.empty(lib().bn_bwd_work(M, C), **f)
+        lib().bn_backward(dout.view(1, 1, M, C), out, y4, mean, invstd, gamma, dg, db, 0.0, mode,
+                          scale, shift, None, None, 3, 2, 1, dy, dres, work)
+        assert _rel(dy.view(M, C), yr.grad) < 1e-2, mode
+        assert _rel(dg, g_.grad) < 1e-2, mode
+        assert _rel(db, b_.grad) < 1e-2, mode
 
 
 def test_maxpool_avgpool(dev):
@@ -205,3 +207,39 @@ def test_stem_space_to_depth(dev, H):
         dw = torch.empty_like(w)
         lib().conv_wgrad(xs, _nhwc(dy), dw, slab, C, 4, 4, 1, 2, 0.0, S, cfg, True)
         assert _rel(dw, dref) < 2e-3
+
+
+def test_fused_bn_relu_maxpool_and_gather_backward(dev):
+    """Stem tail: maxpool(relu(bn(y))) forward and the pool-gather BN backward (mode 3)."""
+    torch.manual_seed(0)
+    N, H, C = 2, 18, 64
+    y = (torch.randn(N, H, H, C, device=dev) * 1.5).bfloat16()
+    gamma = torch.rand(C, device=dev) + 0.5
+    beta = torch.randn(C, device=dev) * 0.5
+    yr = y.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    g_, b_ = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    z = F.batch_norm(yr, rm, rv, g_, b_, True, 0.1, 1e-5)
+    pooled_ref = F.max_pool2d(F.relu(z), 3, 2, 1)
+    dp = torch.randn_like(pooled_ref).bfloat16()
+    pooled_ref.backward(dp.float())
+    f = dict(device=dev, dtype=torch.float32)
+    M = N * H * H
+    yf = y.float().view(M, C)
+    stats = torch.stack([yf.sum(0), (yf ** 2).sum(0)]).reshape(-1).contiguous()
+    scale, shift, mean, invstd = (torch.empty(C, **f) for _ in range(4))
+    lib().bn_stats_finalize(stats, 1, float(M), gamma, beta, None, None, 0.1, 1e-5, scale, shift,
+                            mean, invstd, torch.empty(128 * C, **f))
+    OH = (H + 2 - 3) // 2 + 1
+    out = torch.empty(N, OH, OH, C, device=dev, dtype=torch.bfloat16)
+    idx = torch.empty(N, OH, OH, C, device=dev, dtype=torch.uint8)
+    lib().bn_relu_maxpool(y, scale, shift, out, idx, 3, 2, 1)
+    assert _rel(_nchw(out), pooled_ref.detach()) < 5e-3
+    dy = torch.empty_like(y)
+    dg, db = torch.zeros(C, **f), torch.zeros(C, **f)
+    work = torch.empty(lib().bn_bwd_work(M, C), **f)
+    lib().bn_backward(None, None, y, mean, invstd, gamma, dg, db, 0.0, 3, scale, shift,
+                      _nhwc(dp), idx, 3, 2, 1, dy, None, work)
+    assert _rel(_nchw(dy), yr.grad) < 1e-2
+    assert _rel(dg, g_.grad) < 1e-2
+    assert _rel(db, b_.grad) < 1e-2
