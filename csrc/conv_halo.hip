@@ -1,0 +1,251 @@
+// Halo-staged implicit-GEMM convolution for unit-stride tap grids (|dy|, |dx| <= 1), gfx950.
+//
+// The igemm kernels (conv_igemm.hip) stage one (tap, 64-channel) slice of the implicit
+// im2col matrix per K-tile, so every input pixel is fetched from L2 once per tap — 9x
+// for a 3x3 conv — and written to LDS 9x.  Measured on MI355X that staging traffic,
+// not the MFMA issue rate, bounds those kernels at ~600-700 TFLOP/s.
+//
+// Here a block owns 128 consecutive output pixels m (flattened n, y, x).  Because the
+// tap grid is unit-stride, all of their taps live inside the contiguous flattened input
+// row range [r0 - 1, r1 + 1] (r = n*H + y), the "halo": at most (ceil(127/W) + 3) * W
+// pixels.  The halo of one 64-channel chunk is staged into LDS ONCE and every tap's A
+// fragment is read straight out of it:
+//     A[p, tap] = halo[(m0 + p) - hbase + dy*W + dx]          (hbase = (r0 - 1) * W)
+// — consecutive output pixels are consecutive halo rows, so the XOR-swizzled fragment
+// reads stay conflict-free.  A tap that leaves the image (x+dx or y+dy out of range, or
+// rows past M) is redirected to an all-zero LDS row, which is exactly the conv's zero
+// padding (and crosses image/row boundaries of the flattened layout correctly).
+//
+// Per (chunk, tap) step the block stages only the weight tile (BN x 64 bf16), double
+// buffered through registers as in the igemm kernels; the next chunk's halo is loaded
+// into VGPRs while the current chunk's taps run and written once per chunk.  Per-step
+// L2->LDS traffic drops from 16 KB (A) + BN*128 B (B) to ~2.5-5 KB + BN*128 B.
+//
+// Used for: stride-1 forward convs (3x3/p1, 1x1/p0), stride-1 dgrad (tap flip) and the
+// parity classes of stride-2 dgrad (their dY grid is the launch grid, taps are unit-
+// stride).  MFMA v_mfma_f32_32x32x16_bf16, 4 waves each owning 64 x BN/2.
+#include "common.h"
+#include "conv_geom.h"
+#include "igemm_common.h"
+#include "kernels.h"
+
+namespace dm {
+
+namespace {
+constexpr int HBM = 128;  // output pixels per block
+constexpr int HBK = 64;   // channels per chunk (one 128-B LDS row per pixel)
+constexpr unsigned OOB = 0x80000000u;
+
+template <int BN, int HR>
+__global__ void __launch_bounds__(256, 2) conv_halo_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
+    float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes) {
+  constexpr int WM = 2, WN = 2, TM = HBM / WM, TN = BN / WN;
+  constexpr int RM = TM / 32, RN = TN / 32;
+  constexpr int BR = BN / 32;
+  constexpr int HP_MAX = 32 * HR;                    // halo rows the LDS image holds
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Hs = reinterpret_cast<bf16_t*>(smem);      // [HP_MAX + 1][64], last row = zeros
+  bf16_t* Bs = Hs + (HP_MAX + 1) * HBK;              // [2][BN][64]
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * HBK);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * HBM;
+  const int n0 = blockIdx.y * BN;
+  const int ntaps = g.nth * g.ntw;
+  const int nchunk = g.C / HBK;
+  const int HW = g.H * g.W;
+  const int NHW = g.N * HW;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
+    taps[tid] = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C,
+                          dy * g.W + dx);
+  }
+  if (tid < 8) *reinterpret_cast<uint4*>(Hs + HP_MAX * HBK + tid * 8) = make_uint4(0, 0, 0, 0);
+
+  // halo extent (flattened rows r0-1 .. r1+1)
+  const int r0 = (int)fdiv((unsigned)m0, g.wg_mul, g.wg_shr);
+  const long long mlast = (m0 + HBM - 1 < g.M) ? m0 + HBM - 1 : g.M - 1;
+  const int r1 = (int)fdiv((unsigned)mlast, g.wg_mul, g.wg_shr);
+  const int hbase = (r0 - 1) * g.W;
+  const int hp = (r1 - r0 + 3) * g.W;
+
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
+  const int chunk = tid & 7;
+
+  // per-lane A-fragment rows: halo row of the centre tap and the pixel coordinates
+  int a_h[RM], a_x[RM], a_y[RM];
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    const long long m = m0 + wm * TM + i * 32 + (lane & 31);
+    const unsigned r = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+    a_x[i] = (int)((unsigned)m - r * (unsigned)g.W);
+    const unsigned n = fdiv(r, g.hg_mul, g.hg_shr);
+    a_y[i] = (m < g.M) ? (int)(r - n * (unsigned)g.H) : -(1 << 28);  // rows >= M: never valid
+    a_h[i] = (int)(m - hbase);
+  }
+  unsigned b_off[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + 32 * i;
+    b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
+  }
+  __syncthreads();
+
+  uint4 rh[HR], rb[BR];
+  auto load_halo = [&](int cc) {
+    const unsigned cb = (unsigned)(cc * HBK + chunk * 8) * 2u;
+#pragma unroll
+    for (int j = 0; j < HR; ++j) {
+      const int hh = (tid >> 3) + 32 * j;
+      const int gp = hbase + hh;
+      const bool ok = hh < hp && (unsigned)gp < (unsigned)NHW;
+      const unsigned off = ok ? (unsigned)gp * (unsigned)g.C * 2u + cb : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int j = 0; j < HR; ++j) {
+      const int hh = (tid >> 3) + 32 * j;
+      *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) = rh[j];
+    }
+  };
+  auto load_b = [&](int cc, int t) {
+    const unsigned kb = (unsigned)(taps[t].z + cc * HBK + chunk * 8) * 2u;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const unsigned off = b_off[i] != OOB ? b_off[i] + kb : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_b = [&](int buf) {
+    bf16_t* bs = Bs + buf * BN * HBK;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(bs + r * HBK + swz(r, chunk) * 8) = rb[i];
+    }
+  };
+
+  f32x16 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto compute = [&](int buf, int t) {
+    const int4 tp = taps[t];
+    int hrow[RM];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) {
+      const bool ok = (unsigned)(a_x[i] + tp.y) < (unsigned)g.W &&
+                      (unsigned)(a_y[i] + tp.x) < (unsigned)g.H;
+      hrow[i] = ok ? a_h[i] + tp.w : HP_MAX;
+    }
+    const bf16_t* bs = Bs + buf * BN * HBK;
+#pragma unroll
+    for (int ks = 0; ks < HBK / 16; ++ks) {
+      const int ch = ks * 2 + (lane >> 5);
+      bf16x8 af[RM], bfr[RN];
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+        af[i] = *reinterpret_cast<const bf16x8*>(Hs + hrow[i] * HBK + swz(hrow[i], ch) * 8);
+#pragma unroll
+      for (int j = 0; j < RN; ++j) {
+        const int r = wn * TN + j * 32 + (lane & 31);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * HBK + swz(r, ch) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int S = nchunk * ntaps;
+  load_halo(0);
+  load_b(0, 0);
+  store_halo();
+  store_b(0);
+  __syncthreads();
+  if (nchunk > 1) load_halo(1);
+  int cc = 0, t = 0;
+  for (int s = 0; s < S; ++s) {
+    int nt = t + 1, ncc = cc;
+    if (nt == ntaps) {
+      nt = 0;
+      ++ncc;
+    }
+    if (s + 1 < S) load_b(ncc, nt);
+    compute(s & 1, t);
+    if (s + 1 < S) store_b((s + 1) & 1);
+    __syncthreads();
+    if (ncc != cc && s + 1 < S) {
+      store_halo();  // every wave is past the last tap of chunk cc
+      __syncthreads();
+      if (ncc + 1 < nchunk) load_halo(ncc + 1);
+    }
+    t = nt;
+    cc = ncc;
+  }
+  mfma_tile_epilogue<HBM, BN, WM, WN, true>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
+}
+
+int halo_rows_needed(const ConvGeom& g) {
+  // worst case over blocks: a 128-pixel run starting at the last pixel of a row
+  return ((g.W - 1 + HBM - 1) / g.W + 3) * g.W;
+}
+
+template <int BN, int HR>
+void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+                 const ConvGeom& g, hipStream_t st) {
+  const size_t main = (size_t)(32 * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
+  const size_t epi = (size_t)HBM * (BN + 4) * 4;
+  const size_t sm = main > epi ? main : epi;
+  dim3 grid((unsigned)((g.M + HBM - 1) / HBM), (g.Ncols + BN - 1) / BN);
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
+  auto k = conv_halo_kernel<BN, HR>;
+  set_smem_attr(k, sm);
+  k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+}
+}  // namespace
+
+bool conv_halo_supported(const ConvGeom& g) {
+  if (g.isy != 1 || g.isx != 1 || g.Hg != g.H || g.Wg != g.W) return false;
+  if (g.C % HBK != 0 || g.nth * g.ntw > 16 || g.nth < 1 || g.ntw < 1) return false;
+  const int dya = g.dy0, dyb = g.dy0 + (g.nth - 1) * g.dys;
+  const int dxa = g.dx0, dxb = g.dx0 + (g.ntw - 1) * g.dxs;
+  auto in1 = [](int v) { return v >= -1 && v <= 1; };
+  if (!in1(dya) || !in1(dyb) || !in1(dxa) || !in1(dxb)) return false;
+  if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31)) return false;
+  if ((long long)g.Ncols * g.wK * 2 >= (1LL << 31)) return false;
+  return halo_rows_needed(g) <= 32 * 12;
+}
+
+void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+               const ConvGeom& g, int bn, hipStream_t st) {
+  const int hp = halo_rows_needed(g);
+  const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
+  if (bn == 128) {
+    if (hr == 6) launch_halo<128, 6>(X, Wp, Y, ADD, stats, g, st);
+    else if (hr == 8) launch_halo<128, 8>(X, Wp, Y, ADD, stats, g, st);
+    else launch_halo<128, 12>(X, Wp, Y, ADD, stats, g, st);
+  } else {
+    if (hr == 6) launch_halo<64, 6>(X, Wp, Y, ADD, stats, g, st);
+    else if (hr == 8) launch_halo<64, 8>(X, Wp, Y, ADD, stats, g, st);
+    else launch_halo<64, 12>(X, Wp, Y, ADD, stats, g, st);
+  }
+  DM_CHECK(hipGetLastError());
+}
+
+}  // namespace dm

@@ -29,19 +29,13 @@
 // reduce that also permutes to the OIHW fp32 gradient layout and applies beta.
 #include "common.h"
 #include "conv_geom.h"
+#include "igemm_common.h"
+#include "kernels.h"
+
+#include <type_traits>
 
 namespace dm {
 
-template <typename K>
-static void set_smem_attr(K kernel, size_t bytes) {
-  // dynamic LDS above 64 KiB must be opted into per kernel (idempotent, cheap)
-  if (bytes > 65536)
-    DM_CHECK(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)bytes));
-}
-
-
-__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
 // ------------------------------------------------------------------ shared epilogue
 template <int BM, int BN, int WM, int WN>
@@ -295,6 +289,204 @@ __global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
   }
 
   igemm_epilogue<BM, BN, WM, WN>(acc, smem, Y, ADD, stats, g, m0, n0);
+}
+
+// ------------------------------------------------------------------ forward / dgrad, v3
+// Register-staged buffer loads (as igemm_fwd_kernel<...,BUF=true>) with
+//   * cheaper per-tile addressing: each staged row keeps its pixel base and its
+//     (y*isy, x*isx) origin, so a chunk costs one add + two unsigned bound checks;
+//   * MF32 = true: v_mfma_f32_32x32x16_bf16 (half the MFMA issues of 16x16x32 for the
+//     same 64x64 wave tile; same LDS bytes per FLOP; the chunk swizzle stays
+//     conflict-free for its 32-row fragment reads).
+template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
+__global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd3_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
+    float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes) {
+  constexpr int BK = 64;
+  constexpr int TM = BM / WM, TN = BN / WN;
+  constexpr int FM = MF32 ? 32 : 16;                 // MFMA block edge
+  constexpr int RM = TM / FM, RN = TN / FM;
+  constexpr int NT = WM * WN * 64, RPP = NT / 8;   // threads, staged rows per pass
+  constexpr int AR = BM / RPP, BR = BN / RPP;
+  static_assert(AR * RPP == BM && BR * RPP == BN, "tile rows must be a multiple of NT/8");
+  constexpr unsigned OOB = 0x80000000u;
+  typedef typename std::conditional<MF32, f32x16, f32x4>::type accT;
+  constexpr int NR = MF32 ? 16 : 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = As + 2 * BM * BK;
+  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const long long m0 = (long long)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ntaps = g.nth * g.ntw;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
+    // .w = pixel offset of the tap (dy*W + dx)
+    taps[tid] = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C,
+                          dy * g.W + dx);
+  }
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
+  const int chunk = tid & 7;
+  int a_y[AR], a_x[AR];
+  unsigned a_pix[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const long long m = m0 + (tid >> 3) + RPP * i;
+    if (m < g.M) {
+      const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
+      const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+      const int y = (int)(t - n * (unsigned)g.Hg);
+      a_y[i] = y * g.isy;
+      a_x[i] = x * g.isx;
+      a_pix[i] = (n * (unsigned)g.H + (unsigned)a_y[i]) * (unsigned)g.W + (unsigned)a_x[i];
+    } else {
+      a_y[i] = -(1 << 28);
+      a_x[i] = 0;
+      a_pix[i] = 0;
+    }
+  }
+  unsigned b_off[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int n = n0 + (tid >> 3) + RPP * i;
+    b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
+  }
+  __syncthreads();
+  uint4 ra[DEPTH][AR], rb[DEPTH][BR];
+  const int nk = (g.K + BK - 1) / BK;
+  const unsigned C2 = (unsigned)g.C * 2u;
+
+  auto load = [&](int kt, auto S) {
+    const int kc = kt * (BK / 8) + chunk;
+    const int tap = kc >> g.lgC8;
+    const unsigned c0b = (unsigned)((kc & ((1 << g.lgC8) - 1)) * 16);  // byte offset in pixel
+    const bool kval = tap < ntaps;
+    int4 tp = make_int4(0, 0, 0, 0);
+    if (kval) tp = taps[tap];
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const bool ok = kval && (unsigned)(a_y[i] + tp.x) < (unsigned)g.H &&
+                      (unsigned)(a_x[i] + tp.y) < (unsigned)g.W;
+      const unsigned off = ok ? (a_pix[i] + (unsigned)tp.w) * C2 + c0b : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      ra[S][i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const unsigned off = (kval && b_off[i] != OOB) ? b_off[i] + (unsigned)tp.z * 2u + c0b : OOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0);
+      rb[S][i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store = [&](int buf, auto S) {
+    bf16_t* as = As + buf * BM * BK;
+    bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int r = (tid >> 3) + RPP * i;
+      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[S][i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int r = (tid >> 3) + RPP * i;
+      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[S][i];
+    }
+  };
+
+  accT acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) acc[i][j][r] = 0.f;
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, (DEPTH > 1 ? 1 : 0)>;
+  auto compute = [&](int buf) {
+      const bf16_t* as = As + buf * BM * BK;
+      const bf16_t* bs = Bs + buf * BN * BK;
+      if constexpr (MF32) {
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+          const int ch = ks * 2 + (lane >> 5);
+          bf16x8 af[RM], bfr[RN];
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            const int r = wm * TM + i * 32 + (lane & 31);
+            af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
+          }
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            const int r = wn * TN + j * 32 + (lane & 31);
+            bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
+          }
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < BK / 32; ++ks) {
+          const int ch = ks * 4 + (lane >> 4);
+          bf16x8 af[RM], bfr[RN];
+#pragma unroll
+          for (int i = 0; i < RM; ++i) {
+            const int r = wm * TM + i * 16 + (lane & 15);
+            af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
+          }
+#pragma unroll
+          for (int j = 0; j < RN; ++j) {
+            const int r = wn * TN + j * 16 + (lane & 15);
+            bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
+          }
+#pragma unroll
+          for (int i = 0; i < RM; ++i)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+      }
+  };
+  if constexpr (DEPTH == 1) {
+    load(0, S0{});
+    store(0, S0{});
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) load(kt + 1, S0{});
+      compute(buf);
+      if (kt + 1 < nk) store(buf ^ 1, S0{});
+      __syncthreads();
+    }
+  } else {
+    // tile t is staged through register set t & 1, issued two tiles ahead of its use
+    load(0, S0{});
+    if (nk > 1) load(1, S1{});
+    store(0, S0{});
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) load(kt + 2, S0{});
+      compute(0);
+      if (kt + 1 < nk) store(1, S1{});
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) load(kt + 3, S1{});
+      compute(1);
+      if (kt + 2 < nk) store(0, S0{});
+      __syncthreads();
+    }
+  }
+
+  mfma_tile_epilogue<BM, BN, WM, WN, MF32>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
 }
 
 // ------------------------------------------------------------------ forward / dgrad, LDS-DMA
@@ -587,9 +779,6 @@ __global__ void __launch_bounds__(256, 2) igemm_wgrad_kernel(
       }
 }
 
-__device__ __forceinline__ unsigned fdiv(unsigned n, unsigned mul, unsigned shr) {
-  return (__umulhi(n, mul) + n) >> shr;
-}
 
 // Weight gradient, v2: 64 m-rows per barrier (two MFMA k-steps), branch-free buffer
 // loads with range-check zero fill, magic-number row decomposition.
@@ -842,13 +1031,18 @@ static size_t fwd_smem(int BM, int BN) {
 
 template <int BM, int BN, int WM, int WN>
 static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                       float* stats, const ConvGeom& g, bool dma, bool buf, hipStream_t st) {
+                       float* stats, const ConvGeom& g, bool dma, bool buf, bool v3, bool mf32,
+                       hipStream_t st) {
   const size_t sm = fwd_smem(BM, BN);
   dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
   if (dma) {
     auto k = igemm_fwd_dma_kernel<BM, BN, WM, WN>;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+  } else if (v3) {
+    auto k = mf32 ? igemm_fwd3_kernel<BM, BN, WM, WN, true, 1> : igemm_fwd3_kernel<BM, BN, WM, WN, false, 1>;
     set_smem_attr(k, sm);
     k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
   } else if (buf) {
@@ -862,20 +1056,46 @@ static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_
   }
 }
 
+template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
+static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                        float* stats, const ConvGeom& g, hipStream_t st) {
+  const size_t sm = fwd_smem(BM, BN);
+  dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
+  auto k = igemm_fwd3_kernel<BM, BN, WM, WN, MF32, DEPTH>;
+  set_smem_attr(k, sm);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+}
+
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st) {
+  // v3 with two tiles of register prefetch: 15 = 128x128 mf32, 16 = 128x64 mf32, 17 = 64x64
+  // 16x16; 18 = 8-wave 256x128 mf32 (measured slower: one workgroup per CU)
+  // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64; shapes it does not
+  // cover fall back to the v3 tiles 12 / 13
+  if (cfg == 20 || cfg == 21) {
+    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, cfg == 20 ? 128 : 64, st);
+    cfg = cfg == 20 ? 12 : 13;
+  }
+  if (cfg == 15) return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 16) return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 17) return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 18) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
   // cfg % 3: 0 = 128x128 (2x2 waves, 64x64 per wave), 1 = 128x64, 2 = 64x64
   // cfg / 3: 0 = register-staged global loads, 1 = LDS-DMA (buffer_load ... lds),
   //          2 = register-staged buffer loads (branch-free zero fill)
-  const bool dma = cfg / 3 == 1, buf = cfg / 3 == 2;
+  //          3 = v3 (cheaper addressing) on 16x16x32 MFMA, 4 = v3 on 32x32x16 MFMA
+  const int ld = cfg / 3;
+  const bool dma = ld == 1, buf = ld == 2, v3 = ld >= 3, mf32 = ld == 4;
   switch (cfg % 3) {
-    case 0: launch_fwd<128, 128, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, st); break;
-    case 1: launch_fwd<128, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, st); break;
-    default: launch_fwd<64, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, st); break;
+    case 0: launch_fwd<128, 128, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st); break;
+    case 1: launch_fwd<128, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st); break;
+    default: launch_fwd<64, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st); break;
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return cfg >= 20 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -28,20 +28,34 @@ def _cpad(c):
 
 # forward-style kernel configs (csrc/conv_igemm.hip igemm_fwd): tile = cfg % 3
 # (0: 128x128, 1: 128x64, 2: 64x64); loader = cfg // 3 (0: predicated global loads,
-# 1: LDS-DMA, 2: branch-free buffer loads).  Measured on MI355X (tools/bench_conv.py,
-# profiles/conv_kernels_r1.jsonl) the buffer-load loader is fastest on every shape.
-LOADER = 2
+# 1: LDS-DMA, 2: branch-free buffer loads, 3: v3 addressing on 16x16x32 MFMA,
+# 4: v3 on 32x32x16 MFMA); 15-17: v3 with two tiles of register prefetch; 18: 8-wave
+# 256x128; 20/21: halo-staged unit-stride kernel (csrc/conv_halo.hip, BN 128/64).
+# Measured on MI355X (tools/bench_conv.py -> profiles/conv_kernels_r1.jsonl):
+#   * unit-stride 3x3 with >= 128 output channels: halo kernel (20) fastest
+#     (l2/l3/l4: 714/749/787 TFLOP/s fwd vs 661/708/730 for the best igemm tile);
+#   * 64 output channels at 56x56 (one 64-channel chunk, the halo prologue is not
+#     amortised): v3 depth-2 128x64 (16);
+#   * everything else (strided taps, stride-2 dgrad parity classes, 1x1/s2, stem):
+#     v3 tiles 15 / 13 / 11 by the block-count rule below; 256-row tiles lose
+#     (one workgroup per CU exposes the staging latency).
+TILE_CFG = (15, 13, 11)
 
 
-def pick_cfg(M, ncols):
-    """Block tile for the forward-style kernel (see LOADER)."""
+def pick_cfg(M, ncols, k=0, stride=0, cin=0):
+    """Kernel config for a forward-style conv GEMM with M output pixels and ncols
+    output channels.  ``k``/``stride``/``cin`` (kernel size, tap stride, input
+    channels) enable the unit-stride halo kernel when they describe a k x k conv with
+    unit tap stride over 64-channel-aligned input."""
+    if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
+        return 20 if ncols >= 128 else 16
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
         t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
     elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
         t = 1
     else:
         t = 2
-    return t + 3 * LOADER
+    return TILE_CFG[t]
 
 
 def _wgrad_plan(M, cout, K):
@@ -138,7 +152,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
     if wf is None:
         wf, _ = packed_weights(layer, need_wd=train and not first)
     y = empty_nhwc(N, OH, OW, cout, x)
-    cfg = pick_cfg(M, cout)
+    cfg = pick_cfg(M, cout, k, s, C)
     f32 = dict(device=x.device, dtype=torch.float32)
     scale = torch.empty(cout, **f32)
     shift = torch.empty(cout, **f32)
@@ -221,7 +235,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)
         N_, H, W, Cin = x.shape
-        cfg = pick_cfg(N_ * H * W, Cin)
+        cfg = pick_cfg(N_ * H * W, Cin, k, s, cout)
         if dx_into is not None:
             L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
             dx = dx_into

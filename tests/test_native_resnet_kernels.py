@@ -19,6 +19,17 @@ GEOMS = [  # (N, H, Cin, Cout, k, stride, pad)
     (2, 14, 128, 256, 3, 2, 1),
     (2, 16, 3, 64, 7, 2, 3),  # stem (channels padded to 8)
 ]
+# unit-stride shapes for the halo-staged kernel (cfg 20/21): wide rows (W=56: a
+# 128-pixel block spans 4 rows), several 64-channel chunks, blocks crossing images
+# (W=7), partial last block, 1x1 taps
+HALO_GEOMS = [
+    (3, 56, 64, 64, 3, 1, 1),
+    (2, 28, 128, 128, 3, 1, 1),
+    (5, 7, 128, 64, 3, 1, 1),
+    (3, 14, 256, 256, 3, 1, 1),
+    (2, 14, 64, 128, 1, 1, 0),
+]
+FWD_CFGS = list(range(19)) + [20, 21]
 
 
 def _rel(a, b):
@@ -47,10 +58,20 @@ def _setup(dev, N, H, Cin, Cout, k, s, p, seed=0):
 
 
 @pytest.mark.parametrize("geom", GEOMS)
-@pytest.mark.parametrize("cfg", list(range(9)))
+@pytest.mark.parametrize("cfg", FWD_CFGS)
 def test_conv_fwd_and_stats(dev, geom, cfg):
+    _check_fwd(dev, geom, cfg)
+
+
+@pytest.mark.parametrize("geom", HALO_GEOMS)
+@pytest.mark.parametrize("cfg", [12, 20, 21])
+def test_conv_fwd_halo(dev, geom, cfg):
+    _check_fwd(dev, geom, cfg)
+
+
+def _check_fwd(dev, geom, cfg):
     N, H, Cin, Cout, k, s, p = geom
-    if cfg % 3 == 0 and Cout % 128:
+    if cfg in (0, 3, 6, 9, 12, 15, 18) and Cout % 128:
         pytest.skip("128-wide tile needs Cout % 128 == 0")
     x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
     ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
@@ -78,7 +99,7 @@ def test_conv_fwd_add(dev):
 
 @pytest.mark.parametrize("geom", GEOMS[:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [2, 3, 4, 5])
 def test_conv_dgrad(dev, geom, accumulate, variant):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
@@ -90,6 +111,24 @@ def test_conv_dgrad(dev, geom, accumulate, variant):
     base = dx.clone()
     lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None,
                      pick_cfg(N * H * H, Cin) % 3 + 3 * variant)
+    if accumulate:
+        ref = ref + _nchw(base).float()
+    assert _rel(_nchw(dx), ref) < 6e-3
+
+
+@pytest.mark.parametrize("geom", HALO_GEOMS + GEOMS[:2] + GEOMS[3:5])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("cfg", [20, 21])
+def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    wb = w.bfloat16().float()
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wb, dy.float(), s, p)
+    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    base = dx.clone()
+    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, cfg)
     if accumulate:
         ref = ref + _nchw(base).float()
     assert _rel(_nchw(dx), ref) < 6e-3
