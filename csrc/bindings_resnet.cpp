@@ -217,7 +217,7 @@ void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gam
                        at::Tensor mean, at::Tensor invstd, at::Tensor work) {
   const int C = gamma.numel();
   need_f32(stats, "stats", T * 2 * C);
-  need_f32(work, "work", 64 * 2 * C);
+  need_f32(work, "work", 256 * 2 * C);
   for (auto* t : {&gamma, &beta, &scale, &shift, &mean, &invstd}) need_f32(*t, "bn vec", C);
   const DeviceGuard guard(stats.device());
   dm::bn_stats_finalize(fp(stats), T, C, count, fp(gamma), fp(beta),
@@ -248,7 +248,7 @@ void bn_apply(at::Tensor y, c10::optional<at::Tensor> res, at::Tensor scale, at:
   dm::bn_apply(bp(y), rp, fp(scale), fp(shift), bp(out), y.numel(), C, relu, cur_stream());
 }
 
-int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C + 32 * 2 * C; }
+int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C + 256 * 2 * C; }
 
 // mode: 0 no ReLU, 1 mask from `out`, 2 mask from y*scale+shift, 3 (stem) dz gathered
 // from the following max-pool's gradient (pdy, pidx; pool K/S/P) with mask from y.

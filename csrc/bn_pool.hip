@@ -26,36 +26,67 @@ __device__ __forceinline__ uint4 pack8(const float f[8]) {
 }
 
 // ------------------------------------------------------------------ slab column reduce
-// in: [T][W] fp32 (W = 2C) ; out: [G][W] partial sums over row groups (fixed order).
+// Fixed-order (deterministic) reductions of per-tile partial rows [T][W] fp32.  Every
+// lane keeps 8 independent loads in flight: these reductions are latency-bound chains
+// otherwise (a 6272-row slab summed one dependent load at a time costs ~40 us).
+__device__ __forceinline__ double sum_rows8(const float* __restrict__ p, int r, int rend, int step,
+                                            long long W) {
+  double acc = 0.0;
+  for (; r + 7 * step < rend; r += 8 * step) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = p[(long long)(r + j * step) * W];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  for (; r < rend; r += step) acc += p[(long long)r * W];
+  return acc;
+}
+
+// in: [T][W] -> out: [G][W] (G = gridDim.y); group gi sums rows [gi*R, (gi+1)*R), R = ceil(T/G)
 __global__ void __launch_bounds__(256) slab_colsum_kernel(const float* __restrict__ in, int T,
                                                           int W, float* __restrict__ out) {
   const int G = gridDim.y, gi = blockIdx.y;
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;  // 4 row lanes
-  __shared__ float red[4][64];
-  float s = 0.f;
-  if (col < W)
-    for (int t = gi * 4 + rl; t < T; t += 4 * G) s += in[(long long)t * W + col];
-  red[rl][threadIdx.x & 63] = s;
+  const int R = (T + G - 1) / G;
+  const int r0 = gi * R, r1 = min(T, r0 + R);
+  __shared__ double red[4][64];
+  red[rl][threadIdx.x & 63] = col < W ? sum_rows8(in + col, r0 + rl, r1, 4, W) : 0.0;
   __syncthreads();
   if (rl == 0 && col < W)
-    out[(long long)gi * W + col] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                   red[3][threadIdx.x];
+    out[(long long)gi * W + col] = (float)(red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                           red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
+// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment), 4 lanes
+// x 64 channels per 256-thread block; valid in lane 0 (threadIdx.x < 64) afterwards.
+__device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G, int C, int c,
+                                           double& s, double& q) {
+  __shared__ double red[2][4][64];
+  const int rl = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  const long long W = 2LL * C;
+  red[0][rl][cl] = c < C ? sum_rows8(part + c, rl, G, 4, W) : 0.0;
+  red[1][rl][cl] = c < C ? sum_rows8(part + C + c, rl, G, 4, W) : 0.0;
+  __syncthreads();
+  s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+}
+
+// level-1 groups for a [T][2C] slab: none when the finalize block can sum it directly
+static inline int colsum_groups(int T) { return T <= 128 ? 0 : min(256, (T + 31) / 32); }
+
 // stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
+// grid ceil(C/64) x 256 threads
 __global__ void __launch_bounds__(256) bn_finalize_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ mean_out, float* __restrict__ invstd_out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s += part[(long long)g * 2 * C + c];
-    q += part[(long long)g * 2 * C + C + c];
-  }
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s, q;
+  block_sum2(part, G, C, c, s, q);
+  if (threadIdx.x >= 64 || c >= C) return;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -100,20 +131,32 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   __syncthreads();
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int C8 = C >> 3;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    const int c0 = (int)(i % C8) * 8;
-    float f[8];
-    unpack8(reinterpret_cast<const uint4*>(y)[i], f);
-    float r[8];
-    if (RES) unpack8(reinterpret_cast<const uint4*>(res)[i], r);
+  constexpr int U = 4;  // loads of U grid-strided chunks in flight before any is consumed
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
+    uint4 yr[U], rr[U];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float v = f[j] * sc_sh[c0 + j] + sc_sh[C + c0 + j];
-      if (RES) v += r[j];
-      if (RELU) v = fmaxf(v, 0.f);
-      f[j] = v;
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * stride < n8 ? i0 + u * stride : 0;
+      yr[u] = reinterpret_cast<const uint4*>(y)[i];
+      if (RES) rr[u] = reinterpret_cast<const uint4*>(res)[i];
     }
-    reinterpret_cast<uint4*>(out)[i] = pack8(f);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= n8) continue;
+      const int c0 = (int)(i % C8) * 8;
+      float f[8], r[8];
+      unpack8(yr[u], f);
+      if (RES) unpack8(rr[u], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = f[j] * sc_sh[c0 + j] + sc_sh[C + c0 + j];
+        if (RES) v += r[j];
+        if (RELU) v = fmaxf(v, 0.f);
+        f[j] = v;
+      }
+      reinterpret_cast<uint4*>(out)[i] = pack8(f);
+    }
   }
 }
 
@@ -139,54 +182,77 @@ struct BnBwdArgs {
   int C;
 };
 
-template <int MODE>
-__device__ __forceinline__ void load_dz(const BnBwdArgs& a, long long r, int chunk, int C8,
-                                        const float yv[8], const float* sc, const float* sh,
-                                        float d[8]) {
-  const long long i = r * C8 + chunk;
-  if (MODE == 3) {
-    const int iw = r % a.W;
-    const long long t = r / a.W;
-    const int ih = t % a.H;
-    const int n = t / a.H;
+// mode 3: dz of one 8-channel chunk of input pixel r, gathered from the pool windows
+__device__ __forceinline__ void gather_pool_dz(const BnBwdArgs& a, long long r, int chunk, int C8,
+                                               float d[8]) {
+  const int iw = r % a.W;
+  const long long t = r / a.W;
+  const int ih = t % a.H;
+  const int n = t / a.H;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = 0.f;
-    const int oh_lo = max(0, (ih + a.P - a.K + a.S) / a.S), oh_hi = min(a.OH - 1, (ih + a.P) / a.S);
-    const int ow_lo = max(0, (iw + a.P - a.K + a.S) / a.S), ow_hi = min(a.OW - 1, (iw + a.P) / a.S);
-    for (int oh = oh_lo; oh <= oh_hi; ++oh)
-      for (int ow = ow_lo; ow <= ow_hi; ++ow) {
-        const unsigned code = (ih - (oh * a.S - a.P)) * a.K + (iw - (ow * a.S - a.P));
-        const long long o = (((long long)n * a.OH + oh) * a.OW + ow) * C8 + chunk;
-        const uint2 ix = reinterpret_cast<const uint2*>(a.pidx)[o];
-        const uint32_t aw[2] = {ix.x, ix.y};
-        bool any = false;
+  for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  const int oh_lo = max(0, (ih + a.P - a.K + a.S) / a.S), oh_hi = min(a.OH - 1, (ih + a.P) / a.S);
+  const int ow_lo = max(0, (iw + a.P - a.K + a.S) / a.S), ow_hi = min(a.OW - 1, (iw + a.P) / a.S);
+  for (int oh = oh_lo; oh <= oh_hi; ++oh)
+    for (int ow = ow_lo; ow <= ow_hi; ++ow) {
+      const unsigned code = (ih - (oh * a.S - a.P)) * a.K + (iw - (ow * a.S - a.P));
+      const long long o = (((long long)n * a.OH + oh) * a.OW + ow) * C8 + chunk;
+      const uint2 ix = reinterpret_cast<const uint2*>(a.pidx)[o];
+      const uint32_t aw[2] = {ix.x, ix.y};
+      bool any = false;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) any |= ((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code;
-        if (!any) continue;
-        float g[8];
-        unpack8(reinterpret_cast<const uint4*>(a.pdy)[o], g);
+      for (int j = 0; j < 8; ++j) any |= ((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code;
+      if (!any) continue;
+      float g[8];
+      unpack8(reinterpret_cast<const uint4*>(a.pdy)[o], g);
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += g[j];
-      }
-  } else {
-    unpack8(reinterpret_cast<const uint4*>(a.dout)[i], d);
-  }
-  if (MODE == 1) {
-    float o[8];
-    unpack8(reinterpret_cast<const uint4*>(a.out)[i], o);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
-  } else if (MODE >= 2) {
-    const int c0 = chunk * 8;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = (yv[j] * sc[c0 + j] + sh[c0 + j]) > 0.f ? d[j] : 0.f;
-  }
+      for (int j = 0; j < 8; ++j)
+        if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += g[j];
+    }
 }
 
-// grid (G); block 256; each thread owns 8 channels of rows r ≡ tid/C8 (mod 256/C8)
+// Raw operands of U grid-strided 8-channel chunks i0 + u*stride, all loads issued before
+// any is consumed (memory-level parallelism: these kernels are pure HBM streams).
+template <int MODE, int U>
+struct BnBwdBatch {
+  uint4 y[U], dout[U], out[U];
+  bool ok[U];
+  __device__ __forceinline__ void load(const BnBwdArgs& a, long long i0, long long stride,
+                                       long long n8) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * stride;
+      ok[u] = i < n8;
+      const long long ii = ok[u] ? i : 0;
+      y[u] = reinterpret_cast<const uint4*>(a.y)[ii];
+      if (MODE != 3) dout[u] = reinterpret_cast<const uint4*>(a.dout)[ii];
+      if (MODE == 1) out[u] = reinterpret_cast<const uint4*>(a.out)[ii];
+    }
+  }
+  // dz (upstream grad with the ReLU mask) and y of chunk u
+  __device__ __forceinline__ void dz(const BnBwdArgs& a, int u, long long i, int chunk, int C8,
+                                     const float* sc, const float* sh, float d[8],
+                                     float yv[8]) const {
+    unpack8(y[u], yv);
+    if (MODE == 3) gather_pool_dz(a, i / C8, chunk, C8, d);
+    else unpack8(dout[u], d);
+    if (MODE == 1) {
+      float o[8];
+      unpack8(out[u], o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+    } else if (MODE >= 2) {
+      const int c0 = chunk * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = (yv[j] * sc[c0 + j] + sh[c0 + j]) > 0.f ? d[j] : 0.f;
+    }
+  }
+};
+
+// grid (G); block 256; thread t owns channel chunk t % C8 of the rows ≡ t / C8 (mod 256 / C8)
 template <int MODE>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* __restrict__ part) {
+  constexpr int U = MODE == 3 ? 2 : 4;
   extern __shared__ float red[];  // [256][16] partials, then [2][C] scale/shift
   const int C = a.C, C8 = C >> 3;
   float* sc = red + 256 * 16;
@@ -209,14 +275,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
     s[j] = 0.f;
     q[j] = 0.f;
   }
-  for (long long r = (long long)blockIdx.x * RL + rl; r < a.M; r += (long long)gridDim.x * RL) {
-    float d[8], yv[8];
-    unpack8(reinterpret_cast<const uint4*>(a.y)[r * C8 + chunk], yv);
-    load_dz<MODE>(a, r, chunk, C8, yv, sc, sh, d);
+  // chunk index i = r*C8 + chunk; rows strided by gridDim.x*RL keep the channel fixed
+  const long long n8 = a.M * C8;
+  const long long rstride = (long long)gridDim.x * RL;
+  const long long stride = rstride * C8;
+  for (long long i0 = ((long long)blockIdx.x * RL + rl) * C8 + chunk; i0 < n8; i0 += U * stride) {
+    BnBwdBatch<MODE, U> bt;
+    bt.load(a, i0, stride, n8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      s[j] += d[j];
-      q[j] += d[j] * (yv[j] - mu[j]) * is[j];
+    for (int u = 0; u < U; ++u) {
+      if (!bt.ok[u]) continue;
+      float d[8], yv[8];
+      bt.dz(a, u, i0 + u * stride, chunk, C8, sc, sh, d, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[j] += d[j];
+        q[j] += d[j] * (yv[j] - mu[j]) * is[j];
+      }
     }
   }
 #pragma unroll
@@ -235,18 +310,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
 }
 
 // finalize: Σ over G partials -> dgamma, dbeta (written with beta-accumulate into grad
-// slots) and the affine dy coefficients a, b, c.
+// slots) and the affine dy coefficients a, b, c.  grid ceil(C/64) x 256 threads.
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dgamma,
     float* __restrict__ dbeta, float gbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, q = 0.0;
-  for (int g = 0; g < G; ++g) {
-    s += part[(long long)g * 2 * C + c];
-    q += part[(long long)g * 2 * C + C + c];
-  }
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  double s, q;
+  block_sum2(part, G, C, c, s, q);
+  if (threadIdx.x >= 64 || c >= C) return;
   dbeta[c] = (gbeta != 0.f ? gbeta * dbeta[c] : 0.f) + (float)s;
   dgamma[c] = (gbeta != 0.f ? gbeta * dgamma[c] : 0.f) + (float)q;
   const float a = gamma[c] * invstd[c];
@@ -263,6 +335,7 @@ template <int MODE, bool DRES>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const float* __restrict__ coef,
                                                            bf16_t* __restrict__ dy,
                                                            bf16_t* __restrict__ dres) {
+  constexpr int U = MODE == 3 ? 2 : 4;
   extern __shared__ float cf[];  // [3][C] coefficients, [2][C] forward scale/shift
   const int C = a.C, C8 = C >> 3;
   for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
@@ -276,18 +349,24 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
   __syncthreads();
   const long long n8 = a.M * C8;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-    const int chunk = (int)(i % C8);
-    const int c0 = chunk * 8;
-    float d[8], yv[8];
-    unpack8(reinterpret_cast<const uint4*>(a.y)[i], yv);
-    load_dz<MODE>(a, i / C8, chunk, C8, yv, sc, sh, d);
-    if (DRES) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
-    float r[8];
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
+    BnBwdBatch<MODE, U> bt;
+    bt.load(a, i0, stride, n8);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
-    reinterpret_cast<uint4*>(dy)[i] = pack8(r);
+    for (int u = 0; u < U; ++u) {
+      if (!bt.ok[u]) continue;
+      const long long i = i0 + u * stride;
+      const int chunk = (int)(i % C8);
+      const int c0 = chunk * 8;
+      float d[8], yv[8];
+      bt.dz(a, u, i, chunk, C8, sc, sh, d, yv);
+      if (DRES) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+      float r[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
+      reinterpret_cast<uint4*>(dy)[i] = pack8(r);
+    }
   }
 }
 
@@ -555,10 +634,15 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
                        float* scale, float* shift, float* mean, float* invstd, float* work,
                        hipStream_t st) {
   const int W = 2 * C;
-  const int G = min(32, max(1, T / 16));
-  slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
-  bn_finalize_kernel<<<(C + 63) / 64, 64, 0, st>>>(work, G, C, count, gamma, beta, rmean, rvar,
-                                                      momentum, eps, scale, shift, mean, invstd);
+  const int G = colsum_groups(T);
+  const float* fin = stats;
+  if (G) {
+    slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
+    fin = work;
+  }
+  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(fin, G ? G : T, C, count, gamma, beta, rmean,
+                                                       rvar, momentum, eps, scale, shift, mean,
+                                                       invstd);
 }
 
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
@@ -596,7 +680,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
                  hipStream_t st) {
-  // work: [G][2C] partials + [3C] coefficients + [32][2C] second-level partials
+  // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
   BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C};
   const int G = bn_bwd_groups(M, C);
   float* part = work;
@@ -609,15 +693,14 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
-  int Gf = G;
+  const int G2 = colsum_groups(G);
   const float* fin = part;
-  if (G > 32) {  // parallel fixed-order pre-reduction so the finalize loop stays short
-    Gf = 32;
-    slab_colsum_kernel<<<dim3((2 * C + 63) / 64, Gf), 256, 0, st>>>(part, G, 2 * C, part2);
+  if (G2) {  // parallel fixed-order pre-reduction so the finalize sums stay short
+    slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
     fin = part2;
   }
-  bn_bwd_finalize_kernel<<<(C + 63) / 64, 64, 0, st>>>(fin, Gf, C, (double)M, gamma, mean,
-                                                       invstd, dgamma, dbeta, gbeta, coef);
+  bn_bwd_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(fin, G2 ? G2 : G, C, (double)M, gamma,
+                                                        mean, invstd, dgamma, dbeta, gbeta, coef);
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;

@@ -36,14 +36,16 @@ constexpr int HBM = 128;  // output pixels per block
 constexpr int HBK = 64;   // channels per chunk (one 128-B LDS row per pixel)
 constexpr unsigned OOB = 0x80000000u;
 
-template <int BN, int HR>
-__global__ void __launch_bounds__(256, 2) conv_halo_kernel(
+template <int BN, int HR, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes) {
-  constexpr int WM = 2, WN = 2, TM = HBM / WM, TN = BN / WN;
+  constexpr int TM = HBM / WM, TN = BN / WN;
   constexpr int RM = TM / 32, RN = TN / 32;
-  constexpr int BR = BN / 32;
-  constexpr int HP_MAX = 32 * HR;                    // halo rows the LDS image holds
+  constexpr int NT = WM * WN * 64, RPP = NT / 8;     // threads, staged rows per pass
+  constexpr int BR = BN / RPP;
+  static_assert(BR * RPP == BN && RM >= 1 && RN >= 1, "tile / wave layout");
+  constexpr int HP_MAX = RPP * HR;                   // halo rows the LDS image holds
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Hs = reinterpret_cast<bf16_t*>(smem);      // [HP_MAX + 1][64], last row = zeros
   bf16_t* Bs = Hs + (HP_MAX + 1) * HBK;              // [2][BN][64]
@@ -90,7 +92,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(
   unsigned b_off[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
+    const int n = n0 + (tid >> 3) + RPP * i;
     b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
   }
   __syncthreads();
@@ -100,7 +102,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(
     const unsigned cb = (unsigned)(cc * HBK + chunk * 8) * 2u;
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
-      const int hh = (tid >> 3) + 32 * j;
+      const int hh = (tid >> 3) + RPP * j;
       const int gp = hbase + hh;
       const bool ok = hh < hp && (unsigned)gp < (unsigned)NHW;
       const unsigned off = ok ? (unsigned)gp * (unsigned)g.C * 2u + cb : OOB;
@@ -111,7 +113,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(
   auto store_halo = [&]() {
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
-      const int hh = (tid >> 3) + 32 * j;
+      const int hh = (tid >> 3) + RPP * j;
       *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) = rh[j];
     }
   };
@@ -128,7 +130,7 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(
     bf16_t* bs = Bs + buf * BN * HBK;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
+      const int r = (tid >> 3) + RPP * i;
       *reinterpret_cast<uint4*>(bs + r * HBK + swz(r, chunk) * 8) = rb[i];
     }
   };
@@ -151,23 +153,30 @@ __global__ void __launch_bounds__(256, 2) conv_halo_kernel(
       hrow[i] = ok ? a_h[i] + tp.w : HP_MAX;
     }
     const bf16_t* bs = Bs + buf * BN * HBK;
-#pragma unroll
-    for (int ks = 0; ks < HBK / 16; ++ks) {
+    // fragments double-buffered across the 4 k-substeps (reads of ks+1 overlap MFMAs of ks)
+    bf16x8 af[2][RM], bfr[2][RN];
+    auto frag = [&](int ks, int set) {
       const int ch = ks * 2 + (lane >> 5);
-      bf16x8 af[RM], bfr[RN];
 #pragma unroll
       for (int i = 0; i < RM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(Hs + hrow[i] * HBK + swz(hrow[i], ch) * 8);
+        af[set][i] = *reinterpret_cast<const bf16x8*>(Hs + hrow[i] * HBK + swz(hrow[i], ch) * 8);
 #pragma unroll
       for (int j = 0; j < RN; ++j) {
         const int r = wn * TN + j * 32 + (lane & 31);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * HBK + swz(r, ch) * 8);
+        bfr[set][j] = *reinterpret_cast<const bf16x8*>(bs + r * HBK + swz(r, ch) * 8);
       }
+    };
+    frag(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < HBK / 16; ++ks) {
+      if (ks + 1 < HBK / 16) frag(ks + 1, (ks + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < RM; ++i)
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j],
+                                                              acc[i][j], 0, 0, 0);
     }
   };
 
@@ -205,18 +214,19 @@ int halo_rows_needed(const ConvGeom& g) {
   return ((g.W - 1 + HBM - 1) / g.W + 3) * g.W;
 }
 
-template <int BN, int HR>
+template <int BN, int HR, int WM, int WN>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, hipStream_t st) {
-  const size_t main = (size_t)(32 * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
+  constexpr int RPP = WM * WN * 8;
+  const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)HBM * (BN + 4) * 4;
   const size_t sm = main > epi ? main : epi;
   dim3 grid((unsigned)((g.M + HBM - 1) / HBM), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = conv_halo_kernel<BN, HR>;
+  auto k = conv_halo_kernel<BN, HR, WM, WN>;
   set_smem_attr(k, sm);
-  k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
 }
 }  // namespace
 
@@ -233,17 +243,24 @@ bool conv_halo_supported(const ConvGeom& g) {
 }
 
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int bn, hipStream_t st) {
+               const ConvGeom& g, int bn, int waves, hipStream_t st) {
   const int hp = halo_rows_needed(g);
-  const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-  if (bn == 128) {
-    if (hr == 6) launch_halo<128, 6>(X, Wp, Y, ADD, stats, g, st);
-    else if (hr == 8) launch_halo<128, 8>(X, Wp, Y, ADD, stats, g, st);
-    else launch_halo<128, 12>(X, Wp, Y, ADD, stats, g, st);
-  } else {
-    if (hr == 6) launch_halo<64, 6>(X, Wp, Y, ADD, stats, g, st);
-    else if (hr == 8) launch_halo<64, 8>(X, Wp, Y, ADD, stats, g, st);
-    else launch_halo<64, 12>(X, Wp, Y, ADD, stats, g, st);
+  if (waves == 8) {  // 4 x 2 waves of 32 x BN/2
+    const int hr = hp <= 192 ? 3 : hp <= 256 ? 4 : 6;
+#define DM_HALO8(BN_)                                                            \
+  if (hr == 3) launch_halo<BN_, 3, 4, 2>(X, Wp, Y, ADD, stats, g, st);           \
+  else if (hr == 4) launch_halo<BN_, 4, 4, 2>(X, Wp, Y, ADD, stats, g, st);      \
+  else launch_halo<BN_, 6, 4, 2>(X, Wp, Y, ADD, stats, g, st);
+    if (bn == 128) { DM_HALO8(128) } else { DM_HALO8(64) }
+#undef DM_HALO8
+  } else {  // 2 x 2 waves of 64 x BN/2
+    const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
+#define DM_HALO4(BN_)                                                            \
+  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, st);           \
+  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, st);      \
+  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, st);
+    if (bn == 128) { DM_HALO4(128) } else { DM_HALO4(64) }
+#undef DM_HALO4
   }
   DM_CHECK(hipGetLastError());
 }

@@ -322,12 +322,16 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
   const long long m0 = (long long)blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int ntaps = g.nth * g.ntw;
-  if (tid < ntaps) {
-    const int th = tid / g.ntw, tw = tid % g.ntw;
-    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
-    // .w = pixel offset of the tap (dy*W + dx)
-    taps[tid] = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C,
-                          dy * g.W + dx);
+  if (tid < MAXTAPS) {  // every entry written: the loader reads it without a branch
+    int4 e = make_int4(0, 0, 0, 0);
+    if (tid < ntaps) {
+      const int th = tid / g.ntw, tw = tid % g.ntw;
+      const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
+      // .w = pixel offset of the tap (dy*W + dx)
+      e = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C,
+                    dy * g.W + dx);
+    }
+    taps[tid] = e;
   }
   const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
   const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
@@ -367,8 +371,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     const int tap = kc >> g.lgC8;
     const unsigned c0b = (unsigned)((kc & ((1 << g.lgC8) - 1)) * 16);  // byte offset in pixel
     const bool kval = tap < ntaps;
-    int4 tp = make_int4(0, 0, 0, 0);
-    if (kval) tp = taps[tap];
+    const int4 tp = taps[tap < MAXTAPS ? tap : MAXTAPS - 1];
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const bool ok = kval && (unsigned)(a_y[i] + tp.x) < (unsigned)g.H &&
@@ -413,25 +416,33 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
       const bf16_t* as = As + buf * BM * BK;
       const bf16_t* bs = Bs + buf * BN * BK;
       if constexpr (MF32) {
-#pragma unroll
-        for (int ks = 0; ks < BK / 16; ++ks) {
+        // fragments double-buffered across the 4 k-substeps: the reads of substep ks+1
+        // are in flight while the MFMAs of substep ks issue
+        bf16x8 af[2][RM], bfr[2][RN];
+        auto frag = [&](int ks, int set) {
           const int ch = ks * 2 + (lane >> 5);
-          bf16x8 af[RM], bfr[RN];
 #pragma unroll
           for (int i = 0; i < RM; ++i) {
             const int r = wm * TM + i * 32 + (lane & 31);
-            af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
+            af[set][i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
           }
 #pragma unroll
           for (int j = 0; j < RN; ++j) {
             const int r = wn * TN + j * 32 + (lane & 31);
-            bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
+            bfr[set][j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
           }
+        };
+        frag(0, 0);
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+          if (ks + 1 < BK / 16) frag(ks + 1, (ks + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);  // keep those reads ahead of this substep's MFMAs
 #pragma unroll
           for (int i = 0; i < RM; ++i)
 #pragma unroll
             for (int j = 0; j < RN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j],
+                                                                  acc[i][j], 0, 0, 0);
         }
       } else {
 #pragma unroll
@@ -1072,16 +1083,22 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const ConvGeom& g, int cfg, hipStream_t st) {
   // v3 with two tiles of register prefetch: 15 = 128x128 mf32, 16 = 128x64 mf32, 17 = 64x64
   // 16x16; 18 = 8-wave 256x128 mf32 (measured slower: one workgroup per CU)
-  // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64; shapes it does not
-  // cover fall back to the v3 tiles 12 / 13
-  if (cfg == 20 || cfg == 21) {
-    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, cfg == 20 ? 128 : 64, st);
-    cfg = cfg == 20 ? 12 : 13;
+  // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64, 4 waves;
+  // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
+  if (cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25) {
+    const int bn = (cfg == 20 || cfg == 24) ? 128 : 64;
+    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, cfg >= 24 ? 8 : 4, st);
+    cfg = bn == 128 ? 12 : 13;
   }
   if (cfg == 15) return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
   if (cfg == 16) return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
   if (cfg == 17) return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st);
   if (cfg == 18) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  // 8-wave 128-row tiles (4 waves per SIMD at 2 workgroups per CU): 19 = 128x128 as 4x2
+  // waves of 32x64, 22 = 128x128 as 2x4 waves of 64x32, 23 = 128x64 as 4x2 waves of 32x32
+  if (cfg == 19) return launch_fwd3<128, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 22) return launch_fwd3<128, 128, 2, 4, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 23) return launch_fwd3<128, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
   // cfg % 3: 0 = 128x128 (2x2 waves, 64x64 per wave), 1 = 128x64, 2 = 64x64
   // cfg / 3: 0 = register-staged global loads, 1 = LDS-DMA (buffer_load ... lds),
   //          2 = register-staged buffer loads (branch-free zero fill)
@@ -1095,7 +1112,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return cfg >= 20 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -163,7 +163,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
         L.conv_fwd(x, wf, y, stats, None, k, k, s, p, cfg)
         mean = torch.empty(cout, **f32)
         invstd = torch.empty(cout, **f32)
-        work = torch.empty(64 * 2 * cout, **f32)
+        work = torch.empty(256 * 2 * cout, **f32)
         L.bn_stats_finalize(stats, T, float(M), layer.bn_weight.detach(), layer.bn_bias.detach(),
                             layer.running_mean, layer.running_var, layer.momentum, layer.eps,
                             scale, shift, mean, invstd, work)

@@ -29,7 +29,7 @@ HALO_GEOMS = [
     (3, 14, 256, 256, 3, 1, 1),
     (2, 14, 64, 128, 1, 1, 0),
 ]
-FWD_CFGS = list(range(19)) + [20, 21]
+FWD_CFGS = list(range(20)) + [20, 21, 22, 23, 24, 25]
 
 
 def _rel(a, b):
@@ -64,7 +64,7 @@ def test_conv_fwd_and_stats(dev, geom, cfg):
 
 
 @pytest.mark.parametrize("geom", HALO_GEOMS)
-@pytest.mark.parametrize("cfg", [12, 20, 21])
+@pytest.mark.parametrize("cfg", [12, 20, 21, 24, 25])
 def test_conv_fwd_halo(dev, geom, cfg):
     _check_fwd(dev, geom, cfg)
 
@@ -118,7 +118,7 @@ def test_conv_dgrad(dev, geom, accumulate, variant):
 
 @pytest.mark.parametrize("geom", HALO_GEOMS + GEOMS[:2] + GEOMS[3:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [20, 21])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25])
 def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
@@ -181,7 +181,7 @@ def test_bn_forward_backward(dev, C, M, relu, res):
     scale, shift, mean, invstd = (torch.empty(C, **f) for _ in range(4))
     rm, rv = torch.zeros(C, **f), torch.ones(C, **f)
     lib().bn_stats_finalize(stats, 1, float(M), gamma, beta, rm, rv, 0.1, 1e-5, scale, shift, mean,
-                            invstd, torch.empty(128 * C, **f))
+                            invstd, torch.empty(512 * C, **f))
     torch.testing.assert_close(rm, rm_ref, rtol=1e-4, atol=1e-4)
     torch.testing.assert_close(rv, rv_ref, rtol=1e-3, atol=1e-3)
     y4, out = y.view(1, 1, M, C), torch.empty(1, 1, M, C, device=dev, dtype=torch.bfloat16)
@@ -268,7 +268,7 @@ def test_fused_bn_relu_maxpool_and_gather_backward(dev):
     stats = torch.stack([yf.sum(0), (yf ** 2).sum(0)]).reshape(-1).contiguous()
     scale, shift, mean, invstd = (torch.empty(C, **f) for _ in range(4))
     lib().bn_stats_finalize(stats, 1, float(M), gamma, beta, None, None, 0.1, 1e-5, scale, shift,
-                            mean, invstd, torch.empty(128 * C, **f))
+                            mean, invstd, torch.empty(512 * C, **f))
     OH = (H + 2 - 3) // 2 + 1
     out = torch.empty(N, OH, OH, C, device=dev, dtype=torch.bfloat16)
     idx = torch.empty(N, OH, OH, C, device=dev, dtype=torch.uint8)
@@ -282,3 +282,23 @@ def test_fused_bn_relu_maxpool_and_gather_backward(dev):
     assert _rel(_nchw(dy), yr.grad) < 1e-2
     assert _rel(dg, g_.grad) < 1e-2
     assert _rel(db, b_.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T", [1, 100, 129, 6272])
+def test_bn_stats_finalize_slab_rows(dev, T):
+    """Σ over a [T][2][C] per-tile statistics slab (direct and two-level reductions)."""
+    C, M = 64, 1000.0
+    f = dict(device=dev, dtype=torch.float32)
+    g = torch.Generator(device=dev).manual_seed(3)
+    s = torch.rand(T, C, device=dev, generator=g) * 2.0
+    q = s * s + torch.rand(T, C, device=dev, generator=g)
+    stats = torch.stack([s, q], 1).contiguous()
+    gamma, beta = torch.rand(C, **f) + 0.5, torch.randn(C, **f)
+    scale, shift, mean, invstd = (torch.empty(C, **f) for _ in range(4))
+    lib().bn_stats_finalize(stats.view(-1), T, M, gamma, beta, None, None, 0.1, 1e-5, scale, shift,
+                            mean, invstd, torch.empty(512 * C, **f))
+    sd, qd = s.double().sum(0), q.double().sum(0)
+    mu = sd / M
+    var = (qd / M - mu * mu).clamp_min(0)
+    torch.testing.assert_close(mean.double(), mu, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-6)

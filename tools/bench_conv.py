@@ -27,6 +27,11 @@ SHAPES = [
     ("l4_3x3s2", 14, 256, 512, 3, 2, 1),
     ("l4_3x3", 7, 512, 512, 3, 1, 1),
 ]
+# plain GEMMs through the same kernels (1x1 conv, K = C): structure ceiling without im2col
+EXTRA = [
+    ("gemm_k2048_n256", 14, 2048, 256, 1, 1, 0),
+    ("gemm_k1024_n512", 7, 1024, 512, 1, 1, 0),
+]
 
 
 def timeit(fn, iters):
@@ -45,16 +50,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--cfgs", default="11,12,13,15,16,20,21")
+    ap.add_argument("--cfgs", default="12,15,16,19,22,23,20,21,24,25")
     ap.add_argument("--wcfgs", default="v1,v2")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default: ResNet-18)")
     a = ap.parse_args()
     L = lib()
     dev = torch.device("cuda")
     N = a.batch
     cfgs = [int(c) for c in a.cfgs.split(",")]
     out = []
-    for name, H, C, Co, k, s, p in SHAPES:
+    shapes = SHAPES + EXTRA if a.shapes else SHAPES
+    if a.shapes:
+        shapes = [sh for sh in shapes if sh[0] in a.shapes.split(",")]
+    for name, H, C, Co, k, s, p in shapes:
         OH = (H + 2 * p - k) // s + 1
         flops = 2.0 * N * OH * OH * Co * k * k * C
         x = torch.randn(N, H, H, C, device=dev).bfloat16()
@@ -67,7 +76,7 @@ def main():
         if "fwd" in a.passes:
             ref = None
             for cfg in cfgs:
-                if cfg in (0, 3, 6, 9, 12, 15, 18, 20) and Co % 128:
+                if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24) and Co % 128:
                     continue
                 M = N * OH * OH
                 T = L.conv_stats_rows(M, cfg)
@@ -81,7 +90,7 @@ def main():
         if "dgrad" in a.passes and name != "stem7x7":
             ref = None
             for cfg in cfgs:
-                if cfg in (0, 3, 6, 9, 12, 15, 18, 20) and C % 128:
+                if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24) and C % 128:
                     continue
                 t = timeit(lambda: L.conv_dgrad(dy, wd, dx, k, k, s, p, None, cfg), a.iters)
                 row[f"dgrad_c{cfg}_TF"] = round(flops / t / 1e12, 1)

@@ -7,12 +7,12 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 import torch  # noqa: E402
 
-from tools.bench_conv import SHAPES, timeit  # noqa: E402
+from tools.bench_conv import EXTRA, SHAPES, timeit  # noqa: E402
 
 
 def main():
     N = 256
-    for name, H, C, Co, k, s, p in SHAPES:
+    for name, H, C, Co, k, s, p in SHAPES + EXTRA:
         OH = (H + 2 * p - k) // s + 1
         M, K = N * OH * OH, k * k * C
         a = torch.randn(M, K, device="cuda").bfloat16()
