@@ -938,22 +938,43 @@ __global__ void __launch_bounds__(256, 2) igemm_wgrad2_kernel(
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            int S, int Cout, int C, int Cin,
                                                            int KH, int KW,
-                                                           float* __restrict__ dw, float beta) {
-  const long long total = (long long)Cout * Cin * KH * KW;
+                                                           float* __restrict__ dw, float beta,
+                                                           int lanes) {
+  // block = (256 / lanes) consecutive slab elements x `lanes` split lanes; lane l sums the
+  // slabs l, l + lanes, ... (8 loads in flight), lanes combine in fixed order.  Reads follow
+  // the slab layout [S][Cout][K] (coalesced); the OIHW write is a permutation.
+  __shared__ float red[256];
   const long long K = (long long)KH * KW * C;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
-    const int kw = o % KW;
-    long long t = o / KW;
-    const int kh = t % KH;
-    t /= KH;
-    const int ci = t % Cin;
-    const int co = t / Cin;
-    const long long src = (long long)co * K + (kh * KW + kw) * C + ci;
-    float s = 0.f;
-    for (int i = 0; i < S; ++i) s += slab[(long long)i * Cout * K + src];
-    dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + s;
+  const long long total = (long long)Cout * K;
+  const long long plane = total;
+  const int E = 256 / lanes;
+  const int el = threadIdx.x % E, ln = threadIdx.x / E;
+  const long long e = (long long)blockIdx.x * E + el;
+  float acc = 0.f;
+  if (e < total) {
+    const float* src = slab + e;
+    int i = ln;
+    for (; i + 7 * lanes < S; i += 8 * lanes) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[(long long)(i + j * lanes) * plane];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; i < S; i += lanes) acc += src[(long long)i * plane];
   }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (ln != 0 || e >= total) return;
+  float sum = 0.f;
+  for (int l = 0; l < lanes; ++l) sum += red[l * E + el];
+  const int co = (int)(e / K);
+  const int k = (int)(e - (long long)co * K);
+  const int tap = k / C, ci = k - tap * C;
+  if (ci >= Cin) return;  // channel padding of the packed input
+  const int kh = tap / KW, kw = tap - kh * KW;
+  const long long o = (((long long)co * Cin + ci) * KH + kh) * KW + kw;
+  dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + sum;
 }
 
 // ------------------------------------------------------------------ weight packing
@@ -1122,6 +1143,12 @@ void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom&
                  long long mchunk, int cfg, hipStream_t st) {
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
+  // 4 / 5: halo-staged 3x3 unit-stride kernel (wgrad_halo.hip) with 9 / 3 taps per block;
+  // other shapes fall back to the v2 tiles
+  if (cfg == 4 || cfg == 5) {
+    if (wgrad_halo_supported(g)) return wgrad_halo(X, DY, slab, g, S, mchunk, cfg == 4 ? 3 : 1, st);
+    cfg = g.Ncols % 128 == 0 ? 2 : 3;
+  }
   if (cfg == 0) {
     dim3 grid((g.Ncols + 127) / 128, (g.K + 127) / 128, S);
     igemm_wgrad_kernel<128, 128, 2, 2><<<grid, 256, wgrad_smem(128, 128), st>>>(X, DY, slab, g, mchunk);
@@ -1145,8 +1172,12 @@ void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom&
 
 void wgrad_reduce(const float* slab, int S, int Cout, int C, int Cin, int KH, int KW, float* dw,
                   float beta, hipStream_t st) {
-  const long long total = (long long)Cout * Cin * KH * KW;
-  wgrad_reduce_kernel<<<grid_for(total, 256), 256, 0, st>>>(slab, S, Cout, C, Cin, KH, KW, dw, beta);
+  const long long total = (long long)Cout * KH * KW * C;
+  int lanes = 1;  // split the S-sum over lanes so small gradients with many slabs stay parallel
+  while (lanes < 16 && lanes * 8 < S) lanes *= 2;
+  const int E = 256 / lanes;
+  wgrad_reduce_kernel<<<(unsigned)((total + E - 1) / E), 256, 0, st>>>(slab, S, Cout, C, Cin, KH,
+                                                                      KW, dw, beta, lanes);
 }
 
 void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int Cpad, int KH,

@@ -54,6 +54,9 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
 bool conv_halo_supported(const ConvGeom& g);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st);
+bool wgrad_halo_supported(const ConvGeom& g);
+void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                long long mchunk, int nty, hipStream_t st);
 int igemm_fwd_rowtile(int cfg);
 void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                  long long mchunk, int cfg, hipStream_t st);

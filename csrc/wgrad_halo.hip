@@ -1,0 +1,221 @@
+// Halo-staged weight gradient for 3x3 / unit-stride / pad-1 convolutions, gfx950.
+//
+//   dW[co, tap, c] = Σ_m dY[m, co] · X[m + dy_t*W + dx_t, c]        (m = flattened n, y, x)
+//
+// The igemm wgrad kernel (conv_igemm.hip) stages one (tap, channel) column block of the
+// implicit im2col matrix per K-tile, so each block re-fetches the same input pixels once
+// per tap and re-stages the dY tile for every K-tile — measured 250-470 TFLOP/s.
+//
+// Here a block owns 64 output channels x ALL 9 taps x 64 input channels (a 64 x 576
+// gradient tile) and walks a slice of m in steps of 64 pixels.  Per step it stages
+//   * the dY tile   [64 m][64 co]                      (8 KB), and
+//   * the input halo [64 + 2W + 2 pixels][64 c]        (the pixels every tap of the 64
+//     rows touches: m0 - W - 1 ... m0 + 64 + W, contiguous in the flattened NHWC layout)
+// once, and the 9 taps read their B fragments straight out of the halo at row offset
+// dy*W + dx.  One dY fragment feeds 9 MFMAs; per step the block issues 2 x 4 x 9 x 4
+// v_mfma_f32_16x16x32_bf16 against ~31 KB of staging (vs 2.1 MFLOP per 24 KB before).
+// A tap whose source pixel leaves the image (x+dx or y+dy out of range) reads an all-zero
+// LDS row instead — exactly the conv's zero padding, also across the row / image
+// boundaries of the flattened layout.  Rows past the block's m-slice have zero dY.
+//
+// Both operands are m-major in memory and in LDS, so fragments come from the CDNA4
+// transpose read ds_read_b64_tr_b16 (row pitch 80 elements: conflict-free, see
+// docs/KERNELS.md).  Waves split the 64 input channels (16 each) and share the dY
+// fragments.  The m reduction is split over blocks into fp32 slabs [S][Cout][9*C] reduced
+// by wgrad_reduce (fixed order, deterministic).
+#include "common.h"
+#include "conv_geom.h"
+#include "igemm_common.h"
+#include "kernels.h"
+
+namespace dm {
+
+namespace {
+constexpr int WBM = 64;    // output channels per block
+constexpr int WBC = 64;    // input channels per block
+constexpr int WBK = 64;    // m rows per step
+constexpr int WPITCH = 80; // LDS row pitch (elements) for the transpose reads
+constexpr unsigned WOOB = 0x80000000u;
+
+typedef short s4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s4 tr_read(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)p);
+}
+
+// NTY = kernel rows (dy values) per block: 3 = all 9 taps share the dY fragments; 1 = one
+// row of 3 taps (smaller halo, 3x more output tiles -> 3x fewer m-splits and slab bytes)
+template <int HRN, int NTY>
+__global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
+    ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes) {
+  constexpr int HROWS_MAX = HRN * 32;  // halo rows a buffer holds (8 chunks per row)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][64][WPITCH] dY
+  bf16_t* Hs = As + 2 * WBK * WPITCH;                       // [2][HROWS_MAX][WPITCH] input
+  bf16_t* Zr = Hs + 2 * HROWS_MAX * WPITCH;                 // one zero row
+
+  constexpr int NT = 3 * NTY;  // taps per block
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int co0 = blockIdx.x * WBM;
+  const int cc0 = (blockIdx.y / (3 / NTY)) * WBC;
+  const int dy_lo = -1 + (int)(blockIdx.y % (3 / NTY)) * NTY;  // first kernel row of the block
+  const long long mb = (long long)blockIdx.z * mchunk;
+  const long long me = min(g.M, mb + mchunk);
+  const int W = g.W, H = g.H;
+  const int hrows = WBK + 2 + (NTY - 1) * W;  // pixels m0 + dy_lo*W - 1 ... m0 + (dy_hi)*W + 64
+  const int NHW = g.N * H * W;
+  if (tid < WPITCH / 8) *reinterpret_cast<uint4*>(Zr + tid * 8) = make_uint4(0, 0, 0, 0);
+
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsd = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, (int)dybytes, 0x00020000);
+  const int chunk = tid & 7, row0 = tid >> 3;  // staging: 32 rows x 8 chunks per pass
+
+  uint4 ra[2], rh[HRN];
+  auto load = [&](long long m0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long m = m0 + row0 + 32 * i;
+      const unsigned off = m < me ? (unsigned)((m * g.Ncols + co0 + chunk * 8) * 2) : WOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsd, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    const long long hb = m0 + dy_lo * W - 1;
+#pragma unroll
+    for (int j = 0; j < HRN; ++j) {
+      const int h = row0 + 32 * j;
+      const long long p = hb + h;
+      const bool ok = h < hrows && p >= 0 && p < NHW;
+      const unsigned off = ok ? (unsigned)((p * g.C + cc0 + chunk * 8) * 2) : WOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store = [&](int buf) {
+    bf16_t* as = As + buf * WBK * WPITCH;
+    bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
+#pragma unroll
+    for (int j = 0; j < HRN; ++j)
+      *reinterpret_cast<uint4*>(hs + (row0 + 32 * j) * WPITCH + chunk * 8) = rh[j];
+  };
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // transpose-read lane roles (as igemm_wgrad2): row grp*4+q (+16), column 4p
+  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int rbase = grp * 4 + q;
+  const int nsteps = me > mb ? (int)((me - mb + WBK - 1) / WBK) : 0;
+  if (nsteps > 0) {
+    load(mb);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    const long long m0 = mb + (long long)s * WBK;
+    if (s + 1 < nsteps) load(m0 + WBK);
+    const bf16_t* as = As + buf * WBK * WPITCH;
+    const bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // pixel coordinates of this lane's two rows (lo: r, hi: r + 16)
+      int xr[2], yr[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const unsigned m = (unsigned)(m0 + ks * 32 + rbase + 16 * u);
+        const unsigned t = fdiv(m, g.wg_mul, g.wg_shr);
+        xr[u] = (int)(m - t * (unsigned)W);
+        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+        yr[u] = (int)(t - n * (unsigned)H);
+      }
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = i * 16 + 4 * p;
+        const s4 lo = tr_read(as + (ks * 32 + rbase) * WPITCH + col);
+        const s4 hi = tr_read(as + (ks * 32 + rbase + 16) * WPITCH + col);
+        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int bcol = wid * 16 + 4 * p;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int dyl = t / 3, dx = t % 3 - 1;  // kernel row relative to dy_lo
+        const int dy = dy_lo + dyl;
+        const bf16_t* src[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bool ok = (unsigned)(xr[u] + dx) < (unsigned)W && (unsigned)(yr[u] + dy) < (unsigned)H;
+          const int h = ks * 32 + rbase + 16 * u + 1 + dyl * W + dx;
+          src[u] = ok ? hs + h * WPITCH + bcol : Zr + 4 * p;
+        }
+        const s4 lo = tr_read(src[0]);
+        const s4 hi = tr_read(src[1]);
+        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][t], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+  // slab[z][co][tap*C + c]; 16x16 C map: col = lane & 15 (channel), row = (lane>>4)*4 + r (co)
+  float* out = slab + (long long)blockIdx.z * g.Ncols * g.K;
+  const int c = cc0 + wid * 16 + (lane & 15);
+  const int t0 = (dy_lo + 1) * 3;  // global tap index of the block's first tap
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + i * 16 + (lane >> 4) * 4 + r;
+        if (co < g.Ncols) out[(long long)co * g.K + (t0 + t) * g.C + c] = acc[i][t][r];
+      }
+}
+
+template <int HRN, int NTY>
+void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                       long long mchunk, hipStream_t st) {
+  const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
+  dim3 grid((g.Ncols + WBM - 1) / WBM, (g.C / WBC) * (3 / NTY), S);
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned db = (unsigned)(g.M * g.Ncols * 2);
+  auto k = wgrad_halo_kernel<HRN, NTY>;
+  set_smem_attr(k, sm);
+  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db);
+}
+}  // namespace
+
+bool wgrad_halo_supported(const ConvGeom& g) {
+  // 3x3, unit stride, pad 1, tap order (kh, kw) row-major with dy = kh - 1, dx = kw - 1
+  if (g.isy != 1 || g.isx != 1 || g.Hg != g.H || g.Wg != g.W) return false;
+  if (g.nth != 3 || g.ntw != 3 || g.dy0 != -1 || g.dys != 1 || g.dx0 != -1 || g.dxs != 1) return false;
+  if (g.kh0 != 0 || g.khs != 1 || g.kw0 != 0 || g.kws != 1 || g.KW != 3) return false;
+  if (g.C % WBC != 0 || g.Ncols % 8 != 0 || g.K != 9 * g.C) return false;
+  if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31) || g.M * g.Ncols * 2 >= (1LL << 31))
+    return false;
+  return WBK + 2 * g.W + 2 <= 6 * 32;
+}
+
+void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                long long mchunk, int nty, hipStream_t st) {
+  if (nty == 1) {
+    launch_wgrad_halo<3, 1>(X, DY, slab, g, S, mchunk, st);  // 66 rows
+  } else {
+    const int rows = WBK + 2 * g.W + 2;
+    if (rows <= 96) launch_wgrad_halo<3, 3>(X, DY, slab, g, S, mchunk, st);
+    else if (rows <= 128) launch_wgrad_halo<4, 3>(X, DY, slab, g, S, mchunk, st);
+    else launch_wgrad_halo<6, 3>(X, DY, slab, g, S, mchunk, st);
+  }
+  DM_CHECK(hipGetLastError());
+}
+
+}  // namespace dm

@@ -58,15 +58,30 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     return TILE_CFG[t]
 
 
-def _wgrad_plan(M, cout, K):
-    # cfg 2/3: v2 weight-gradient kernel (64 rows per barrier, buffer loads), tile
-    # 128x128 / 64x128; cfg 0/1 are the v1 kernels kept for A/B measurements.
-    cfg = 2 if cout % 128 == 0 else 3
-    bm = 128 if cfg == 2 else 64
-    tiles = math.ceil(cout / bm) * math.ceil(K / 128)
-    max_split = max(1, M // 2048)  # >= 64 K-steps of 32 rows per split
-    # ~2 blocks per CU: enough to fill 256 CUs while keeping the fp32 slab traffic
-    # of the fixed-order reduce small (S * Cout * K * 4 bytes)
+def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
+    """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
+
+    cfg 4/5: halo-staged 3x3 unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per
+    block; cfg 2/3: v2 igemm tiles 128x128 / 64x128 (cfg 0/1: v1, kept for A/B).
+    S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
+    ~2 blocks per CU, each split >= 8 row steps, slab bytes S*cout*K*4."""
+    halo = k == 3 and stride == 1 and cin % 64 == 0 and cout % 8 == 0
+    if force is not None:
+        cfg = force
+    elif halo:
+        # 9 taps per block share every dY fragment, but a layer with few (cout, cin)
+        # tiles then needs many m-splits (slab traffic ~ S * cout * K); 3 taps per block
+        # triples the tiles
+        cfg = 4 if math.ceil(cout / 64) * (cin // 64) >= 4 else 5
+    else:
+        cfg = 2 if cout % 128 == 0 else 3
+    if cfg in (4, 5):
+        tiles = max(1, math.ceil(cout / 64) * (cin // 64) * (1 if cfg == 4 else 3))
+        max_split = max(1, M // 512)
+    else:
+        bm = 128 if cfg in (0, 2) else 64
+        tiles = math.ceil(cout / bm) * math.ceil(K / 128)
+        max_split = max(1, M // 2048)  # >= 64 K-steps of 32 rows per split
     S = max(1, min(max_split, math.ceil(512 / tiles)))
     return cfg, S
 
@@ -228,7 +243,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     # weight gradient
     C = x.shape[3]
     K = k * k * C
-    wcfg, S = _wgrad_plan(M, cout, K)
+    wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
     slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
     L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg, s2d)
     dx = None

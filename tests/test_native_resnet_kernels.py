@@ -156,6 +156,22 @@ def test_conv_wgrad(dev, geom):
     assert M > 0
 
 
+@pytest.mark.parametrize("geom", [g for g in HALO_GEOMS if g[4] == 3])
+@pytest.mark.parametrize("cfg", [4, 5])
+@pytest.mark.parametrize("S", [1, 3])
+def test_conv_wgrad_halo(dev, geom, cfg, S):
+    """Halo-staged 3x3 weight gradient (9 / 3 taps per block), split-m slabs."""
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, p)
+    K = k * k * Cin
+    slab = torch.empty(S * Cout * K, device=dev)
+    d = torch.empty_like(w)
+    lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, 0.0, S, cfg, False)
+    assert _rel(d, ref) < 2e-3
+
+
 @pytest.mark.parametrize("C,M", [(64, 4096), (512, 98), (128, 1000)])
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
 def test_bn_forward_backward(dev, C, M, relu, res):

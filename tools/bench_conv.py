@@ -103,20 +103,24 @@ def main():
 
             M = N * OH * OH
             K = k * k * C
-            wcfg, S = _wgrad_plan(M, Co, K)
-            wcfg = (wcfg - 2) % 2
-            slab = torch.empty(S * Co * K, device=dev)
             dw = torch.empty(Co, C, k, k, device=dev)
             ref = None
             for v in a.wcfgs.split(","):
-                c = wcfg + (2 if v == "v2" else 0)
+                force = {"v1": None, "v2": None, "h9": 4, "h3": 5}[v]
+                if force is None:
+                    c, S = _wgrad_plan(M, Co, K)
+                    if v == "v1":
+                        c = (c - 2) % 2
+                else:
+                    c, S = _wgrad_plan(M, Co, K, k, s, C, force=force)
+                slab = torch.empty(S * Co * K, device=dev)
                 t = timeit(lambda: L.conv_wgrad(x, dy, dw, slab, C, k, k, s, p, 0.0, S, c, False), a.iters)
                 row[f"wgrad_{v}_TF"] = round(flops / t / 1e12, 1)
+                row[f"wgrad_{v}_S"] = S
                 if ref is None:
                     ref = dw.clone()
                 else:
                     row[f"wgrad_{v}_reldiff"] = float((dw - ref).norm() / ref.norm())
-            row["wgrad_S"] = S
         out.append(row)
         print(json.dumps(row), flush=True)
 

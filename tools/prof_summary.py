@@ -10,7 +10,7 @@ fam = defaultdict(float)
 tot = 0.0
 for r in rows:
     n = r["Name"]
-    key = re.sub(r"\(.*", "", n)
+    key = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", ""))
     key = re.sub(r"<.*>", lambda m: m.group(0)[:40], key)
     t = float(r["TotalDurationNs"]) / 1e6 / steps
     fam[key] += t
