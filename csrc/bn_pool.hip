@@ -144,7 +144,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
     for (int u = 0; u < U; ++u) {
       const long long i = i0 + u * stride;
       if (i >= n8) continue;
-      const int c0 = (int)(i % C8) * 8;
+      const int c0 = (int)((unsigned long long)i & (unsigned)(C8 - 1)) * 8;  // C8 | 256: power of 2
       float f[8], r[8];
       unpack8(yr[u], f);
       if (RES) unpack8(rr[u], r);
@@ -183,26 +183,52 @@ struct BnBwdArgs {
 };
 
 // mode 3: dz of one 8-channel chunk of input pixel r, gathered from the pool windows
+// that contain it.  For K <= 2S a pixel lies in at most 2 x 2 windows: all candidate
+// (codes, grads) are loaded up front — 8 independent loads instead of a chain of
+// dependent ones — then matched against the pixel's position in each window.
 __device__ __forceinline__ void gather_pool_dz(const BnBwdArgs& a, long long r, int chunk, int C8,
                                                float d[8]) {
-  const int iw = r % a.W;
-  const long long t = r / a.W;
-  const int ih = t % a.H;
-  const int n = t / a.H;
+  const unsigned ru = (unsigned)r;  // pixel counts < 2^31: 32-bit divisions
+  const unsigned tq = ru / (unsigned)a.W;
+  const int iw = (int)(ru - tq * (unsigned)a.W);
+  const int n = (int)(tq / (unsigned)a.H);
+  const int ih = (int)(tq - (unsigned)n * (unsigned)a.H);
 #pragma unroll
   for (int j = 0; j < 8; ++j) d[j] = 0.f;
   const int oh_lo = max(0, (ih + a.P - a.K + a.S) / a.S), oh_hi = min(a.OH - 1, (ih + a.P) / a.S);
   const int ow_lo = max(0, (iw + a.P - a.K + a.S) / a.S), ow_hi = min(a.OW - 1, (iw + a.P) / a.S);
+  if (a.K <= 2 * a.S) {
+    uint2 ix[4];
+    uint4 gv[4];
+    bool ok[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int oh = oh_lo + (w >> 1), ow = ow_lo + (w & 1);
+      ok[w] = oh <= oh_hi && ow <= ow_hi;
+      const long long o = (((long long)n * a.OH + min(oh, oh_hi)) * a.OW + min(ow, ow_hi)) * C8 + chunk;
+      ix[w] = reinterpret_cast<const uint2*>(a.pidx)[o];
+      gv[w] = reinterpret_cast<const uint4*>(a.pdy)[o];
+    }
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (!ok[w]) continue;
+      const int oh = oh_lo + (w >> 1), ow = ow_lo + (w & 1);
+      const unsigned code = (ih - (oh * a.S - a.P)) * a.K + (iw - (ow * a.S - a.P));
+      const uint32_t aw[2] = {ix[w].x, ix[w].y};
+      float g[8];
+      unpack8(gv[w], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += g[j];
+    }
+    return;
+  }
   for (int oh = oh_lo; oh <= oh_hi; ++oh)
     for (int ow = ow_lo; ow <= ow_hi; ++ow) {
       const unsigned code = (ih - (oh * a.S - a.P)) * a.K + (iw - (ow * a.S - a.P));
       const long long o = (((long long)n * a.OH + oh) * a.OW + ow) * C8 + chunk;
       const uint2 ix = reinterpret_cast<const uint2*>(a.pidx)[o];
       const uint32_t aw[2] = {ix.x, ix.y};
-      bool any = false;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) any |= ((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code;
-      if (!any) continue;
       float g[8];
       unpack8(reinterpret_cast<const uint4*>(a.pdy)[o], g);
 #pragma unroll
@@ -234,7 +260,7 @@ struct BnBwdBatch {
                                      const float* sc, const float* sh, float d[8],
                                      float yv[8]) const {
     unpack8(y[u], yv);
-    if (MODE == 3) gather_pool_dz(a, i / C8, chunk, C8, d);
+    if (MODE == 3) gather_pool_dz(a, (long long)((unsigned long long)i >> (31 - __builtin_clz(C8))), chunk, C8, d);
     else unpack8(dout[u], d);
     if (MODE == 1) {
       float o[8];
@@ -356,7 +382,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
     for (int u = 0; u < U; ++u) {
       if (!bt.ok[u]) continue;
       const long long i = i0 + u * stride;
-      const int chunk = (int)(i % C8);
+      const int chunk = (int)((unsigned long long)i & (unsigned)(C8 - 1));
       const int c0 = chunk * 8;
       float d[8], yv[8];
       bt.dz(a, u, i, chunk, C8, sc, sh, d, yv);
@@ -386,12 +412,13 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
   const long long total = (long long)N * OH * OW * C8;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c8 = i % C8;
-    long long t = i / C8;
-    const int ow = t % OW;
-    t /= OW;
-    const int oh = t % OH;
-    const int n = t / OH;
+    const unsigned iu = (unsigned)i;  // element counts < 2^31: 32-bit index math
+    const int c8 = (int)(iu % (unsigned)C8);
+    unsigned t = iu / (unsigned)C8;
+    const int ow = (int)(t % (unsigned)OW);
+    t /= (unsigned)OW;
+    const int oh = (int)(t % (unsigned)OH);
+    const int n = (int)(t / (unsigned)OH);
     const int c0 = c8 * 8;
     float best[8];
     int arg[8];
@@ -431,12 +458,13 @@ __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restri
   const long long total = (long long)N * OH * OW * C8;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c8 = i % C8;
-    long long t = i / C8;
-    const int ow = t % OW;
-    t /= OW;
-    const int oh = t % OH;
-    const int n = t / OH;
+    const unsigned iu = (unsigned)i;  // element counts < 2^31: 32-bit index math
+    const int c8 = (int)(iu % (unsigned)C8);
+    unsigned t = iu / (unsigned)C8;
+    const int ow = (int)(t % (unsigned)OW);
+    t /= (unsigned)OW;
+    const int oh = (int)(t % (unsigned)OH);
+    const int n = (int)(t / (unsigned)OH);
     float best[8];
     int arg[8];
 #pragma unroll
@@ -472,12 +500,13 @@ __global__ void __launch_bounds__(256) maxpool_bwd_kernel(const bf16_t* __restri
   const long long total = (long long)N * H * W * C8;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-    const int c8 = i % C8;
-    long long t = i / C8;
-    const int iw = t % W;
-    t /= W;
-    const int ih = t % H;
-    const int n = t / H;
+    const unsigned iu = (unsigned)i;
+    const int c8 = (int)(iu % (unsigned)C8);
+    unsigned t = iu / (unsigned)C8;
+    const int iw = (int)(t % (unsigned)W);
+    t /= (unsigned)W;
+    const int ih = (int)(t % (unsigned)H);
+    const int n = (int)(t / (unsigned)H);
     float g[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // output windows covering ih: oh in [ceil((ih+P-K+1)/S), floor((ih+P)/S)]
     const int oh_lo = max(0, (ih + P - K + S) / S), oh_hi = min(OH - 1, (ih + P) / S);
