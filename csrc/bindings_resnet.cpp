@@ -214,15 +214,22 @@ void pack_weights(at::Tensor w, at::Tensor wf, c10::optional<at::Tensor> wd, int
 void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gamma, at::Tensor beta,
                        c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
                        double momentum, double eps, at::Tensor scale, at::Tensor shift,
-                       at::Tensor mean, at::Tensor invstd, at::Tensor work) {
+                       at::Tensor mean, at::Tensor invstd, at::Tensor work,
+                       c10::optional<at::Tensor> num_batches) {
   const int C = gamma.numel();
   need_f32(stats, "stats", T * 2 * C);
+  long long* nb = nullptr;  // BatchNorm num_batches_tracked, incremented in the finalize kernel
+  if (num_batches.has_value()) {
+    TORCH_CHECK(num_batches->scalar_type() == at::kLong && num_batches->numel() == 1 &&
+                num_batches->device() == stats.device(), "num_batches: int64 scalar on the device");
+    nb = (long long*)num_batches->data_ptr();
+  }
   need_f32(work, "work", 256 * 2 * C);
   for (auto* t : {&gamma, &beta, &scale, &shift, &mean, &invstd}) need_f32(*t, "bn vec", C);
   const DeviceGuard guard(stats.device());
   dm::bn_stats_finalize(fp(stats), T, C, count, fp(gamma), fp(beta),
                         rmean.has_value() ? fp(*rmean) : nullptr, rvar.has_value() ? fp(*rvar) : nullptr,
-                        momentum, eps, fp(scale), fp(shift), fp(mean), fp(invstd), fp(work),
+                        momentum, eps, fp(scale), fp(shift), fp(mean), fp(invstd), fp(work), nb,
                         cur_stream());
 }
 
@@ -376,7 +383,10 @@ void register_resnet(pybind11::module_& m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("pack_weights", &pack_weights);
-  m.def("bn_stats_finalize", &bn_stats_finalize);
+  m.def("bn_stats_finalize", &bn_stats_finalize, py::arg("stats"), py::arg("T"), py::arg("count"),
+        py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
+        py::arg("eps"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),
+        py::arg("work"), py::arg("num_batches") = py::none());
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_work", &bn_bwd_work);

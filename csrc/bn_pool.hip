@@ -82,8 +82,9 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift,
-    float* __restrict__ mean_out, float* __restrict__ invstd_out) {
+    float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (num_batches && blockIdx.x == 0 && threadIdx.x == 0) *num_batches += 1;
   double s, q;
   block_sum2(part, G, C, c, s, q);
   if (threadIdx.x >= 64 || c >= C) return;
@@ -661,7 +662,7 @@ void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, i
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
                        float* scale, float* shift, float* mean, float* invstd, float* work,
-                       hipStream_t st) {
+                       long long* num_batches, hipStream_t st) {
   const int W = 2 * C;
   const int G = colsum_groups(T);
   const float* fin = stats;
@@ -671,7 +672,7 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
   }
   bn_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(fin, G ? G : T, C, count, gamma, beta, rmean,
                                                        rvar, momentum, eps, scale, shift, mean,
-                                                       invstd);
+                                                       invstd, num_batches);
 }
 
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,

@@ -67,7 +67,7 @@ void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int
 // bn_pool.hip
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
-                       float* scale, float* shift, float* mean, float* invstd, float* work,
+                       float* scale, float* shift, float* mean, float* invstd, float* work, long long* num_batches,
                        hipStream_t st);
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                     float eps, int C, float* scale, float* shift, hipStream_t st);

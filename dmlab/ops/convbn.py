@@ -181,8 +181,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
         work = torch.empty(256 * 2 * cout, **f32)
         L.bn_stats_finalize(stats, T, float(M), layer.bn_weight.detach(), layer.bn_bias.detach(),
                             layer.running_mean, layer.running_var, layer.momentum, layer.eps,
-                            scale, shift, mean, invstd, work)
-        layer.num_batches_tracked.add_(1)
+                            scale, shift, mean, invstd, work, layer.num_batches_tracked)
     else:
         L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg)
         L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
