@@ -211,6 +211,17 @@ void pack_weights(at::Tensor w, at::Tensor wf, c10::optional<at::Tensor> wd, int
 }
 
 // ------------------------------------------------------------------ BN
+// every conv layer's weight packing in one launch (see pack_weights_multi_kernel)
+void pack_weights_multi(at::Tensor desc, at::Tensor prefix, int64_t total) {
+  TORCH_CHECK(desc.is_cuda() && prefix.is_cuda() && desc.scalar_type() == at::kLong &&
+              prefix.scalar_type() == at::kLong, "desc/prefix: int64 device tensors");
+  const int nl = prefix.numel() - 1;
+  TORCH_CHECK(nl >= 1 && nl <= 32 && desc.numel() == 8 * nl, "pack_weights_multi: 1..32 layers");
+  const DeviceGuard guard(desc.device());
+  dm::pack_weights_multi((const long long*)desc.data_ptr(), (const long long*)prefix.data_ptr(), nl,
+                         total, cur_stream());
+}
+
 void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gamma, at::Tensor beta,
                        c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
                        double momentum, double eps, at::Tensor scale, at::Tensor shift,
@@ -383,6 +394,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("conv_dgrad", &conv_dgrad);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("pack_weights", &pack_weights);
+  m.def("pack_weights_multi", &pack_weights_multi);
   m.def("bn_stats_finalize", &bn_stats_finalize, py::arg("stats"), py::arg("T"), py::arg("count"),
         py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),

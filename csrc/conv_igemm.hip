@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
   }
   __syncthreads();
-  uint4 ra[DEPTH][AR], rb[DEPTH][BR];
+  uint4 ra[DEPTH > 1 ? DEPTH : 1][AR], rb[DEPTH > 1 ? DEPTH : 1][BR];
   const int nk = (g.K + BK - 1) / BK;
   const unsigned C2 = (unsigned)g.C * 2u;
 
@@ -399,6 +399,69 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     for (int i = 0; i < BR; ++i) {
       const int r = (tid >> 3) + RPP * i;
       *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[S][i];
+    }
+  };
+
+  // DEPTH == 0: LDS-DMA loader (buffer_load ... lds): no VGPR staging and no ds_write.
+  // Wave-instruction i of wave wid fills rows (i*NW + wid)*8 + lane/8, physical 16-B slot
+  // lane%8 (the LDS destination is lane-linear), so the swizzle is applied to the SOURCE:
+  // the lane fetches logical chunk slot ^ ((row >> 1) & 7).
+  constexpr int NW = WM * WN;
+  constexpr int DAR = DEPTH == 0 ? BM / (NW * 8) : 1, DBR = DEPTH == 0 ? BN / (NW * 8) : 1;
+  int d_y[DAR], d_x[DAR], d_lc[DAR], db_lc[DBR];
+  unsigned d_pix[DAR], db_off[DBR];
+  if constexpr (DEPTH == 0) {
+#pragma unroll
+    for (int i = 0; i < DAR; ++i) {
+      const int r = (i * NW + wid) * 8 + (lane >> 3);
+      d_lc[i] = (lane & 7) ^ ((r >> 1) & 7);
+      const long long m = m0 + r;
+      if (m < g.M) {
+        const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+        const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
+        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+        const int y = (int)(t - n * (unsigned)g.Hg);
+        d_y[i] = y * g.isy;
+        d_x[i] = x * g.isx;
+        d_pix[i] = (n * (unsigned)g.H + (unsigned)d_y[i]) * (unsigned)g.W + (unsigned)d_x[i];
+      } else {
+        d_y[i] = -(1 << 28);
+        d_x[i] = 0;
+        d_pix[i] = 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < DBR; ++i) {
+      const int r = (i * NW + wid) * 8 + (lane >> 3);
+      db_lc[i] = (lane & 7) ^ ((r >> 1) & 7);
+      const int n = n0 + r;
+      db_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
+    }
+  }
+  auto issue = [&](int kt, int buf) {
+    bf16_t* as = As + buf * BM * BK;
+    bf16_t* bs = Bs + buf * BN * BK;
+    const int cmask = (1 << g.lgC8) - 1;
+#pragma unroll
+    for (int i = 0; i < DAR; ++i) {
+      const int kc = kt * (BK / 8) + d_lc[i];
+      const int tap = kc >> g.lgC8;
+      const int4 tp = taps[tap < MAXTAPS ? tap : MAXTAPS - 1];
+      const bool ok = tap < ntaps && (unsigned)(d_y[i] + tp.x) < (unsigned)g.H &&
+                      (unsigned)(d_x[i] + tp.y) < (unsigned)g.W;
+      const unsigned off = ok ? (d_pix[i] + (unsigned)tp.w) * C2 + (unsigned)((kc & cmask) * 16) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsx, (__attribute__((address_space(3))) void*)(as + (i * NW + wid) * 8 * BK), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < DBR; ++i) {
+      const int kc = kt * (BK / 8) + db_lc[i];
+      const int tap = kc >> g.lgC8;
+      const int4 tp = taps[tap < MAXTAPS ? tap : MAXTAPS - 1];
+      const unsigned off = (tap < ntaps && db_off[i] != OOB)
+                               ? db_off[i] + (unsigned)tp.z * 2u + (unsigned)((kc & cmask) * 16) : OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsw, (__attribute__((address_space(3))) void*)(bs + (i * NW + wid) * 8 * BK), 16, off, 0, 0, 0);
     }
   };
 
@@ -467,16 +530,30 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
         }
       }
   };
-  if constexpr (DEPTH == 1) {
+  if constexpr (DEPTH == 0) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
+      compute(buf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if constexpr (DEPTH <= 1) {
+    // DEPTH < 0: measurement-only ablations (wrong results): bit 0 drops the in-loop global
+    // loads, bit 1 the LDS stores, bit 2 the barrier (tools/bench_conv.py --cfgs 30..33)
+    constexpr int ABL = DEPTH < 0 ? -DEPTH : 0;
     load(0, S0{});
     store(0, S0{});
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nk) load(kt + 1, S0{});
+      if (!(ABL & 1) && kt + 1 < nk) load(kt + 1, S0{});
       compute(buf);
-      if (kt + 1 < nk) store(buf ^ 1, S0{});
-      __syncthreads();
+      if (!(ABL & 2) && kt + 1 < nk) store(buf ^ 1, S0{});
+      if (!(ABL & 4)) __syncthreads();
     }
   } else {
     // tile t is staged through register set t & 1, issued two tiles ahead of its use
@@ -1037,6 +1114,43 @@ __global__ void __launch_bounds__(256) pack_weights_any_kernel(const float* __re
   }
 }
 
+// All conv layers of a model in one launch: desc[l] = {w, wf, wd, Cout, Cin, Cpad, KH, KW}
+// (pointers as int64), prefix[l] = first packed element of layer l (prefix[nl] = total).
+__global__ void __launch_bounds__(256) pack_weights_multi_kernel(const long long* __restrict__ desc,
+                                                                 const long long* __restrict__ prefix,
+                                                                 int nl) {
+  __shared__ long long pre[33];
+  for (int i = threadIdx.x; i <= nl; i += blockDim.x) pre[i] = prefix[i];
+  __syncthreads();
+  const long long total = pre[nl];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    int l = 0;
+    while (l + 1 < nl && o >= pre[l + 1]) ++l;
+    const long long* d = desc + 8 * l;
+    const float* w = (const float*)d[0];
+    bf16_t* wf = (bf16_t*)d[1];
+    bf16_t* wd = (bf16_t*)d[2];
+    const int Cout = (int)d[3], Cin = (int)d[4], Cpad = (int)d[5], KH = (int)d[6], KW = (int)d[7];
+    const unsigned e = (unsigned)(o - pre[l]);
+    const int ci = (int)(e % (unsigned)Cpad);
+    unsigned t = e / (unsigned)Cpad;
+    const int kw = (int)(t % (unsigned)KW);
+    t /= (unsigned)KW;
+    const int kh = (int)(t % (unsigned)KH);
+    const int co = (int)(t / (unsigned)KH);
+    const float v = ci < Cin ? w[(((long long)co * Cin + ci) * KH + kh) * KW + kw] : 0.f;
+    const bf16_t b = f2bf(v);
+    wf[e] = b;
+    if (wd && ci < Cin) wd[(((long long)ci * KH + kh) * KW + kw) * Cout + co] = b;
+  }
+}
+
+void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
+                        hipStream_t st) {
+  pack_weights_multi_kernel<<<grid_for(total, 256, 8192), 256, 0, st>>>(desc, prefix, nl);
+}
+
 // Space-to-depth stem weights: W[co][c][7][7] -> W'[co][4][4][Cp] with
 // W'[co][u][v][(dy*2+dx)*C + c] = W[co][c][2u+dy-1][2v+dx-1] (0 outside the 7x7 window)
 __global__ void __launch_bounds__(256) pack_weights_s2d_kernel(const float* __restrict__ w,
@@ -1155,6 +1269,15 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 8-wave 128-row tiles (4 waves per SIMD at 2 workgroups per CU): 19 = 128x128 as 4x2
   // waves of 32x64, 22 = 128x128 as 2x4 waves of 64x32, 23 = 128x64 as 4x2 waves of 32x32
   if (cfg == 19) return launch_fwd3<128, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  // 26 / 27 / 28: v3 with the LDS-DMA loader, tiles 128x128 / 128x64 mf32, 64x64 16x16
+  if (cfg == 26) return launch_fwd3<128, 128, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 27) return launch_fwd3<128, 64, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 28) return launch_fwd3<64, 64, 2, 2, false, 0>(X, Wp, Y, ADD, stats, g, st);
+  // 30-33: ablations of tile 12 for measurement only (results are wrong)
+  if (cfg == 30) return launch_fwd3<128, 128, 2, 2, true, -1>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 31) return launch_fwd3<128, 128, 2, 2, true, -2>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 32) return launch_fwd3<128, 128, 2, 2, true, -3>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 33) return launch_fwd3<128, 128, 2, 2, true, -7>(X, Wp, Y, ADD, stats, g, st);
   if (cfg == 22) return launch_fwd3<128, 128, 2, 4, true, 1>(X, Wp, Y, ADD, stats, g, st);
   if (cfg == 23) return launch_fwd3<128, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
   // cfg % 3: 0 = 128x128 (2x2 waves, 64x64 per wave), 1 = 128x64, 2 = 64x64
@@ -1170,7 +1293,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -57,6 +57,8 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st);
+void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
+                        hipStream_t st);
 int igemm_fwd_rowtile(int cfg);
 void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                  long long mchunk, int cfg, hipStream_t st);

@@ -43,3 +43,10 @@ class ResNet18(Program):
     def prepare_native(self, x):
         if self.compute_dtype != torch.bfloat16:
             raise ValueError("the native ResNet path computes in bf16")
+        # all conv weights re-packed to bf16 in one launch per weight version
+        if getattr(self, "_packed_ver", None) != self._wver:
+            from dmlab.nn.layers import ConvBN
+            from dmlab.ops.convbn import pack_all
+
+            pack_all(self, [m for m in self.modules() if type(m) is ConvBN])
+            self._packed_ver = self._wver

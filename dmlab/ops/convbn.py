@@ -142,6 +142,39 @@ def packed_weights(layer, need_wd=True):
     return cache[1], cache[2]
 
 
+def pack_all(prog, layers):
+    """Refresh the packed bf16 weights (wf [Cout][KH][KW][Cpad], wd [Cin][KH][KW][Cout]) of
+    every conv in ``layers`` with ONE kernel launch; :func:`packed_weights` then hits the
+    cache.  Buffers persist across steps (stable pointers, graph-capturable); the device
+    descriptor table is rebuilt only when a weight's storage moves."""
+    ver = prog._wver
+    layers = [m for m in layers if m.k * m.k <= 64][:32]
+    if not layers:
+        return
+    key = tuple(m.weight.data_ptr() for m in layers)
+    st = getattr(prog, "_pack_state", None)
+    if st is None or st["key"] != key:
+        dev = layers[0].weight.device
+        bufs, rows, pre = [], [], [0]
+        for m in layers:
+            cp = _cpad(m.cin)
+            wf = torch.empty((m.cout, m.k, m.k, cp), device=dev, dtype=torch.bfloat16)
+            wd = torch.empty((m.cin, m.k, m.k, m.cout), device=dev, dtype=torch.bfloat16)
+            bufs.append((wf, wd))
+            rows.append([m.weight.data_ptr(), wf.data_ptr(), wd.data_ptr(), m.cout, m.cin, cp,
+                         m.k, m.k])
+            pre.append(pre[-1] + m.cout * m.k * m.k * cp)
+        st = dict(key=key, bufs=bufs, total=pre[-1],
+                  desc=torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev),
+                  prefix=torch.tensor(pre, dtype=torch.int64).to(dev))
+        object.__setattr__(prog, "_pack_state", st)
+    for m in layers:
+        assert m.weight.is_contiguous()
+    lib().pack_weights_multi(st["desc"], st["prefix"], st["total"])
+    for m, (wf, wd) in zip(layers, st["bufs"]):
+        object.__setattr__(m, "_wcache", (ver, wf, wd))
+
+
 def convbn_fwd(layer, x, ctx, train, residual=None):
     L = lib()
     first = not (x.dim() == 4 and getattr(x, "_dm_nhwc", False))
