@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--small-allreduce", default="rccl", choices=["rccl", "xgmi"],
+                    help="buckets <= 4 MB via the one-shot xGMI peer-memory kernel")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--graph", type=int, default=-1,
@@ -87,7 +89,8 @@ def main():
         model.set_backend("torch")
     opt = SGD(model.parameters(), lr=lr, momentum=0.9)
     net = DDP(model, bucket_cap_mb=a.bucket_mb,
-              comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None)
+              comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None,
+              small_allreduce="xgmi" if a.small_allreduce == "xgmi" else None)
     net.fold_average_into(opt)
 
     def train_step(x, y):

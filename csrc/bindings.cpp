@@ -161,7 +161,7 @@ int64_t conv_small_workspace(int64_t B, int64_t Cin, int64_t H, int64_t W, int64
 void gemm(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor B, c10::optional<at::Tensor> C,
           c10::optional<at::Tensor> C32, c10::optional<at::Tensor> bias, int64_t M, int64_t N,
           int64_t K, int64_t sam, int64_t sak, int64_t sbk, int64_t sbn, int64_t scm,
-          double alpha, double beta, bool relu) {
+          double alpha, double beta, bool relu, bool lowp) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda());
   auto span_ok = [](const at::Tensor& t, int64_t r, int64_t c, int64_t sr, int64_t sc) {
     return (r - 1) * sr + (c - 1) * sc < t.numel();
@@ -177,9 +177,54 @@ void gemm(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor B, c10::opti
   TORCH_CHECK(cp || c32, "an output is required");
   if (bias.has_value()) { CHECK_F32(*bias); TORCH_CHECK(bias->numel() >= N); }
   const DeviceGuard guard(A.device());
+  // bf16 path: split K over blocks when the output tile grid alone cannot fill the chip
+  // (the ResNet head: 64 output tiles), partial sums in an fp32 workspace reduced in order
+  int S = 1;
+  at::Tensor part;
+  if (lowp && is_bf16(A)) {
+    const long long tiles = ((M + 63) / 64) * ((N + 63) / 64);
+    while (S < 16 && tiles * S < 256 && K / (S * 2) >= 64) S *= 2;
+    if (S > 1) part = at::empty({(long long)S * M * N}, A.options().dtype(at::kFloat));
+  }
   dm::gemm_strided(A.data_ptr(), optp(Amask), is_bf16(A), B.data_ptr(), is_bf16(B), cp, cbf, c32,
                    bias.has_value() ? bias->data_ptr<float>() : nullptr, M, N, K, sam, sak, sbk,
-                   sbn, scm, (float)alpha, (float)beta, relu ? 1 : 0, cur_stream());
+                   sbn, scm, (float)alpha, (float)beta, relu ? 1 : 0, lowp ? 1 : 0,
+                   S > 1 ? part.data_ptr<float>() : nullptr, S, cur_stream());
+}
+
+// ------------------------------------------------------------ xGMI one-shot all-reduce
+int64_t xgmi_alloc(int64_t bytes) { return (int64_t)(uintptr_t)dm::xgmi_alloc((size_t)bytes); }
+void xgmi_free(int64_t ptr) { dm::xgmi_free((void*)(uintptr_t)ptr); }
+py::bytes xgmi_get_handle(int64_t ptr) {
+  char h[64];
+  dm::xgmi_get_handle((void*)(uintptr_t)ptr, h);
+  return py::bytes(h, 64);
+}
+int64_t xgmi_open_handle(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK(h.size() == 64, "IPC handle must be 64 bytes");
+  return (int64_t)(uintptr_t)dm::xgmi_open_handle(h.data());
+}
+void xgmi_close_handle(int64_t ptr) { dm::xgmi_close_handle((void*)(uintptr_t)ptr); }
+void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int64_t> data,
+                    std::vector<int64_t> flags, int64_t rank, double scale, int64_t epoch,
+                    at::Tensor err) {
+  CHECK_F32(in);
+  CHECK_F32(out);
+  TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel());
+  TORCH_CHECK(in.numel() <= cap, "tensor larger than the shared buffer");
+  const int W = data.size();
+  TORCH_CHECK(W >= 1 && W <= 8 && (int)flags.size() == W && rank >= 0 && rank < W);
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.is_cuda());
+  std::vector<void*> d(W), f(W);
+  for (int q = 0; q < W; ++q) {
+    d[q] = (void*)(uintptr_t)data[q];
+    f[q] = (void*)(uintptr_t)flags[q];
+  }
+  const DeviceGuard guard(in.device());
+  dm::xgmi_allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cap, d.data(),
+                     f.data(), (int)rank, W, (unsigned)epoch, (float)scale, err.data_ptr<int>(),
+                     cur_stream());
 }
 
 void colsum(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor out, double beta) {
@@ -231,8 +276,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_small_fwd", &conv_small_fwd);
   m.def("conv_small_bwd", &conv_small_bwd);
   m.def("conv_small_workspace", &conv_small_workspace);
-  m.def("gemm", &gemm);
+  m.def("gemm", &gemm, py::arg("A"), py::arg("Amask"), py::arg("B"), py::arg("C"), py::arg("C32"),
+        py::arg("bias"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("sam"), py::arg("sak"),
+        py::arg("sbk"), py::arg("sbn"), py::arg("scm"), py::arg("alpha"), py::arg("beta"),
+        py::arg("relu"), py::arg("lowp") = false);
   m.def("colsum", &colsum);
+  m.def("xgmi_alloc", &xgmi_alloc);
+  m.def("xgmi_free", &xgmi_free);
+  m.def("xgmi_get_handle", &xgmi_get_handle);
+  m.def("xgmi_open_handle", &xgmi_open_handle);
+  m.def("xgmi_close_handle", &xgmi_close_handle);
+  m.def("xgmi_allreduce", &xgmi_allreduce);
   m.def("cross_entropy", &cross_entropy);
   m.def("argmax_count", &argmax_count);
   m.def("spin_us", &spin_us);

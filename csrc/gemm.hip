@@ -108,6 +108,126 @@ __global__ void __launch_bounds__(256) gemm_f32mfma_kernel(
       }
 }
 
+// bf16 operands on v_mfma_f32_16x16x32_bf16 (fp32 accumulation): the ResNet classifier head
+// (A = bf16 activations / gradients, B = bf16 or the fp32 master weight, rounded to bf16 while
+// staging).  Same strided semantics and epilogue as gemm_f32mfma_kernel.  Tile 64x64, 4 waves
+// of 32x32, BK 32; LDS rows k-contiguous (pitch 40 elements) for the 8-k fragment reads.
+template <typename TB, typename TC>
+__global__ void __launch_bounds__(256) gemm_bf16mfma_kernel(
+    const bf16_t* __restrict__ A, const bf16_t* __restrict__ Amask, const TB* __restrict__ B,
+    TC* __restrict__ C, float* __restrict__ C32, const float* __restrict__ bias, int M, int N,
+    int K, long long sam, long long sak, long long sbk, long long sbn, long long scm,
+    float alpha, float beta, int relu, float* __restrict__ part, int kchunk) {
+  // split-K (part != nullptr): block z reduces k in [z*kchunk, (z+1)*kchunk) and stores
+  // alpha*acc into part[z][M][N]; gemm_splitk_reduce_kernel applies the epilogue
+  constexpr int BK = 32, P = 40;
+  __shared__ __attribute__((aligned(16))) bf16_t As[GBM][P];
+  __shared__ __attribute__((aligned(16))) bf16_t Bs[GBN][P];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
+  const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int kb = part ? blockIdx.z * kchunk : 0;
+  const int ke = part ? min(K, kb + kchunk) : K;
+  for (int k0 = kb; k0 < ke; k0 += BK) {
+    // 64 x 32 elements per operand, 8 per thread, walking the contiguous dimension fastest
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + r * 256;
+      int mm, kk;
+      if (sak == 1) { mm = e / BK; kk = e % BK; }
+      else { kk = e / GBM; mm = e % GBM; }
+      const int gm = m0 + mm, gk = k0 + kk;
+      bf16_t v = 0;
+      if (gm < M && gk < ke) {
+        const long long o = (long long)gm * sam + (long long)gk * sak;
+        v = A[o];
+        if (Amask && !(bf2f(Amask[o]) > 0.f)) v = 0;
+      }
+      As[mm][kk] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + r * 256;
+      int nn, kk;
+      if (sbk == 1) { nn = e / BK; kk = e % BK; }
+      else { kk = e / GBN; nn = e % GBN; }
+      const int gn = n0 + nn, gk = k0 + kk;
+      bf16_t v = 0;
+      if (gn < N && gk < ke) {
+        const long long o = (long long)gk * sbk + (long long)gn * sbn;
+        if constexpr (sizeof(TB) == 4) v = f2bf(B[o]);
+        else v = B[o];
+      }
+      Bs[nn][kk] = v;
+    }
+    __syncthreads();
+    const int kq = (lane >> 4) * 8;
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = *reinterpret_cast<const bf16x8*>(&As[wm + i * 16 + (lane & 15)][kq]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(&Bs[wn + j * 16 + (lane & 15)][kq]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int gm = m0 + wm + i * 16 + (lane >> 4) * 4 + r;
+        const int gn = n0 + wn + j * 16 + (lane & 15);
+        if (gm < M && gn < N) {
+          float v = alpha * acc[i][j][r];
+          if (part) {
+            part[((long long)blockIdx.z * M + gm) * N + gn] = v;
+            continue;
+          }
+          const long long o = (long long)gm * scm + gn;
+          if (beta != 0.f) v += beta * (C32 ? C32[o] : ldx(C, o));
+          if (bias) v += bias[gn];
+          if (relu) v = fmaxf(v, 0.f);
+          if (C32) C32[o] = v;
+          if (C) {
+            if constexpr (sizeof(TC) == 4) C[o] = v;
+            else C[o] = f2bf(v);
+          }
+        }
+      }
+}
+
+template <typename TC>
+__global__ void __launch_bounds__(256) gemm_splitk_reduce_kernel(
+    const float* __restrict__ part, int S, int M, int N, TC* __restrict__ C,
+    float* __restrict__ C32, const float* __restrict__ bias, long long scm, float beta, int relu) {
+  const long long total = (long long)M * N;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int z = 0; z < S; ++z) v += part[z * total + e];  // fixed order: deterministic
+    const int gm = (int)(e / N), gn = (int)(e % N);
+    const long long o = (long long)gm * scm + gn;
+    if (beta != 0.f) v += beta * (C32 ? C32[o] : ldx(C, o));
+    if (bias) v += bias[gn];
+    if (relu) v = fmaxf(v, 0.f);
+    if (C32) C32[o] = v;
+    if (C) {
+      if constexpr (sizeof(TC) == 4) C[o] = v;
+      else C[o] = f2bf(v);
+    }
+  }
+}
+
 // db[n] = beta*db[n] + sum_m A(m,n) [masked by Amask(m,n) > 0]   (bias gradient)
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ A,
@@ -140,8 +260,33 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ A,
 void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, int b_bf16,
                   void* C, int c_bf16, float* C32, const float* bias, int M, int N, int K,
                   long long sam, long long sak, long long sbk, long long sbn, long long scm,
-                  float alpha, float beta, int relu, hipStream_t st) {
+                  float alpha, float beta, int relu, int lowp, float* part, int S,
+                  hipStream_t st) {
   dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM);
+  if (lowp && a_bf16) {  // bf16 MFMA (B rounded to bf16 while staging)
+    const int kchunk = S > 1 ? ((K + S - 1) / S + 31) / 32 * 32 : K;
+    if (S > 1) grid.z = S;
+    float* pp = S > 1 ? part : nullptr;
+#define DM_GEMM16(TB, TC)                                                                    \
+  gemm_bf16mfma_kernel<TB, TC><<<grid, 256, 0, st>>>(                                        \
+      (const bf16_t*)A, (const bf16_t*)Amask, (const TB*)B, (TC*)C, C32, bias, M, N, K, sam, \
+      sak, sbk, sbn, scm, alpha, beta, relu, pp, kchunk)
+    if (b_bf16 && c_bf16) DM_GEMM16(bf16_t, bf16_t);
+    else if (b_bf16) DM_GEMM16(bf16_t, float);
+    else if (c_bf16) DM_GEMM16(float, bf16_t);
+    else DM_GEMM16(float, float);
+#undef DM_GEMM16
+    if (S > 1) {
+      const int g = grid_for((long long)M * N, 256, 2048);
+      if (c_bf16)
+        gemm_splitk_reduce_kernel<bf16_t><<<g, 256, 0, st>>>(part, S, M, N, (bf16_t*)C, C32, bias,
+                                                              scm, beta, relu);
+      else
+        gemm_splitk_reduce_kernel<float><<<g, 256, 0, st>>>(part, S, M, N, (float*)C, C32, bias,
+                                                             scm, beta, relu);
+    }
+    return;
+  }
 #define DM_GEMM(TA, TB, TC)                                                                  \
   gemm_f32mfma_kernel<TA, TB, TC><<<grid, 256, 0, st>>>(                                     \
       (const TA*)A, (const TA*)Amask, (const TB*)B, (TC*)C, C32, bias, M, N, K, sam, sak, sbk, \

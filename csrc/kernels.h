@@ -34,7 +34,8 @@ void conv_small_bwd(const void* x, const float* w, const void* dp, const void* y
 void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, int b_bf16,
                   void* C, int c_bf16, float* C32, const float* bias, int M, int N, int K,
                   long long sam, long long sak, long long sbk, long long sbn, long long scm,
-                  float alpha, float beta, int relu, hipStream_t st);
+                  float alpha, float beta, int relu, int lowp, float* part, int S,
+                  hipStream_t st);
 void colsum(const void* A, const void* Amask, int bf16, float* out, int M, int N, float beta,
             hipStream_t st);
 // loss.hip
@@ -47,6 +48,15 @@ void spin_us(double us, hipStream_t st);
 }  // namespace dm
 
 namespace dm {
+// comm_xgmi.hip
+void* xgmi_alloc(size_t bytes);
+void xgmi_free(void* ptr);
+void xgmi_get_handle(void* ptr, void* handle64);
+void* xgmi_open_handle(const void* handle64);
+void xgmi_close_handle(void* ptr);
+void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
+                    void* const* flags, int rank, int W, unsigned epoch, float scale, int* err,
+                    hipStream_t st);
 // conv_igemm.hip
 struct ConvGeom;
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,

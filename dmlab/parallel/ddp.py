@@ -22,6 +22,9 @@ task3/dist_utils.py:40-46).  Here:
   smaller (``first_bucket_mb``) so communication starts early in backward.
 * Optional bf16 gradient communication (``comm_dtype=torch.bfloat16``) halves
   the bytes on the links.
+* ``small_allreduce="xgmi"``: buckets of at most ``small_cap_mb`` go through the
+  one-shot xGMI peer-memory all-reduce (:mod:`dmlab.parallel.xgmi`, one kernel, no ring
+  steps) instead of RCCL — the latency-bound case of the labs' LeNet (207 KB of grads).
 """
 from __future__ import annotations
 
@@ -36,13 +39,14 @@ from .comm import avg_supported, init_parameters
 
 
 class _Bucket:
-    __slots__ = ("lo", "hi", "params", "pending", "work", "comm_buf")
+    __slots__ = ("lo", "hi", "params", "pending", "work", "comm_buf", "scaled")
 
     def __init__(self, lo, hi, params):
         self.lo, self.hi, self.params = lo, hi, params
         self.pending = set(params)
         self.work = None
         self.comm_buf = None
+        self.scaled = False
 
 
 
@@ -50,7 +54,8 @@ class _Bucket:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: float = 4.0, comm_dtype=None, broadcast_init: bool = True,
-                 process_group=None, average: bool = True):
+                 process_group=None, average: bool = True, small_allreduce: str | None = None,
+                 small_cap_mb: float = 4.0):
         super().__init__()
         self.module = module
         self.ws = env.get_world_size()
@@ -68,6 +73,16 @@ class DistributedDataParallel(nn.Module):
             self._setup_generic(bucket_cap_mb, first_bucket_mb)
         self.buckets_launched = 0
         self._sync_enabled = True
+        self._xgmi = None
+        if small_allreduce not in (None, "rccl", "xgmi"):
+            raise ValueError("small_allreduce: None | 'rccl' | 'xgmi'")
+        if small_allreduce == "xgmi" and self.ws > 1:
+            cap = int(small_cap_mb * 2**20 / 4)
+            small = [b.hi - b.lo for b in self.buckets if b.hi - b.lo <= cap]
+            if self.grad_buf.dtype == torch.float32 and self.grad_buf.is_cuda and small:
+                from .xgmi import XGMIAllReduce
+
+                self._xgmi = XGMIAllReduce(cap=max(small), group=self.pg)
 
     # ------------------------------------------------------------------ layout
     def _make_buckets(self, sizes, cap, first):
@@ -160,6 +175,13 @@ class DistributedDataParallel(nn.Module):
             b.work = b.work or True
             return
         view = self.grad_buf[b.lo:b.hi]
+        if self._xgmi is not None and self.comm_dtype is None and view.numel() <= self._xgmi.cap:
+            # one stream-ordered kernel, averaging folded into its epilogue
+            scale = 1.0 / self.ws if (self.average and not self._fold) else 1.0
+            self._xgmi(view, scale=scale)
+            b.work, b.scaled = True, True
+            self.buckets_launched += 1
+            return
         if self.comm_dtype is not None and self.comm_dtype != view.dtype:
             b.comm_buf = view.to(self.comm_dtype)
             t = b.comm_buf
@@ -202,9 +224,9 @@ class DistributedDataParallel(nn.Module):
             if b.comm_buf is not None:
                 view.copy_(b.comm_buf)
                 b.comm_buf = None
-            if scale is not None and self.ws > 1:
+            if scale is not None and self.ws > 1 and not b.scaled:
                 view.mul_(scale)
-            b.work = None
+            b.work, b.scaled = None, False
             b.pending = set(b.params)
         if self.program is None:
             self._final_queued = False

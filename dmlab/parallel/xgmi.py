@@ -1,0 +1,82 @@
+"""One-shot all-reduce over xGMI peer memory for small messages (``csrc/comm_xgmi.hip``).
+
+SURVEY §2.7 / build plan step 4: RCCL's ring all-reduce takes 2(W-1) latency-bound steps,
+which dominates for the labs' small gradient messages (LeNet: 51,902 floats).  Every rank
+allocates one IPC-shareable, uncached device buffer ([2][cap] floats of data in two parity
+halves + a [64][8] flag array), exchanges its ``hipIpcMemHandle`` through the process
+group (``all_gather_object``) and opens every peer's.  A call is ONE kernel: copy the
+slice in, flag every peer, wait for every peer's flag, sum the W slices in rank order
+(identical bits on every rank).  Waits are bounded: a missing peer raises
+:class:`RuntimeError` on :meth:`check` instead of hanging the GPU.
+
+Requirements: one process per GPU on one node (or several processes sharing one GPU, as
+the tests do), ``HSA_ENABLE_IPC_MODE_LEGACY=0`` (dmabuf IPC), fp32 contiguous tensors of
+at most ``cap`` elements.  RCCL stays the default everywhere; this path is opted into
+(``DistributedDataParallel(..., small_allreduce="xgmi")``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from dmlab.ops._native import lib
+
+_FLAG_BYTES = 64 * 8 * 4
+
+
+class XGMIAllReduce:
+    def __init__(self, cap: int = 1 << 20, group=None, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.world > 8:
+            raise ValueError("xGMI one-shot all-reduce supports up to 8 ranks (one node)")
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.cap = int(cap)
+        L = lib()
+        self._base = L.xgmi_alloc(8 * self.cap + _FLAG_BYTES)
+        handle = L.xgmi_get_handle(self._base)
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle, group=group)
+        self._opened = []
+        bases = []
+        for q, h in enumerate(handles):
+            if q == self.rank:
+                bases.append(self._base)
+            else:
+                p = L.xgmi_open_handle(h)
+                self._opened.append(p)
+                bases.append(p)
+        self._data = bases
+        self._flags = [b + 8 * self.cap for b in bases]
+        self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._epoch = 0
+        dist.barrier(group=group)
+
+    def __call__(self, t: torch.Tensor, scale: float = 1.0, out: torch.Tensor | None = None):
+        """out (default: t, in place) = scale * Σ_ranks t.  Stream-ordered on the current
+        stream; returns ``out``."""
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() > self.cap:
+            raise ValueError("xGMI all-reduce: fp32 contiguous tensor of <= cap elements")
+        out = t if out is None else out
+        self._epoch += 1
+        lib().xgmi_allreduce(t, out, self.cap, self._data, self._flags, self.rank, float(scale),
+                             self._epoch, self._err)
+        return out
+
+    def check(self):
+        """Raise if any call so far timed out waiting for a peer (synchronises)."""
+        if int(self._err.item()):
+            raise RuntimeError("xGMI all-reduce: a peer never arrived (timed out)")
+
+    def close(self):
+        L = lib()
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+        for p in self._opened:
+            L.xgmi_close_handle(p)
+        self._opened = []
+        dist.barrier(group=self.group)
+        if self._base:
+            L.xgmi_free(self._base)
+            self._base = 0

@@ -46,6 +46,8 @@ def parse_args(argv=None):
     p.add_argument("--lr", type=float, default=0.001)
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--bucket-mb", type=float, default=25.0)
+    p.add_argument("--allreduce", default="rccl", choices=["rccl", "xgmi"],
+                   help="small-bucket all-reduce: RCCL ring or the one-shot xGMI kernel")
     p.add_argument("--data", default="./data")
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--train-samples", type=int, default=None)
@@ -86,7 +88,8 @@ def main(argv=None):
 
         checkpoint.load(a.resume, model, opt)
     if a.dp == "ddp":
-        net = DDP(model, bucket_cap_mb=a.bucket_mb)  # broadcasts rank-0 params
+        net = DDP(model, bucket_cap_mb=a.bucket_mb,  # broadcasts rank-0 params
+                  small_allreduce="xgmi" if a.allreduce == "xgmi" and dev.type == "cuda" else None)
         net.fold_average_into(opt)
         agg = None
     else:

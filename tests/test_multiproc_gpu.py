@@ -35,12 +35,26 @@ def _entry(rank, ws, port, kind, q):
         torch.manual_seed(0)
         ref = Net().to(dev)
         ropt = SGD(ref.parameters(), lr=0.1, momentum=0.9)
-        if kind == "ddp":
+        if kind == "xgmi":
+            from dmlab.parallel.xgmi import XGMIAllReduce
+
+            ar = XGMIAllReduce(cap=1 << 16)
+            err = 0.0
+            for it, n in enumerate([1, 1000, 51902, 65536, 7]):
+                t = torch.arange(n, device=dev, dtype=torch.float32) * (rank + 1) + it
+                exp = torch.arange(n, device=dev, dtype=torch.float32) * 3 + 2 * it
+                out = ar(t.clone(), scale=0.5) if it % 2 else ar(t)  # in place / scaled copy
+                ref_v = exp * (0.5 if it % 2 else 1.0)
+                err = max(err, (out - ref_v).abs().max().item())
+            ar.check()
+            ar.close()
+        elif kind in ("ddp", "ddp_xgmi"):
             from dmlab.parallel import DDP
 
             torch.manual_seed(0)
             model = Net().to(dev)
-            ddp = DDP(model)
+            ddp = DDP(model, small_allreduce="xgmi" if kind == "ddp_xgmi" else None)
+            assert (ddp._xgmi is not None) == (kind == "ddp_xgmi")
             opt = SGD(model.parameters(), lr=0.1, momentum=0.9)
             ddp.fold_average_into(opt)
             for _ in range(2):
@@ -75,7 +89,7 @@ def _entry(rank, ws, port, kind, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["ddp", "pipeline"])
+@pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "pipeline", "xgmi"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 

@@ -108,3 +108,27 @@ def test_gemm_strided(dev, M, N, K, relu):
     if relu:
         ref = ref.relu()
     torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-4 * K ** 0.5)
+
+
+@pytest.mark.parametrize("M,N,K", [(5, 70, 33), (256, 1000, 512)])
+def test_gemm_bf16_lowp(dev, M, N, K):
+    """bf16-MFMA path (ResNet head): fwd (fp32 weight rounded while staging, bias, bf16
+    out), wgrad (transposed A, fp32 out with beta) and dgrad, vs fp32 math on the same
+    bf16-rounded operands."""
+    g = torch.Generator(device=dev).manual_seed(1)
+    x = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    W = torch.randn(N, K, device=dev, generator=g) / K ** 0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    Wb = W.bfloat16().float()
+    y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    lib().gemm(x, None, W, y, None, bias, M, N, K, K, 1, 1, K, N, 1.0, 0.0, False, lowp=True)
+    ref = x.float() @ Wb.T + bias
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    dy = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    gw = torch.randn(N, K, device=dev, generator=g)
+    base = gw.clone()
+    lib().gemm(dy, None, x, None, gw, None, N, K, M, 1, N, K, 1, K, 1.0, 1.0, False, lowp=True)
+    torch.testing.assert_close(gw, base + dy.float().T @ x.float(), rtol=1e-3, atol=1e-3 * M ** 0.5)
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    lib().gemm(dy, None, W, dx, None, None, M, K, N, N, 1, K, 1, K, 1.0, 0.0, False, lowp=True)
+    torch.testing.assert_close(dx.float(), dy.float() @ Wb, rtol=1e-2, atol=2e-2)
