@@ -32,15 +32,15 @@
 namespace dm {
 
 namespace {
-constexpr int HBM = 128;  // output pixels per block
+constexpr int HBM = 128;  // output pixels per block (default tile)
 constexpr int HBK = 64;   // channels per chunk (one 128-B LDS row per pixel)
 constexpr unsigned OOB = 0x80000000u;
 
-template <int BN, int HR, int WM, int WN>
+template <int BN, int HR, int WM, int WN, int BMH>
 __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes) {
-  constexpr int TM = HBM / WM, TN = BN / WN;
+  constexpr int TM = BMH / WM, TN = BN / WN;
   constexpr int RM = TM / 32, RN = TN / 32;
   constexpr int NT = WM * WN * 64, RPP = NT / 8;     // threads, staged rows per pass
   constexpr int BR = BN / RPP;
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = (long long)blockIdx.x * HBM;
+  const long long m0 = (long long)blockIdx.x * BMH;
   const int n0 = blockIdx.y * BN;
   const int ntaps = g.nth * g.ntw;
   const int nchunk = g.C / HBK;
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
 
   // halo extent (flattened rows r0-1 .. r1+1)
   const int r0 = (int)fdiv((unsigned)m0, g.wg_mul, g.wg_shr);
-  const long long mlast = (m0 + HBM - 1 < g.M) ? m0 + HBM - 1 : g.M - 1;
+  const long long mlast = (m0 + BMH - 1 < g.M) ? m0 + BMH - 1 : g.M - 1;
   const int r1 = (int)fdiv((unsigned)mlast, g.wg_mul, g.wg_shr);
   const int hbase = (r0 - 1) * g.W;
   const int hp = (r1 - r0 + 3) * g.W;
@@ -206,25 +206,25 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
     t = nt;
     cc = ncc;
   }
-  mfma_tile_epilogue<HBM, BN, WM, WN, true>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
 }
 
-int halo_rows_needed(const ConvGeom& g) {
-  // worst case over blocks: a 128-pixel run starting at the last pixel of a row
-  return ((g.W - 1 + HBM - 1) / g.W + 3) * g.W;
+int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
+  // worst case over blocks: a bm-pixel run starting at the last pixel of a row
+  return ((g.W - 1 + bm - 1) / g.W + 3) * g.W;
 }
 
-template <int BN, int HR, int WM, int WN>
+template <int BN, int HR, int WM, int WN, int BMH = HBM>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, hipStream_t st) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
-  const size_t epi = (size_t)HBM * (BN + 4) * 4;
+  const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
   const size_t sm = main > epi ? main : epi;
-  dim3 grid((unsigned)((g.M + HBM - 1) / HBM), (g.Ncols + BN - 1) / BN);
+  dim3 grid((unsigned)((g.M + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = conv_halo_kernel<BN, HR, WM, WN>;
+  auto k = conv_halo_kernel<BN, HR, WM, WN, BMH>;
   set_smem_attr(k, sm);
   k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
 }
@@ -239,11 +239,23 @@ bool conv_halo_supported(const ConvGeom& g) {
   if (!in1(dya) || !in1(dyb) || !in1(dxa) || !in1(dxb)) return false;
   if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31)) return false;
   if ((long long)g.Ncols * g.wK * 2 >= (1LL << 31)) return false;
-  return halo_rows_needed(g) <= 32 * 12;
+  return halo_rows_needed(g) <= 32 * 12 && halo_rows_needed(g, 256) <= 32 * 14;
 }
 
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st) {
+  if (waves == 2) {  // 256-pixel tile: 2 x 2 waves of 128 x BN/2 (twice the weight reuse)
+    const int hp2 = halo_rows_needed(g, 256);
+    const int hr = (hp2 + 31) / 32;
+#define DM_HALO256(BN_)                                                                      \
+  if (hr <= 10) launch_halo<BN_, 10, 2, 2, 256>(X, Wp, Y, ADD, stats, g, st);                \
+  else if (hr <= 12) launch_halo<BN_, 12, 2, 2, 256>(X, Wp, Y, ADD, stats, g, st);           \
+  else launch_halo<BN_, 14, 2, 2, 256>(X, Wp, Y, ADD, stats, g, st);
+    if (bn == 128) { DM_HALO256(128) } else { DM_HALO256(64) }
+#undef DM_HALO256
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   const int hp = halo_rows_needed(g);
   if (waves == 8) {  // 4 x 2 waves of 32 x BN/2
     const int hr = hp <= 192 ? 3 : hp <= 256 ? 4 : 6;

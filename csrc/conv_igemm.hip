@@ -309,6 +309,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
   constexpr int NT = WM * WN * 64, RPP = NT / 8;   // threads, staged rows per pass
   constexpr int AR = BM / RPP, BR = BN / RPP;
   static_assert(AR * RPP == BM && BR * RPP == BN, "tile rows must be a multiple of NT/8");
+  static_assert(DEPTH != 3 || (MF32 && AR <= 4 && BR <= 4), "interleaved stores: 4 substeps");
   constexpr unsigned OOB = 0x80000000u;
   typedef typename std::conditional<MF32, f32x16, f32x4>::type accT;
   constexpr int NR = MF32 ? 16 : 4;
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
   }
   __syncthreads();
-  uint4 ra[DEPTH > 1 ? DEPTH : 1][AR], rb[DEPTH > 1 ? DEPTH : 1][BR];
+  uint4 ra[DEPTH > 1 ? 2 : 1][AR], rb[DEPTH > 1 ? 2 : 1][BR];
   const int nk = (g.K + BK - 1) / BK;
   const unsigned C2 = (unsigned)g.C * 2u;
 
@@ -475,7 +476,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
 
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, (DEPTH > 1 ? 1 : 0)>;
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf, auto post) {
       const bf16_t* as = As + buf * BM * BK;
       const bf16_t* bs = Bs + buf * BN * BK;
       if constexpr (MF32) {
@@ -506,6 +507,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
             for (int j = 0; j < RN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ks & 1][i], bfr[ks & 1][j],
                                                                   acc[i][j], 0, 0, 0);
+          post(ks);
         }
       } else {
 #pragma unroll
@@ -527,8 +529,27 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
 #pragma unroll
             for (int j = 0; j < RN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          post(ks);
         }
       }
+  };
+  auto nopost = [](int) {};
+  // part p of a tile's LDS stores: A rows i and B rows i with i % 4 == p
+  auto store_part = [&](int buf, auto S, int part) {
+    bf16_t* as = As + buf * BM * BK;
+    bf16_t* bs = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      if (i % 4 != part) continue;
+      const int r = (tid >> 3) + RPP * i;
+      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[S][i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      if (i % 4 != part) continue;
+      const int r = (tid >> 3) + RPP * i;
+      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[S][i];
+    }
   };
   if constexpr (DEPTH == 0) {
     issue(0, 0);
@@ -537,7 +558,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
       if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-      compute(buf);
+      compute(buf, nopost);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -551,9 +572,31 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
       if (!(ABL & 1) && kt + 1 < nk) load(kt + 1, S0{});
-      compute(buf);
+      compute(buf, nopost);
       if (!(ABL & 2) && kt + 1 < nk) store(buf ^ 1, S0{});
       if (!(ABL & 4)) __syncthreads();
+    }
+  } else if constexpr (DEPTH == 3) {
+    // register sets as DEPTH 2, but tile kt+1's LDS stores are spread over the MFMA
+    // substeps of tile kt (its loads landed an iteration ago), not bunched before the barrier
+    load(0, S0{});
+    if (nk > 1) load(1, S1{});
+    store(0, S0{});
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) load(kt + 2, S0{});
+      const bool st1 = kt + 1 < nk;
+      compute(0, [&](int ks) {
+        if (st1) store_part(1, S1{}, ks);
+      });
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) load(kt + 3, S1{});
+      const bool st0 = kt + 2 < nk;
+      compute(1, [&](int ks) {
+        if (st0) store_part(0, S0{}, ks);
+      });
+      __syncthreads();
     }
   } else {
     // tile t is staged through register set t & 1, issued two tiles ahead of its use
@@ -563,12 +606,12 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     __syncthreads();
     for (int kt = 0; kt < nk; kt += 2) {
       if (kt + 2 < nk) load(kt + 2, S0{});
-      compute(0);
+      compute(0, nopost);
       if (kt + 1 < nk) store(1, S1{});
       __syncthreads();
       if (kt + 1 >= nk) break;
       if (kt + 3 < nk) load(kt + 3, S1{});
-      compute(1);
+      compute(1, nopost);
       if (kt + 2 < nk) store(0, S0{});
       __syncthreads();
     }
@@ -1257,9 +1300,16 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 16x16; 18 = 8-wave 256x128 mf32 (measured slower: one workgroup per CU)
   // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64, 4 waves;
   // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
-  if (cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25) {
-    const int bn = (cfg == 20 || cfg == 24) ? 128 : 64;
-    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, cfg >= 24 ? 8 : 4, st);
+  // 36 / 37: 256-pixel halo tile (2 x 2 waves of 128 x BN/2), BN 128 / 64
+  if (cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || cfg == 36 || cfg == 37) {
+    const int bn = (cfg == 20 || cfg == 24 || cfg == 36) ? 128 : 64;
+    const int waves = cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
+    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st);
+    // fallback keeps the row tile (stats slab rows = igemm_fwd_rowtile(cfg))
+    if (cfg >= 36) {
+      if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+      return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+    }
     cfg = bn == 128 ? 12 : 13;
   }
   if (cfg == 15) return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
@@ -1269,6 +1319,9 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 8-wave 128-row tiles (4 waves per SIMD at 2 workgroups per CU): 19 = 128x128 as 4x2
   // waves of 32x64, 22 = 128x128 as 2x4 waves of 64x32, 23 = 128x64 as 4x2 waves of 32x32
   if (cfg == 19) return launch_fwd3<128, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  // 34 / 35: v3 with the next tile's LDS stores interleaved into the MFMA substeps
+  if (cfg == 34) return launch_fwd3<128, 128, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 35) return launch_fwd3<128, 64, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st);
   // 26 / 27 / 28: v3 with the LDS-DMA loader, tiles 128x128 / 128x64 mf32, 64x64 16x16
   if (cfg == 26) return launch_fwd3<128, 128, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st);
   if (cfg == 27) return launch_fwd3<128, 64, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st);
@@ -1293,7 +1346,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return cfg == 36 || cfg == 37 ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

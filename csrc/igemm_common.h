@@ -31,8 +31,9 @@ using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 //  * optional BN statistics: per-column Σy, Σy² of the fp32 tile -> stats[stat_row][2][Ncols]
 //  * fp32 tile staged through LDS (row pitch BN+4) -> coalesced 16-B bf16 stores at the
 //    output pixel (y*osy+oy0, x*osx+ox0), optionally adding ADD (which may alias Y).
-// Rows >= g.M must hold zeros when stats are requested.  Requires BM*(BN+4)*4 B of LDS.
-template <int BM, int BN, int WM, int WN, bool MF32>
+// Rows >= g.M must hold zeros when stats are requested.  Requires (BM/PASSES)*(BN+4)*4 B of
+// LDS: with PASSES > 1 the tile is staged one band of BM/PASSES rows (whole wave rows) at a time.
+template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1>
 __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / WM / (MF32 ? 32 : 16)][BN / WN / (MF32 ? 32 : 16)],
                                                    unsigned char* smem, long long m0, int n0,
                                                    int stat_row, float* stats, const ConvGeom& g,
@@ -87,41 +88,49 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
     __syncthreads();
   }
   constexpr int LDC = BN + 4;
+  constexpr int RPB = BM / PASSES;  // rows per band
+  static_assert(RPB % TM == 0, "a band holds whole wave rows");
   float* cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-        cs[(wm * TM + i * FM + frow(r)) * LDC + wn * TN + j * FM + fcol] = acc[i][j][r];
-  __syncthreads();
   constexpr int CPR = BN / 8;
-  for (int e = tid; e < BM * CPR; e += NT) {
-    const int row = e / CPR, cc = e % CPR;
-    const long long m = m0 + row;
-    const int col = n0 + cc * 8;
-    if (m >= g.M || col >= g.Ncols) continue;
-    const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
-    const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
-    const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
-    const int y = (int)(t - n * (unsigned)g.Hg);
-    const long long o =
-        (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
-    const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
-    const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
-    float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    if (ADD) {
-      const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
-      const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
-      }
+  for (int pb = 0; pb < PASSES; ++pb) {
+    if (PASSES > 1) __syncthreads();  // previous band's LDS reads done
+    if (wm * TM >= pb * RPB && wm * TM < (pb + 1) * RPB) {
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+            cs[(wm * TM - pb * RPB + i * FM + frow(r)) * LDC + wn * TN + j * FM + fcol] = acc[i][j][r];
     }
-    *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                                  pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+    __syncthreads();
+    for (int e = tid; e < RPB * CPR; e += NT) {
+      const int row = e / CPR, cc = e % CPR;
+      const long long m = m0 + pb * RPB + row;
+      const int col = n0 + cc * 8;
+      if (m >= g.M || col >= g.Ncols) continue;
+      const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
+      const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+      const int y = (int)(t - n * (unsigned)g.Hg);
+      const long long o =
+          (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+      const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
+      const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (ADD) {
+        const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
+        const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
+          v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+        }
+      }
+      *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                                    pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+    }
   }
 }
 
