@@ -59,35 +59,42 @@ __global__ void __launch_bounds__(256) slab_colsum_kernel(const float* __restric
                                            red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment), 4 lanes
-// x 64 channels per 256-thread block; valid in lane 0 (threadIdx.x < 64) afterwards.
+// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment): 16 row lanes
+// x 16 channels per 256-thread block, 8 loads in flight per lane, lanes combined in fixed
+// order; the result is valid in threads 0..15 (channel blockIdx.x*16 + threadIdx.x).
+constexpr int FIN_CH = 16;
 __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G, int C, int c,
                                            double& s, double& q) {
-  __shared__ double red[2][4][64];
-  const int rl = threadIdx.x >> 6, cl = threadIdx.x & 63;
+  __shared__ double red[2][16][FIN_CH];
+  const int rl = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH;
   const long long W = 2LL * C;
-  red[0][rl][cl] = c < C ? sum_rows8(part + c, rl, G, 4, W) : 0.0;
-  red[1][rl][cl] = c < C ? sum_rows8(part + C + c, rl, G, 4, W) : 0.0;
+  red[0][rl][cl] = c < C ? sum_rows8(part + c, rl, G, 16, W) : 0.0;
+  red[1][rl][cl] = c < C ? sum_rows8(part + C + c, rl, G, 16, W) : 0.0;
   __syncthreads();
-  s = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-  q = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  s = 0.0;
+  q = 0.0;
+  if (threadIdx.x < FIN_CH)
+    for (int l = 0; l < 16; ++l) {
+      s += red[0][l][cl];
+      q += red[1][l][cl];
+    }
 }
 
 // level-1 groups for a [T][2C] slab: none when the finalize block can sum it directly
-static inline int colsum_groups(int T) { return T <= 128 ? 0 : min(256, (T + 31) / 32); }
+static inline int colsum_groups(int T) { return T <= 256 ? 0 : min(256, (T + 31) / 32); }
 
 // stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
-// grid ceil(C/64) x 256 threads
+// grid ceil(C/16) x 256 threads
 __global__ void __launch_bounds__(256) bn_finalize_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
     float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift,
     float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
   if (num_batches && blockIdx.x == 0 && threadIdx.x == 0) *num_batches += 1;
   double s, q;
   block_sum2(part, G, C, c, s, q);
-  if (threadIdx.x >= 64 || c >= C) return;
+  if (threadIdx.x >= FIN_CH || c >= C) return;
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
@@ -337,15 +344,15 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
 }
 
 // finalize: Σ over G partials -> dgamma, dbeta (written with beta-accumulate into grad
-// slots) and the affine dy coefficients a, b, c.  grid ceil(C/64) x 256 threads.
+// slots) and the affine dy coefficients a, b, c.  grid ceil(C/16) x 256 threads.
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
     const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dgamma,
     float* __restrict__ dbeta, float gbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
   double s, q;
   block_sum2(part, G, C, c, s, q);
-  if (threadIdx.x >= 64 || c >= C) return;
+  if (threadIdx.x >= FIN_CH || c >= C) return;
   dbeta[c] = (gbeta != 0.f ? gbeta * dbeta[c] : 0.f) + (float)s;
   dgamma[c] = (gbeta != 0.f ? gbeta * dgamma[c] : 0.f) + (float)q;
   const float a = gamma[c] * invstd[c];
@@ -670,7 +677,7 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
     slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
     fin = work;
   }
-  bn_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(fin, G ? G : T, C, count, gamma, beta, rmean,
+  bn_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G ? G : T, C, count, gamma, beta, rmean,
                                                        rvar, momentum, eps, scale, shift, mean,
                                                        invstd, num_batches);
 }
@@ -698,8 +705,10 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
 int bn_bwd_groups(long long M, int C);
 int bn_bwd_groups(long long M, int C) {
   const int RL = 256 / (C / 8);
-  long long g = (M + RL * 64 - 1) / (RL * 64);  // >= 64 rows per row lane
-  if (g > 1024) g = 1024;
+  // >= 16 rows per row lane (4 batched iterations): enough workgroups to keep every CU
+  // streaming on the small late layers (C 512 x 12544 rows -> 196 groups, not 49)
+  long long g = (M + RL * 16 - 1) / (RL * 16);
+  if (g > 2048) g = 2048;
   if (g < 1) g = 1;
   return (int)g;
 }
@@ -729,7 +738,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
     fin = part2;
   }
-  bn_bwd_finalize_kernel<<<(C + 63) / 64, 256, 0, st>>>(fin, G2 ? G2 : G, C, (double)M, gamma,
+  bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C, (double)M, gamma,
                                                         mean, invstd, dgamma, dbeta, gbeta, coef);
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
