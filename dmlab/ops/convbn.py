@@ -83,7 +83,9 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
     else:
         bm = 128 if cfg in (0, 2) else 64
         tiles = math.ceil(cout / bm) * math.ceil(K / 128)
-        max_split = max(1, M // 2048)  # >= 64 K-steps of 32 rows per split
+        # >= 8 row steps of 64 per split: the small-K layers (1x1/s2 downsample: K = Cin)
+        # have one or two output tiles, so the m-split is their only parallelism
+        max_split = max(1, M // 512)
     S = max(1, min(max_split, math.ceil(512 / tiles)))
     return cfg, S
 
