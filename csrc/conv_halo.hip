@@ -244,6 +244,18 @@ bool conv_halo_supported(const ConvGeom& g) {
 
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st) {
+  if (waves == 16) {  // 256-pixel tile, 4 x 2 waves of 64 x BN/2 (twice the weight reuse per FLOP)
+    const int hp2 = halo_rows_needed(g, 256);
+    const int hr = (hp2 + 63) / 64;
+#define DM_HALO256W8(BN_)                                                                    \
+  if (hr <= 5) launch_halo<BN_, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, st);                  \
+  else if (hr <= 6) launch_halo<BN_, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, st);             \
+  else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, st);
+    if (bn == 128) { DM_HALO256W8(128) } else { DM_HALO256W8(64) }
+#undef DM_HALO256W8
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   if (waves == 2) {  // 256-pixel tile: 2 x 2 waves of 128 x BN/2 (twice the weight reuse)
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 31) / 32;

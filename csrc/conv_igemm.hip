@@ -1301,9 +1301,10 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64, 4 waves;
   // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
   // 36 / 37: 256-pixel halo tile (2 x 2 waves of 128 x BN/2), BN 128 / 64
-  if (cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || cfg == 36 || cfg == 37) {
-    const int bn = (cfg == 20 || cfg == 24 || cfg == 36) ? 128 : 64;
-    const int waves = cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
+  // 38 / 39: 256-pixel halo tile with 4 x 2 waves of 64 x BN/2, BN 128 / 64
+  if (cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39)) {
+    const int bn = (cfg == 20 || cfg == 24 || cfg == 36 || cfg == 38) ? 128 : 64;
+    const int waves = cfg >= 38 ? 16 : cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
     if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st);
     // fallback keeps the row tile (stats slab rows = igemm_fwd_rowtile(cfg))
     if (cfg >= 36) {
@@ -1346,7 +1347,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return cfg == 36 || cfg == 37 ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return (cfg >= 36 && cfg <= 39) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -34,8 +34,10 @@ def _cpad(c):
 # Measured on MI355X (tools/bench_conv.py -> profiles/conv_kernels_r1.jsonl):
 #   * unit-stride 3x3 with >= 128 output channels: halo kernel (20) fastest
 #     (l2/l3/l4: 714/749/787 TFLOP/s fwd vs 661/708/730 for the best igemm tile);
-#   * 64 output channels at 56x56 (one 64-channel chunk): the 256-pixel halo tile (37),
-#     557/593 TFLOP/s fwd/dgrad vs 497/582 for the v3 depth-2 128x64 tile (16);
+#   * 64 output channels at 56x56 (one 64-channel chunk): the 256-pixel halo tile with
+#     8 waves (39), 549/663 TFLOP/s fwd/dgrad vs 497/582 for the v3 128x64 tile (16);
+#   * 512 output channels (layer4): the 256-pixel 8-wave halo tile (38), 737/786 vs
+#     697/748 for the 128-pixel one;
 #   * everything else (strided taps, stride-2 dgrad parity classes, 1x1/s2, stem):
 #     v3 tiles 15 / 13 / 11 by the block-count rule below; 256-row tiles lose
 #     (one workgroup per CU exposes the staging latency).
@@ -50,7 +52,9 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
         # 64 output channels: the 256-pixel halo tile (2 x 2 waves of 128 x 32) amortises
         # the single-chunk halo prologue over twice the rows
-        return 20 if ncols >= 128 else 37
+        if ncols >= 512:
+            return 38  # 256-pixel tile, 8 waves: half the weight staging per FLOP
+        return 20 if ncols >= 128 else 39
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
         t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
     elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:

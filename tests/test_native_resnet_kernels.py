@@ -29,7 +29,7 @@ HALO_GEOMS = [
     (3, 14, 256, 256, 3, 1, 1),
     (2, 14, 64, 128, 1, 1, 0),
 ]
-FWD_CFGS = list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27, 28, 34, 35, 36, 37]
+FWD_CFGS = list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39]
 
 
 def _rel(a, b):
@@ -64,14 +64,14 @@ def test_conv_fwd_and_stats(dev, geom, cfg):
 
 
 @pytest.mark.parametrize("geom", HALO_GEOMS)
-@pytest.mark.parametrize("cfg", [12, 20, 21, 24, 25, 36, 37])
+@pytest.mark.parametrize("cfg", [12, 20, 21, 24, 25, 36, 37, 38, 39])
 def test_conv_fwd_halo(dev, geom, cfg):
     _check_fwd(dev, geom, cfg)
 
 
 def _check_fwd(dev, geom, cfg):
     N, H, Cin, Cout, k, s, p = geom
-    if cfg in (0, 3, 6, 9, 12, 15, 18, 26, 34, 36) and Cout % 128:
+    if cfg in (0, 3, 6, 9, 12, 15, 18, 26, 34, 36, 38) and Cout % 128:
         pytest.skip("128-wide tile needs Cout % 128 == 0")
     x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
     ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
@@ -118,7 +118,7 @@ def test_conv_dgrad(dev, geom, accumulate, variant):
 
 @pytest.mark.parametrize("geom", HALO_GEOMS + GEOMS[:2] + GEOMS[3:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 27, 28, 34, 35, 36, 37])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39])
 def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)

@@ -76,7 +76,7 @@ def main():
         if "fwd" in a.passes:
             ref = None
             for cfg in cfgs:
-                if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24, 26, 34, 36) and Co % 128:
+                if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24, 26, 34, 36, 38) and Co % 128:
                     continue
                 M = N * OH * OH
                 T = L.conv_stats_rows(M, cfg)
@@ -90,7 +90,7 @@ def main():
         if "dgrad" in a.passes and name != "stem7x7":
             ref = None
             for cfg in cfgs:
-                if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24, 26, 34, 36) and C % 128:
+                if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24, 26, 34, 36, 38) and C % 128:
                     continue
                 t = timeit(lambda: L.conv_dgrad(dy, wd, dx, k, k, s, p, None, cfg), a.iters)
                 row[f"dgrad_c{cfg}_TF"] = round(flops / t / 1e12, 1)
