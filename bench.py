@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--phases", type=int, default=0,
+                    help="after the timed run, N extra eager steps timed per phase with HIP "
+                         "events (fwd, bwd compute, exposed comm, optimizer) -> 'phases_ms'")
     ap.add_argument("--small-allreduce", default="rccl", choices=["rccl", "xgmi"],
                     help="buckets <= 4 MB via the one-shot xGMI peer-memory kernel")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
@@ -135,6 +138,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     final_loss = float(loss)
+    phases = None
+    if a.phases > 0 and a.backend == "native":
+        phases = measure_phases(net, opt, pool, labels, a.phases)
     ms = dt / a.steps * 1e3
     value = bs * ws * a.steps / dt
     if rank == 0:
@@ -166,8 +172,36 @@ def main():
             },
             "final_loss": round(final_loss, 4),
         }
+        if phases is not None:
+            res["phases_ms"] = phases
         print(json.dumps(res), flush=True)
     env.destroy()
+
+
+def measure_phases(net, opt, pool, labels, n):
+    """Per-phase device time of n eager steps (HIP events, one sync at the end):
+    forward+loss, backward compute, communication still outstanding when backward
+    compute ends (exposed), optimizer."""
+    from dmlab.nn import cross_entropy
+
+    names = ("fwd", "bwd_compute", "comm_exposed", "opt")
+    acc = {k: 0.0 for k in names}
+    for i in range(n):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+        net.on_compute_done = ev[2].record
+        ev[0].record()
+        loss = cross_entropy(net(pool[i % 2]), labels[i % 2])
+        ev[1].record()
+        opt.zero_grad()
+        loss.backward()
+        ev[3].record()
+        opt.step()
+        ev[4].record()
+        net.on_compute_done = None
+        torch.cuda.synchronize()
+        for k, (a_, b_) in zip(names, ((0, 1), (1, 2), (2, 3), (3, 4))):
+            acc[k] += ev[a_].elapsed_time(ev[b_])
+    return {k: round(v / n, 3) for k, v in acc.items()}
 
 
 if __name__ == "__main__":

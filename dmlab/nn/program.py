@@ -22,6 +22,9 @@ while replacing the per-op autograd graph with an explicit schedule.
 """
 from __future__ import annotations
 
+import contextlib
+import os
+
 from typing import Callable, Optional
 
 import torch
@@ -110,14 +113,32 @@ class Layer(nn.Module):
         return self.torch_forward(x)
 
 
+_ROCTX = os.environ.get("DMLAB_ROCTX", "0") == "1"
+
+
+@contextlib.contextmanager
+def _range(name):
+    """roctx range (``DMLAB_ROCTX=1``) around a layer's forward/backward, visible in
+    ``rocprofv3 --marker-trace``; a no-op otherwise."""
+    if not _ROCTX:
+        yield
+        return
+    torch.cuda.nvtx.range_push(name)  # ROCm builds of torch route nvtx to roctx
+    try:
+        yield
+    finally:
+        torch.cuda.nvtx.range_pop()
+
+
 class _ProgramFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, anchor, prog):
         ctxs = []
         h = x
-        for layer in prog.layers:
+        for li, layer in enumerate(prog.layers):
             c = Ctx()
-            h = layer.fwd(h, c, True)
+            with _range(f"fwd:{li}:{type(layer).__name__}"):
+                h = layer.fwd(h, c, True)
             ctxs.append(c)
         ctx.prog = prog
         ctx.ctxs = ctxs
@@ -133,7 +154,8 @@ class _ProgramFn(torch.autograd.Function):
         for i in range(n - 1, -1, -1):
             layer = prog.layers[i]
             need_dx = i > 0 or ctx.need_dx
-            dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
+            with _range(f"bwd:{i}:{type(layer).__name__}"):
+                dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
             ctx.ctxs[i] = None  # free saved activations as soon as possible
             for hook in prog._grad_hooks:
                 hook(prog, i)

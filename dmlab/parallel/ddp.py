@@ -73,6 +73,9 @@ class DistributedDataParallel(nn.Module):
             self._setup_generic(bucket_cap_mb, first_bucket_mb)
         self.buckets_launched = 0
         self._sync_enabled = True
+        # optional callback at the end of backward COMPUTE, before the bucket waits
+        # (PhaseTimer uses it to measure the communication left exposed after backward)
+        self.on_compute_done = None
         self._xgmi = None
         if small_allreduce not in (None, "rccl", "xgmi"):
             raise ValueError("small_allreduce: None | 'rccl' | 'xgmi'")
@@ -209,6 +212,8 @@ class DistributedDataParallel(nn.Module):
             self._mark_ready(i)
 
     def _finalize(self):
+        if self.on_compute_done is not None:
+            self.on_compute_done()
         if not self._sync_enabled:
             if self.program is None:
                 self._final_queued = False
