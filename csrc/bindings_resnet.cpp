@@ -57,7 +57,10 @@ dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride,
 // y = conv(x, w)  (+add) ; stats [T][2][Cout] optional
 void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Tensor> stats,
               c10::optional<at::Tensor> add, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-              int64_t cfg) {
+              int64_t cfg, c10::optional<at::Tensor> pre_scale,
+              c10::optional<at::Tensor> pre_shift) {
+  // pre_scale/pre_shift: x is the previous conv's raw output and the conv consumes
+  // relu(x*pre_scale + pre_shift) (fused BN-apply + ReLU; halo kernels only)
   need_bf16_nhwc(x, "x");
   need_bf16_nhwc(y, "y");
   const int Cout = y.size(3), OH = y.size(1), OW = y.size(2);
@@ -77,6 +80,17 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
   const bf* ap = nullptr;
   if (add.has_value()) { need_bf16_nhwc(*add, "add"); TORCH_CHECK(add->sizes() == y.sizes()); ap = bp(*add); }
   const DeviceGuard guard(x.device());
+  if (pre_scale.has_value()) {
+    int bn, waves;
+    TORCH_CHECK(pre_shift.has_value(), "pre_scale needs pre_shift");
+    need_f32(*pre_scale, "pre_scale", x.size(3));
+    need_f32(*pre_shift, "pre_shift", x.size(3));
+    TORCH_CHECK(dm::halo_cfg((int)cfg, bn, waves) && dm::conv_halo_supported(g),
+                "fused pre-BN needs a halo-kernel cfg and a unit-stride 3x3 geometry");
+    dm::conv_halo(bp(x), bp(wpack), bp(y), ap, sp, g, bn, waves, cur_stream(), fp(*pre_scale),
+                  fp(*pre_shift));
+    return;
+  }
   dm::igemm_fwd(bp(x), bp(wpack), bp(y), ap, sp, g, cfg, cur_stream());
 }
 
@@ -151,7 +165,8 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
 // dw (fp32 OIHW [Cout][Cin][KH][KW]) = beta*dw + Σ_m dy ⊗ im2col(x)
 void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int64_t Cin,
                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, double beta, int64_t S,
-                int64_t cfg, bool s2d) {
+                int64_t cfg, bool s2d, c10::optional<at::Tensor> pre_scale,
+                c10::optional<at::Tensor> pre_shift) {
   // s2d: x/dy are the space-to-depth stem operands (4x4/s1 conv over 4*Cin channels);
   // dw is the original [Cout][Cin][7][7] gradient
   need_bf16_nhwc(x, "x");
@@ -165,7 +180,17 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   const long long mchunk = ((steps + S - 1) / S) * 64;  // multiple of both kernels' row step
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
-  dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
+  if (pre_scale.has_value()) {  // x = previous conv's raw output, operand relu(x*sc + sh)
+    TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
+    need_f32(*pre_scale, "pre_scale", x.size(3));
+    need_f32(*pre_shift, "pre_shift", x.size(3));
+    TORCH_CHECK((cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
+                "fused pre-BN needs the halo wgrad (cfg 4/5) and a 3x3/s1/p1 geometry");
+    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st,
+                   fp(*pre_scale), fp(*pre_shift));
+  } else {
+    dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
+  }
   if (s2d)
     dm::wgrad_reduce_s2d(fp(slab), (int)S, Cout, (int)Cin, g.C, fp(dw), (float)beta, st);
   else
@@ -389,10 +414,15 @@ void pack_input(at::Tensor x, at::Tensor y) {
 }  // namespace
 
 void register_resnet(pybind11::module_& m) {
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wpack"), py::arg("y"), py::arg("stats"),
+        py::arg("add"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
+        py::arg("cfg"), py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
   m.def("conv_stats_rows", &conv_stats_rows);
   m.def("conv_dgrad", &conv_dgrad);
-  m.def("conv_wgrad", &conv_wgrad);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
+        py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
+        py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),
+        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
   m.def("pack_weights", &pack_weights);
   m.def("pack_weights_multi", &pack_weights_multi);
   m.def("bn_stats_finalize", &bn_stats_finalize, py::arg("stats"), py::arg("T"), py::arg("count"),

@@ -36,10 +36,15 @@ constexpr int HBM = 128;  // output pixels per block (default tile)
 constexpr int HBK = 64;   // channels per chunk (one 128-B LDS row per pixel)
 constexpr unsigned OOB = 0x80000000u;
 
-template <int BN, int HR, int WM, int WN, int BMH>
-__global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
+// 8-wave BN-64 tiles must stay <= 128 VGPRs to keep two workgroups (4 waves) per SIMD
+template <int BN, int HR, int WM, int WN, int BMH, bool PRE>
+__global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
-    float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes) {
+    float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
+  // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
+  // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
+  // image taps still read the zero row, i.e. the padding stays zero AFTER the BN.
   constexpr int TM = BMH / WM, TN = BN / WN;
   constexpr int RM = TM / 32, RN = TN / 32;
   constexpr int NT = WM * WN * 64, RPP = NT / 8;     // threads, staged rows per pass
@@ -110,11 +115,24 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
       rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
-  auto store_halo = [&]() {
+  auto store_halo = [&](int cc) {
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
       const int hh = (tid >> 3) + RPP * j;
       *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) = rh[j];
+    }
+    if constexpr (PRE) {
+      // normalise in place once the staging registers are dead (each thread rewrites
+      // only its own chunks: program order suffices, no barrier), so the fused BN costs
+      // no registers across the tap loop
+      PreBN pbn;
+      pbn.load(pre_sc, pre_sh, cc * HBK + chunk * 8);
+#pragma unroll
+      for (int j = 0; j < HR; ++j) {
+        const int hh = (tid >> 3) + RPP * j;
+        uint4* q = reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8);
+        *q = pbn.apply(*q);
+      }
     }
   };
   auto load_b = [&](int cc, int t) {
@@ -183,7 +201,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
   const int S = nchunk * ntaps;
   load_halo(0);
   load_b(0, 0);
-  store_halo();
+  store_halo(0);
   store_b(0);
   __syncthreads();
   if (nchunk > 1) load_halo(1);
@@ -199,7 +217,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 2) conv_halo_kernel(
     if (s + 1 < S) store_b((s + 1) & 1);
     __syncthreads();
     if (ncc != cc && s + 1 < S) {
-      store_halo();  // every wave is past the last tap of chunk cc
+      store_halo(ncc);  // every wave is past the last tap of chunk cc
       __syncthreads();
       if (ncc + 1 < nchunk) load_halo(ncc + 1);
     }
@@ -216,7 +234,7 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
 
 template <int BN, int HR, int WM, int WN, int BMH = HBM>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                 const ConvGeom& g, hipStream_t st) {
+                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
@@ -224,9 +242,10 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   dim3 grid((unsigned)((g.M + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = conv_halo_kernel<BN, HR, WM, WN, BMH>;
+  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true>
+                  : conv_halo_kernel<BN, HR, WM, WN, BMH, false>;
   set_smem_attr(k, sm);
-  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh);
 }
 }  // namespace
 
@@ -243,14 +262,15 @@ bool conv_halo_supported(const ConvGeom& g) {
 }
 
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int bn, int waves, hipStream_t st) {
+               const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
+               const float* pre_sh) {
   if (waves == 16) {  // 256-pixel tile, 4 x 2 waves of 64 x BN/2 (twice the weight reuse per FLOP)
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 63) / 64;
 #define DM_HALO256W8(BN_)                                                                    \
-  if (hr <= 5) launch_halo<BN_, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, st);                  \
-  else if (hr <= 6) launch_halo<BN_, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, st);             \
-  else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, st);
+  if (hr <= 5) launch_halo<BN_, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);                  \
+  else if (hr <= 6) launch_halo<BN_, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);             \
+  else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     if (bn == 128) { DM_HALO256W8(128) } else { DM_HALO256W8(64) }
 #undef DM_HALO256W8
     DM_CHECK(hipGetLastError());
@@ -260,9 +280,9 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 31) / 32;
 #define DM_HALO256(BN_)                                                                      \
-  if (hr <= 10) launch_halo<BN_, 10, 2, 2, 256>(X, Wp, Y, ADD, stats, g, st);                \
-  else if (hr <= 12) launch_halo<BN_, 12, 2, 2, 256>(X, Wp, Y, ADD, stats, g, st);           \
-  else launch_halo<BN_, 14, 2, 2, 256>(X, Wp, Y, ADD, stats, g, st);
+  if (hr <= 10) launch_halo<BN_, 10, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);                \
+  else if (hr <= 12) launch_halo<BN_, 12, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
+  else launch_halo<BN_, 14, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     if (bn == 128) { DM_HALO256(128) } else { DM_HALO256(64) }
 #undef DM_HALO256
     DM_CHECK(hipGetLastError());
@@ -272,17 +292,17 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   if (waves == 8) {  // 4 x 2 waves of 32 x BN/2
     const int hr = hp <= 192 ? 3 : hp <= 256 ? 4 : 6;
 #define DM_HALO8(BN_)                                                            \
-  if (hr == 3) launch_halo<BN_, 3, 4, 2>(X, Wp, Y, ADD, stats, g, st);           \
-  else if (hr == 4) launch_halo<BN_, 4, 4, 2>(X, Wp, Y, ADD, stats, g, st);      \
-  else launch_halo<BN_, 6, 4, 2>(X, Wp, Y, ADD, stats, g, st);
+  if (hr == 3) launch_halo<BN_, 3, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
+  else if (hr == 4) launch_halo<BN_, 4, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);      \
+  else launch_halo<BN_, 6, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     if (bn == 128) { DM_HALO8(128) } else { DM_HALO8(64) }
 #undef DM_HALO8
   } else {  // 2 x 2 waves of 64 x BN/2
     const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
 #define DM_HALO4(BN_)                                                            \
-  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, st);           \
-  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, st);      \
-  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, st);
+  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
+  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);      \
+  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     if (bn == 128) { DM_HALO4(128) } else { DM_HALO4(64) }
 #undef DM_HALO4
   }

@@ -1294,6 +1294,15 @@ static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16
   k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
 }
 
+// halo-kernel configs (conv_halo.hip): 20/21 128-pixel 4 waves, 24/25 128-pixel 8 waves,
+// 36/37 256-pixel 2x2 waves, 38/39 256-pixel 4x2 waves; even = BN 128, odd = BN 64
+bool halo_cfg(int cfg, int& bn, int& waves) {
+  if (!(cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39))) return false;
+  bn = (cfg == 20 || cfg == 24 || cfg == 36 || cfg == 38) ? 128 : 64;
+  waves = cfg >= 38 ? 16 : cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
+  return true;
+}
+
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st) {
   // v3 with two tiles of register prefetch: 15 = 128x128 mf32, 16 = 128x64 mf32, 17 = 64x64
@@ -1302,9 +1311,8 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
   // 36 / 37: 256-pixel halo tile (2 x 2 waves of 128 x BN/2), BN 128 / 64
   // 38 / 39: 256-pixel halo tile with 4 x 2 waves of 64 x BN/2, BN 128 / 64
-  if (cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39)) {
-    const int bn = (cfg == 20 || cfg == 24 || cfg == 36 || cfg == 38) ? 128 : 64;
-    const int waves = cfg >= 38 ? 16 : cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
+  int bn, waves;
+  if (halo_cfg(cfg, bn, waves)) {
     if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st);
     // fallback keeps the row tile (stats slab rows = igemm_fwd_rowtile(cfg))
     if (cfg >= 36) {

@@ -23,6 +23,35 @@ __device__ __forceinline__ unsigned fdiv(unsigned n, unsigned mul, unsigned shr)
 // 16- and 32-row fragment reads of both MFMA shapes
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// Fused BatchNorm-apply + ReLU of a staged 16-B chunk (8 bf16 channels c0..c0+7):
+// v = max(v * sc[c] + sh[c], 0).  Used by the halo kernels to read a conv's RAW output and
+// consume BN(y) directly, so the normalised activation is never written to memory.
+struct PreBN {
+  float sc[8], sh[8];
+  __device__ __forceinline__ void load(const float* __restrict__ scale,
+                                       const float* __restrict__ shift, int c0) {
+    const float4 a = *reinterpret_cast<const float4*>(scale + c0);
+    const float4 b = *reinterpret_cast<const float4*>(scale + c0 + 4);
+    const float4 c = *reinterpret_cast<const float4*>(shift + c0);
+    const float4 d = *reinterpret_cast<const float4*>(shift + c0 + 4);
+    sc[0] = a.x; sc[1] = a.y; sc[2] = a.z; sc[3] = a.w;
+    sc[4] = b.x; sc[5] = b.y; sc[6] = b.z; sc[7] = b.w;
+    sh[0] = c.x; sh[1] = c.y; sh[2] = c.z; sh[3] = c.w;
+    sh[4] = d.x; sh[5] = d.y; sh[6] = d.z; sh[7] = d.w;
+  }
+  __device__ __forceinline__ uint4 apply(uint4 v) const {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float lo = fmaxf(bf2f((bf16_t)(w[q] & 0xffff)) * sc[2 * q] + sh[2 * q], 0.f);
+      const float hi = fmaxf(bf2f((bf16_t)(w[q] >> 16)) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
+      o[q] = pack_bf2(lo, hi);
+    }
+    return make_uint4(o[0], o[1], o[2], o[3]);
+  }
+};
+
 template <bool MF32>
 using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 

@@ -62,11 +62,14 @@ struct ConvGeom;
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st);
 bool conv_halo_supported(const ConvGeom& g);
+bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int bn, int waves, hipStream_t st);
+               const ConvGeom& g, int bn, int waves, hipStream_t st,
+               const float* pre_sc = nullptr, const float* pre_sh = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
-                long long mchunk, int nty, hipStream_t st);
+                long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
+                const float* pre_sh = nullptr);
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
                         hipStream_t st);
 int igemm_fwd_rowtile(int cfg);

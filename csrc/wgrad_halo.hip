@@ -45,10 +45,13 @@ __device__ __forceinline__ s4 tr_read(const bf16_t* p) {
 
 // NTY = kernel rows (dy values) per block: 3 = all 9 taps share the dY fragments; 1 = one
 // row of 3 taps (smaller halo, 3x more output tiles -> 3x fewer m-splits and slab bytes)
-template <int HRN, int NTY>
+template <int HRN, int NTY, bool PRE>
 __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
-    ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes) {
+    ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes,
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
+  // pre_sc/pre_sh (optional): X is the previous conv's raw output; the operand is
+  // relu(x*sc + sh) applied while staging (out-of-image taps read the zero row)
   constexpr int HROWS_MAX = HRN * 32;  // halo rows a buffer holds (8 chunks per row)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][64][WPITCH] dY
@@ -92,6 +95,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     }
   };
   auto store = [&](int buf) {
+    PreBN pbn;  // PRE: loaded per store (L1 hits) instead of 16 registers live all kernel
+    if constexpr (PRE) pbn.load(pre_sc, pre_sh, cc0 + chunk * 8);
     bf16_t* as = As + buf * WBK * WPITCH;
     bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
 #pragma unroll
@@ -99,7 +104,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
       *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
 #pragma unroll
     for (int j = 0; j < HRN; ++j)
-      *reinterpret_cast<uint4*>(hs + (row0 + 32 * j) * WPITCH + chunk * 8) = rh[j];
+      *reinterpret_cast<uint4*>(hs + (row0 + 32 * j) * WPITCH + chunk * 8) =
+          PRE ? pbn.apply(rh[j]) : rh[j];
   };
 
   f32x4 acc[4][NT];
@@ -183,14 +189,15 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
 
 template <int HRN, int NTY>
 void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
-                       long long mchunk, hipStream_t st) {
+                       long long mchunk, hipStream_t st, const float* pre_sc,
+                       const float* pre_sh) {
   const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
   dim3 grid((g.Ncols + WBM - 1) / WBM, (g.C / WBC) * (3 / NTY), S);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
-  auto k = wgrad_halo_kernel<HRN, NTY>;
+  auto k = pre_sc ? wgrad_halo_kernel<HRN, NTY, true> : wgrad_halo_kernel<HRN, NTY, false>;
   set_smem_attr(k, sm);
-  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db);
+  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh);
 }
 }  // namespace
 
@@ -206,14 +213,15 @@ bool wgrad_halo_supported(const ConvGeom& g) {
 }
 
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
-                long long mchunk, int nty, hipStream_t st) {
+                long long mchunk, int nty, hipStream_t st, const float* pre_sc,
+                const float* pre_sh) {
   if (nty == 1) {
-    launch_wgrad_halo<3, 1>(X, DY, slab, g, S, mchunk, st);  // 66 rows
+    launch_wgrad_halo<3, 1>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);  // 66 rows
   } else {
     const int rows = WBK + 2 * g.W + 2;
-    if (rows <= 96) launch_wgrad_halo<3, 3>(X, DY, slab, g, S, mchunk, st);
-    else if (rows <= 128) launch_wgrad_halo<4, 3>(X, DY, slab, g, S, mchunk, st);
-    else launch_wgrad_halo<6, 3>(X, DY, slab, g, S, mchunk, st);
+    if (rows <= 96) launch_wgrad_halo<3, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);
+    else if (rows <= 128) launch_wgrad_halo<4, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);
+    else launch_wgrad_halo<6, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);
   }
   DM_CHECK(hipGetLastError());
 }

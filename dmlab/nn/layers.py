@@ -150,10 +150,13 @@ class ConvBN(Layer):
             y = y + residual
         return F.relu(y) if self.relu else y
 
-    def native_fwd(self, x, ctx, train, residual=None):
+    def native_fwd(self, x, ctx, train, residual=None, raw=False, pre=None):
+        """raw: return the conv output y un-normalised (BN scale/shift left in ctx for the
+        consumer); pre=(scale, shift): x is a raw conv output to be consumed as
+        relu(x*scale + shift) — the BN-apply of the previous layer fused into this conv."""
         from dmlab.ops import convbn as CB
 
-        return CB.convbn_fwd(self, x, ctx, train, residual)
+        return CB.convbn_fwd(self, x, ctx, train, residual, raw=raw, pre=pre)
 
     def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None):
         from dmlab.ops import convbn as CB
@@ -192,8 +195,10 @@ class BasicBlock(Layer):
     def native_fwd(self, x, ctx, train):
         c1, c2, cd = Ctx(), Ctx(), Ctx()
         idt = x if self.down is None else self.down.native_fwd(x, cd, train)
-        y = self.c1.native_fwd(x, c1, train)
-        out = self.c2.native_fwd(y, c2, train, residual=idt)
+        # c1's BN-apply + ReLU is fused into c2's operand staging: relu(bn1(y1)) is never
+        # written (c2's forward and weight-gradient halo kernels normalise y1 on the fly)
+        y1 = self.c1.native_fwd(x, c1, train, raw=True)
+        out = self.c2.native_fwd(y1, c2, train, residual=idt, pre=(c1["scale"], c1["shift"]))
         ctx.update(c1=c1, c2=c2, cd=cd)
         return out
 

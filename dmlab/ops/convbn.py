@@ -183,7 +183,14 @@ def pack_all(prog, layers):
         object.__setattr__(m, "_wcache", (ver, wf, wd))
 
 
-def convbn_fwd(layer, x, ctx, train, residual=None):
+def _materialise(x, pre):
+    """relu(x*scale + shift) as a tensor (fallback when a consumer cannot fuse it)."""
+    out = empty_nhwc(*x.shape, x)
+    lib().bn_apply(x, None, pre[0], pre[1], out, True)
+    return out
+
+
+def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     L = lib()
     first = not (x.dim() == 4 and getattr(x, "_dm_nhwc", False))
     s2d = first and use_s2d(layer, x)
@@ -209,6 +216,13 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
         wf, _ = packed_weights(layer, need_wd=train and not first)
     y = empty_nhwc(N, OH, OW, cout, x)
     cfg = pick_cfg(M, cout, k, s, C)
+    pre_kw = {}
+    if pre is not None:
+        if cfg in (20, 21, 24, 25, 36, 37, 38, 39):
+            pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
+        else:  # not a halo-kernel shape: materialise the previous BN output
+            x = _materialise(x, pre)
+            pre = None
     f32 = dict(device=x.device, dtype=torch.float32)
     scale = torch.empty(cout, **f32)
     shift = torch.empty(cout, **f32)
@@ -216,7 +230,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
     if use_batch:
         T = L.conv_stats_rows(M, cfg)
         stats = torch.empty(T * 2 * cout, **f32)
-        L.conv_fwd(x, wf, y, stats, None, k, k, s, p, cfg)
+        L.conv_fwd(x, wf, y, stats, None, k, k, s, p, cfg, **pre_kw)
         mean = torch.empty(cout, **f32)
         invstd = torch.empty(cout, **f32)
         work = torch.empty(256 * 2 * cout, **f32)
@@ -224,13 +238,16 @@ def convbn_fwd(layer, x, ctx, train, residual=None):
                             layer.running_mean, layer.running_var, layer.momentum, layer.eps,
                             scale, shift, mean, invstd, work, layer.num_batches_tracked)
     else:
-        L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg)
+        L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg, **pre_kw)
         L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
                          layer.running_var, layer.eps, scale, shift)
         mean = invstd = None
     if train:
         ctx.update(x=x, y=y, mean=mean, invstd=invstd, has_res=residual is not None,
-                   first=first, s2d=s2d, scale=scale, shift=shift)
+                   first=first, s2d=s2d, scale=scale, shift=shift, pre=pre)
+    if raw:
+        ctx["scale"], ctx["shift"] = scale, shift
+        return y
     pool = getattr(layer, "pool_k", 0)
     if pool:
         # fused BN + ReLU + max-pool: the BN output is never materialised
@@ -285,7 +302,15 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     K = k * k * C
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
     slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
-    L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg, s2d)
+    pre = ctx.get("pre")
+    pre_kw = {}
+    if pre is not None:
+        if wcfg in (4, 5):
+            pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
+        else:
+            x = _materialise(x, pre)
+    L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg, s2d,
+                 **pre_kw)
     dx = None
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)

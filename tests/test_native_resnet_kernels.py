@@ -318,3 +318,47 @@ def test_bn_stats_finalize_slab_rows(dev, T):
     var = (qd / M - mu * mu).clamp_min(0)
     torch.testing.assert_close(mean.double(), mu, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("geom", [g for g in HALO_GEOMS if g[4] == 3])
+@pytest.mark.parametrize("cfg", [20, 21, 38, 39])
+def test_conv_fwd_prebn(dev, geom, cfg):
+    """Halo conv consuming relu(y*scale + shift) of a RAW previous-conv output (fused
+    BN-apply + ReLU in the staging); zero padding stays zero after the BN."""
+    N, H, Cin, Cout, k, s, p = geom
+    g = torch.Generator(device=dev).manual_seed(2)
+    y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    sc = torch.rand(Cin, device=dev, generator=g) + 0.5
+    sh = torch.randn(Cin, device=dev, generator=g) * 0.5
+    w = torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k)
+    wf = torch.empty(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16)
+    lib().pack_weights(w.contiguous(), wf, None, Cin)
+    a = (y.float() * sc + sh).relu().bfloat16().float()
+    ref = F.conv2d(_nchw(a), w.bfloat16().float(), None, s, p)
+    out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
+    M = N * H * H
+    T = lib().conv_stats_rows(M, cfg)
+    stats = torch.empty(T * 2 * Cout, device=dev)
+    lib().conv_fwd(y, wf, out, stats, None, k, k, s, p, cfg, pre_scale=sc, pre_shift=sh)
+    assert _rel(_nchw(out), ref) < 6e-3
+    st = stats.view(T, 2, Cout).sum(0)
+    torch.testing.assert_close(st[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
+
+
+@pytest.mark.parametrize("geom", [g for g in HALO_GEOMS if g[4] == 3])
+@pytest.mark.parametrize("cfg", [4, 5])
+def test_conv_wgrad_prebn(dev, geom, cfg):
+    N, H, Cin, Cout, k, s, p = geom
+    g = torch.Generator(device=dev).manual_seed(3)
+    y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    sc = torch.rand(Cin, device=dev, generator=g) + 0.5
+    sh = torch.randn(Cin, device=dev, generator=g) * 0.5
+    a = (y.float() * sc + sh).relu().bfloat16().float()
+    dy = torch.randn(N, Cout, H, H, device=dev, generator=g).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(_nchw(a), (Cout, Cin, k, k), dy.float(), s, p)
+    S = 2
+    slab = torch.empty(S * Cout * k * k * Cin, device=dev)
+    d = torch.empty(Cout, Cin, k, k, device=dev)
+    lib().conv_wgrad(y, _nhwc(dy), d, slab, Cin, k, k, s, p, 0.0, S, cfg, False,
+                     pre_scale=sc, pre_shift=sh)
+    assert _rel(d, ref) < 2e-3
