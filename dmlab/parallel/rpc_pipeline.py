@@ -33,7 +33,12 @@ class RPCStage(nn.Module):
 
     def __init__(self, kind: str, arg: int, device: str = "cpu"):
         super().__init__()
+        if device == "cuda":  # one GPU per stage owner: worker k -> GPU (k-1) mod #GPUs
+            wid = rpc.get_worker_info().id
+            device = f"cuda:{(wid - 1) % max(1, torch.cuda.device_count())}"
         self.device = torch.device(device)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
         self.module = (SubNetConv(arg) if kind == "conv" else SubNetFC(arg)).to(self.device)
 
     def forward(self, x):

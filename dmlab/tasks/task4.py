@@ -14,7 +14,7 @@ driver ``worker0`` (data, loss, ``DistributedOptimizer``), ranks 1/2 own
   tp        "horizontal" split: conv trunk replicated, fc head column/row
             tensor-parallel with one all-reduce per direction; any #ranks
 
-    torchrun --nproc-per-node 3 -m dmlab.tasks.task4 --mode rpc
+    torchrun --nproc-per-node 3 -m dmlab.tasks.task4 --mode rpc [--device cuda]
     torchrun --nproc-per-node 2 -m dmlab.tasks.task4 --mode pipeline --micro 4
 """
 from __future__ import annotations
@@ -82,7 +82,8 @@ def run_rpc(a):
     if rank == 0:
         print("Device {} starts training ...".format(rank))
         train_loader, test_loader = _data(a, torch.device("cpu"))
-        model = ParallelNet(1, 10, relay=a.relay)
+        sdev = "cuda" if a.device == "cuda" else "cpu"  # stage owners' GPUs (BASELINE cfg 4)
+        model = ParallelNet(1, 10, relay=a.relay, devices=(sdev, sdev))
         opt = make_distributed_optimizer(model, lr=a.lr)
         loss_fn = CrossEntropyLoss()
         t0 = time.perf_counter()

@@ -109,3 +109,24 @@ def test_two_ranks_one_gpu(kind):
     for rank, err, tb in res:
         assert tb is None, tb
         assert err < 2e-4, (rank, err)
+
+
+def test_rpc_stages_on_gpu(tmp_path):
+    """BASELINE config 4: the reference RPC/RRef programming model with both stage owners
+    on the GPU (native HIP kernels inside each stage; the box has one GPU, so both share it)."""
+    import re
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    env = dict(os.environ, PYTHONPATH=str(root), OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "3",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+                        "dmlab.tasks.task4", "--mode", "rpc", "--device", "cuda", "--synthetic",
+                        "--train-samples", "3200", "--epochs", "1", "--lr", "0.05"],
+                       cwd=tmp_path, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ls = [float(x) for x in re.findall(r"loss: (\d+\.\d+)", r.stdout)]
+    assert len(ls) == 5 and ls[-1] < ls[0]
+    assert "Test set: Accuracy" in r.stdout
