@@ -113,10 +113,13 @@ def main():
     if a.graph and a.backend == "native":
         from dmlab.utils.graph import CapturedStep
 
-        captured = CapturedStep(train_step, [pool[0], labels[0]], warmup=3)
+        # one graph per device-resident batch slot, bound to it (no per-step input copy,
+        # as with a loader that prefetches straight into the graph's input buffer)
+        captured = [CapturedStep(train_step, [pool[k], labels[k]], warmup=3, bind_inputs=True)
+                    for k in range(2)]
 
         def step(i):
-            return captured(pool[i % 2], labels[i % 2])
+            return captured[i % 2](pool[i % 2], labels[i % 2])
     else:
         def step(i):
             return train_step(pool[i % 2], labels[i % 2])

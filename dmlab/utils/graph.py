@@ -10,7 +10,9 @@ replayed with a single launch per step.
 Requirements honoured by the engine: no host synchronisation inside a step, all
 temporaries from the caching allocator (graph-private pool during capture), and
 state that changes every step (weights, momentum, BN running stats) kept in
-device tensors.  Inputs are copied into static buffers before each replay.
+device tensors.  Inputs are copied into static buffers before each replay, or, with
+``bind_inputs=True``, the example inputs ARE the static buffers (a loader that fills
+them in place — or one graph per device-resident batch slot — skips the copy).
 """
 from __future__ import annotations
 
@@ -22,9 +24,10 @@ class CapturedStep:
     iterations on a side stream (so lazy initialisation, allocator growth and the
     optimiser's first-step branch happen outside the capture)."""
 
-    def __init__(self, step_fn, example_inputs, warmup: int = 3):
+    def __init__(self, step_fn, example_inputs, warmup: int = 3, bind_inputs: bool = False):
         self.step_fn = step_fn
-        self.static_inputs = [t.detach().clone() for t in example_inputs]
+        self.static_inputs = [t.detach() if bind_inputs else t.detach().clone()
+                              for t in example_inputs]
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -39,7 +42,7 @@ class CapturedStep:
 
     def __call__(self, *inputs):
         for dst, src in zip(self.static_inputs, inputs):
-            if src is not dst:
+            if src is not dst and src.data_ptr() != dst.data_ptr():
                 dst.copy_(src, non_blocking=True)
         self.graph.replay()
         self.replays += 1
