@@ -1,21 +1,62 @@
-"""Summarise a rocprofv3 kernel-stats CSV into per-step times (ms) per kernel family."""
+"""Summarise rocprofv3 kernel times into per-step times (ms) per kernel family.
+
+    python tools/prof_summary.py <kernel_stats.csv | results.db> [steps] [--last K]
+
+Accepts the ``--stats`` CSV (``*_kernel_stats.csv``) or the SQLite database that
+rocprofv3 writes by default (``*_results.db``).  With a database, ``--last K`` keeps
+only the last K dispatches of the most frequent kernel family boundary, i.e. drops
+warmup: the timed window is the final ``steps`` fraction of the trace.
+"""
 import csv
 import re
+import sqlite3
 import sys
 from collections import defaultdict
 
-path, steps = sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
-rows = list(csv.DictReader(open(path)))
-fam = defaultdict(float)
-tot = 0.0
-for r in rows:
-    n = r["Name"]
+
+def family(n):
     key = re.sub(r"\(.*", "", n.replace("(anonymous namespace)::", ""))
-    key = re.sub(r"<.*>", lambda m: m.group(0)[:40], key)
-    t = float(r["TotalDurationNs"]) / 1e6 / steps
-    fam[key] += t
-    tot += t
-for k, v in sorted(fam.items(), key=lambda kv: -kv[1]):
-    if v > 0.01:
-        print(f"{v:8.3f} ms  {100 * v / tot:5.1f}%  {k}")
-print(f"{tot:8.3f} ms  total GPU kernel time per step")
+    return re.sub(r"<.*>", lambda m: m.group(0)[:40], key)
+
+
+def rows_csv(path):
+    for r in csv.DictReader(open(path)):
+        yield r["Name"], float(r["TotalDurationNs"])
+
+
+def rows_db(path, keep_frac=None):
+    c = sqlite3.connect(path)
+    rs = list(c.execute("select name, start, end from kernels order by start"))
+    if keep_frac:
+        rs = rs[int(len(rs) * (1 - keep_frac)):]
+    for n, s, e in rs:
+        yield n, float(e - s)
+
+
+def main():
+    args = [a for a in sys.argv[1:]]
+    frac = None
+    if "--frac" in args:
+        i = args.index("--frac")
+        frac = float(args[i + 1])
+        del args[i:i + 2]
+    path = args[0]
+    steps = float(args[1]) if len(args) > 1 else 1.0
+    rows = rows_db(path, frac) if path.endswith(".db") else rows_csv(path)
+    fam = defaultdict(float)
+    cnt = defaultdict(int)
+    tot = 0.0
+    for n, ns in rows:
+        t = ns / 1e6 / steps
+        k = family(n)
+        fam[k] += t
+        cnt[k] += 1
+        tot += t
+    for k, v in sorted(fam.items(), key=lambda kv: -kv[1]):
+        if v > 0.01:
+            print(f"{v:8.3f} ms  {100 * v / tot:5.1f}%  {cnt[k] / steps:5.1f}/step  {k}")
+    print(f"{tot:8.3f} ms  total GPU kernel time per step")
+
+
+if __name__ == "__main__":
+    main()
