@@ -247,6 +247,18 @@ void pack_weights_multi(at::Tensor desc, at::Tensor prefix, int64_t total) {
                          total, cur_stream());
 }
 
+// LDS-tiled variant: tprefix[l] = first 32x32 (co, ci) tile of layer l
+void pack_weights_tiled(at::Tensor desc, at::Tensor tprefix, int64_t ntiles) {
+  TORCH_CHECK(desc.is_cuda() && tprefix.is_cuda() && desc.scalar_type() == at::kLong &&
+              tprefix.scalar_type() == at::kInt, "desc int64 / tprefix int32 device tensors");
+  const int nl = tprefix.numel() - 1;
+  TORCH_CHECK(nl >= 1 && nl <= 32 && desc.numel() == 8 * nl, "pack_weights_tiled: 1..32 layers");
+  TORCH_CHECK(ntiles >= 1 && ntiles < (1 << 24), "pack_weights_tiled: tile count");
+  const DeviceGuard guard(desc.device());
+  dm::pack_weights_tiled((const long long*)desc.data_ptr(), tprefix.data_ptr<int>(), nl, (int)ntiles,
+                         cur_stream());
+}
+
 void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gamma, at::Tensor beta,
                        c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
                        double momentum, double eps, at::Tensor scale, at::Tensor shift,
@@ -425,6 +437,7 @@ void register_resnet(pybind11::module_& m) {
         py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
   m.def("pack_weights", &pack_weights);
   m.def("pack_weights_multi", &pack_weights_multi);
+  m.def("pack_weights_tiled", &pack_weights_tiled);
   m.def("bn_stats_finalize", &bn_stats_finalize, py::arg("stats"), py::arg("T"), py::arg("count"),
         py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),

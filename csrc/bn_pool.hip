@@ -404,6 +404,167 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
   }
 }
 
+// ------------------------------------------------------------------ stem BN backward, quads
+// 3x3/s2/p1 max-pool after the stem (even H, W): the 2x2 pixel quad (2qa+dy, 2qb+dx) is
+// covered by exactly the pooled windows (qa+wa, qb+wb), wa, wb in {0, 1}; pixel row dy=0
+// lies in window row 1 of wa=0 only, dy=1 in row 2 of wa=0 and row 0 of wa=1 (same for
+// columns).  One thread handles a quad x 8 channels: the 4 pooled gradients + argmax codes
+// are loaded once for 4 pixels (the per-pixel gather loaded them for every pixel: 4x the
+// L2 traffic, which bound those passes at ~2.4 TB/s).
+struct QuadPool {
+  uint4 y[4];
+  uint4 gv[4];
+  uint2 ix[4];
+  bool ok[4];
+  float d[4][8];
+  long long pix0;
+  // issue every load of quad q (8 channels `chunk`); consumed by finish()
+  __device__ __forceinline__ void load(const BnBwdArgs& a, unsigned q, int chunk, int C8) {
+    const int W2 = a.W >> 1, H2 = a.H >> 1;
+    const unsigned qb = q % (unsigned)W2;
+    const unsigned t = q / (unsigned)W2;
+    const unsigned qa = t % (unsigned)H2;
+    const unsigned n = t / (unsigned)H2;
+    pix0 = ((long long)n * a.H + 2 * qa) * a.W + 2 * qb;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      y[p] = reinterpret_cast<const uint4*>(a.y)[(pix0 + (p >> 1) * a.W + (p & 1)) * C8 + chunk];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const unsigned oh = qa + (w >> 1), ow = qb + (w & 1);
+      ok[w] = oh < (unsigned)a.OH && ow < (unsigned)a.OW;
+      const long long o = (((long long)n * a.OH + (ok[w] ? oh : qa)) * a.OW + (ok[w] ? ow : qb)) * C8 + chunk;
+      ix[w] = reinterpret_cast<const uint2*>(a.pidx)[o];
+      gv[w] = reinterpret_cast<const uint4*>(a.pdy)[o];
+    }
+  }
+  // d[p] = ReLU-masked gradient of pixel p gathered from the windows whose argmax it is
+  __device__ __forceinline__ void finish(int chunk, const float* sc, const float* sh) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[p][j] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (!ok[w]) continue;
+      const int wa = w >> 1, wb = w & 1;
+      float g[8];
+      unpack8(gv[w], g);
+      const uint32_t aw[2] = {ix[w].x, ix[w].y};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int dy = p >> 1, dx = p & 1;
+        if (wa == 1 && dy == 0) continue;  // pixel row outside the window
+        if (wb == 1 && dx == 0) continue;
+        const unsigned code = (unsigned)((dy ? (wa ? 0 : 2) : 1) * 3 + (dx ? (wb ? 0 : 2) : 1));
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[p][j] += g[j];
+      }
+    }
+    const int c0 = chunk * 8;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float yv[8];
+      unpack8(y[p], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[p][j] = (yv[j] * sc[c0 + j] + sh[c0 + j]) > 0.f ? d[p][j] : 0.f;
+    }
+  }
+};
+
+__global__ void __launch_bounds__(256) bn_bwd_reduce_quad_kernel(BnBwdArgs a, float* __restrict__ part) {
+  extern __shared__ float red[];  // [256][16] partials, then [2][C] scale/shift
+  const int C = a.C, C8 = C >> 3;
+  float* sc = red + 256 * 16;
+  float* sh = sc + C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sc[c] = a.scale[c];
+    sh[c] = a.shift[c];
+  }
+  __syncthreads();
+  const int chunk = threadIdx.x % C8, rl = threadIdx.x / C8, RL = blockDim.x / C8;
+  const int c0 = chunk * 8;
+  float mu[8], is[8], s[8], qq[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = a.mean[c0 + j];
+    is[j] = a.invstd[c0 + j];
+    s[j] = 0.f;
+    qq[j] = 0.f;
+  }
+  const unsigned nq = (unsigned)(a.M >> 2);
+  const unsigned qs = gridDim.x * RL;
+  // two quads in flight per thread (all 24 loads issued before either is consumed)
+  for (unsigned q = blockIdx.x * RL + rl; q < nq; q += 2 * qs) {
+    QuadPool qp[2];
+    const bool two = q + qs < nq;
+    qp[0].load(a, q, chunk, C8);
+    qp[1].load(a, two ? q + qs : q, chunk, C8);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (u == 1 && !two) break;
+      qp[u].finish(chunk, sc, sh);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float yv[8];
+        unpack8(qp[u].y[p], yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          s[j] += qp[u].d[p][j];
+          qq[j] += qp[u].d[p][j] * (yv[j] - mu[j]) * is[j];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[threadIdx.x * 16 + j] = s[j];
+    red[threadIdx.x * 16 + 8 + j] = qq[j];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < C8 * 16; e += blockDim.x) {
+    const int ch = e / 16, j = e % 16;
+    float acc = 0.f;
+    for (int l = 0; l < RL; ++l) acc += red[(l * C8 + ch) * 16 + j];
+    const int c = ch * 8 + (j & 7);
+    part[(long long)blockIdx.x * 2 * C + (j < 8 ? 0 : C) + c] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_apply_quad_kernel(BnBwdArgs a, const float* __restrict__ coef,
+                                                                bf16_t* __restrict__ dy) {
+  extern __shared__ float cf[];  // [3][C] coefficients, [2][C] forward scale/shift
+  const int C = a.C, C8 = C >> 3;
+  for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
+  float* sc = cf + 3 * C;
+  float* sh = sc + C;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sc[c] = a.scale[c];
+    sh[c] = a.shift[c];
+  }
+  __syncthreads();
+  const unsigned n8 = (unsigned)((a.M >> 2) * C8);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += gridDim.x * blockDim.x) {
+    const int chunk = (int)(i & (unsigned)(C8 - 1));
+    const unsigned q = i >> (31 - __builtin_clz(C8));
+    QuadPool qp;
+    qp.load(a, q, chunk, C8);
+    qp.finish(chunk, sc, sh);
+    const int c0 = chunk * 8;
+    const long long pix0 = qp.pix0;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      float yv[8], r[8];
+      unpack8(qp.y[p], yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        r[j] = cf[c0 + j] * qp.d[p][j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
+      reinterpret_cast<uint4*>(dy)[(pix0 + (p >> 1) * a.W + (p & 1)) * C8 + chunk] = pack8(r);
+    }
+  }
+}
+
 // Fused stem tail: pooled = maxpool_KxK/S(relu(y*scale + shift)) with argmax codes; the
 // BN output itself is never written.
 __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
@@ -721,12 +882,16 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  hipStream_t st) {
   // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
   BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C};
-  const int G = bn_bwd_groups(M, C);
+  // stem 3x3/s2/p1 pool with even H, W: quad gather (4 pixels share their 4 windows)
+  const bool quad = mode == 3 && K == 3 && S == 2 && P == 1 && H % 2 == 0 && W % 2 == 0 &&
+                    OH == H / 2 && OW == W / 2 && !dres && (long long)M * C / 8 < (1LL << 31);
+  const int G = quad ? bn_bwd_groups(M / 4, C) : bn_bwd_groups(M, C);
   float* part = work;
   float* coef = work + (long long)G * 2 * C;
   float* part2 = coef + 3 * C;
   const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
-  switch (mode) {
+  if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
+  else switch (mode) {
     case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
     case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
     case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
@@ -744,6 +909,10 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;
 #define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
+  if (quad) {
+    bn_bwd_apply_quad_kernel<<<grid_for(n8 / 4, 256, 4096), 256, sh, st>>>(a, coef, dy);
+    return;
+  }
   switch (mode * 2 + (dres ? 1 : 0)) {
     case 0: DM_BNB(0, false); break;
     case 1: DM_BNB(0, true); break;

@@ -1189,9 +1189,99 @@ __global__ void __launch_bounds__(256) pack_weights_multi_kernel(const long long
   }
 }
 
+// All conv layers in one launch, LDS-tiled: block = (layer, 32 co, 32 ci) over all taps
+// (tap chunks of <= 9).  Reads are contiguous OIHW runs of 32*T floats, both packed
+// layouts are written as contiguous 64-B rows (2 bf16 per lane), so neither the strided
+// fp32 reads nor the scattered 2-byte dgrad-layout writes of the element-per-thread
+// kernel remain (that kernel: ~100 us for ResNet-18's 11.2 M conv weights).
+// tprefix[l] = first tile of layer l (tprefix[nl] = number of blocks).
+__global__ void __launch_bounds__(256) pack_weights_tiled_kernel(const long long* __restrict__ desc,
+                                                                 const int* __restrict__ tprefix,
+                                                                 int nl) {
+  __shared__ float tile[32 * 9 * 33];
+  __shared__ int pre[33];
+  for (int i = threadIdx.x; i <= nl; i += blockDim.x) pre[i] = tprefix[i];
+  __syncthreads();
+  int l = 0;
+  while (l + 1 < nl && (int)blockIdx.x >= pre[l + 1]) ++l;
+  const long long* d = desc + 8 * l;
+  const float* w = (const float*)d[0];
+  bf16_t* wf = (bf16_t*)d[1];
+  bf16_t* wd = (bf16_t*)d[2];
+  const int Cout = (int)d[3], Cin = (int)d[4], Cpad = (int)d[5];
+  const int T = (int)(d[6] * d[7]);
+  const int CI = Cpad > Cin ? Cpad : Cin;
+  const int nci = (CI + 31) / 32;
+  const int tl = (int)blockIdx.x - pre[l];
+  const int co0 = (tl / nci) * 32, ci0 = (tl % nci) * 32;
+  for (int t0 = 0; t0 < T; t0 += 9) {
+    const int TT = T - t0 < 9 ? T - t0 : 9;
+    if (t0) __syncthreads();
+    if (TT == T && Cin % 32 == 0) {
+      // whole-tap tile of full channel groups: 32 contiguous runs of 32*T floats, read as
+      // float4 with every load of the thread issued before the first LDS store
+      const int R4 = 8 * T;
+      float4 v[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int e = threadIdx.x + k * 256;
+        const int co = e / R4;
+        v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < 32 * R4 && co0 + co < Cout)
+          v[k] = reinterpret_cast<const float4*>(w + ((long long)(co0 + co) * Cin + ci0) * T)[e - co * R4];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int e = threadIdx.x + k * 256;
+        if (e >= 32 * R4) break;
+        const int co = e / R4, f = 4 * (e - co * R4);
+        const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ci = (f + j) / T, t = (f + j) - ci * T;
+          tile[(co * TT + t) * 33 + ci] = vv[j];
+        }
+      }
+    } else
+    for (int e = threadIdx.x; e < 32 * 32 * TT; e += 256) {
+      const int co = e / (32 * TT), r = e - co * (32 * TT);
+      const int ci = r / TT, t = r - ci * TT;
+      float v = 0.f;
+      if (co0 + co < Cout && ci0 + ci < Cin) v = w[((long long)(co0 + co) * Cin + ci0 + ci) * T + t0 + t];
+      tile[(co * TT + t) * 33 + ci] = v;
+    }
+    __syncthreads();
+    // wf[co][t][ci]: pairs of channels (Cpad is a multiple of 8)
+    for (int e = threadIdx.x; e < 32 * TT * 16; e += 256) {
+      const int ci = 2 * (e & 15), r = e >> 4;
+      const int t = r % TT, co = r / TT;
+      if (co0 + co < Cout && ci0 + ci < Cpad) {
+        const float* q = tile + (co * TT + t) * 33 + ci;
+        *reinterpret_cast<uint32_t*>(wf + ((long long)(co0 + co) * T + t0 + t) * Cpad + ci0 + ci) =
+            pack_bf2(q[0], q[1]);
+      }
+    }
+    if (wd) {
+      // wd[ci][t][co]: pairs of output channels (Cout even)
+      for (int e = threadIdx.x; e < 32 * TT * 16; e += 256) {
+        const int co = 2 * (e & 15), r = e >> 4;
+        const int t = r % TT, ci = r / TT;
+        if (co0 + co < Cout && ci0 + ci < Cin)
+          *reinterpret_cast<uint32_t*>(wd + ((long long)(ci0 + ci) * T + t0 + t) * Cout + co0 + co) =
+              pack_bf2(tile[(co * TT + t) * 33 + ci], tile[((co + 1) * TT + t) * 33 + ci]);
+      }
+    }
+  }
+}
+
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
                         hipStream_t st) {
   pack_weights_multi_kernel<<<grid_for(total, 256, 8192), 256, 0, st>>>(desc, prefix, nl);
+}
+
+void pack_weights_tiled(const long long* desc, const int* tprefix, int nl, int ntiles,
+                        hipStream_t st) {
+  pack_weights_tiled_kernel<<<ntiles, 256, 0, st>>>(desc, tprefix, nl);
 }
 
 // Space-to-depth stem weights: W[co][c][7][7] -> W'[co][4][4][Cp] with
@@ -1217,23 +1307,49 @@ __global__ void __launch_bounds__(256) pack_weights_s2d_kernel(const float* __re
 }
 
 // dw[co][c][kh][kw] = beta*dw + Σ_s slab[s][co][(u*4+v)*Cp + (dy*2+dx)*C + c]
+// Reduced in the slab's own layout [S][Cout][16*Cp] (coalesced reads), the S-sum split over
+// `lanes` lanes per element with 8 loads in flight each, lanes combined in fixed order
+// (deterministic); the write is the s2d -> 7x7 permutation (slab elements that fall outside
+// the 7x7 window or into channel padding are structural zeros of the packed weight and
+// are dropped).  The stem wgrad has many m-splits (S = 256) over few elements (64 x 256), so
+// one thread per output element (9408 threads summing 256 dependent loads) was ~80 us.
 __global__ void __launch_bounds__(256) wgrad_reduce_s2d_kernel(const float* __restrict__ slab,
                                                                int S, int Cout, int C, int Cp,
-                                                               float* __restrict__ dw, float beta) {
-  const long long total = (long long)Cout * C * 49;
+                                                               float* __restrict__ dw, float beta,
+                                                               int lanes) {
+  __shared__ float red[256];
   const long long K = 16LL * Cp;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
-    const int kw = o % 7;
-    const int kh = (o / 7) % 7;
-    const int c = (o / 49) % C;
-    const int co = o / (49 * C);
-    const int u = (kh + 1) >> 1, dy = (kh + 1) & 1, v = (kw + 1) >> 1, dx = (kw + 1) & 1;
-    const long long src = (long long)co * K + (u * 4 + v) * Cp + (dy * 2 + dx) * C + c;
-    float sacc = 0.f;
-    for (int i = 0; i < S; ++i) sacc += slab[(long long)i * Cout * K + src];
-    dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + sacc;
+  const long long total = (long long)Cout * K;
+  const int E = 256 / lanes;
+  const int el = threadIdx.x % E, ln = threadIdx.x / E;
+  const long long e = (long long)blockIdx.x * E + el;
+  float acc = 0.f;
+  if (e < total) {
+    const float* src = slab + e;
+    int i = ln;
+    for (; i + 7 * lanes < S; i += 8 * lanes) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = src[(long long)(i + j * lanes) * total];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc += v[j];
+    }
+    for (; i < S; i += lanes) acc += src[(long long)i * total];
   }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (ln != 0 || e >= total) return;
+  float sum = 0.f;
+  for (int l = 0; l < lanes; ++l) sum += red[l * E + el];
+  const int co = (int)(e / K);
+  const int k = (int)(e - (long long)co * K);
+  const int uv = k / Cp, ch = k - uv * Cp;
+  const int sub = ch / C, c = ch - sub * C;
+  if (sub >= 4) return;
+  const int kh = 2 * (uv >> 2) + (sub >> 1) - 1, kw = 2 * (uv & 3) + (sub & 1) - 1;
+  if (kh < 0 || kh >= 7 || kw < 0 || kw >= 7) return;
+  const long long o = (((long long)co * C + c) * 7 + kh) * 7 + kw;
+  dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + sum;
 }
 
 void pack_weights_s2d(const float* w, bf16_t* wf, int Cout, int C, int Cp, hipStream_t st) {
@@ -1243,8 +1359,12 @@ void pack_weights_s2d(const float* w, bf16_t* wf, int Cout, int C, int Cp, hipSt
 
 void wgrad_reduce_s2d(const float* slab, int S, int Cout, int C, int Cp, float* dw, float beta,
                       hipStream_t st) {
-  const long long total = (long long)Cout * C * 49;
-  wgrad_reduce_s2d_kernel<<<grid_for(total, 256), 256, 0, st>>>(slab, S, Cout, C, Cp, dw, beta);
+  const long long total = (long long)Cout * 16 * Cp;
+  int lanes = 1;
+  while (lanes < 16 && lanes * 8 < S) lanes *= 2;
+  const int E = 256 / lanes;
+  wgrad_reduce_s2d_kernel<<<(unsigned)((total + E - 1) / E), 256, 0, st>>>(slab, S, Cout, C, Cp,
+                                                                          dw, beta, lanes);
 }
 
 // ------------------------------------------------------------------ launchers

@@ -72,6 +72,8 @@ void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& 
                 const float* pre_sh = nullptr);
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
                         hipStream_t st);
+void pack_weights_tiled(const long long* desc, const int* tprefix, int nl, int ntiles,
+                        hipStream_t st);
 int igemm_fwd_rowtile(int cfg);
 void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                  long long mchunk, int cfg, hipStream_t st);

@@ -163,7 +163,7 @@ def pack_all(prog, layers):
     st = getattr(prog, "_pack_state", None)
     if st is None or st["key"] != key:
         dev = layers[0].weight.device
-        bufs, rows, pre = [], [], [0]
+        bufs, rows, pre, tpre = [], [], [0], [0]
         for m in layers:
             cp = _cpad(m.cin)
             wf = torch.empty((m.cout, m.k, m.k, cp), device=dev, dtype=torch.bfloat16)
@@ -172,13 +172,15 @@ def pack_all(prog, layers):
             rows.append([m.weight.data_ptr(), wf.data_ptr(), wd.data_ptr(), m.cout, m.cin, cp,
                          m.k, m.k])
             pre.append(pre[-1] + m.cout * m.k * m.k * cp)
-        st = dict(key=key, bufs=bufs, total=pre[-1],
+            tpre.append(tpre[-1] + -(-m.cout // 32) * -(-max(cp, m.cin) // 32))
+        st = dict(key=key, bufs=bufs, total=pre[-1], ntiles=tpre[-1],
+                  tprefix=torch.tensor(tpre, dtype=torch.int32).to(dev),
                   desc=torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev),
                   prefix=torch.tensor(pre, dtype=torch.int64).to(dev))
         object.__setattr__(prog, "_pack_state", st)
     for m in layers:
         assert m.weight.is_contiguous()
-    lib().pack_weights_multi(st["desc"], st["prefix"], st["total"])
+    lib().pack_weights_tiled(st["desc"], st["tprefix"], st["ntiles"])
     for m, (wf, wd) in zip(layers, st["bufs"]):
         object.__setattr__(m, "_wcache", (ver, wf, wd))
 

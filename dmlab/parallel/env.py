@@ -56,7 +56,7 @@ def default_backend(device: torch.device | str | None = None) -> str:
 def device() -> torch.device:
     global _DEVICE
     if _DEVICE is None:
-        if torch.cuda.is_available():
+        if torch.cuda.is_available() and os.environ.get("DMLAB_DEVICE", "cuda") != "cpu":
             _DEVICE = torch.device("cuda", get_local_rank() % max(torch.cuda.device_count(), 1))
         else:
             _DEVICE = torch.device("cpu")
@@ -81,7 +81,9 @@ def init(world_size: int | None = None, rank: int | None = None, master_addr: st
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "12355")
     if device_type is None:
-        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+        # DMLAB_DEVICE=cpu (set by ``dmlab.launch --cpu``) forces gloo/CPU ranks
+        device_type = os.environ.get("DMLAB_DEVICE") or (
+            "cuda" if torch.cuda.is_available() else "cpu")
     if device_type == "cuda":
         lr = int(os.environ.get("LOCAL_RANK", rk % max(torch.cuda.device_count(), 1)))
         _DEVICE = torch.device("cuda", lr)

@@ -264,10 +264,12 @@ def test_stem_space_to_depth(dev, H):
         assert _rel(dw, dref) < 2e-3
 
 
-def test_fused_bn_relu_maxpool_and_gather_backward(dev):
-    """Stem tail: maxpool(relu(bn(y))) forward and the pool-gather BN backward (mode 3)."""
+@pytest.mark.parametrize("H,C", [(18, 64), (17, 64), (56, 32)])
+def test_fused_bn_relu_maxpool_and_gather_backward(dev, H, C):
+    """Stem tail: maxpool(relu(bn(y))) forward and the pool-gather BN backward (mode 3;
+    even H takes the 2x2-quad gather kernels, odd H the per-pixel gather)."""
     torch.manual_seed(0)
-    N, H, C = 2, 18, 64
+    N = 2
     y = (torch.randn(N, H, H, C, device=dev) * 1.5).bfloat16()
     gamma = torch.rand(C, device=dev) + 0.5
     beta = torch.randn(C, device=dev) * 0.5
@@ -362,3 +364,28 @@ def test_conv_wgrad_prebn(dev, geom, cfg):
     lib().conv_wgrad(y, _nhwc(dy), d, slab, Cin, k, k, s, p, 0.0, S, cfg, False,
                      pre_scale=sc, pre_shift=sh)
     assert _rel(d, ref) < 2e-3
+
+
+def test_pack_weights_tiled_matches_per_layer(dev):
+    # one launch over several layers (3x3, 1x1, 7x7 stem with padded channels, Cout not a
+    # multiple of 32 tiles' worth of ci) must be bit-identical to the per-layer packer
+    shapes = [(64, 3, 7, 8), (64, 64, 3, 64), (128, 64, 1, 64), (96, 160, 3, 160), (512, 512, 3, 512)]
+    g = torch.Generator(device=dev).manual_seed(3)
+    rows, pre, outs = [], [0], []
+    for co, ci, k, cp in shapes:
+        w = torch.randn(co, ci, k, k, device=dev, generator=g)
+        wf = torch.full((co, k, k, cp), 7.0, device=dev, dtype=torch.bfloat16)
+        wd = torch.full((ci, k, k, co), 7.0, device=dev, dtype=torch.bfloat16)
+        rf = torch.empty_like(wf)
+        rd = torch.empty_like(wd)
+        lib().pack_weights(w, rf, rd, cp)
+        outs.append((w, wf, wd, rf, rd))
+        rows.append([w.data_ptr(), wf.data_ptr(), wd.data_ptr(), co, ci, cp, k, k])
+        pre.append(pre[-1] + -(-co // 32) * -(-max(cp, ci) // 32))
+    desc = torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev)
+    tpre = torch.tensor(pre, dtype=torch.int32).to(dev)
+    lib().pack_weights_tiled(desc, tpre, pre[-1])
+    torch.cuda.synchronize()
+    for w, wf, wd, rf, rd in outs:
+        assert torch.equal(wf, rf)
+        assert torch.equal(wd, rd)

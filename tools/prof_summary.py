@@ -24,6 +24,25 @@ def rows_csv(path):
         yield r["Name"], float(r["TotalDurationNs"])
 
 
+def rows_trace(path, keep_frac=None):
+    rs = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                 for r in csv.DictReader(open(path))), key=lambda t: t[1])
+    if keep_frac:
+        rs = rs[int(len(rs) * (1 - keep_frac)):]
+    for n, s, e in rs:
+        yield n, float(e - s)
+
+
+def step_rows(path):
+    """(name, start, end, grid, wg) of the last complete step (between the last two
+    optimizer launches) of a kernel-trace CSV."""
+    rs = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                  r["Grid_Size_X"], r["Workgroup_Size_X"]) for r in csv.DictReader(open(path))),
+                key=lambda t: t[1])
+    idx = [i for i, r in enumerate(rs) if "sgd_kernel" in r[0]]
+    return rs[idx[-2] + 1: idx[-1] + 1]
+
+
 def rows_db(path, keep_frac=None):
     c = sqlite3.connect(path)
     rs = list(c.execute("select name, start, end from kernels order by start"))
@@ -42,7 +61,16 @@ def main():
         del args[i:i + 2]
     path = args[0]
     steps = float(args[1]) if len(args) > 1 else 1.0
-    rows = rows_db(path, frac) if path.endswith(".db") else rows_csv(path)
+    if "--step" in args:
+        for n, s0, e, gx, wg in step_rows(path):
+            print(f"{(e - s0) / 1e3:8.1f} us  grid {int(gx) // int(wg):6d}  {family(n)[:70]}")
+        return
+    if path.endswith(".db"):
+        rows = rows_db(path, frac)
+    elif "kernel_trace" in path:
+        rows = rows_trace(path, frac)
+    else:
+        rows = rows_csv(path)
     fam = defaultdict(float)
     cnt = defaultdict(int)
     tot = 0.0
