@@ -205,8 +205,19 @@ def main(argv=None) -> int:
     ap.add_argument("--no-prefix", action="store_true")
     ap.add_argument("-m", dest="module", help="run a module (python -m) on every rank")
     ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    # everything after `-m MODULE` (or after `--`) belongs to the ranks' command line
+    tail, module = [], None
+    for i, t in enumerate(argv):
+        if t == "--":
+            argv, tail = argv[:i], argv[i + 1:]
+            break
+        if t == "-m" and i + 1 < len(argv):
+            argv, module, tail = argv[:i], argv[i + 1], argv[i + 2:]
+            break
     a = ap.parse_args(argv)
-    cmd = a.cmd[1:] if a.cmd[:1] == ["--"] else a.cmd
+    a.module = module or a.module
+    cmd = tail + a.cmd
     if a.config:
         cmds, envs, order = from_config(a.config, a.master_addr, a.cpu)
     else:
