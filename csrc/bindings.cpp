@@ -264,9 +264,11 @@ void spin_us(double us) { dm::spin_us(us, cur_stream()); }
 }  // namespace
 
 void register_resnet(pybind11::module_& m);
+void register_reducer(pybind11::module_& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_resnet(m);
+  register_reducer(m);
   m.doc() = "dmlab native HIP kernels for MI355X (gfx950)";
   m.def("sgd_step", &sgd_step, "fused flat SGD/GD step");
   m.def("adam_step", &adam_step, "fused flat Adam step");

@@ -1,0 +1,201 @@
+// Native gradient-bucket reducer for data parallelism (module dmlab._C, class Reducer).
+//
+// Reference behaviour it replaces: after a full loss.backward() the labs issue one
+// blocking all_reduce per parameter, then `grad /= ws` (codes/task2/dist_utils.py:39-42,
+// codes/task3/dist_utils.py:40-46).
+//
+// Here gradients live in ONE flat buffer (dmlab/nn/flat.py) laid out in the order
+// backward produces them; a bucket is a contiguous [lo, hi) slice of it.  The reducer
+// keeps a per-bucket countdown of parameters still to be produced; the instant a
+// bucket's last gradient is written (the Program's per-layer hook calls mark_layer), its
+// all-reduce is issued on the process group (RCCL over xGMI; gloo on CPU).  ProcessGroup-
+// NCCL orders the collective after the kernels already queued on the current HIP stream
+// and runs it on its own communication stream, so the remaining backward layers overlap
+// with the transfer.  finalize() — the end of backward — issues any bucket that never
+// filled (unused parameters), then makes the current stream wait on every bucket
+// (Work::wait on RCCL is a device-side stream wait, not a host sync), casts reduced
+// low-precision communication buffers back, and applies the 1/ws average (`avg_scale`)
+// unless ReduceOp.AVG already did (RCCL; gloo has no AVG).  When the fused optimiser
+// applies 1/ws itself (`fold_average_into`) avg_scale is 1 and buckets are plain SUMs.
+//
+// Buckets at or below `small_cap` elements may instead be handed to a Python callable
+// (the one-shot xGMI peer-memory all-reduce, dmlab/parallel/xgmi.py), which folds the
+// scale into its own epilogue.
+//
+// Everything here runs on the host thread that drives autograd, under the GIL; the
+// state machine is plain counters (no allocation on the hot path besides the optional
+// communication-dtype buffers).
+#include <torch/extension.h>
+#include <torch/csrc/distributed/c10d/ProcessGroup.hpp>
+#include <torch/csrc/distributed/c10d/Types.hpp>
+#include <torch/csrc/utils/pybind.h>
+
+#include <vector>
+
+namespace {
+
+class Reducer {
+ public:
+  Reducer(at::Tensor grad_buf, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
+          std::vector<std::vector<int64_t>> layer_params,
+          c10::intrusive_ptr<c10d::ProcessGroup> pg, bool use_avg, double avg_scale,
+          int64_t comm_code, int64_t small_cap, py::object small_fn)
+      : buf_(std::move(grad_buf)), param_bucket_(std::move(param_bucket)),
+        layer_params_(std::move(layer_params)), pg_(pg), use_avg_(use_avg),
+        avg_scale_(avg_scale), small_cap_(small_cap), small_fn_(std::move(small_fn)) {
+    // communication dtype: 0 = the gradient dtype, 1 = bfloat16, 2 = float16
+    TORCH_CHECK(comm_code >= 0 && comm_code <= 2, "comm_code: 0 (native), 1 (bf16), 2 (fp16)");
+    if (comm_code == 1) comm_dtype_ = at::kBFloat16;
+    if (comm_code == 2) comm_dtype_ = at::kHalf;
+    TORCH_CHECK(bounds.size() % 2 == 0 && !bounds.empty(), "bounds: [lo0, hi0, lo1, hi1, ...]");
+    TORCH_CHECK(buf_.dim() == 1 && buf_.is_contiguous(), "grad_buf: flat contiguous buffer");
+    const int64_t nb = (int64_t)bounds.size() / 2;
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t lo = bounds[2 * b], hi = bounds[2 * b + 1];
+      TORCH_CHECK(0 <= lo && lo < hi && hi <= buf_.numel(), "bucket bounds out of range");
+      buckets_.push_back(Bucket{lo, hi, 0, 0});
+    }
+    for (size_t i = 0; i < param_bucket_.size(); ++i) {
+      const int64_t b = param_bucket_[i];
+      TORCH_CHECK(b >= -1 && b < nb, "param_bucket: bucket id out of range");
+      if (b >= 0) buckets_[b].nparams++;
+    }
+    for (const auto& lp : layer_params_)
+      for (int64_t i : lp)
+        TORCH_CHECK(i >= 0 && i < (int64_t)param_bucket_.size(), "layer_params: bad param id");
+    reset();
+  }
+
+  // one parameter's gradient is final
+  void mark_ready(int64_t i) {
+    if (!enabled_) return;
+    TORCH_CHECK(i >= 0 && i < (int64_t)param_bucket_.size(), "mark_ready: bad param id");
+    const int64_t b = param_bucket_[i];
+    if (b < 0) return;
+    Bucket& bk = buckets_[b];
+    TORCH_CHECK(bk.pending > 0, "mark_ready: parameter ", i, " reported twice in one backward");
+    if (--bk.pending == 0) launch(b);
+  }
+
+  // every parameter of a Program layer is final (called from the layer's backward hook)
+  void mark_layer(int64_t l) {
+    if (!enabled_) return;
+    TORCH_CHECK(l >= 0 && l < (int64_t)layer_params_.size(), "mark_layer: bad layer id");
+    for (int64_t i : layer_params_[l]) mark_ready(i);
+  }
+
+  // end of backward: launch stragglers, wait (device-side), cast back, scale
+  void finalize() {
+    if (!enabled_) return;
+    for (size_t b = 0; b < buckets_.size(); ++b)
+      if (!launched_[b]) launch((int64_t)b);
+    for (size_t b = 0; b < buckets_.size(); ++b) {
+      if (works_[b]) works_[b]->wait();
+      at::Tensor view = buf_.slice(0, buckets_[b].lo, buckets_[b].hi);
+      if (comm_[b].defined()) {
+        view.copy_(comm_[b]);
+        comm_[b] = at::Tensor();
+      }
+      if (avg_scale_ != 1.0 && !scaled_[b]) view.mul_(avg_scale_);
+    }
+    reset();
+  }
+
+  void reset() {
+    const size_t nb = buckets_.size();
+    launched_.assign(nb, false);
+    scaled_.assign(nb, false);
+    works_.assign(nb, c10::intrusive_ptr<c10d::Work>());
+    comm_.assign(nb, at::Tensor());
+    for (auto& bk : buckets_) bk.pending = bk.nparams;
+  }
+
+  void set_enabled(bool e) { enabled_ = e; }
+  bool enabled() const { return enabled_; }
+  void set_avg_scale(double s) { avg_scale_ = s; }
+  int64_t launched_total() const { return launched_total_; }
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  std::vector<int64_t> bucket_bounds() const {
+    std::vector<int64_t> v;
+    for (const auto& b : buckets_) {
+      v.push_back(b.lo);
+      v.push_back(b.hi);
+    }
+    return v;
+  }
+
+ private:
+  struct Bucket {
+    int64_t lo, hi, nparams, pending;
+  };
+
+  void launch(int64_t b) {
+    if (launched_[b]) return;
+    launched_[b] = true;
+    ++launched_total_;
+    // the process group is held weakly: a reducer must not keep it (and its transport
+    // threads) alive past destroy_process_group(), e.g. when the owning DDP module is only
+    // collected at interpreter shutdown
+    auto pg = pg_.lock();
+    TORCH_CHECK(pg, "Reducer: the process group was destroyed");
+    if (pg->getSize() <= 1) return;
+    at::Tensor view = buf_.slice(0, buckets_[b].lo, buckets_[b].hi);
+    if (!small_fn_.is_none() && !comm_dtype_ && view.numel() <= small_cap_) {
+      small_fn_(view, avg_scale_);  // one stream-ordered kernel, scale in its epilogue
+      scaled_[b] = true;
+      return;
+    }
+    at::Tensor t = view;
+    if (comm_dtype_ && *comm_dtype_ != view.scalar_type()) {
+      comm_[b] = view.to(*comm_dtype_);
+      t = comm_[b];
+    }
+    c10d::AllreduceOptions opts;
+    if (use_avg_ && avg_scale_ != 1.0) {
+      opts.reduceOp = c10d::ReduceOp(c10d::ReduceOp::AVG);
+      scaled_[b] = true;
+    } else {
+      opts.reduceOp = c10d::ReduceOp(c10d::ReduceOp::SUM);
+    }
+    std::vector<at::Tensor> ts{t};
+    works_[b] = pg->allreduce(ts, opts);
+  }
+
+  at::Tensor buf_;
+  std::vector<Bucket> buckets_;
+  std::vector<int64_t> param_bucket_;
+  std::vector<std::vector<int64_t>> layer_params_;
+  c10::weak_intrusive_ptr<c10d::ProcessGroup> pg_;
+  bool use_avg_;
+  double avg_scale_;  // 1/ws when the reduced gradient must be averaged here, else 1
+  c10::optional<at::ScalarType> comm_dtype_;
+  int64_t small_cap_;
+  py::object small_fn_;
+  bool enabled_ = true;
+  int64_t launched_total_ = 0;
+  std::vector<bool> launched_, scaled_;
+  std::vector<c10::intrusive_ptr<c10d::Work>> works_;
+  std::vector<at::Tensor> comm_;
+};
+
+}  // namespace
+
+void register_reducer(pybind11::module_& m) {
+  py::class_<Reducer>(m, "Reducer")
+      .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>,
+                    std::vector<std::vector<int64_t>>, c10::intrusive_ptr<c10d::ProcessGroup>,
+                    bool, double, int64_t, int64_t, py::object>(),
+           py::arg("grad_buf"), py::arg("bounds"), py::arg("param_bucket"),
+           py::arg("layer_params"), py::arg("pg"), py::arg("use_avg"), py::arg("avg_scale"),
+           py::arg("comm_code"), py::arg("small_cap"), py::arg("small_fn"))
+      .def("mark_ready", &Reducer::mark_ready)
+      .def("mark_layer", &Reducer::mark_layer)
+      .def("finalize", &Reducer::finalize)
+      .def("reset", &Reducer::reset)
+      .def("set_enabled", &Reducer::set_enabled)
+      .def("set_avg_scale", &Reducer::set_avg_scale)
+      .def_property_readonly("enabled", &Reducer::enabled)
+      .def_property_readonly("launched_total", &Reducer::launched_total)
+      .def_property_readonly("num_buckets", &Reducer::num_buckets)
+      .def("bucket_bounds", &Reducer::bucket_bounds);
+}

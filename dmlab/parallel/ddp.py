@@ -25,6 +25,10 @@ task3/dist_utils.py:40-46).  Here:
 * ``small_allreduce="xgmi"``: buckets of at most ``small_cap_mb`` go through the
   one-shot xGMI peer-memory all-reduce (:mod:`dmlab.parallel.xgmi`, one kernel, no ring
   steps) instead of RCCL — the latency-bound case of the labs' LeNet (207 KB of grads).
+* The bucket state machine (per-bucket countdowns, collective launch, the end-of-
+  backward wait / cast-back / average) runs in C++ (``dmlab._C.Reducer``,
+  ``csrc/reducer.cpp``) against the c10d ProcessGroup directly; ``native=False`` keeps
+  the equivalent Python implementation below (used when the extension is absent).
 """
 from __future__ import annotations
 
@@ -55,7 +59,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: float = 4.0, comm_dtype=None, broadcast_init: bool = True,
                  process_group=None, average: bool = True, small_allreduce: str | None = None,
-                 small_cap_mb: float = 4.0):
+                 small_cap_mb: float = 4.0, native: bool | None = None):
         super().__init__()
         self.module = module
         self.ws = env.get_world_size()
@@ -86,6 +90,51 @@ class DistributedDataParallel(nn.Module):
                 from .xgmi import XGMIAllReduce
 
                 self._xgmi = XGMIAllReduce(cap=max(small), group=self.pg)
+        self._native = None
+        if native is None:
+            native = self.ws > 1 and _native_reducer_available()
+        if native and self.ws > 1:
+            self._build_native(small_cap_mb)
+
+    # ------------------------------------------------------------------ native reducer
+    def _avg_scale(self):
+        return 1.0 / self.ws if (self.average and not self._fold and self.ws > 1) else 1.0
+
+    def _build_native(self, small_cap_mb):
+        from dmlab import _C
+        from torch.distributed import distributed_c10d as c10d
+
+        pg = self.pg if self.pg is not None else c10d._get_default_group()
+        nparams = max(self._bucket_of_index) + 1 if self._bucket_of_index else 0
+        param_bucket = [-1] * nparams
+        bid = {id(b): k for k, b in enumerate(self.buckets)}
+        for i, b in self._bucket_of_index.items():
+            param_bucket[i] = bid[id(b)]
+        bounds = []
+        for b in self.buckets:
+            bounds += [int(b.lo), int(b.hi)]
+        layer_params = [list(lp) for lp in getattr(self, "_layer_params", [])]
+        code = {None: 0, torch.bfloat16: 1, torch.float16: 2}
+        if self.comm_dtype not in code:
+            raise ValueError(f"comm_dtype {self.comm_dtype} not supported")
+        small_fn = None
+        if self._xgmi is not None:
+            xg = self._xgmi
+
+            def small_fn(view, scale):
+                xg(view, scale=scale)
+        self._native = _C.Reducer(self.grad_buf, bounds, param_bucket, layer_params, pg,
+                                  bool(self._use_avg), self._avg_scale(),
+                                  code[self.comm_dtype],
+                                  self._xgmi.cap if self._xgmi is not None else 0, small_fn)
+
+    @property
+    def buckets_launched(self):
+        return self._native.launched_total if self._native is not None else self._py_launched
+
+    @buckets_launched.setter
+    def buckets_launched(self, v):
+        self._py_launched = v
 
     # ------------------------------------------------------------------ layout
     def _make_buckets(self, sizes, cap, first):
@@ -119,6 +168,8 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             for i in b.params:
                 self._bucket_of[i] = b
+        self._bucket_of_index = {i: self._bucket_of[i] for i in range(len(flat.params))
+                                 if i in self._bucket_of}
         self._layer_params = [prog.layer_params(i) for i in range(len(prog.layers))]
         prog.register_grad_hook(self._on_layer_done)
         prog.register_post_backward_hook(lambda _p: self._finalize())
@@ -142,6 +193,8 @@ class DistributedDataParallel(nn.Module):
         for b in self.buckets:
             for i in b.params:
                 self._bucket_of[i] = b
+        self._bucket_of_index = {i: self._bucket_of[i] for i in range(len(params))
+                                 if i in self._bucket_of}
         self._final_queued = False
         for i, p in enumerate(params):
             p.register_post_accumulate_grad_hook(self._make_generic_hook(i))
@@ -171,6 +224,8 @@ class DistributedDataParallel(nn.Module):
         if self.ws > 1 and self.average:
             optimizer.grad_scale = 1.0 / self.ws
             self._fold = True
+            if self._native is not None:
+                self._native.set_avg_scale(1.0)
         return optimizer
 
     def _launch(self, b: _Bucket):
@@ -200,6 +255,9 @@ class DistributedDataParallel(nn.Module):
     def _mark_ready(self, i):
         if not self._sync_enabled:
             return
+        if self._native is not None:
+            self._native.mark_ready(i)
+            return
         b = self._bucket_of.get(i)
         if b is None:
             return
@@ -208,6 +266,10 @@ class DistributedDataParallel(nn.Module):
             self._launch(b)
 
     def _on_layer_done(self, prog, layer_idx):
+        if self._native is not None:
+            if self._sync_enabled:
+                self._native.mark_layer(layer_idx)
+            return
         for i in self._layer_params[layer_idx]:
             self._mark_ready(i)
 
@@ -215,6 +277,11 @@ class DistributedDataParallel(nn.Module):
         if self.on_compute_done is not None:
             self.on_compute_done()
         if not self._sync_enabled:
+            if self.program is None:
+                self._final_queued = False
+            return
+        if self._native is not None:
+            self._native.finalize()
             if self.program is None:
                 self._final_queued = False
             return
@@ -249,6 +316,14 @@ class DistributedDataParallel(nn.Module):
             yield
         finally:
             self._sync_enabled = old
+
+
+def _native_reducer_available() -> bool:
+    try:
+        from dmlab import _C
+    except ImportError:
+        return False
+    return hasattr(_C, "Reducer")
 
 
 DDP = DistributedDataParallel

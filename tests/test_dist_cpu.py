@@ -177,3 +177,37 @@ def _straggler(rank, ws, path):
 
 def test_straggler_slows_the_other_rank():
     run_dist(_straggler, 2, None)
+
+
+def _native_vs_python_reducer(rank, ws, path):
+    """The C++ bucket reducer (dmlab._C.Reducer) and the Python one give identical
+    gradients: Program (layer hooks) and plain-module (param hooks) paths, SUM+1/ws and
+    folded averaging, bf16 communication, no_sync accumulation."""
+    from dmlab.models import Net
+    from dmlab.models.reference import TorchLeNet
+    from dmlab.parallel import DDP
+
+    g = torch.Generator().manual_seed(11 + rank)
+    X = torch.rand(5, 1, 28, 28, generator=g)
+    Y = torch.randint(0, 10, (5,), generator=g)
+    for cls in (Net, TorchLeNet):
+        for comm_dtype in (None, torch.bfloat16):
+            grads = []
+            for native in (True, False):
+                torch.manual_seed(0)
+                m = cls()
+                ddp = DDP(m, bucket_cap_mb=0.05, first_bucket_mb=0.01, comm_dtype=comm_dtype,
+                          native=native)
+                assert (ddp._native is not None) == native
+                with ddp.no_sync():  # accumulate locally, no communication
+                    F.cross_entropy(ddp(X), Y).backward()
+                assert ddp.buckets_launched == 0
+                F.cross_entropy(ddp(X * 0.5), Y).backward()
+                assert ddp.buckets_launched == len(ddp.buckets)
+                grads.append(torch.cat([p.grad.reshape(-1) for p in m.parameters()]))
+            tol = dict(rtol=0, atol=0) if comm_dtype is None else dict(rtol=1e-2, atol=1e-4)
+            torch.testing.assert_close(grads[0], grads[1], **tol)
+
+
+def test_native_reducer_matches_python():
+    run_dist(_native_vs_python_reducer, 2, None)
