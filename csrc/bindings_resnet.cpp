@@ -144,6 +144,8 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     }
   if (any_empty && !accumulate)
     TORCH_CHECK(hipMemsetAsync(dx.data_ptr(), 0, dx.numel() * 2, st) == hipSuccess);
+  dm::ConvGeomSet set{};
+  int ng = 0;
   for (int a = 0; a < 2; ++a)
     for (int b = 0; b < 2; ++b) {
       auto g = base;
@@ -158,8 +160,14 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       g.kh0 = kh0; g.khs = 2; g.kw0 = kw0; g.kws = 2;
       g.M = (long long)N * g.Hg * g.Wg; g.K = nth * ntw * Cout;
       dm::geom_finalize(g);
-      dm::igemm_fwd(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr, g, cfg, st);
+      set.g[ng++] = g;
     }
+  // all parity classes in one launch (blockIdx.z = class) when the tile supports it
+  if (ng > 0 && dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, ng,
+                                    (int)cfg, st))
+    return;
+  for (int i = 0; i < ng; ++i)
+    dm::igemm_fwd(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr, set.g[i], cfg, st);
 }
 
 // dw (fp32 OIHW [Cout][Cin][KH][KW]) = beta*dw + Σ_m dy ⊗ im2col(x)

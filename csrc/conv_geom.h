@@ -24,6 +24,16 @@ struct ConvGeom {
   unsigned wg_mul, wg_shr, hg_mul, hg_shr;
 };
 
+// several geometries for one launch (selected by blockIdx.z)
+struct ConvGeomSet {
+  ConvGeom g[4];
+  static ConvGeomSet one(const ConvGeom& g0) {
+    ConvGeomSet s{};
+    s.g[0] = g0;
+    return s;
+  }
+};
+
 inline void fastdiv_init(unsigned d, unsigned& mul, unsigned& shr) {
   unsigned l = 0;
   while ((1u << l) < d) ++l;

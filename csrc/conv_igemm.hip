@@ -301,7 +301,11 @@ __global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
 template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd3_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
-    float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes) {
+    float* __restrict__ stats, ConvGeomSet gs, unsigned xbytes, unsigned wbytes) {
+  // blockIdx.z selects the geometry: the parity classes of a stride-2 dgrad (disjoint
+  // output pixels, 1..4 taps each) run as ONE launch instead of four small serial ones
+  const ConvGeom g = gs.g[blockIdx.z];
+  if ((long long)blockIdx.x * BM >= g.M) return;  // classes with fewer rows (odd sizes)
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = MF32 ? 32 : 16;                 // MFMA block edge
@@ -1390,7 +1394,7 @@ static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_
   } else if (v3) {
     auto k = mf32 ? igemm_fwd3_kernel<BM, BN, WM, WN, true, 1> : igemm_fwd3_kernel<BM, BN, WM, WN, false, 1>;
     set_smem_attr(k, sm);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), xb, wb);
   } else if (buf) {
     auto k = igemm_fwd_kernel<BM, BN, WM, WN, true>;
     set_smem_attr(k, sm);
@@ -1403,15 +1407,37 @@ static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_
 }
 
 template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
-static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                        float* stats, const ConvGeom& g, hipStream_t st) {
+static void launch_fwd3_set(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                            float* stats, const ConvGeomSet& gs, int ng, hipStream_t st) {
+  const ConvGeom& g = gs.g[0];
+  long long mmax = 0;
+  for (int i = 0; i < ng; ++i) mmax = gs.g[i].M > mmax ? gs.g[i].M : mmax;
   const size_t sm = fwd_smem(BM, BN);
-  dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
+  dim3 grid((unsigned)((mmax + BM - 1) / BM), (g.Ncols + BN - 1) / BN, ng);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
   auto k = igemm_fwd3_kernel<BM, BN, WM, WN, MF32, DEPTH>;
   set_smem_attr(k, sm);
-  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb);
+}
+
+template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
+static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                        float* stats, const ConvGeom& g, hipStream_t st) {
+  launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1, st);
+}
+
+// up to four geometries sharing X / W / Y (the parity classes of a stride-2 dgrad) in one
+// launch on the v3 128x128 mf32 tile (no statistics: the classes' row tiles would collide)
+bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st) {
+  switch (cfg) {  // the v3 mf32 tiles of igemm_fwd (12/13: one tile of prefetch, 15/16: two)
+    case 12: launch_fwd3_set<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
+    case 13: launch_fwd3_set<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
+    case 15: launch_fwd3_set<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
+    case 16: launch_fwd3_set<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
+    default: return false;
+  }
 }
 
 // halo-kernel configs (conv_halo.hip): 20/21 128-pixel 4 waves, 24/25 128-pixel 8 waves,

@@ -59,6 +59,9 @@ void xgmi_allreduce(const float* in, float* out, long long n, long long cap, voi
                     hipStream_t st);
 // conv_igemm.hip
 struct ConvGeom;
+struct ConvGeomSet;
+bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st);
 bool conv_halo_supported(const ConvGeom& g);

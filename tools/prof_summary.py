@@ -59,9 +59,11 @@ def main():
         i = args.index("--frac")
         frac = float(args[i + 1])
         del args[i:i + 2]
+    step_mode = "--step" in args
+    args = [x for x in args if x != "--step"]
     path = args[0]
     steps = float(args[1]) if len(args) > 1 else 1.0
-    if "--step" in args:
+    if step_mode:
         for n, s0, e, gx, wg in step_rows(path):
             print(f"{(e - s0) / 1e3:8.1f} us  grid {int(gx) // int(wg):6d}  {family(n)[:70]}")
         return
