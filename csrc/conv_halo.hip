@@ -37,7 +37,9 @@ constexpr int HBK = 64;   // channels per chunk (one 128-B LDS row per pixel)
 constexpr unsigned OOB = 0x80000000u;
 
 // 8-wave BN-64 tiles must stay <= 128 VGPRs to keep two workgroups (4 waves) per SIMD
-template <int BN, int HR, int WM, int WN, int BMH, bool PRE>
+// PF: weight-tile register prefetch depth (1: the tile of step s+1 is loaded during step s;
+// 2: the tile of step s+2, so a load has two steps of MFMA work to land in)
+template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
@@ -135,23 +137,25 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       }
     }
   };
-  auto load_b = [&](int cc, int t) {
+  auto load_b_into = [&](uint4 (&dst)[BR], int cc, int t) {
     const unsigned kb = (unsigned)(taps[t].z + cc * HBK + chunk * 8) * 2u;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const unsigned off = b_off[i] != OOB ? b_off[i] + kb : OOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0);
-      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      dst[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
-  auto store_b = [&](int buf) {
+  auto store_b_from = [&](const uint4 (&src)[BR], int buf) {
     bf16_t* bs = Bs + buf * BN * HBK;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int r = (tid >> 3) + RPP * i;
-      *reinterpret_cast<uint4*>(bs + r * HBK + swz(r, chunk) * 8) = rb[i];
+      *reinterpret_cast<uint4*>(bs + r * HBK + swz(r, chunk) * 8) = src[i];
     }
   };
+  auto load_b = [&](int cc, int t) { load_b_into(rb, cc, t); };
+  auto store_b = [&](int buf) { store_b_from(rb, buf); };
 
   f32x16 acc[RM][RN];
 #pragma unroll
@@ -199,30 +203,78 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
   };
 
   const int S = nchunk * ntaps;
-  load_halo(0);
-  load_b(0, 0);
-  store_halo(0);
-  store_b(0);
-  __syncthreads();
-  if (nchunk > 1) load_halo(1);
-  int cc = 0, t = 0;
-  for (int s = 0; s < S; ++s) {
-    int nt = t + 1, ncc = cc;
-    if (nt == ntaps) {
-      nt = 0;
-      ++ncc;
-    }
-    if (s + 1 < S) load_b(ncc, nt);
-    compute(s & 1, t);
-    if (s + 1 < S) store_b((s + 1) & 1);
+  if constexpr (PF == 1) {
+    load_halo(0);
+    load_b(0, 0);
+    store_halo(0);
+    store_b(0);
     __syncthreads();
-    if (ncc != cc && s + 1 < S) {
-      store_halo(ncc);  // every wave is past the last tap of chunk cc
+    if (nchunk > 1) load_halo(1);
+    int cc = 0, t = 0;
+    for (int s = 0; s < S; ++s) {
+      int nt = t + 1, ncc = cc;
+      if (nt == ntaps) {
+        nt = 0;
+        ++ncc;
+      }
+      if (s + 1 < S) load_b(ncc, nt);
+      compute(s & 1, t);
+      if (s + 1 < S) store_b((s + 1) & 1);
       __syncthreads();
-      if (ncc + 1 < nchunk) load_halo(ncc + 1);
+      if (ncc != cc && s + 1 < S) {
+        store_halo(ncc);  // every wave is past the last tap of chunk cc
+        __syncthreads();
+        if (ncc + 1 < nchunk) load_halo(ncc + 1);
+      }
+      t = nt;
+      cc = ncc;
     }
-    t = nt;
-    cc = ncc;
+  } else {
+    // two weight tiles in flight: step s computes from LDS buffer s&1, stores tile s+1
+    // (loaded during step s-1) and issues the loads of tile s+2 into the register set
+    // that tile s used; the loop is unrolled by two so each set is a static register array
+    uint4 rb2[BR];
+    auto nxt = [&](int& cc_, int& t_) {
+      if (++t_ == ntaps) {
+        t_ = 0;
+        ++cc_;
+      }
+    };
+    load_halo(0);
+    load_b_into(rb, 0, 0);
+    int lc = 0, lt = 0;  // (chunk, tap) of the next tile to load
+    nxt(lc, lt);
+    store_halo(0);
+    store_b_from(rb, 0);
+    if (S > 1) load_b_into(rb2, lc, lt);  // tile 1
+    nxt(lc, lt);
+    __syncthreads();
+    if (nchunk > 1) load_halo(1);
+    int cc = 0, t = 0;
+    auto step = [&](int s, uint4 (&rnext)[BR], uint4 (&rfree)[BR]) {
+      // rnext holds tile s+1; rfree receives tile s+2
+      int nt = t + 1, ncc = cc;
+      if (nt == ntaps) {
+        nt = 0;
+        ++ncc;
+      }
+      if (s + 2 < S) load_b_into(rfree, lc, lt);
+      nxt(lc, lt);
+      compute(s & 1, t);
+      if (s + 1 < S) store_b_from(rnext, (s + 1) & 1);
+      __syncthreads();
+      if (ncc != cc && s + 1 < S) {
+        store_halo(ncc);
+        __syncthreads();
+        if (ncc + 1 < nchunk) load_halo(ncc + 1);
+      }
+      t = nt;
+      cc = ncc;
+    };
+    for (int s = 0; s < S; s += 2) {
+      step(s, rb2, rb);
+      if (s + 1 < S) step(s + 1, rb, rb2);
+    }
   }
   mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
 }
@@ -232,7 +284,7 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
   return ((g.W - 1 + bm - 1) / g.W + 3) * g.W;
 }
 
-template <int BN, int HR, int WM, int WN, int BMH = HBM>
+template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st) {
   constexpr int RPP = WM * WN * 8;
@@ -242,8 +294,8 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   dim3 grid((unsigned)((g.M + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true>
-                  : conv_halo_kernel<BN, HR, WM, WN, BMH, false>;
+  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
+                  : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
   set_smem_attr(k, sm);
   k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh);
 }
@@ -264,6 +316,26 @@ bool conv_halo_supported(const ConvGeom& g) {
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
                const float* pre_sh) {
+  if (waves & 0x100) {  // two-deep weight prefetch (BN 128 only): 4 waves / 128 px, 8 waves / 256 px
+    waves &= 0xff;
+    if (bn == 128 && waves == 4) {
+      const int hp = halo_rows_needed(g);
+      const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
+      if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      DM_CHECK(hipGetLastError());
+      return;
+    }
+    if (bn == 128 && waves == 16) {
+      const int hr = (halo_rows_needed(g, 256) + 63) / 64;
+      if (hr <= 5) launch_halo<128, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      else if (hr <= 6) launch_halo<128, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      else launch_halo<128, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      DM_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if (waves == 16) {  // 256-pixel tile, 4 x 2 waves of 64 x BN/2 (twice the weight reuse per FLOP)
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 63) / 64;
@@ -273,6 +345,19 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     if (bn == 128) { DM_HALO256W8(128) } else { DM_HALO256W8(64) }
 #undef DM_HALO256W8
+    DM_CHECK(hipGetLastError());
+    return;
+  }
+  if (waves == 32 && bn == 64) {  // 256-pixel tile: 4 x 1 waves of 64 x 64 (1 LDS read per MFMA;
+                                  // BN 128 as 64 x 128 per wave spills: not instantiated)
+    const int hp2 = halo_rows_needed(g, 256);
+    const int hr = (hp2 + 31) / 32;
+#define DM_HALO256W41(BN_)                                                                   \
+  if (hr <= 10) launch_halo<BN_, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);                \
+  else if (hr <= 12) launch_halo<BN_, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
+  else launch_halo<BN_, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    DM_HALO256W41(64)
+#undef DM_HALO256W41
     DM_CHECK(hipGetLastError());
     return;
   }

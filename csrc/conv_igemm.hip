@@ -1442,10 +1442,19 @@ bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
 
 // halo-kernel configs (conv_halo.hip): 20/21 128-pixel 4 waves, 24/25 128-pixel 8 waves,
 // 36/37 256-pixel 2x2 waves, 38/39 256-pixel 4x2 waves; even = BN 128, odd = BN 64
+// 41 256-pixel 4x1 waves of 64 x 64 (BN 64 only); 42 / 43 = 20 / 38 with two weight tiles
+// of register prefetch (waves bit 8)
+int igemm_fwd_rowtile(int cfg);
 bool halo_cfg(int cfg, int& bn, int& waves) {
-  if (!(cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39))) return false;
+  if (cfg == 42 || cfg == 43) {
+    bn = 128;
+    waves = (cfg == 42 ? 4 : 16) | 0x100;
+    return true;
+  }
+  if (!(cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39) || cfg == 41))
+    return false;
   bn = (cfg == 20 || cfg == 24 || cfg == 36 || cfg == 38) ? 128 : 64;
-  waves = cfg >= 38 ? 16 : cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
+  waves = cfg == 41 ? 32 : cfg >= 38 ? 16 : cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
   return true;
 }
 
@@ -1461,7 +1470,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   if (halo_cfg(cfg, bn, waves)) {
     if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st);
     // fallback keeps the row tile (stats slab rows = igemm_fwd_rowtile(cfg))
-    if (cfg >= 36) {
+    if (igemm_fwd_rowtile(cfg) == 256) {
       if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
       return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
     }
@@ -1501,7 +1510,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return (cfg >= 36 && cfg <= 39) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

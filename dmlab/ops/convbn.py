@@ -52,8 +52,12 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
         # 64 output channels: the 256-pixel halo tile (2 x 2 waves of 128 x 32) amortises
         # the single-chunk halo prologue over twice the rows
+        # 42 / 43: the 20 / 38 tiles with two weight tiles of register prefetch
+        # (tools/bench_conv.py: +3-4 % on layer3/4, -3 % fwd on layer2)
         if ncols >= 512:
-            return 38  # 256-pixel tile, 8 waves: half the weight staging per FLOP
+            return 43  # 256-pixel tile, 8 waves: half the weight staging per FLOP
+        if ncols >= 256:
+            return 42
         return 20 if ncols >= 128 else 39
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
         t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
@@ -220,7 +224,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 24, 25, 36, 37, 38, 39):
+        if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)
