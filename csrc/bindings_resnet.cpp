@@ -100,8 +100,24 @@ int64_t conv_stats_rows(int64_t M, int64_t cfg) {
 }
 
 // dx = conv_transpose(dy, w) for stride 1 or 2; accumulate => dx += ...
-void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
-                int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg) {
+// Slab rows the BN-backward epilogue of conv_dgrad writes (0: the shape/cfg cannot fuse it).
+int64_t dgrad_bnb_rows(int64_t N, int64_t H, int64_t W, int64_t stride, int64_t cfg) {
+  if (cfg < 9) return 0;
+  if (stride == 1) return conv_stats_rows(N * H * W, cfg);
+  if (!(cfg == 12 || cfg == 13 || cfg == 15 || cfg == 16)) return 0;
+  const long long mmax = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);  // class (0, 0) is largest
+  return ((mmax + 127) / 128) * 4;
+}
+
+// dx = conv_transpose(dy, w) for stride 1 or 2; accumulate => dx += ...
+// bnb_*: optional BN-backward sums of the BN whose input gradient dx is (see BnBwdEpi):
+// written to bnb_slab [dgrad_bnb_rows][2][Cin]; returns the row count (0 = not computed).
+int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
+                   int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg,
+                   c10::optional<at::Tensor> bnb_y, c10::optional<at::Tensor> bnb_out,
+                   c10::optional<at::Tensor> bnb_mean, c10::optional<at::Tensor> bnb_invstd,
+                   c10::optional<at::Tensor> bnb_scale, c10::optional<at::Tensor> bnb_shift,
+                   int64_t bnb_mode, c10::optional<at::Tensor> bnb_slab) {
   // add: tensor added to the result (may alias dx for in-place accumulation)
   need_bf16_nhwc(dy, "dy");
   need_bf16_nhwc(dx, "dx");
@@ -120,6 +136,45 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
               "stride-2 dgrad accumulates only in place (add must alias dx)");
   const DeviceGuard guard(dy.device());
   auto st = cur_stream();
+  dm::BnBwdEpi bnb{};
+  int64_t bnb_rows = 0;
+  float* slabp = nullptr;
+  // the fused sums need every output pixel written by this launch: a stride-2 dgrad with
+  // a tap-less parity class (1x1/s2) only qualifies when it overwrites (those pixels are 0)
+  bool empty_class = false;
+  if (stride == 2)
+    for (int a = 0; a < 2; ++a)
+      for (int b = 0; b < 2; ++b)
+        if ((KH - ((a + pad) & 1) + 1) / 2 <= 0 || (KW - ((b + pad) & 1) + 1) / 2 <= 0)
+          empty_class = true;
+  if (bnb_y.has_value() && !(empty_class && addp)) bnb_rows = dgrad_bnb_rows(N, H, W, stride, cfg);
+  if (bnb_rows > 0) {
+    need_bf16_nhwc(*bnb_y, "bnb_y");
+    TORCH_CHECK(bnb_y->sizes() == dx.sizes(), "bnb_y: the BN input, shaped like dx");
+    TORCH_CHECK(bnb_mode >= 0 && bnb_mode <= 2, "bnb_mode: 0, 1 or 2");
+    TORCH_CHECK(bnb_slab.has_value(), "bnb_slab required");
+    need_f32(*bnb_slab, "bnb_slab", bnb_rows * 2 * Cin);
+    need_f32(*bnb_mean, "bnb_mean", Cin);
+    need_f32(*bnb_invstd, "bnb_invstd", Cin);
+    bnb.y = bp(*bnb_y);
+    bnb.mean = fp(*bnb_mean);
+    bnb.invstd = fp(*bnb_invstd);
+    bnb.mode = (int)bnb_mode;
+    if (bnb_mode == 1) {
+      TORCH_CHECK(bnb_out.has_value(), "bnb_out required for mode 1");
+      need_bf16_nhwc(*bnb_out, "bnb_out");
+      TORCH_CHECK(bnb_out->sizes() == dx.sizes());
+      bnb.out = bp(*bnb_out);
+    }
+    if (bnb_mode == 2) {
+      need_f32(*bnb_scale, "bnb_scale", Cin);
+      need_f32(*bnb_shift, "bnb_shift", Cin);
+      bnb.sc = fp(*bnb_scale);
+      bnb.sh = fp(*bnb_shift);
+    }
+    slabp = fp(*bnb_slab);
+  }
+  const dm::BnBwdEpi* bnbp = bnb.y ? &bnb : nullptr;
   dm::ConvGeom base{};
   base.N = N; base.H = OH; base.W = OW; base.C = Cout; base.lgC8 = ilog2(Cout / 8);
   base.OH = H; base.OW = W; base.OC = Cin;
@@ -131,8 +186,8 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
-    dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
-    return;
+    dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, slabp, g, cfg, st, bnbp);
+    return bnb_rows;
   }
   // parity classes write disjoint output pixels; a class with no taps (e.g. the odd
   // pixels of a 1x1/s2 conv) is exactly zero, so zero-fill once up front when needed
@@ -163,11 +218,21 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       set.g[ng++] = g;
     }
   // all parity classes in one launch (blockIdx.z = class) when the tile supports it
-  if (ng > 0 && dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, ng,
-                                    (int)cfg, st))
-    return;
+  if (bnbp) {
+    // slab rows of absent classes, or of row tiles past a smaller class's M (odd sizes),
+    // are never written: zero the slab first
+    bool uneven = ng != 4;
+    for (int i = 0; i < ng; ++i) uneven |= set.g[i].M != set.g[0].M;
+    if (uneven) TORCH_CHECK(hipMemsetAsync(slabp, 0, (size_t)bnb_rows * 2 * Cin * 4, st) == hipSuccess);
+    set.bnb = bnb;
+  }
+  if (ng > 0 && dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, slabp,
+                                    set, ng, (int)cfg, st))
+    return bnb_rows;
+  TORCH_CHECK(!bnbp, "conv_dgrad: BN-backward epilogue unsupported for this cfg");
   for (int i = 0; i < ng; ++i)
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr, set.g[i], cfg, st);
+  return 0;
 }
 
 // dw (fp32 OIHW [Cout][Cin][KH][KW]) = beta*dw + Σ_m dy ⊗ im2col(x)
@@ -320,7 +385,8 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
                  at::Tensor dbeta, double gbeta, int64_t mode, c10::optional<at::Tensor> scale,
                  c10::optional<at::Tensor> shift, c10::optional<at::Tensor> pdy,
                  c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P, at::Tensor dy,
-                 c10::optional<at::Tensor> dres, at::Tensor work) {
+                 c10::optional<at::Tensor> dres, at::Tensor work,
+                 c10::optional<at::Tensor> pre_slab, int64_t pre_rows) {
   need_bf16_nhwc(y, "y");
   need_bf16_nhwc(dy, "dy");
   TORCH_CHECK(dy.sizes() == y.sizes());
@@ -329,6 +395,10 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "bn_backward: C/8 must divide 256");
   const long long M = y.numel() / C;
   need_f32(work, "work", bn_bwd_work(M, C));
+  if (pre_slab.has_value()) {
+    TORCH_CHECK(mode <= 2 && pre_rows >= 1, "pre_slab: modes 0-2, >= 1 row");
+    need_f32(*pre_slab, "pre_slab", pre_rows * 2 * C);
+  }
   const bf* doutp = nullptr;
   if (mode < 3) {
     TORCH_CHECK(dout.has_value());
@@ -370,7 +440,8 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   const DeviceGuard guard(y.device());
   dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
                   (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
-                  OW, K, S, P, bp(dy), drp, fp(work), cur_stream());
+                  OW, K, S, P, bp(dy), drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
+                  (int)pre_rows);
 }
 
 void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,
@@ -438,7 +509,13 @@ void register_resnet(pybind11::module_& m) {
         py::arg("add"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg"), py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
   m.def("conv_stats_rows", &conv_stats_rows);
-  m.def("conv_dgrad", &conv_dgrad);
+  m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("dx"), py::arg("KH"),
+        py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("add"), py::arg("cfg"),
+        py::arg("bnb_y") = py::none(), py::arg("bnb_out") = py::none(),
+        py::arg("bnb_mean") = py::none(), py::arg("bnb_invstd") = py::none(),
+        py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(),
+        py::arg("bnb_mode") = 0, py::arg("bnb_slab") = py::none());
+  m.def("dgrad_bnb_rows", &dgrad_bnb_rows);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),
@@ -453,7 +530,8 @@ void register_resnet(pybind11::module_& m) {
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply);
   m.def("bn_bwd_work", &bn_bwd_work);
-  m.def("bn_backward", &bn_backward);
+  m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
+        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0);
   m.def("bn_relu_maxpool", &bn_relu_maxpool);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

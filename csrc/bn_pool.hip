@@ -879,18 +879,21 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  float gbeta, long long M, int C, int mode, const float* scale,
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
-                 hipStream_t st) {
+                 hipStream_t st, const float* pre_part, int pre_rows) {
+  // pre_part (optional): [pre_rows][2C] partial Σdz, Σdz·x̂ already reduced by the producing
+  // dgrad's epilogue (BnBwdEpi) — the reduction pass over dout and y is skipped
   // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
   BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C};
   // stem 3x3/s2/p1 pool with even H, W: quad gather (4 pixels share their 4 windows)
   const bool quad = mode == 3 && K == 3 && S == 2 && P == 1 && H % 2 == 0 && W % 2 == 0 &&
                     OH == H / 2 && OW == W / 2 && !dres && (long long)M * C / 8 < (1LL << 31);
-  const int G = quad ? bn_bwd_groups(M / 4, C) : bn_bwd_groups(M, C);
-  float* part = work;
-  float* coef = work + (long long)G * 2 * C;
+  const int G = pre_part ? pre_rows : quad ? bn_bwd_groups(M / 4, C) : bn_bwd_groups(M, C);
+  float* part = pre_part ? const_cast<float*>(pre_part) : work;
+  float* coef = pre_part ? work : work + (long long)G * 2 * C;
   float* part2 = coef + 3 * C;
   const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
-  if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
+  if (pre_part) {
+  } else if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
   else switch (mode) {
     case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
     case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;

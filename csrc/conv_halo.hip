@@ -43,7 +43,7 @@ template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb) {
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
   // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
   // image taps still read the zero row, i.e. the padding stays zero AFTER the BN.
@@ -276,7 +276,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       if (s + 1 < S) step(s + 1, rb, rb2);
     }
   }
-  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD,
+                                                       bnb);
 }
 
 int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
@@ -286,7 +287,8 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
 
 template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st) {
+                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
+                 const BnBwdEpi& bnb) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
@@ -297,7 +299,7 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
                   : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
   set_smem_attr(k, sm);
-  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb);
 }
 }  // namespace
 
@@ -315,23 +317,24 @@ bool conv_halo_supported(const ConvGeom& g) {
 
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
-               const float* pre_sh) {
+               const float* pre_sh, const BnBwdEpi* bnbp) {
+  const BnBwdEpi bnb = bnbp ? *bnbp : BnBwdEpi{};
   if (waves & 0x100) {  // two-deep weight prefetch (BN 128 only): 4 waves / 128 px, 8 waves / 256 px
     waves &= 0xff;
     if (bn == 128 && waves == 4) {
       const int hp = halo_rows_needed(g);
       const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-      if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
-      else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
-      else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
       DM_CHECK(hipGetLastError());
       return;
     }
     if (bn == 128 && waves == 16) {
       const int hr = (halo_rows_needed(g, 256) + 63) / 64;
-      if (hr <= 5) launch_halo<128, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
-      else if (hr <= 6) launch_halo<128, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
-      else launch_halo<128, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+      if (hr <= 5) launch_halo<128, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      else if (hr <= 6) launch_halo<128, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      else launch_halo<128, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
       DM_CHECK(hipGetLastError());
       return;
     }
@@ -340,9 +343,9 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 63) / 64;
 #define DM_HALO256W8(BN_)                                                                    \
-  if (hr <= 5) launch_halo<BN_, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);                  \
-  else if (hr <= 6) launch_halo<BN_, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);             \
-  else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+  if (hr <= 5) launch_halo<BN_, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);                  \
+  else if (hr <= 6) launch_halo<BN_, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);             \
+  else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
     if (bn == 128) { DM_HALO256W8(128) } else { DM_HALO256W8(64) }
 #undef DM_HALO256W8
     DM_CHECK(hipGetLastError());
@@ -353,9 +356,9 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 31) / 32;
 #define DM_HALO256W41(BN_)                                                                   \
-  if (hr <= 10) launch_halo<BN_, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);                \
-  else if (hr <= 12) launch_halo<BN_, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
-  else launch_halo<BN_, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+  if (hr <= 10) launch_halo<BN_, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);                \
+  else if (hr <= 12) launch_halo<BN_, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
+  else launch_halo<BN_, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
     DM_HALO256W41(64)
 #undef DM_HALO256W41
     DM_CHECK(hipGetLastError());
@@ -365,9 +368,9 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 31) / 32;
 #define DM_HALO256(BN_)                                                                      \
-  if (hr <= 10) launch_halo<BN_, 10, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);                \
-  else if (hr <= 12) launch_halo<BN_, 12, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
-  else launch_halo<BN_, 14, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+  if (hr <= 10) launch_halo<BN_, 10, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);                \
+  else if (hr <= 12) launch_halo<BN_, 12, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
+  else launch_halo<BN_, 14, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
     if (bn == 128) { DM_HALO256(128) } else { DM_HALO256(64) }
 #undef DM_HALO256
     DM_CHECK(hipGetLastError());
@@ -377,17 +380,17 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   if (waves == 8) {  // 4 x 2 waves of 32 x BN/2
     const int hr = hp <= 192 ? 3 : hp <= 256 ? 4 : 6;
 #define DM_HALO8(BN_)                                                            \
-  if (hr == 3) launch_halo<BN_, 3, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
-  else if (hr == 4) launch_halo<BN_, 4, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);      \
-  else launch_halo<BN_, 6, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+  if (hr == 3) launch_halo<BN_, 3, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
+  else if (hr == 4) launch_halo<BN_, 4, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);      \
+  else launch_halo<BN_, 6, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
     if (bn == 128) { DM_HALO8(128) } else { DM_HALO8(64) }
 #undef DM_HALO8
   } else {  // 2 x 2 waves of 64 x BN/2
     const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
 #define DM_HALO4(BN_)                                                            \
-  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);           \
-  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);      \
-  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
+  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);      \
+  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
     if (bn == 128) { DM_HALO4(128) } else { DM_HALO4(64) }
 #undef DM_HALO4
   }

@@ -32,6 +32,8 @@
 #include "igemm_common.h"
 #include "kernels.h"
 
+#include <stdexcept>
+
 #include <type_traits>
 
 namespace dm {
@@ -621,7 +623,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     }
   }
 
-  mfma_tile_epilogue<BM, BN, WM, WN, MF32>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD);
+  mfma_tile_epilogue<BM, BN, WM, WN, MF32>(acc, smem, m0, n0, blockIdx.z * gridDim.x + blockIdx.x,
+                                           stats, g, Y, ADD, gs.bnb);
 }
 
 // ------------------------------------------------------------------ forward / dgrad, LDS-DMA
@@ -1382,7 +1385,7 @@ static size_t fwd_smem(int BM, int BN) {
 template <int BM, int BN, int WM, int WN>
 static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
                        float* stats, const ConvGeom& g, bool dma, bool buf, bool v3, bool mf32,
-                       hipStream_t st) {
+                       hipStream_t st, const BnBwdEpi* bnb = nullptr) {
   const size_t sm = fwd_smem(BM, BN);
   dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
@@ -1394,7 +1397,7 @@ static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_
   } else if (v3) {
     auto k = mf32 ? igemm_fwd3_kernel<BM, BN, WM, WN, true, 1> : igemm_fwd3_kernel<BM, BN, WM, WN, false, 1>;
     set_smem_attr(k, sm);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), xb, wb);
+    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g, bnb), xb, wb);
   } else if (buf) {
     auto k = igemm_fwd_kernel<BM, BN, WM, WN, true>;
     set_smem_attr(k, sm);
@@ -1423,19 +1426,22 @@ static void launch_fwd3_set(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const 
 
 template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
 static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                        float* stats, const ConvGeom& g, hipStream_t st) {
-  launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1, st);
+                        float* stats, const ConvGeom& g, hipStream_t st,
+                        const BnBwdEpi* bnb = nullptr) {
+  launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g, bnb), 1,
+                                               st);
 }
 
 // up to four geometries sharing X / W / Y (the parity classes of a stride-2 dgrad) in one
 // launch on the v3 128x128 mf32 tile (no statistics: the classes' row tiles would collide)
-bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+// stats (optional, with gs.bnb set): BN-backward sums, slab rows class * grid.x + row tile
+bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st) {
   switch (cfg) {  // the v3 mf32 tiles of igemm_fwd (12/13: one tile of prefetch, 15/16: two)
-    case 12: launch_fwd3_set<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
-    case 13: launch_fwd3_set<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
-    case 15: launch_fwd3_set<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
-    case 16: launch_fwd3_set<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st); return true;
+    case 12: launch_fwd3_set<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
+    case 13: launch_fwd3_set<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
+    case 15: launch_fwd3_set<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
+    case 16: launch_fwd3_set<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
     default: return false;
   }
 }
@@ -1459,7 +1465,9 @@ bool halo_cfg(int cfg, int& bn, int& waves) {
 }
 
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st) {
+               const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb) {
+  // bnb (BN-backward sums in the epilogue) is supported by the v3 (fwd3) and halo kernels
+  if (bnb && cfg < 9) throw std::runtime_error("igemm_fwd: BN-backward epilogue needs cfg >= 9");
   // v3 with two tiles of register prefetch: 15 = 128x128 mf32, 16 = 128x64 mf32, 17 = 64x64
   // 16x16; 18 = 8-wave 256x128 mf32 (measured slower: one workgroup per CU)
   // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64, 4 waves;
@@ -1468,35 +1476,35 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 38 / 39: 256-pixel halo tile with 4 x 2 waves of 64 x BN/2, BN 128 / 64
   int bn, waves;
   if (halo_cfg(cfg, bn, waves)) {
-    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st);
+    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st, nullptr, nullptr, bnb);
     // fallback keeps the row tile (stats slab rows = igemm_fwd_rowtile(cfg))
     if (igemm_fwd_rowtile(cfg) == 256) {
-      if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
-      return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+      if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+      return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
     }
     cfg = bn == 128 ? 12 : 13;
   }
-  if (cfg == 15) return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 16) return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 17) return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 18) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 15) return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 16) return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 17) return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 18) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
   // 8-wave 128-row tiles (4 waves per SIMD at 2 workgroups per CU): 19 = 128x128 as 4x2
   // waves of 32x64, 22 = 128x128 as 2x4 waves of 64x32, 23 = 128x64 as 4x2 waves of 32x32
-  if (cfg == 19) return launch_fwd3<128, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 19) return launch_fwd3<128, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
   // 34 / 35: v3 with the next tile's LDS stores interleaved into the MFMA substeps
-  if (cfg == 34) return launch_fwd3<128, 128, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 35) return launch_fwd3<128, 64, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 34) return launch_fwd3<128, 128, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 35) return launch_fwd3<128, 64, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st, bnb);
   // 26 / 27 / 28: v3 with the LDS-DMA loader, tiles 128x128 / 128x64 mf32, 64x64 16x16
-  if (cfg == 26) return launch_fwd3<128, 128, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 27) return launch_fwd3<128, 64, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 28) return launch_fwd3<64, 64, 2, 2, false, 0>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 26) return launch_fwd3<128, 128, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 27) return launch_fwd3<128, 64, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 28) return launch_fwd3<64, 64, 2, 2, false, 0>(X, Wp, Y, ADD, stats, g, st, bnb);
   // 30-33: ablations of tile 12 for measurement only (results are wrong)
-  if (cfg == 30) return launch_fwd3<128, 128, 2, 2, true, -1>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 31) return launch_fwd3<128, 128, 2, 2, true, -2>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 32) return launch_fwd3<128, 128, 2, 2, true, -3>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 33) return launch_fwd3<128, 128, 2, 2, true, -7>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 22) return launch_fwd3<128, 128, 2, 4, true, 1>(X, Wp, Y, ADD, stats, g, st);
-  if (cfg == 23) return launch_fwd3<128, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+  if (cfg == 30) return launch_fwd3<128, 128, 2, 2, true, -1>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 31) return launch_fwd3<128, 128, 2, 2, true, -2>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 32) return launch_fwd3<128, 128, 2, 2, true, -3>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 33) return launch_fwd3<128, 128, 2, 2, true, -7>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 22) return launch_fwd3<128, 128, 2, 4, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+  if (cfg == 23) return launch_fwd3<128, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
   // cfg % 3: 0 = 128x128 (2x2 waves, 64x64 per wave), 1 = 128x64, 2 = 64x64
   // cfg / 3: 0 = register-staged global loads, 1 = LDS-DMA (buffer_load ... lds),
   //          2 = register-staged buffer loads (branch-free zero fill)
@@ -1504,9 +1512,9 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   const int ld = cfg / 3;
   const bool dma = ld == 1, buf = ld == 2, v3 = ld >= 3, mf32 = ld == 4;
   switch (cfg % 3) {
-    case 0: launch_fwd<128, 128, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st); break;
-    case 1: launch_fwd<128, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st); break;
-    default: launch_fwd<64, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st); break;
+    case 0: launch_fwd<128, 128, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st, bnb); break;
+    case 1: launch_fwd<128, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st, bnb); break;
+    default: launch_fwd<64, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st, bnb); break;
   }
 }
 

@@ -62,11 +62,15 @@ using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 //    output pixel (y*osy+oy0, x*osx+ox0), optionally adding ADD (which may alias Y).
 // Rows >= g.M must hold zeros when stats are requested.  Requires (BM/PASSES)*(BN+4)*4 B of
 // LDS: with PASSES > 1 the tile is staged one band of BM/PASSES rows (whole wave rows) at a time.
+//  * optional BN-backward sums (bnb.y set; stats then receives Σdz, Σdz·x̂ — see BnBwdEpi)
 template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1>
 __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / WM / (MF32 ? 32 : 16)][BN / WN / (MF32 ? 32 : 16)],
                                                    unsigned char* smem, long long m0, int n0,
                                                    int stat_row, float* stats, const ConvGeom& g,
-                                                   bf16_t* Y, const bf16_t* ADD) {
+                                                   bf16_t* Y, const bf16_t* ADD,
+                                                   const BnBwdEpi& bnb = BnBwdEpi{}) {
+  const bool bwd = stats && bnb.y;
+  float* fstats = bwd ? nullptr : stats;  // forward Σy, Σy² of the fp32 tile
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = MF32 ? 32 : 16;
   constexpr int RM = TM / FM, RN = TN / FM;
@@ -77,7 +81,7 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
   auto frow = [&](int r) { return MF32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r; };
   const int fcol = MF32 ? (lane & 31) : (lane & 15);
   float* red = reinterpret_cast<float*>(smem);
-  if (stats) {
+  if (fstats) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
       float sm = 0.f, q = 0.f;
@@ -110,8 +114,8 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
         q += red[(w * BN + c) * 2 + 1];
       }
       if (n0 + c < g.Ncols) {
-        stats[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = sm;
-        stats[((long long)stat_row * 2 + 1) * g.Ncols + n0 + c] = q;
+        fstats[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = sm;
+        fstats[((long long)stat_row * 2 + 1) * g.Ncols + n0 + c] = q;
       }
     }
     __syncthreads();
@@ -121,6 +125,22 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
   static_assert(RPB % TM == 0, "a band holds whole wave rows");
   float* cs = reinterpret_cast<float*>(smem);
   constexpr int CPR = BN / 8;
+  static_assert(NT % CPR == 0, "a thread keeps one 8-column group across rows");
+  // BN-backward sums: this thread's 8 columns are fixed (e ≡ tid mod CPR)
+  float bs_[8], bq_[8], bmu[8], bis[8], bsc[8], bsh[8];
+  const int bcol = n0 + (tid % CPR) * 8;
+  if (bwd) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      bs_[j] = 0.f;
+      bq_[j] = 0.f;
+      const bool okc = bcol + j < g.Ncols;
+      bmu[j] = okc ? bnb.mean[bcol + j] : 0.f;
+      bis[j] = okc ? bnb.invstd[bcol + j] : 0.f;
+      bsc[j] = okc && bnb.mode == 2 ? bnb.sc[bcol + j] : 0.f;
+      bsh[j] = okc && bnb.mode == 2 ? bnb.sh[bcol + j] : 0.f;
+    }
+  }
 #pragma unroll
   for (int pb = 0; pb < PASSES; ++pb) {
     if (PASSES > 1) __syncthreads();  // previous band's LDS reads done
@@ -134,31 +154,98 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
             cs[(wm * TM - pb * RPB + i * FM + frow(r)) * LDC + wn * TN + j * FM + fcol] = acc[i][j][r];
     }
     __syncthreads();
-    for (int e = tid; e < RPB * CPR; e += NT) {
-      const int row = e / CPR, cc = e % CPR;
-      const long long m = m0 + pb * RPB + row;
-      const int col = n0 + cc * 8;
-      if (m >= g.M || col >= g.Ncols) continue;
-      const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
-      const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
-      const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
-      const int y = (int)(t - n * (unsigned)g.Hg);
-      const long long o =
-          (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
-      const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
-      const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
-      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if (ADD) {
-        const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
-        const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+    // rows in groups of UNR: every global load of a group (ADD, and y / out for the
+    // BN-backward sums) is issued before its first store, so they overlap
+    constexpr int ITERS = RPB * CPR / NT;
+    static_assert(ITERS * NT == RPB * CPR, "rows per band divisible by the block");
+    constexpr int UNR = ITERS < 4 ? ITERS : 4;
+    static_assert(ITERS % UNR == 0, "row groups");
+    const int cc = tid % CPR;
+    const int col = n0 + cc * 8;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
-          v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+    for (int i0 = 0; i0 < ITERS; i0 += UNR) {
+      long long o[UNR];
+      bool ok[UNR];
+      uint4 av[UNR], yv[UNR], ov[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int row = (tid + (i0 + u) * NT) / CPR;
+        const long long m = m0 + pb * RPB + row;
+        ok[u] = m < g.M && col < g.Ncols;
+        const long long mm = ok[u] ? m : m0;
+        const unsigned t = fdiv((unsigned)mm, g.wg_mul, g.wg_shr);
+        const int x = (int)((unsigned)mm - t * (unsigned)g.Wg);
+        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+        const int y = (int)(t - n * (unsigned)g.Hg);
+        o[u] = (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+        av[u] = yv[u] = ov[u] = make_uint4(0, 0, 0, 0);
+        if (ok[u]) {
+          if (ADD) av[u] = *reinterpret_cast<const uint4*>(ADD + o[u]);
+          if (bwd) {
+            yv[u] = *reinterpret_cast<const uint4*>(bnb.y + o[u]);
+            if (bnb.mode == 1) ov[u] = *reinterpret_cast<const uint4*>(bnb.out + o[u]);
+          }
         }
       }
-      *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                                    pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        if (!ok[u]) continue;
+        const int row = (tid + (i0 + u) * NT) / CPR;
+        const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
+        const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
+        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        if (ADD) {
+          const uint32_t aw[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
+            v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+          }
+        }
+        const uint4 packed = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                        pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+        *reinterpret_cast<uint4*>(Y + o[u]) = packed;
+        if (bwd) {
+          // sums over the values as stored (bf16), exactly what a separate pass would read
+          const uint32_t pw[4] = {packed.x, packed.y, packed.z, packed.w};
+          const uint32_t yw[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
+          const uint32_t ow[4] = {ov[u].x, ov[u].y, ov[u].z, ov[u].w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int sh16 = (j & 1) * 16;
+            float d = bf2f((bf16_t)(pw[j >> 1] >> sh16));
+            const float yf = bf2f((bf16_t)(yw[j >> 1] >> sh16));
+            if (bnb.mode == 1) d = bf2f((bf16_t)(ow[j >> 1] >> sh16)) > 0.f ? d : 0.f;
+            else if (bnb.mode == 2) d = yf * bsc[j] + bsh[j] > 0.f ? d : 0.f;
+            bs_[j] += d;
+            bq_[j] += d * (yf - bmu[j]) * bis[j];
+          }
+        }
+      }
+    }
+  }
+  if (bwd) {
+    // fixed-order combine of the NT / CPR threads that share each 8-column group
+    __syncthreads();  // the staging tile is dead
+    float* rb = reinterpret_cast<float*>(smem);  // [NT][16]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      rb[tid * 16 + j] = bs_[j];
+      rb[tid * 16 + 8 + j] = bq_[j];
+    }
+    __syncthreads();
+    constexpr int RL = NT / CPR;
+    for (int c = tid; c < BN; c += NT) {
+      const int grp = c >> 3, j = c & 7;
+      float a0 = 0.f, a1 = 0.f;
+      for (int r = 0; r < RL; ++r) {
+        a0 += rb[(r * CPR + grp) * 16 + j];
+        a1 += rb[(r * CPR + grp) * 16 + 8 + j];
+      }
+      if (n0 + c < g.Ncols) {
+        stats[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = a0;
+        stats[((long long)stat_row * 2 + 1) * g.Ncols + n0 + c] = a1;
+      }
     }
   }
 }

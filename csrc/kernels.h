@@ -60,15 +60,17 @@ void xgmi_allreduce(const float* in, float* out, long long n, long long cap, voi
 // conv_igemm.hip
 struct ConvGeom;
 struct ConvGeomSet;
-bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+struct BnBwdEpi;
+bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st);
+               const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,
-               const float* pre_sc = nullptr, const float* pre_sh = nullptr);
+               const float* pre_sc = nullptr, const float* pre_sh = nullptr,
+               const BnBwdEpi* bnb = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
@@ -99,7 +101,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  float gbeta, long long M, int C, int mode, const float* scale,
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
-                 hipStream_t st);
+                 hipStream_t st, const float* pre_part = nullptr, int pre_rows = 0);
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
                      int P, hipStream_t st);

@@ -154,6 +154,10 @@ class _ProgramFn(torch.autograd.Function):
         for i in range(n - 1, -1, -1):
             layer = prog.layers[i]
             need_dx = i > 0 or ctx.need_dx
+            if i > 0 and ctx.ctxs[i] is not None:
+                # the layer whose backward consumes this one's dx (lets a producer fuse
+                # work of the consumer into its own kernels, e.g. BN-backward sums)
+                ctx.ctxs[i]["_prev"] = (prog.layers[i - 1], ctx.ctxs[i - 1])
             with _range(f"bwd:{i}:{type(layer).__name__}"):
                 dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
             ctx.ctxs[i] = None  # free saved activations as soon as possible

@@ -16,6 +16,7 @@ cached per layer and refreshed when the fp32 master changes.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -272,11 +273,35 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
+# Fused BN-backward sums in the dgrad epilogue: opt-in.  Measured on MI355X (ResNet-18,
+# batch 256): the separate reductions it removes cost ~460 us/step, but the heavier dgrad
+# epilogues (reading y, and `out` for residual BNs, behind the output store) cost ~600 us,
+# e.g. layer1 dgrad 84 -> 139 us.  Kept for A/B runs: DMLAB_FUSE_BN_BWD=1.
+_FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
+
+
+def bnb_spec(layer, ctx):
+    """conv_dgrad keyword arguments that make a dgrad epilogue reduce the BN-backward sums
+    (Σdz, Σdz·x̂) of ``layer`` — the ConvBN whose BN-output gradient the dgrad produces —
+    or None when that BN's backward cannot use them (stem pool gather, eval mode)."""
+    if getattr(layer, "pool_k", 0) or ctx.get("mean") is None or "y" not in ctx:
+        return None
+    mode = 1 if ctx["has_res"] else (2 if layer.relu else 0)
+    return dict(bnb_y=ctx["y"], bnb_out=ctx.get("out") if mode == 1 else None,
+                bnb_mean=ctx["mean"], bnb_invstd=ctx["invstd"],
+                bnb_scale=ctx["scale"] if mode == 2 else None,
+                bnb_shift=ctx["shift"] if mode == 2 else None, bnb_mode=mode)
+
+
+def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=None):
     """Returns dx (or (dx, dres) when the forward had a residual input).
 
     ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient)
-    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)."""
+    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)
+    ``consumer``: (ConvBN, ctx) whose BN backward consumes dx; the dgrad epilogue then
+                  also reduces that BN's backward sums (stored in its ctx as
+                  ``dz_stats``), so its reduction pass over dx and y is skipped.  dx must
+                  be final after this call (the last writer of dx computes the sums)."""
     L = lib()
     x, y = ctx["x"], ctx["y"]
     N, OH, OW, cout = y.shape
@@ -288,6 +313,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     dy = empty_nhwc(N, OH, OW, cout, y)
     dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
+    pre_sums = {}
+    zs = ctx.pop("dz_stats", None)
+    if zs is not None and zs[2].data_ptr() == dout.data_ptr() and zs[2].shape == dout.shape:
+        pre_sums = dict(pre_slab=zs[0], pre_rows=zs[1])  # sums from the producer's epilogue
     pool = getattr(layer, "pool_k", 0)
     if pool:
         mode = 3       # dz gathered from the max-pool gradient, ReLU mask from y
@@ -302,7 +331,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
-                  getattr(layer, "pool_p", 1), dy, dres, work)
+                  getattr(layer, "pool_p", 1), dy, dres, work, **pre_sums)
     # weight gradient
     C = x.shape[3]
     K = k * k * C
@@ -322,12 +351,21 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
         _, wd = packed_weights(layer, need_wd=True)
         N_, H, W, Cin = x.shape
         cfg = pick_cfg(N_ * H * W, Cin, k, s, cout)
+        bkw = {}
+        spec = bnb_spec(*consumer) if (consumer is not None and _FUSE_BN_BWD) else None
+        if spec is not None:
+            rows = L.dgrad_bnb_rows(N_, H, W, s, cfg)
+            if rows:
+                bkw = dict(spec, bnb_slab=torch.empty(rows * 2 * Cin, device=y.device,
+                                                      dtype=torch.float32))
         if dx_into is not None:
-            L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
             dx = dx_into
+            r = L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg, **bkw)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)
+            r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **bkw)
+        if bkw and r:
+            consumer[1]["dz_stats"] = (bkw["bnb_slab"], r, dx)
     if ctx["has_res"]:
         return dx, dres
     return dx
