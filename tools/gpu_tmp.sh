@@ -1,7 +1,12 @@
+# Scratch GPU session script (overwritten per experiment).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_native_resnet_model.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_q9.log 2>&1 && \
-DMLAB_FUSE_BN_BWD=1 timeout -k 10 300 python -u -m pytest tests/test_native_resnet_model.py -m gpu -x -q --timeout 120 --timeout-method thread >> gpurun_out/pytest_q9.log 2>&1 && \
-timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_q9.json 2> gpurun_out/bench_q9.err && \
-DMLAB_FUSE_BN_BWD=1 timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_q9f.json 2> gpurun_out/bench_q9f.err
-rc=$?; grep passed gpurun_out/pytest_q9.log; cat gpurun_out/bench_q9.json gpurun_out/bench_q9f.json | cut -c1-140; exit $rc
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+t=s4b
+for b in 384 768 1024; do
+  timeout -k 10 200 python bench.py --steps 15 --warmup 3 --batch $b > gpurun_out/bench_${t}_b$b.json 2>> gpurun_out/bench_$t.err || exit $?
+done
+timeout -k 10 300 python tools/probe_stock.py --resnet-batches 512 > gpurun_out/stock_$t.jsonl 2>> gpurun_out/bench_$t.err
+rc=$?
+cat gpurun_out/bench_${t}_*.json gpurun_out/stock_$t.jsonl | cut -c 1-260
+exit $rc

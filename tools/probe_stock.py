@@ -70,8 +70,14 @@ def run_lenet(batch, warmup, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--resnet-batches", default=None,
+                    help="comma-separated ResNet-18 batches (channels_last bf16) only")
     a = ap.parse_args()
     print(json.dumps({"device": torch.cuda.get_device_name(0)}), flush=True)
+    if a.resnet_batches:
+        for b in a.resnet_batches.split(","):
+            print(json.dumps(run_resnet(int(b), 224, torch.bfloat16, True, 5, 20)), flush=True)
+        return
     for b in (32, 4096):
         print(json.dumps(run_lenet(b, 20, 100)), flush=True)
     for b, cl in ((256, True), (256, False), (128, True)):

@@ -64,8 +64,14 @@ def main():
     path = args[0]
     steps = float(args[1]) if len(args) > 1 else 1.0
     if step_mode:
-        for n, s0, e, gx, wg in step_rows(path):
+        rs = step_rows(path)
+        for n, s0, e, gx, wg in rs:
             print(f"{(e - s0) / 1e3:8.1f} us  grid {int(gx) // int(wg):6d}  {family(n)[:70]}")
+        # busy time vs the step's wall span: the difference is launch gaps / idle GPU
+        busy = sum(e - s0 for _, s0, e, _, _ in rs)
+        span = rs[-1][2] - rs[0][1]
+        print(f"{len(rs)} kernels, busy {busy / 1e6:.3f} ms, span {span / 1e6:.3f} ms, "
+              f"gaps {(span - busy) / 1e6:.3f} ms")
         return
     if path.endswith(".db"):
         rows = rows_db(path, frac)
