@@ -56,8 +56,10 @@ def parse():
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole step (fwd+bwd+all-reduce+opt) in a hipGraph; "
-                         "-1 = auto (on for one GPU; off for multi-GPU, where the step is "
-                         "GPU-bound and eager RCCL keeps the launch path simplest)")
+                         "-1 = auto: on for the launch-bound LeNet on one GPU; off for "
+                         "ResNet-18, whose step is GPU-bound and whose weight gradients run "
+                         "on a second stream (eager two-stream 39.4k img/s vs 38.2-38.4k "
+                         "captured, one MI355X, profiles/wgrad_stream_ab_r1s4.txt)")
     return ap.parse_args()
 
 
@@ -115,7 +117,7 @@ def main():
         return loss.detach()
 
     if a.graph < 0:
-        a.graph = 1 if ws == 1 else 0
+        a.graph = 1 if (ws == 1 and a.model == "lenet") else 0
     if a.graph and a.backend == "native":
         from dmlab.utils.graph import CapturedStep
 

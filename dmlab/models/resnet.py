@@ -39,6 +39,8 @@ class ResNet18(Program):
         layers += [self.avgpool, self.fc]
         self.set_dtype(torch.bfloat16)
         self.build(layers)
+        # conv weight gradients run on a second stream, overlapping the dgrad/BN chain
+        self._uses_side_stream = True
 
     def prepare_native(self, x):
         if self.compute_dtype != torch.bfloat16:

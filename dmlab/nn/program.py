@@ -151,18 +151,48 @@ class _ProgramFn(torch.autograd.Function):
         prog._accumulate = prog.flat.prepare_backward()
         dy = dy.contiguous() if not prog._native_active else dy
         n = len(prog.layers)
-        for i in range(n - 1, -1, -1):
-            layer = prog.layers[i]
-            need_dx = i > 0 or ctx.need_dx
-            if i > 0 and ctx.ctxs[i] is not None:
-                # the layer whose backward consumes this one's dx (lets a producer fuse
-                # work of the consumer into its own kernels, e.g. BN-backward sums)
-                ctx.ctxs[i]["_prev"] = (prog.layers[i - 1], ctx.ctxs[i - 1])
-            with _range(f"bwd:{i}:{type(layer).__name__}"):
-                dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
-            ctx.ctxs[i] = None  # free saved activations as soon as possible
-            for hook in prog._grad_hooks:
-                hook(prog, i)
+        # Weight gradients off the critical path: layers that support it (ConvBN) queue
+        # their wgrad on a second stream, which overlaps the data-gradient / BN-backward
+        # chain of the following layers (the chain is a sequence of short and latency-
+        # bound kernels that leave CUs idle).  A layer's grad hooks (DDP bucket launches)
+        # run one layer later, after the main stream has waited for that layer's wgrads.
+        side = prog._side_stream() if prog._native_active else None
+        main = torch.cuda.current_stream() if side is not None else None
+        if side is not None:
+            side.wait_stream(main)  # fork (under hipGraph capture: joins the capture)
+        prog._wgrad_stream = side
+        pending = []  # (layer index, event after its wgrads) whose hooks have not run
+        try:
+            for i in range(n - 1, -1, -1):
+                layer = prog.layers[i]
+                need_dx = i > 0 or ctx.need_dx
+                if i > 0 and ctx.ctxs[i] is not None:
+                    # the layer whose backward consumes this one's dx (lets a producer fuse
+                    # work of the consumer into its own kernels, e.g. BN-backward sums)
+                    ctx.ctxs[i]["_prev"] = (prog.layers[i - 1], ctx.ctxs[i - 1])
+                with _range(f"bwd:{i}:{type(layer).__name__}"):
+                    dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
+                ctx.ctxs[i] = None  # free saved activations as soon as possible
+                if side is None:
+                    for hook in prog._grad_hooks:
+                        hook(prog, i)
+                    continue
+                for j, ev in pending:
+                    main.wait_event(ev)
+                    for hook in prog._grad_hooks:
+                        hook(prog, j)
+                pending = []
+                if prog._grad_hooks:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    pending.append((i, ev))
+        finally:
+            prog._wgrad_stream = None
+        if side is not None:
+            main.wait_stream(side)
+            for j, _ in pending:
+                for hook in prog._grad_hooks:
+                    hook(prog, j)
         prog.flat.grad_valid = True
         for hook in prog._post_backward_hooks:
             hook(prog)
@@ -190,6 +220,9 @@ class Program(nn.Module):
         self._post_backward_hooks: list[Callable] = []
         self._anchor = torch.zeros(1, requires_grad=True)
         self._wver = None
+        self._uses_side_stream = False  # set by subclasses whose layers queue wgrads aside
+        self._side_streams = {}
+        self._wgrad_stream = None
 
     # ---------------------------------------------------------------- construction
     def build(self, layers):
@@ -277,6 +310,17 @@ class Program(nn.Module):
         for layer in self.layers:
             h = layer.fwd(h, Ctx(), False)
         return h
+
+    def _side_stream(self):
+        """Second HIP stream for off-critical-path backward work (weight gradients), or
+        None when disabled (``DMLAB_WGRAD_STREAM=0``) or no layer uses it."""
+        if not self._uses_side_stream or os.environ.get("DMLAB_WGRAD_STREAM", "1") == "0":
+            return None
+        dev = torch.cuda.current_device()
+        st = self._side_streams.get(dev)
+        if st is None:
+            st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
+        return st
 
     def prepare_native(self, x):
         """Hook for subclasses: convert input layout / refresh packed weights."""

@@ -15,6 +15,7 @@ cached per layer and refreshed when the fp32 master changes.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -279,6 +280,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
 # e.g. layer1 dgrad 84 -> 139 us.  Kept for A/B runs: DMLAB_FUSE_BN_BWD=1.
 _FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
 
+# Weight gradients of convs with at least this many output channels go to the Program's
+# side stream (DMLAB_WGRAD_STREAM_MIN_COUT; 0 = all).
+_SIDE_MIN_COUT = int(os.environ.get("DMLAB_WGRAD_STREAM_MIN_COUT", "0"))
+
 
 def bnb_spec(layer, ctx):
     """conv_dgrad keyword arguments that make a dgrad epilogue reduce the BN-backward sums
@@ -332,20 +337,32 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
                   getattr(layer, "pool_p", 1), dy, dres, work, **pre_sums)
-    # weight gradient
+    # weight gradient: on the Program's side stream when it has one (off the critical
+    # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
+    # main stream allocated are recorded on the side stream so the caching allocator does
+    # not hand their memory out again before the wgrad has read them.
     C = x.shape[3]
     K = k * k * C
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
-    slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
     pre = ctx.get("pre")
-    pre_kw = {}
-    if pre is not None:
-        if wcfg in (4, 5):
-            pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
-        else:
-            x = _materialise(x, pre)
-    L.conv_wgrad(x, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg, s2d,
-                 **pre_kw)
+    side = getattr(layer._prog, "_wgrad_stream", None)
+    if side is not None and layer.cout < _SIDE_MIN_COUT:
+        side = None
+    if side is not None:
+        side.wait_stream(torch.cuda.current_stream())
+        for t in (x, dy) + (tuple(pre) if pre is not None else ()):
+            t.record_stream(side)
+    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+        slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
+        pre_kw = {}
+        xw = x
+        if pre is not None:
+            if wcfg in (4, 5):
+                pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
+            else:
+                xw = _materialise(x, pre)
+        L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg,
+                     s2d, **pre_kw)
     dx = None
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)

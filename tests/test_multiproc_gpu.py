@@ -89,7 +89,7 @@ def _entry(rank, ws, port, kind, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "pipeline", "xgmi"])
+@pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "ddp_resnet", "pipeline", "xgmi"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 

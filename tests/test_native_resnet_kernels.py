@@ -264,6 +264,25 @@ def test_stem_space_to_depth(dev, H):
         assert _rel(dw, dref) < 2e-3
 
 
+@pytest.mark.parametrize("layout", ["channels_last", "nchw"])
+@pytest.mark.parametrize("H", [8, 224])
+def test_stem_s2d_packing_layouts(dev, layout, H):
+    """Space-to-depth packing of an fp32 image batch (channels_last takes the vectorised
+    2-pixel kernel, NCHW the generic one): xs[n,i,j,(dy*2+dx)*3+c] = x[n,c,2i+dy,2j+dx]."""
+    N, C = 3, 3
+    x = torch.randn(N, C, H, H, device=dev)
+    if layout == "channels_last":
+        x = x.contiguous(memory_format=torch.channels_last)
+    xs = torch.full((N, H // 2, H // 2, 16), 7.0, device=dev, dtype=torch.bfloat16)
+    lib().pack_input_s2d(x, xs)
+    ref = torch.zeros(N, H // 2, H // 2, 16, device=dev)
+    for dy in range(2):
+        for dx in range(2):
+            sub = x[:, :, dy::2, dx::2].permute(0, 2, 3, 1)
+            ref[..., (dy * 2 + dx) * 3:(dy * 2 + dx) * 3 + 3] = sub
+    assert torch.equal(xs.float(), ref.bfloat16().float())
+
+
 @pytest.mark.parametrize("H,C", [(18, 64), (17, 64), (56, 32)])
 def test_fused_bn_relu_maxpool_and_gather_backward(dev, H, C):
     """Stem tail: maxpool(relu(bn(y))) forward and the pool-gather BN backward (mode 3;
