@@ -223,7 +223,9 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     if wf is None:
         wf, _ = packed_weights(layer, need_wd=train and not first)
     y = empty_nhwc(N, OH, OW, cout, x)
-    cfg = pick_cfg(M, cout, k, s, C)
+    # s2d stem: the 128x64 v3 tile with two K-tiles of register prefetch (16) runs 382 vs
+    # 336 TFLOP/s for the single-prefetch tile (13) at batch 512 (profiles/conv_stem_s2d_r1s4.jsonl)
+    cfg = 16 if s2d else pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
         if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43):

@@ -48,6 +48,33 @@ def _entry(rank, ws, port, kind, q):
                 err = max(err, (out - ref_v).abs().max().item())
             ar.check()
             ar.close()
+        elif kind == "ddp_resnet":
+            # ResNet-18 (bf16 native kernels, conv weight gradients on the side stream):
+            # the DDP-averaged gradient == the mean of the two per-shard gradients computed
+            # one after the other in this process (BN statistics are per shard either way)
+            from dmlab.models import ResNet18
+            from dmlab.parallel import DDP
+
+            gr = torch.Generator().manual_seed(7)
+            Xr = torch.rand(8, 3, 32, 32, generator=gr).to(dev)
+            Yr = torch.randint(0, 10, (8,), generator=gr).to(dev)
+            torch.manual_seed(0)
+            model = ResNet18(num_classes=10).to(dev)
+            ddp = DDP(model)
+            mopt = SGD(model.parameters(), lr=0.1)
+            mopt.zero_grad()
+            cross_entropy(ddp(Xr[rank * 4:(rank + 1) * 4]), Yr[rank * 4:(rank + 1) * 4]).backward()
+            g_ddp = model.flat.grad.clone()
+            torch.manual_seed(0)
+            rmodel = ResNet18(num_classes=10).to(dev)
+            rsgd = SGD(rmodel.parameters(), lr=0.1)
+            gs = []
+            for k in range(2):
+                rsgd.zero_grad()
+                cross_entropy(rmodel(Xr[k * 4:(k + 1) * 4]), Yr[k * 4:(k + 1) * 4]).backward()
+                gs.append(rmodel.flat.grad.clone())
+            want = (gs[0] + gs[1]) / 2
+            err = ((g_ddp - want).abs().max() / want.abs().max().clamp_min(1e-12)).item()
         elif kind in ("ddp", "ddp_xgmi"):
             from dmlab.parallel import DDP
 

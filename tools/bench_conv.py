@@ -18,6 +18,9 @@ from dmlab.ops._native import lib  # noqa: E402
 # (name, H_in, Cin, Cout, k, stride, pad)
 SHAPES = [
     ("stem7x7", 224, 8, 64, 7, 2, 3),
+    # the stem as run: 4x4/s1 conv over the space-to-depth input (16 ch, 112x112, output
+    # 112x112: pad 2 top/left, the 113th row/column is never computed)
+    ("stem_s2d", 112, 16, 64, 4, 1, 2),
     ("l1_3x3", 56, 64, 64, 3, 1, 1),
     ("l2_3x3s2", 56, 64, 128, 3, 2, 1),
     ("l2_3x3", 28, 128, 128, 3, 1, 1),
@@ -64,7 +67,7 @@ def main():
     if a.shapes:
         shapes = [sh for sh in shapes if sh[0] in a.shapes.split(",")]
     for name, H, C, Co, k, s, p in shapes:
-        OH = (H + 2 * p - k) // s + 1
+        OH = H if name == "stem_s2d" else (H + 2 * p - k) // s + 1
         flops = 2.0 * N * OH * OH * Co * k * k * C
         x = torch.randn(N, H, H, C, device=dev).bfloat16()
         wf = (torch.randn(Co, k, k, C, device=dev) * 0.05).bfloat16()
@@ -87,7 +90,7 @@ def main():
                     ref = y.clone()
                 else:
                     row[f"fwd_c{cfg}_maxdiff"] = float((y.float() - ref.float()).abs().max())
-        if "dgrad" in a.passes and name != "stem7x7":
+        if "dgrad" in a.passes and not name.startswith("stem"):
             ref = None
             for cfg in cfgs:
                 if cfg in (0, 3, 6, 9, 12, 15, 18, 19, 20, 22, 24, 26, 34, 36, 38) and C % 128:
