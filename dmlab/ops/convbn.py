@@ -54,13 +54,17 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
         # 64 output channels: the 256-pixel halo tile (2 x 2 waves of 128 x 32) amortises
         # the single-chunk halo prologue over twice the rows
-        # 42 / 43: the 20 / 38 tiles with two weight tiles of register prefetch
-        # (tools/bench_conv.py: +3-4 % on layer3/4, -3 % fwd on layer2)
-        if ncols >= 512:
-            return 43  # 256-pixel tile, 8 waves: half the weight staging per FLOP
+        # 42: the 128-pixel BN-128 tile with two weight tiles of register prefetch;
+        # 41: 256-pixel tile of 4 x 1 waves, each 64 x 64 (one LDS fragment read per MFMA
+        # pair instead of 1.5; BN 64 doubles the column blocks).  tools/bench_conv.py
+        # (profiles/conv_halo_tiles_b512_r1s4.jsonl, batch 512 / 256, TFLOP/s fwd/dgrad):
+        #   layer2 (128 ch): 42 807/834, 20 761/818, 41 781/817   (b256: 42 647/681)
+        #   layer3 (256 ch): 41 852/867, 42 834/840                (b256: 41 722/762)
+        #   layer4 (512 ch): 41 856/867, 43 812/820                (b256: 41 822/848)
+        #   layer1 (64 ch) : 39 612/683, 41 580/642
         if ncols >= 256:
-            return 42
-        return 20 if ncols >= 128 else 39
+            return 41
+        return 42 if ncols >= 128 else 39
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
         t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
     elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
