@@ -26,8 +26,10 @@ SHAPES = [
     ("l2_3x3", 28, 128, 128, 3, 1, 1),
     ("l2_down", 56, 64, 128, 1, 2, 0),
     ("l3_3x3s2", 28, 128, 256, 3, 2, 1),
+    ("l3_down", 28, 128, 256, 1, 2, 0),
     ("l3_3x3", 14, 256, 256, 3, 1, 1),
     ("l4_3x3s2", 14, 256, 512, 3, 2, 1),
+    ("l4_down", 14, 256, 512, 1, 2, 0),
     ("l4_3x3", 7, 512, 512, 3, 1, 1),
 ]
 # plain GEMMs through the same kernels (1x1 conv, K = C): structure ceiling without im2col
@@ -57,6 +59,8 @@ def main():
     ap.add_argument("--wcfgs", default="v1,v2")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default: ResNet-18)")
+    ap.add_argument("--smul", default="1", help="comma list of multipliers of the planned "
+                    "wgrad m-split S (halo variants h9/h3)")
     a = ap.parse_args()
     L = lib()
     dev = torch.device("cuda")
@@ -108,7 +112,9 @@ def main():
             K = k * k * C
             dw = torch.empty(Co, C, k, k, device=dev)
             ref = None
-            for v in a.wcfgs.split(","):
+            variants = [(v, m) for v in a.wcfgs.split(",") for m in
+                        ([float(x) for x in a.smul.split(",")] if v in ("h9", "h3") else [1.0])]
+            for v, mul in variants:
                 force = {"v1": None, "v2": None, "h9": 4, "h3": 5}[v]
                 if force is None:
                     c, S = _wgrad_plan(M, Co, K)
@@ -116,14 +122,16 @@ def main():
                         c = (c - 2) % 2
                 else:
                     c, S = _wgrad_plan(M, Co, K, k, s, C, force=force)
+                    S = max(1, int(S * mul))
+                tag = v if mul == 1.0 else f"{v}x{mul:g}"
                 slab = torch.empty(S * Co * K, device=dev)
                 t = timeit(lambda: L.conv_wgrad(x, dy, dw, slab, C, k, k, s, p, 0.0, S, c, False), a.iters)
-                row[f"wgrad_{v}_TF"] = round(flops / t / 1e12, 1)
-                row[f"wgrad_{v}_S"] = S
+                row[f"wgrad_{tag}_TF"] = round(flops / t / 1e12, 1)
+                row[f"wgrad_{tag}_S"] = S
                 if ref is None:
                     ref = dw.clone()
                 else:
-                    row[f"wgrad_{v}_reldiff"] = float((dw - ref).norm() / ref.norm())
+                    row[f"wgrad_{tag}_reldiff"] = float((dw - ref).norm() / ref.norm())
         out.append(row)
         print(json.dumps(row), flush=True)
 
