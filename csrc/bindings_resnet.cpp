@@ -396,7 +396,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   const long long M = y.numel() / C;
   need_f32(work, "work", bn_bwd_work(M, C));
   if (pre_slab.has_value()) {
-    TORCH_CHECK(mode <= 2 && pre_rows >= 1, "pre_slab: modes 0-2, >= 1 row");
+    TORCH_CHECK(pre_rows >= 1, "pre_slab: >= 1 row");
     need_f32(*pre_slab, "pre_slab", pre_rows * 2 * C);
   }
   const bf* doutp = nullptr;
@@ -445,7 +445,8 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
 }
 
 void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,
-                     at::Tensor idx, int64_t K, int64_t S, int64_t P) {
+                     at::Tensor idx, int64_t K, int64_t S, int64_t P,
+                     c10::optional<at::Tensor> yarg) {
   need_bf16_nhwc(y, "y");
   need_bf16_nhwc(out, "out");
   const int C = y.size(3);
@@ -454,8 +455,36 @@ void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tenso
   TORCH_CHECK(idx.scalar_type() == at::kByte && idx.numel() == out.numel());
   TORCH_CHECK(out.size(1) == (y.size(1) + 2 * P - K) / S + 1 && out.size(2) == (y.size(2) + 2 * P - K) / S + 1);
   const DeviceGuard guard(y.device());
+  bf* yargp = nullptr;
+  if (yarg.has_value()) {
+    need_bf16_nhwc(*yarg, "yarg");
+    TORCH_CHECK(yarg->sizes() == out.sizes(), "yarg: pooled shape");
+    yargp = bp(*yarg);
+  }
   dm::bn_relu_maxpool(bp(y), fp(scale), fp(shift), bp(out), (uint8_t*)idx.data_ptr(), y.size(0),
-                      y.size(1), y.size(2), C, out.size(1), out.size(2), K, S, P, cur_stream());
+                      y.size(1), y.size(2), C, out.size(1), out.size(2), K, S, P, cur_stream(),
+                      yargp);
+}
+
+int64_t bn_bwd_rows(int64_t M, int64_t C) { return dm::bn_bwd_groups(M, C); }
+
+// Σdz, Σdz·x̂ partials of (dout masked by y*scale+shift > 0) -> part [rows][2C]; returns rows
+int64_t bn_bwd_reduce_masked(at::Tensor dout, at::Tensor y, at::Tensor mean, at::Tensor invstd,
+                             at::Tensor scale, at::Tensor shift, at::Tensor part) {
+  need_bf16_nhwc(dout, "dout");
+  need_bf16_nhwc(y, "y");
+  TORCH_CHECK(dout.sizes() == y.sizes());
+  const int C = y.size(3);
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "C/8 must divide 256");
+  need_f32(mean, "mean", C);
+  need_f32(invstd, "invstd", C);
+  need_f32(scale, "scale", C);
+  need_f32(shift, "shift", C);
+  const long long M = y.numel() / C;
+  need_f32(part, "part", (int64_t)dm::bn_bwd_groups(M, C) * 2 * C);
+  const DeviceGuard guard(y.device());
+  return dm::bn_bwd_reduce_masked(bp(dout), bp(y), fp(mean), fp(invstd), fp(scale), fp(shift), M,
+                                  C, fp(part), cur_stream());
 }
 
 // ------------------------------------------------------------------ pooling / packing
@@ -532,7 +561,11 @@ void register_resnet(pybind11::module_& m) {
   m.def("bn_bwd_work", &bn_bwd_work);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
         py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0);
-  m.def("bn_relu_maxpool", &bn_relu_maxpool);
+  m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("y"), py::arg("scale"), py::arg("shift"),
+        py::arg("out"), py::arg("idx"), py::arg("K"), py::arg("S"), py::arg("P"),
+        py::arg("yarg") = py::none());
+  m.def("bn_bwd_rows", &bn_bwd_rows);
+  m.def("bn_bwd_reduce_masked", &bn_bwd_reduce_masked);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("avgpool_fwd", &avgpool_fwd);

@@ -567,10 +567,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_quad_kernel(BnBwdArgs a, con
 
 // Fused stem tail: pooled = maxpool_KxK/S(relu(y*scale + shift)) with argmax codes; the
 // BN output itself is never written.
+// yarg (optional): the raw conv output y at each window's argmax.  The stem's BN-backward
+// sums Σdz, Σdz·x̂ then reduce over the POOLED grid (pooled grad masked by relu at the
+// argmax, x̂ from yarg) instead of gathering over the full-resolution y: 2 pooled-size
+// tensors instead of y + pooled grad + codes (~2.7x fewer bytes); same terms, regrouped.
 __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
     const bf16_t* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
-    bf16_t* __restrict__ out, uint8_t* __restrict__ idx, int N, int H, int W, int C, int OH,
-    int OW, int K, int S, int P) {
+    bf16_t* __restrict__ out, uint8_t* __restrict__ idx, bf16_t* __restrict__ yarg, int N, int H,
+    int W, int C, int OH, int OW, int K, int S, int P) {
   extern __shared__ float ss[];  // [2][C]
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     ss[c] = scale[c];
@@ -589,10 +593,10 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
     const int oh = (int)(t % (unsigned)OH);
     const int n = (int)(t / (unsigned)OH);
     const int c0 = c8 * 8;
-    float best[8];
+    float best[8], raw[8];
     int arg[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; }
+    for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; raw[j] = 0.f; }
     for (int kh = 0; kh < K; ++kh) {
       const int ih = oh * S - P + kh;
       if (ih < 0 || ih >= H) continue;
@@ -604,11 +608,12 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float v = fmaxf(f[j] * ss[c0 + j] + ss[C + c0 + j], 0.f);
-          if (v > best[j]) { best[j] = v; arg[j] = kh * K + kw; }
+          if (v > best[j]) { best[j] = v; arg[j] = kh * K + kw; raw[j] = f[j]; }
         }
       }
     }
     reinterpret_cast<uint4*>(out)[i] = pack8(best);
+    if (yarg) reinterpret_cast<uint4*>(yarg)[i] = pack8(raw);  // raw is bf16-exact
     uint2 a2;
     a2.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
     a2.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
@@ -977,10 +982,24 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
 
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
-                     int P, hipStream_t st) {
+                     int P, hipStream_t st, bf16_t* yarg) {
   const long long total = (long long)N * OH * OW * (C / 8);
   bn_relu_maxpool_kernel<<<grid_for(total, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
-      y, scale, shift, out, idx, N, H, W, C, OH, OW, K, S, P);
+      y, scale, shift, out, idx, yarg, N, H, W, C, OH, OW, K, S, P);
+}
+
+// Σdz, Σdz·x̂ partial rows [G][2C] of a mode-2 operand pair (dz = dout masked by
+// y*scale + shift > 0) over M rows; returns G (= bn_bwd_groups(M, C)).  Used for the stem's
+// pooled-domain sums (dout = pooled grad, y = yarg), handed to bn_backward as pre_part.
+int bn_bwd_reduce_masked(const bf16_t* dout, const bf16_t* y, const float* mean,
+                         const float* invstd, const float* scale, const float* shift, long long M,
+                         int C, float* part, hipStream_t st) {
+  BnBwdArgs a{dout, nullptr, y, mean, invstd, scale, shift, nullptr, nullptr, 0, 0, 0, 0, 0, 0, 0,
+              M, C};
+  const int G = bn_bwd_groups(M, C);
+  const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
+  bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part);
+  return G;
 }
 
 void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,

@@ -104,7 +104,11 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  hipStream_t st, const float* pre_part = nullptr, int pre_rows = 0);
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
-                     int P, hipStream_t st);
+                     int P, hipStream_t st, bf16_t* yarg = nullptr);
+int bn_bwd_groups(long long M, int C);
+int bn_bwd_reduce_masked(const bf16_t* dout, const bf16_t* y, const float* mean,
+                         const float* invstd, const float* scale, const float* shift, long long M,
+                         int C, float* part, hipStream_t st);
 void maxpool_fwd(const bf16_t* x, bf16_t* y, uint8_t* idx, int N, int H, int W, int C, int OH,
                  int OW, int K, int S, int P, hipStream_t st);
 void maxpool_bwd(const bf16_t* dy, const uint8_t* idx, bf16_t* dx, int N, int H, int W, int C,

@@ -269,9 +269,13 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
         PH, PW = (OH + 2 * pp - pk) // ps + 1, (OW + 2 * pp - pk) // ps + 1
         out = empty_nhwc(N, PH, PW, cout, x)
         idx = torch.empty((N, PH, PW, cout), device=x.device, dtype=torch.uint8)
-        L.bn_relu_maxpool(y, scale, shift, out, idx, pk, ps, pp)
+        # training: also keep y at each window's argmax, so the backward reduces the BN
+        # sums over the pooled grid (see bn_relu_maxpool_kernel)
+        yarg = empty_nhwc(N, PH, PW, cout, x) if (train and use_batch) else None
+        L.bn_relu_maxpool(y, scale, shift, out, idx, pk, ps, pp, yarg=yarg)
         if train:
             ctx["idx"] = idx
+            ctx["yarg"] = yarg
         return out
     out = empty_nhwc(N, OH, OW, cout, x)
     L.bn_apply(y, residual, scale, shift, out, layer.relu)
@@ -329,6 +333,15 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     if zs is not None and zs[2].data_ptr() == dout.data_ptr() and zs[2].shape == dout.shape:
         pre_sums = dict(pre_slab=zs[0], pre_rows=zs[1])  # sums from the producer's epilogue
     pool = getattr(layer, "pool_k", 0)
+    if pool and ctx.get("yarg") is not None and not pre_sums:
+        # stem: Σdz, Σdz·x̂ over the pooled grid (pooled grad masked at the argmax, x̂ from
+        # y at the argmax) -- reads 2 pooled-size tensors instead of y + grad + codes
+        Mp = ctx["yarg"].numel() // cout
+        part = torch.empty(L.bn_bwd_rows(Mp, cout) * 2 * cout, device=y.device,
+                           dtype=torch.float32)
+        rows = L.bn_bwd_reduce_masked(dout, ctx["yarg"], ctx["mean"], ctx["invstd"], ctx["scale"],
+                                      ctx["shift"], part)
+        pre_sums = dict(pre_slab=part, pre_rows=rows)
     if pool:
         mode = 3       # dz gathered from the max-pool gradient, ReLU mask from y
     elif not layer.relu:

@@ -319,6 +319,21 @@ def test_fused_bn_relu_maxpool_and_gather_backward(dev, H, C):
     assert _rel(_nchw(dy), yr.grad) < 1e-2
     assert _rel(dg, g_.grad) < 1e-2
     assert _rel(db, b_.grad) < 1e-2
+    # pooled-domain sums: y at the argmax (yarg) + the pooled grad give the same Σdz, Σdz·x̂
+    yarg = torch.empty_like(out)
+    out2 = torch.empty_like(out)
+    lib().bn_relu_maxpool(y, scale, shift, out2, idx, 3, 2, 1, yarg=yarg)
+    assert torch.equal(out2, out)
+    part = torch.empty(lib().bn_bwd_rows(N * OH * OH, C) * 2 * C, **f)
+    rows = lib().bn_bwd_reduce_masked(_nhwc(dp), yarg, mean, invstd, scale, shift, part)
+    dy2 = torch.empty_like(y)
+    dg2, db2 = torch.zeros(C, **f), torch.zeros(C, **f)
+    lib().bn_backward(None, None, y, mean, invstd, gamma, dg2, db2, 0.0, 3, scale, shift,
+                      _nhwc(dp), idx, 3, 2, 1, dy2, None, work, pre_slab=part, pre_rows=rows)
+    assert _rel(dg2, g_.grad) < 1e-2
+    assert _rel(db2, b_.grad) < 1e-2
+    assert _rel(_nchw(dy2), yr.grad) < 1e-2
+    torch.testing.assert_close(db2, db, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("T", [1, 100, 129, 6272])
