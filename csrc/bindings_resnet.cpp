@@ -363,7 +363,7 @@ void bn_eval_coeffs(at::Tensor gamma, at::Tensor beta, at::Tensor rmean, at::Ten
 }
 
 void bn_apply(at::Tensor y, c10::optional<at::Tensor> res, at::Tensor scale, at::Tensor shift,
-              at::Tensor out, bool relu) {
+              at::Tensor out, bool relu, c10::optional<at::Tensor> mask) {
   need_bf16_nhwc(y, "y");
   need_bf16_nhwc(out, "out");
   const int C = y.size(3);
@@ -373,24 +373,33 @@ void bn_apply(at::Tensor y, c10::optional<at::Tensor> res, at::Tensor scale, at:
   if (res.has_value()) { need_bf16_nhwc(*res, "res"); TORCH_CHECK(res->sizes() == y.sizes()); rp = bp(*res); }
   TORCH_CHECK(out.sizes() == y.sizes());
   const DeviceGuard guard(y.device());
-  dm::bn_apply(bp(y), rp, fp(scale), fp(shift), bp(out), y.numel(), C, relu, cur_stream());
+  uint8_t* mp = nullptr;
+  if (mask.has_value()) {
+    TORCH_CHECK(relu, "mask: ReLU outputs only");
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                mask->numel() == y.numel() / 8, "mask: contiguous uint8, one byte per 8 channels");
+    mp = (uint8_t*)mask->data_ptr();
+  }
+  dm::bn_apply(bp(y), rp, fp(scale), fp(shift), bp(out), y.numel(), C, relu, cur_stream(), mp);
 }
 
 int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M, C) * 2 * C + 3 * C + 256 * 2 * C; }
 
 // mode: 0 no ReLU, 1 mask from `out`, 2 mask from y*scale+shift, 3 (stem) dz gathered
-// from the following max-pool's gradient (pdy, pidx; pool K/S/P) with mask from y.
+// from the following max-pool's gradient (pdy, pidx; pool K/S/P) with mask from y, 4 mask
+// from the 1-bit (out > 0) mask that bn_apply wrote in the forward.
 void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, at::Tensor y,
                  at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
                  at::Tensor dbeta, double gbeta, int64_t mode, c10::optional<at::Tensor> scale,
                  c10::optional<at::Tensor> shift, c10::optional<at::Tensor> pdy,
                  c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P, at::Tensor dy,
                  c10::optional<at::Tensor> dres, at::Tensor work,
-                 c10::optional<at::Tensor> pre_slab, int64_t pre_rows) {
+                 c10::optional<at::Tensor> pre_slab, int64_t pre_rows,
+                 c10::optional<at::Tensor> mask) {
   need_bf16_nhwc(y, "y");
   need_bf16_nhwc(dy, "dy");
   TORCH_CHECK(dy.sizes() == y.sizes());
-  TORCH_CHECK(mode >= 0 && mode <= 3);
+  TORCH_CHECK(mode >= 0 && mode <= 4);
   const int C = y.size(3);
   TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "bn_backward: C/8 must divide 256");
   const long long M = y.numel() / C;
@@ -400,7 +409,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
     need_f32(*pre_slab, "pre_slab", pre_rows * 2 * C);
   }
   const bf* doutp = nullptr;
-  if (mode < 3) {
+  if (mode != 3) {
     TORCH_CHECK(dout.has_value());
     need_bf16_nhwc(*dout, "dout");
     TORCH_CHECK(dout->sizes() == y.sizes());
@@ -414,7 +423,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
     outp = bp(*out);
   }
   const float *scp = nullptr, *shp = nullptr;
-  if (mode >= 2) {
+  if (mode == 2 || mode == 3) {
     TORCH_CHECK(scale.has_value() && shift.has_value());
     need_f32(*scale, "scale", C);
     need_f32(*shift, "shift", C);
@@ -435,13 +444,19 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
     pdyp = bp(*pdy);
     pidxp = (const uint8_t*)pidx->data_ptr();
   }
+  const uint8_t* mp = nullptr;
+  if (mode == 4) {
+    TORCH_CHECK(mask.has_value() && mask->is_cuda() && mask->scalar_type() == at::kByte &&
+                mask->is_contiguous() && mask->numel() == y.numel() / 8, "mode 4 needs the uint8 mask");
+    mp = (const uint8_t*)mask->data_ptr();
+  }
   bf* drp = nullptr;
   if (dres.has_value()) { need_bf16_nhwc(*dres, "dres"); drp = bp(*dres); }
   const DeviceGuard guard(y.device());
   dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
                   (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
                   OW, K, S, P, bp(dy), drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
-                  (int)pre_rows);
+                  (int)pre_rows, mp);
 }
 
 void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,
@@ -557,10 +572,11 @@ void register_resnet(pybind11::module_& m) {
         py::arg("eps"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),
         py::arg("work"), py::arg("num_batches") = py::none());
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
-  m.def("bn_apply", &bn_apply);
+  m.def("bn_apply", &bn_apply, py::arg("y"), py::arg("res"), py::arg("scale"), py::arg("shift"),
+        py::arg("out"), py::arg("relu"), py::arg("mask") = py::none());
   m.def("bn_bwd_work", &bn_bwd_work);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
-        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0);
+        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none());
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("out"), py::arg("idx"), py::arg("K"), py::arg("S"), py::arg("P"),
         py::arg("yarg") = py::none());

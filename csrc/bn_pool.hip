@@ -124,13 +124,28 @@ __global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const flo
 }
 
 // out = [relu](y*scale + shift [+ res])
+// mask (optional, RELU only): one bit per element, (out > 0) of the stored bf16 value, one
+// byte per 8-channel chunk -- the BN backward's ReLU mask source for residual layers
+// (mode 4) at 1/16 of the bytes of re-reading `out`.
+__device__ __forceinline__ uint32_t pos_bits8(const uint4& v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t lo = w[q] & 0xffff, hi = w[q] >> 16;
+    b |= (uint32_t)(!(lo & 0x8000) && (lo & 0x7fff)) << (2 * q);
+    b |= (uint32_t)(!(hi & 0x8000) && (hi & 0x7fff)) << (2 * q + 1);
+  }
+  return b;
+}
+
 template <bool RES, bool RELU>
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ y,
                                                        const bf16_t* __restrict__ res,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift,
                                                        bf16_t* __restrict__ out, long long n8,
-                                                       int C) {
+                                                       int C, uint8_t* __restrict__ mask) {
   extern __shared__ float sc_sh[];  // [2][C]
   for (int i = threadIdx.x; i < C; i += blockDim.x) {
     sc_sh[i] = scale[i];
@@ -163,7 +178,9 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
         if (RELU) v = fmaxf(v, 0.f);
         f[j] = v;
       }
-      reinterpret_cast<uint4*>(out)[i] = pack8(f);
+      const uint4 o = pack8(f);
+      reinterpret_cast<uint4*>(out)[i] = o;
+      if (RELU && mask) mask[i] = (uint8_t)pos_bits8(o);
     }
   }
 }
@@ -175,6 +192,7 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
 //   2  dout tensor, mask recomputed from y (y*scale + shift > 0)   -- no `out` read
 //   3  gathered from a following 3x3/s2 max-pool's grads + argmax codes, mask from y
 //      (stem: neither `out` nor the unpooled gradient is ever materialised)
+//   4  dout tensor, mask from the forward's 1-bit (out > 0) mask    -- residual layers
 struct BnBwdArgs {
   const bf16_t* dout;
   const bf16_t* out;
@@ -188,6 +206,7 @@ struct BnBwdArgs {
   int H, W, OH, OW, K, S, P;
   long long M;
   int C;
+  const uint8_t* mask;  // mode 4: bit j of byte i = (out > 0) of chunk i, channel j
 };
 
 // mode 3: dz of one 8-channel chunk of input pixel r, gathered from the pool windows
@@ -250,6 +269,7 @@ __device__ __forceinline__ void gather_pool_dz(const BnBwdArgs& a, long long r, 
 template <int MODE, int U>
 struct BnBwdBatch {
   uint4 y[U], dout[U], out[U];
+  uint32_t mk[U];
   bool ok[U];
   __device__ __forceinline__ void load(const BnBwdArgs& a, long long i0, long long stride,
                                        long long n8) {
@@ -261,6 +281,7 @@ struct BnBwdBatch {
       y[u] = reinterpret_cast<const uint4*>(a.y)[ii];
       if (MODE != 3) dout[u] = reinterpret_cast<const uint4*>(a.dout)[ii];
       if (MODE == 1) out[u] = reinterpret_cast<const uint4*>(a.out)[ii];
+      if (MODE == 4) mk[u] = a.mask[ii];
     }
   }
   // dz (upstream grad with the ReLU mask) and y of chunk u
@@ -275,6 +296,9 @@ struct BnBwdBatch {
       unpack8(out[u], o);
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[j] = o[j] > 0.f ? d[j] : 0.f;
+    } else if (MODE == 4) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = (mk[u] >> j) & 1u ? d[j] : 0.f;
     } else if (MODE >= 2) {
       const int c0 = chunk * 8;
 #pragma unroll
@@ -291,7 +315,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
   const int C = a.C, C8 = C >> 3;
   float* sc = red + 256 * 16;
   float* sh = sc + C;
-  if (MODE >= 2)
+  if (MODE == 2 || MODE == 3)
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       sc[c] = a.scale[c];
       sh[c] = a.shift[c];
@@ -375,7 +399,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
   for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
   float* sc = cf + 3 * C;
   float* sh = sc + C;
-  if (MODE >= 2)
+  if (MODE == 2 || MODE == 3)
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       sc[c] = a.scale[c];
       sh[c] = a.shift[c];
@@ -901,16 +925,16 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, c
 }
 
 void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
-              bf16_t* out, long long n, int C, bool relu, hipStream_t st) {
+              bf16_t* out, long long n, int C, bool relu, hipStream_t st, uint8_t* mask) {
   const long long n8 = n / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 2 * C;
   if (res) {
-    if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
-    else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
+    if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
+    else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
   } else {
-    if (relu) bn_apply_kernel<false, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
-    else bn_apply_kernel<false, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C);
+    if (relu) bn_apply_kernel<false, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
+    else bn_apply_kernel<false, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
   }
 }
 
@@ -930,11 +954,12 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  float gbeta, long long M, int C, int mode, const float* scale,
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
-                 hipStream_t st, const float* pre_part, int pre_rows) {
+                 hipStream_t st, const float* pre_part, int pre_rows, const uint8_t* mask) {
   // pre_part (optional): [pre_rows][2C] partial Σdz, Σdz·x̂ already reduced by the producing
   // dgrad's epilogue (BnBwdEpi) — the reduction pass over dout and y is skipped
   // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
-  BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C};
+  BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C,
+              mask};
   // stem 3x3/s2/p1 pool with even H, W: quad gather (4 pixels share their 4 windows)
   const bool quad = mode == 3 && K == 3 && S == 2 && P == 1 && H % 2 == 0 && W % 2 == 0 &&
                     OH == H / 2 && OW == W / 2 && !dres && (long long)M * C / 8 < (1LL << 31);
@@ -949,6 +974,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
     case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
     case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
+    case 4: bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part); break;
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
   const int G2 = colsum_groups(G);
@@ -975,7 +1001,9 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     case 4: DM_BNB(2, false); break;
     case 5: DM_BNB(2, true); break;
     case 6: DM_BNB(3, false); break;
-    default: DM_BNB(3, true); break;
+    case 7: DM_BNB(3, true); break;
+    case 8: DM_BNB(4, false); break;
+    default: DM_BNB(4, true); break;
   }
 #undef DM_BNB
 }
@@ -995,7 +1023,7 @@ int bn_bwd_reduce_masked(const bf16_t* dout, const bf16_t* y, const float* mean,
                          const float* invstd, const float* scale, const float* shift, long long M,
                          int C, float* part, hipStream_t st) {
   BnBwdArgs a{dout, nullptr, y, mean, invstd, scale, shift, nullptr, nullptr, 0, 0, 0, 0, 0, 0, 0,
-              M, C};
+              M, C, nullptr};
   const int G = bn_bwd_groups(M, C);
   const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
   bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part);

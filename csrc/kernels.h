@@ -94,14 +94,15 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                     float eps, int C, float* scale, float* shift, hipStream_t st);
 void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
-              bf16_t* out, long long n, int C, bool relu, hipStream_t st);
+              bf16_t* out, long long n, int C, bool relu, hipStream_t st, uint8_t* mask = nullptr);
 int bn_bwd_groups(long long M, int C);
 void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const float* mean,
                  const float* invstd, const float* gamma, float* dgamma, float* dbeta,
                  float gbeta, long long M, int C, int mode, const float* scale,
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
-                 hipStream_t st, const float* pre_part = nullptr, int pre_rows = 0);
+                 hipStream_t st, const float* pre_part = nullptr, int pre_rows = 0,
+                 const uint8_t* mask = nullptr);
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
                      int P, hipStream_t st, bf16_t* yarg = nullptr);

@@ -278,9 +278,14 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
             ctx["yarg"] = yarg
         return out
     out = empty_nhwc(N, OH, OW, cout, x)
-    L.bn_apply(y, residual, scale, shift, out, layer.relu)
+    # residual + ReLU in training: a 1-bit (out > 0) mask is the backward's ReLU mask source
+    # (the residual is not kept; re-reading `out` would cost 16x the bytes)
+    mask = (torch.empty(out.numel() // 8, device=x.device, dtype=torch.uint8)
+            if (train and residual is not None and layer.relu) else None)
+    L.bn_apply(y, residual, scale, shift, out, layer.relu, mask=mask)
     if train and residual is not None:
-        ctx["out"] = out  # ReLU mask source (the residual is not kept)
+        ctx["out"] = out
+        ctx["mask"] = mask
     return out
 
 
@@ -347,7 +352,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     elif not layer.relu:
         mode = 0
     elif ctx["has_res"]:
-        mode = 1       # mask needs the residual: read the saved output
+        # mask needs the residual: the forward's 1-bit mask (4), or the saved output (1)
+        mode = 4 if ctx.get("mask") is not None else 1
     else:
         mode = 2       # mask recomputed from y (no `out` read)
     L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
@@ -355,7 +361,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
-                  getattr(layer, "pool_p", 1), dy, dres, work, **pre_sums)
+                  getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"), **pre_sums)
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does

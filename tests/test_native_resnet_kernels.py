@@ -203,17 +203,32 @@ def test_bn_forward_backward(dev, C, M, relu, res):
     y4, out = y.view(1, 1, M, C), torch.empty(1, 1, M, C, device=dev, dtype=torch.bfloat16)
     lib().bn_apply(y4, r.view(1, 1, M, C) if res else None, scale, shift, out, relu)
     assert _rel(out.view(M, C), out_ref.detach()) < 5e-3
-    modes = [0] if not relu else ([1] if res else [1, 2])  # 2: ReLU mask from y
+    mask = None
+    if relu:
+        # 1-bit ReLU mask (bit j of byte i = out[chunk i, channel j] > 0), same out
+        mask = torch.empty(M * C // 8, device=dev, dtype=torch.uint8)
+        out2 = torch.empty_like(out)
+        lib().bn_apply(y4, r.view(1, 1, M, C) if res else None, scale, shift, out2, relu, mask=mask)
+        assert torch.equal(out2, out)
+        bits = (mask[:, None].int() >> torch.arange(8, device=dev)) & 1
+        assert torch.equal(bits.view(M, C).bool(), out.view(M, C).float() > 0)
+    modes = [0] if not relu else ([1, 4] if res else [1, 2, 4])  # 2: mask from y; 4: bits
+    got = {}
     for mode in modes:
         dy = torch.empty_like(out)
         dres = torch.empty_like(out) if res else None
         dg, db = torch.zeros(C, **f), torch.zeros(C, **f)
         work = torch.empty(lib().bn_bwd_work(M, C), **f)
         lib().bn_backward(dout.view(1, 1, M, C), out, y4, mean, invstd, gamma, dg, db, 0.0, mode,
-                          scale, shift, None, None, 3, 2, 1, dy, dres, work)
+                          scale, shift, None, None, 3, 2, 1, dy, dres, work, mask=mask)
         assert _rel(dy.view(M, C), yr.grad) < 1e-2, mode
         assert _rel(dg, g_.grad) < 1e-2, mode
         assert _rel(db, b_.grad) < 1e-2, mode
+        got[mode] = (dy, dg, db, dres)
+    if 4 in got:  # the bit mask selects exactly the elements `out > 0` selects
+        for a_, b_t in zip(got[4], got[1]):
+            if a_ is not None:
+                assert torch.equal(a_, b_t)
 
 
 def test_maxpool_avgpool(dev):
