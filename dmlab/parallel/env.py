@@ -93,7 +93,9 @@ def init(world_size: int | None = None, rank: int | None = None, master_addr: st
         # CPU ranks share the host: split the cores instead of oversubscribing
         lws = int(os.environ.get("LOCAL_WORLD_SIZE", ws))
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(lws, 1)))
-    backend = backend or default_backend(_DEVICE)
+    # DMLAB_BACKEND overrides the choice (e.g. gloo for GPU ranks that share one device in
+    # tests: RCCL refuses two ranks on the same GPU)
+    backend = backend or os.environ.get("DMLAB_BACKEND") or default_backend(_DEVICE)
     if ws > 1 or backend is not None:
         if not is_initialized():
             kw = dict(backend=backend, rank=rk, world_size=ws,

@@ -157,3 +157,32 @@ def test_rpc_stages_on_gpu(tmp_path):
     ls = [float(x) for x in re.findall(r"loss: (\d+\.\d+)", r.stdout)]
     assert len(ls) == 5 and ls[-1] < ls[0]
     assert "Test set: Accuracy" in r.stdout
+
+
+def test_bench_two_ranks(tmp_path):
+    """bench.py's multi-rank path (env init, barrier-bracketed timing, MAX over ranks, one
+    JSON line from rank 0) with two ranks sharing the box's GPU over gloo."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DMLAB_BACKEND="gloo",
+                   OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen(
+            [sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+             "--res", "64", "--batch", "8"], cwd=tmp_path, env=env, stdout=subprocess.PIPE,
+            stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e[-3000:]
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and not [ln for ln in outs[1][0].splitlines() if ln.startswith("{")]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 3 and res["value"] > 0
+    assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 16
