@@ -52,6 +52,9 @@ def parse():
                          "events (fwd, bwd compute, exposed comm, optimizer) -> 'phases_ms'")
     ap.add_argument("--small-allreduce", default="rccl", choices=["rccl", "xgmi"],
                     help="buckets <= 4 MB via the one-shot xGMI peer-memory kernel")
+    ap.add_argument("--xgmi-cap-mb", type=float, default=4.0,
+                    help="largest bucket sent through the xGMI kernel with --small-allreduce "
+                         "xgmi; above the bucket size every bucket goes there (two-shot)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
     ap.add_argument("--graph", type=int, default=-1,
@@ -101,7 +104,8 @@ def main():
     opt = SGD(model.parameters(), lr=lr, momentum=0.9)
     net = DDP(model, bucket_cap_mb=a.bucket_mb,
               comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None,
-              small_allreduce="xgmi" if a.small_allreduce == "xgmi" else None)
+              small_allreduce="xgmi" if a.small_allreduce == "xgmi" else None,
+              small_cap_mb=a.xgmi_cap_mb)
     net.fold_average_into(opt)
 
     def train_step(x, y):

@@ -208,7 +208,7 @@ int64_t xgmi_open_handle(py::bytes handle) {
 void xgmi_close_handle(int64_t ptr) { dm::xgmi_close_handle((void*)(uintptr_t)ptr); }
 void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int64_t> data,
                     std::vector<int64_t> flags, int64_t rank, double scale, int64_t epoch,
-                    at::Tensor err) {
+                    at::Tensor err, int64_t algo) {
   CHECK_F32(in);
   CHECK_F32(out);
   TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel());
@@ -224,7 +224,7 @@ void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int6
   const DeviceGuard guard(in.device());
   dm::xgmi_allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cap, d.data(),
                      f.data(), (int)rank, W, (unsigned)epoch, (float)scale, err.data_ptr<int>(),
-                     cur_stream());
+                     (int)algo, cur_stream());
 }
 
 void colsum(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor out, double beta) {

@@ -15,6 +15,20 @@
 //   4. block b reads slice b of all W buffers (remote loads over xGMI), sums them in a fixed
 //      rank order (bitwise-identical results on every rank) and writes out = scale * sum.
 // Blocks synchronise only with their namesakes on the peers — no grid-wide barrier.
+//
+// Two-shot variant (large buckets, e.g. ResNet-18's 25 MB): the one-shot kernel reads W
+// full copies per rank, (W-1)·n remote bytes.  Two-shot splits the message into W rank
+// slices; block b of rank r
+//   1. copies chunk b of every slice into its shared buffer, flags phase A on every rank;
+//   2. after all W phase-A flags: reduces chunk b of ITS slice r from the W buffers (rank
+//      order), writes scale·sum to out and back into its own buffer (only rank r ever
+//      reads slice r of its own buffer during phase 2, so the in-place write is safe),
+//      flags phase B on every rank;
+//   3. after all W phase-B flags: gathers chunk b of every other slice q from rank q's
+//      buffer.
+// 2·(W-1)/W·n remote bytes per rank, spread over all W-1 xGMI links at once (a ring uses
+// one).  Parity halves: a peer can only rewrite the half read here two calls later, after
+// passing a phase-A wait on OUR next call, which starts after this kernel has drained.
 #include "common.h"
 
 #include <cstring>
@@ -22,12 +36,120 @@
 namespace dm {
 
 constexpr int XG_MAX_RANKS = 8;
-constexpr int XG_BLOCKS = 64;
+constexpr int XG_BLOCKS = 64;        // one-shot grid
+constexpr int XG2_BLOCKS = 256;      // two-shot grid (bandwidth-bound: more loads in flight)
+constexpr int XG_FLAG_BLOCKS = 256;  // flag slots per phase
 
 struct XgmiPtrs {
   float* data[XG_MAX_RANKS];        // each rank's shared buffer: [2][cap] floats (parity halves)
-  unsigned* flags[XG_MAX_RANKS];    // each rank's flag array: [XG_BLOCKS][XG_MAX_RANKS]
+  unsigned* flags[XG_MAX_RANKS];    // each rank's flags: [2 phases][XG_FLAG_BLOCKS][XG_MAX_RANKS]
 };
+
+// block b announces `epoch` in slot (phase, b, rank) of every rank (remote stores over xGMI)
+__device__ inline void xg_signal(const XgmiPtrs& p, int phase, int b, int rank, int W,
+                                 unsigned epoch) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x < W) {
+    unsigned* f = p.flags[threadIdx.x] + (phase * XG_FLAG_BLOCKS + b) * XG_MAX_RANKS + rank;
+    __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// wait until every rank's slot (phase, b, q) carries >= epoch; bounded spin -> false when a
+// peer never arrives (the caller reports through *err and exits instead of hanging the GPU)
+__device__ inline bool xg_wait(const XgmiPtrs& p, int phase, int b, int rank, int W,
+                               unsigned epoch) {
+  __shared__ int timed_out;
+  if (threadIdx.x == 0) timed_out = 0;
+  __syncthreads();
+  if (threadIdx.x < W) {
+    const unsigned* f = p.flags[rank] + (phase * XG_FLAG_BLOCKS + b) * XG_MAX_RANKS + threadIdx.x;
+    long long spins = 0;
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1LL << 22)) {
+        timed_out = 1;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const bool ok = !timed_out;
+  __syncthreads();
+  if (ok) __threadfence_system();
+  return ok;
+}
+
+template <int VEC>
+struct XgVec;
+template <>
+struct XgVec<1> {
+  using T = float;
+  static __device__ inline T add(T a, T b) { return a + b; }
+  static __device__ inline T mul(T a, float s) { return a * s; }
+};
+template <>
+struct XgVec<4> {
+  using T = float4;
+  static __device__ inline T add(T a, T b) {
+    return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  }
+  static __device__ inline T mul(T a, float s) {
+    return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
+  }
+};
+
+// n, cap in units of VEC floats
+template <int VEC>
+__global__ void __launch_bounds__(256) xgmi_allreduce2_kernel(const float* __restrict__ in_,
+                                                              float* __restrict__ out_, long long n,
+                                                              long long cap, XgmiPtrs p, int rank,
+                                                              int W, unsigned epoch, float scale,
+                                                              int* __restrict__ err) {
+  using V = typename XgVec<VEC>::T;
+  const V* in = reinterpret_cast<const V*>(in_);
+  V* out = reinterpret_cast<V*>(out_);
+  const int b = blockIdx.x, G = gridDim.x;
+  const long long S = (n + W - 1) / W, C = (S + G - 1) / G;
+  const long long half = (long long)(epoch & 1u) * cap;
+  auto buf = [&](int q) { return reinterpret_cast<V*>(p.data[q]) + half; };
+  auto range = [&](int q, long long& lo, long long& hi) {
+    lo = q * S + b * C;
+    long long e = (q + 1) * S < n ? (q + 1) * S : n;
+    hi = lo + C < e ? lo + C : e;
+  };
+  V* mine = buf(rank);
+  long long lo, hi;
+  for (int q = 0; q < W; ++q) {
+    range(q, lo, hi);
+    for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = in[i];
+  }
+  xg_signal(p, 0, b, rank, W, epoch);
+  if (!xg_wait(p, 0, b, rank, W, epoch)) {
+    if (threadIdx.x == 0) atomicExch(err, 1);
+    return;
+  }
+  range(rank, lo, hi);
+  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    V s = buf(0)[i];
+    for (int q = 1; q < W; ++q) s = XgVec<VEC>::add(s, buf(q)[i]);
+    s = XgVec<VEC>::mul(s, scale);
+    mine[i] = s;
+    out[i] = s;
+  }
+  xg_signal(p, 1, b, rank, W, epoch);
+  if (!xg_wait(p, 1, b, rank, W, epoch)) {
+    if (threadIdx.x == 0) atomicExch(err, 1);
+    return;
+  }
+  for (int q = 0; q < W; ++q) {
+    if (q == rank) continue;
+    const V* src = buf(q);
+    range(q, lo, hi);
+    for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = src[i];
+  }
+}
 
 __global__ void __launch_bounds__(256) xgmi_allreduce_kernel(const float* __restrict__ in,
                                                              float* __restrict__ out, long long n,
@@ -40,35 +162,13 @@ __global__ void __launch_bounds__(256) xgmi_allreduce_kernel(const float* __rest
   const long long half = (long long)(epoch & 1u) * cap;
   float* mine = p.data[rank] + half;
   for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) mine[i] = in[i];
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x < W) {
-    unsigned* f = p.flags[threadIdx.x] + b * XG_MAX_RANKS + rank;
-    __hip_atomic_store(f, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // wait for every rank's slice b of this epoch
-  __shared__ int timed_out;
-  if (threadIdx.x == 0) timed_out = 0;
-  __syncthreads();
-  if (threadIdx.x < W) {
-    const unsigned* f = p.flags[rank] + b * XG_MAX_RANKS + threadIdx.x;
-    long long spins = 0;
-    // >=: a fast peer may already have stored epoch+1 (it then waits for OUR epoch+1 flag,
-    // so it cannot reach epoch+2 and overwrite the parity half this call reads)
-    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1LL << 22)) {  // ~0.5-1 s: a peer is missing -> report, do not hang
-        timed_out = 1;
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  if (timed_out) {
+  xg_signal(p, 0, b, rank, W, epoch);
+  // >=: a fast peer may already have stored epoch+1 (it then waits for OUR epoch+1 flag,
+  // so it cannot reach epoch+2 and overwrite the parity half this call reads)
+  if (!xg_wait(p, 0, b, rank, W, epoch)) {
     if (threadIdx.x == 0) atomicExch(err, 1);
     return;
   }
-  __threadfence_system();
   for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     float s = 0.f;
     for (int q = 0; q < W; ++q) s += p.data[q][half + i];
@@ -105,13 +205,27 @@ void xgmi_close_handle(void* ptr) { DM_CHECK(hipIpcCloseMemHandle(ptr)); }
 
 void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
                     void* const* flags, int rank, int W, unsigned epoch, float scale, int* err,
-                    hipStream_t st) {
+                    int algo, hipStream_t st) {
   XgmiPtrs p{};
   for (int q = 0; q < W; ++q) {
     p.data[q] = (float*)data[q];
     p.flags[q] = (unsigned*)flags[q];
   }
-  xgmi_allreduce_kernel<<<XG_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, epoch, scale, err);
+  if (algo == 0) {
+    xgmi_allreduce_kernel<<<XG_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, epoch, scale,
+                                                     err);
+    return;
+  }
+  // two-shot: float4 when every rank's view is 16-B aligned (cap % 4 == 0 keeps the parity
+  // halves aligned; the caller checks n % 4 and the tensor addresses)
+  const bool v4 = n % 4 == 0 && cap % 4 == 0 && ((uintptr_t)in % 16) == 0 &&
+                  ((uintptr_t)out % 16) == 0;
+  if (v4)
+    xgmi_allreduce2_kernel<4><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n / 4, cap / 4, p, rank, W,
+                                                          epoch, scale, err);
+  else
+    xgmi_allreduce2_kernel<1><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, epoch,
+                                                          scale, err);
 }
 
 }  // namespace dm

@@ -25,6 +25,9 @@ task3/dist_utils.py:40-46).  Here:
 * ``small_allreduce="xgmi"``: buckets of at most ``small_cap_mb`` go through the
   one-shot xGMI peer-memory all-reduce (:mod:`dmlab.parallel.xgmi`, one kernel, no ring
   steps) instead of RCCL — the latency-bound case of the labs' LeNet (207 KB of grads).
+  Raising ``small_cap_mb`` past the bucket size routes the large buckets too; those take
+  the two-shot kernel (reduce-scatter + all-gather over all xGMI links at once) at >= 3
+  ranks, or always with ``xgmi_algo="two_shot"``.
 * The bucket state machine (per-bucket countdowns, collective launch, the end-of-
   backward wait / cast-back / average) runs in C++ (``dmlab._C.Reducer``,
   ``csrc/reducer.cpp``) against the c10d ProcessGroup directly; ``native=False`` keeps
@@ -59,7 +62,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 25.0,
                  first_bucket_mb: float = 4.0, comm_dtype=None, broadcast_init: bool = True,
                  process_group=None, average: bool = True, small_allreduce: str | None = None,
-                 small_cap_mb: float = 4.0, native: bool | None = None):
+                 small_cap_mb: float = 4.0, native: bool | None = None, xgmi_algo: str = "auto"):
         super().__init__()
         self.module = module
         self.ws = env.get_world_size()
@@ -89,7 +92,7 @@ class DistributedDataParallel(nn.Module):
             if self.grad_buf.dtype == torch.float32 and self.grad_buf.is_cuda and small:
                 from .xgmi import XGMIAllReduce
 
-                self._xgmi = XGMIAllReduce(cap=max(small), group=self.pg)
+                self._xgmi = XGMIAllReduce(cap=max(small), group=self.pg, algo=xgmi_algo)
         self._native = None
         if native is None:
             native = self.ws > 1 and _native_reducer_available()

@@ -1,4 +1,4 @@
-"""One-shot all-reduce over xGMI peer memory for small messages (``csrc/comm_xgmi.hip``).
+"""One-/two-shot all-reduce over xGMI peer memory (``csrc/comm_xgmi.hip``).
 
 SURVEY §2.7 / build plan step 4: RCCL's ring all-reduce takes 2(W-1) latency-bound steps,
 which dominates for the labs' small gradient messages (LeNet: 51,902 floats).  Every rank
@@ -6,7 +6,10 @@ allocates one IPC-shareable, uncached device buffer ([2][cap] floats of data in 
 halves + a [64][8] flag array), exchanges its ``hipIpcMemHandle`` through the process
 group (``all_gather_object``) and opens every peer's.  A call is ONE kernel: copy the
 slice in, flag every peer, wait for every peer's flag, sum the W slices in rank order
-(identical bits on every rank).  Waits are bounded: a missing peer raises
+(identical bits on every rank).  Large messages take the two-shot kernel instead: reduce-scatter of W rank slices (each
+rank sums ITS slice from all W buffers) then all-gather of the reduced slices, two flag
+phases, 2(W-1)/W of the bytes per rank over all W-1 links at once.  Waits are bounded: a
+missing peer raises
 :class:`RuntimeError` on :meth:`check` instead of hanging the GPU.
 
 Requirements: one process per GPU on one node (or several processes sharing one GPU, as
@@ -21,18 +24,25 @@ import torch.distributed as dist
 
 from dmlab.ops._native import lib
 
-_FLAG_BYTES = 64 * 8 * 4
+_FLAG_BYTES = 2 * 256 * 8 * 4  # [2 phases][256 blocks][8 ranks] uint32
+# auto: two-shot from 1 MB up with >= 3 ranks (at W = 2 both read n remote floats)
+_TWO_SHOT_MIN = 1 << 18
+_ALGOS = {"one_shot": 0, "two_shot": 1}
 
 
 class XGMIAllReduce:
-    def __init__(self, cap: int = 1 << 20, group=None, device=None):
+    def __init__(self, cap: int = 1 << 20, group=None, device=None, algo: str = "auto"):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         if self.world > 8:
-            raise ValueError("xGMI one-shot all-reduce supports up to 8 ranks (one node)")
+            raise ValueError("xGMI all-reduce supports up to 8 ranks (one node)")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.cap = int(cap)
+        # multiple of 4 floats: keeps both parity halves 16-B aligned for the float4 path
+        self.cap = (int(cap) + 3) // 4 * 4
+        if algo not in ("auto", *_ALGOS):
+            raise ValueError("algo: 'auto' | 'one_shot' | 'two_shot'")
+        self.algo = algo
         L = lib()
         self._base = L.xgmi_alloc(8 * self.cap + _FLAG_BYTES)
         handle = L.xgmi_get_handle(self._base)
@@ -53,15 +63,23 @@ class XGMIAllReduce:
         self._epoch = 0
         dist.barrier(group=group)
 
-    def __call__(self, t: torch.Tensor, scale: float = 1.0, out: torch.Tensor | None = None):
+    def _algo(self, n: int, algo: str | None) -> int:
+        algo = algo or self.algo
+        if algo == "auto":
+            algo = "two_shot" if (self.world >= 3 and n >= _TWO_SHOT_MIN) else "one_shot"
+        return _ALGOS[algo]
+
+    def __call__(self, t: torch.Tensor, scale: float = 1.0, out: torch.Tensor | None = None,
+                 algo: str | None = None):
         """out (default: t, in place) = scale * Σ_ranks t.  Stream-ordered on the current
-        stream; returns ``out``."""
+        stream; returns ``out``.  ``algo`` overrides the instance's choice for this call
+        (every rank must pass the same)."""
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() > self.cap:
             raise ValueError("xGMI all-reduce: fp32 contiguous tensor of <= cap elements")
         out = t if out is None else out
         self._epoch += 1
         lib().xgmi_allreduce(t, out, self.cap, self._data, self._flags, self.rank, float(scale),
-                             self._epoch, self._err)
+                             self._epoch, self._err, self._algo(t.numel(), algo))
         return out
 
     def check(self):

@@ -38,17 +38,30 @@ def _entry(rank, ws, port, kind, q):
         if kind == "xgmi":
             from dmlab.parallel.xgmi import XGMIAllReduce
 
-            ar = XGMIAllReduce(cap=1 << 16)
+            ar = XGMIAllReduce(cap=(1 << 20) + 8)
             err = 0.0
-            for it, n in enumerate([1, 1000, 51902, 65536, 7]):
+            # one-shot and two-shot interleaved on one instance (shared epochs and parity
+            # halves); two-shot sizes cover the float4 path (n % 4 == 0, aligned), the
+            # scalar path (odd n, misaligned view) and slices shorter than the grid
+            cases = [(1, "one_shot"), (1000, "two_shot"), (51902, "one_shot"),
+                     (65536, "two_shot"), (7, "two_shot"), ((1 << 20) + 8, "two_shot"),
+                     (300001, "two_shot"), (3, "one_shot"), (524288, "two_shot"),
+                     (1 << 19, None), (4096, None)]  # instance default: auto
+            for it, (n, algo) in enumerate(cases):
                 t = torch.arange(n, device=dev, dtype=torch.float32) * (rank + 1) + it
-                exp = torch.arange(n, device=dev, dtype=torch.float32) * 3 + 2 * it
-                out = ar(t.clone(), scale=0.5) if it % 2 else ar(t)  # in place / scaled copy
+                exp = torch.arange(n, device=dev, dtype=torch.float32) * (ws * (ws + 1) // 2) \
+                    + ws * it
+                if it == 6:  # a view 4 B into its storage: not 16-B aligned
+                    t = torch.cat([torch.zeros(1, device=dev), t])[1:]
+                if it % 2:
+                    out = ar(t.clone(), scale=0.5, algo=algo)  # scaled copy
+                else:
+                    out = ar(t, algo=algo)  # in place
                 ref_v = exp * (0.5 if it % 2 else 1.0)
-                err = max(err, (out - ref_v).abs().max().item())
+                err = max(err, ((out - ref_v).abs().max() / ref_v.abs().max().clamp_min(1)).item())
             ar.check()
             ar.close()
-        elif kind == "ddp_resnet":
+        elif kind in ("ddp_resnet", "ddp_resnet_xgmi2"):
             # ResNet-18 (bf16 native kernels, conv weight gradients on the side stream):
             # the DDP-averaged gradient == the mean of the two per-shard gradients computed
             # one after the other in this process (BN statistics are per shard either way)
@@ -60,7 +73,12 @@ def _entry(rank, ws, port, kind, q):
             Yr = torch.randint(0, 10, (8,), generator=gr).to(dev)
             torch.manual_seed(0)
             model = ResNet18(num_classes=10).to(dev)
-            ddp = DDP(model)
+            if kind == "ddp_resnet":
+                ddp = DDP(model)
+            else:  # every bucket (4 MB first, then 25 MB) through the two-shot xGMI kernel
+                ddp = DDP(model, small_allreduce="xgmi", small_cap_mb=1e4, xgmi_algo="two_shot")
+                assert ddp._xgmi is not None and ddp._xgmi.cap >= max(
+                    b.hi - b.lo for b in ddp.buckets)
             mopt = SGD(model.parameters(), lr=0.1)
             mopt.zero_grad()
             cross_entropy(ddp(Xr[rank * 4:(rank + 1) * 4]), Yr[rank * 4:(rank + 1) * 4]).backward()
@@ -116,7 +134,8 @@ def _entry(rank, ws, port, kind, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "ddp_resnet", "pipeline", "xgmi"])
+@pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "ddp_resnet", "ddp_resnet_xgmi2", "pipeline",
+                                  "xgmi"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 
@@ -186,3 +205,26 @@ def test_bench_two_ranks(tmp_path):
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["steps"] == 3 and res["value"] > 0
     assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 16
+
+
+def test_xgmi_four_ranks_one_gpu():
+    """Four ranks: 'auto' picks the two-shot kernel (W >= 3, >= 1 MB) -- four rank slices,
+    reduce-scatter then all-gather through four IPC-mapped buffers."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = free_port()
+    ps = [ctx.Process(target=_entry, args=(r, 4, port, "xgmi", q)) for r in range(4)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(240)
+    res = [q.get() for _ in range(4) if not q.empty()]
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+    assert len(res) == 4, res
+    for rank, err, tb in res:
+        assert tb is None, tb
+        assert err < 2e-4, (rank, err)
