@@ -46,6 +46,9 @@ def parse():
     ap.add_argument("--model", default="resnet18", choices=["resnet18", "lenet"])
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch")
     ap.add_argument("--res", type=int, default=224)
+    ap.add_argument("--dtype", default=None, choices=["fp32", "bf16"],
+                    help="activation dtype; default bf16 for resnet18 (always), fp32 for "
+                         "lenet (the reference dtype; bf16 = BASELINE config 3)")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--phases", type=int, default=0,
                     help="after the timed run, N extra eager steps timed per phase with HIP "
@@ -96,7 +99,8 @@ def main():
         bs = a.batch or 32
         model = Net().to(dev)
         g = torch.Generator(device=dev).manual_seed(1000 + rank)
-        pool = [torch.rand(bs, 1, 28, 28, device=dev, generator=g) for _ in range(2)]
+        act = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+        pool = [torch.rand(bs, 1, 28, 28, device=dev, generator=g).to(act) for _ in range(2)]
         labels = [torch.randint(0, 10, (bs,), device=dev, generator=g) for _ in range(2)]
         lr = 0.001
     if a.backend == "torch":
@@ -171,8 +175,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "vs_stock_pytorch_rocm": (round(value / (STOCK_PER_GPU[(a.model, bs)] * ws), 3)
-                                      if (a.model, bs) in STOCK_PER_GPU else None),
-            "dtype": "bf16" if a.model == "resnet18" else "fp32",
+                                      if (a.model, bs) in STOCK_PER_GPU
+                                      and not (a.model == "lenet" and a.dtype == "bf16")
+                                      else None),
+            "dtype": "bf16" if (a.model == "resnet18" or a.dtype == "bf16") else "fp32",
             "data": "synthetic (device-resident random images, random-init weights)",
             "config": {
                 "model": a.model,

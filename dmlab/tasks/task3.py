@@ -42,6 +42,9 @@ def parse_args(argv=None):
                    choices=["partition", "random", "division"])
     p.add_argument("--dp", default="ddp", choices=["ddp", "manual"])
     p.add_argument("--batch-size", type=int, default=32)
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                   help="activation dtype (master weights and gradients stay fp32); "
+                        "BASELINE config 3 is bf16.  ResNet-18 always runs bf16")
     p.add_argument("--epochs", type=int, default=2)
     p.add_argument("--lr", type=float, default=0.001)
     p.add_argument("--momentum", type=float, default=0.9)
@@ -81,7 +84,12 @@ def main(argv=None):
     # strategy needs a shared permutation so it uses seed 0 on every rank.
     seed = rank if a.sampler == "random" else 0
     sampler = MySampler(train_set, ws, rank, shuffle=True, seed=seed, mode=a.sampler)
-    loader = DeviceLoader(train_set.to(dev), a.batch_size, sampler=sampler)
+    # bf16 activations: the device-resident data is stored in bf16 once; every native
+    # kernel downstream then runs bf16 in / fp32 accumulate (GPU only: the CPU torch path
+    # keeps fp32)
+    act = torch.bfloat16 if (a.dtype == "bf16" and a.model == "lenet" and dev.type == "cuda") \
+        else None
+    loader = DeviceLoader(train_set.to(dev, dtype=act), a.batch_size, sampler=sampler)
     opt = SGD(model.parameters(), lr=a.lr, momentum=a.momentum)
     if a.resume:
         from dmlab.utils import checkpoint
@@ -104,7 +112,7 @@ def main(argv=None):
 
         checkpoint.save(a.save, model, opt, epochs=a.epochs)
     if not a.no_test and rank == 0:
-        stats["accuracy"] = test(model, DeviceLoader(test_set.to(dev), 32))
+        stats["accuracy"] = test(model, DeviceLoader(test_set.to(dev, dtype=act), 32))
     stats.update(rank=rank, world_size=ws, sampler=a.sampler, dp=a.dp,
                  samples_per_s=stats["samples"] * ws / stats["train_time"])
     if a.json and rank == 0:
