@@ -28,9 +28,11 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "samples/sec (whole node) for task3 DDP CNN at 1/2/4/8 MI355X"
 # stock PyTorch-ROCm 2.10 (MIOpen/hipBLASLt, channels_last bf16 autocast, SGD) on one
-# MI355X at the same per-GPU batch, measured by tools/probe_stock.py
-# (profiles/stock_pytorch_rocm_r1.jsonl): ResNet-18 batch 256 / 512, LeNet batch 32
-STOCK_PER_GPU = {("resnet18", 256): 16912.7, ("resnet18", 512): 18185.3, ("lenet", 32): 47836.5}
+# MI355X at the same per-GPU batch, measured by tools/probe_stock.py: the best of the
+# default run (profiles/stock_pytorch_rocm_r1.jsonl) and the --tuned run with
+# cudnn.benchmark = True (MIOpen solver search; LeNet without the per-step loss.item()),
+# profiles/stock_pytorch_rocm_tuned_r1s5.jsonl
+STOCK_PER_GPU = {("resnet18", 256): 16912.7, ("resnet18", 512): 19785.8, ("lenet", 32): 49523.7}
 # per-GPU batch of the headline run: 512 images (a 1.3 ms/step fixed cost -- BN statistic
 # reductions, weight-gradient slab reduces, optimizer, launch floor -- is amortised over
 # twice the work of 256; measured 35.4k -> 39.0k img/s on one MI355X; 288 GB HBM holds it

@@ -2,7 +2,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=s5h
-timeout -k 10 300 python -u -m pytest tests/test_native_lenet.py -m gpu -x -v --timeout 120 --timeout-method thread \
-    > gpurun_out/pytest_$t.log 2>&1 || { tail -40 gpurun_out/pytest_$t.log; exit 1; }
-tail -4 gpurun_out/pytest_$t.log
+t=s5i
+timeout -k 10 900 python -u tools/probe_stock.py --tuned --resnet-batches 512 2> gpurun_out/stock_$t.err | tee gpurun_out/stock_tuned_$t.jsonl || { tail -20 gpurun_out/stock_$t.err; exit 1; }

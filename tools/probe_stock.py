@@ -49,7 +49,7 @@ def run_resnet(batch, res, dtype, channels_last, warmup, iters):
             "channels_last": channels_last, "ms_per_step": t * 1e3, "samples_per_s": batch / t}
 
 
-def run_lenet(batch, warmup, iters):
+def run_lenet(batch, warmup, iters, sync_every_step=True):
     model = TorchLeNet().cuda()
     opt = torch.optim.SGD(model.parameters(), lr=0.001, momentum=0.9)
     x = torch.rand(batch, 1, 28, 28, device="cuda")
@@ -60,11 +60,12 @@ def run_lenet(batch, warmup, iters):
         opt.zero_grad()
         loss.backward()
         opt.step()
-        loss.item()  # reference syncs every iteration (task2/model.py:63)
+        if sync_every_step:
+            loss.item()  # reference syncs every iteration (task2/model.py:63)
 
     t = bench(step, warmup, iters)
     return {"model": "lenet", "batch": batch, "dtype": "fp32", "ms_per_step": t * 1e3,
-            "samples_per_s": batch / t}
+            "samples_per_s": batch / t, "item_sync_per_step": sync_every_step}
 
 
 def main():
@@ -72,8 +73,24 @@ def main():
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--resnet-batches", default=None,
                     help="comma-separated ResNet-18 batches (channels_last bf16) only")
+    ap.add_argument("--tuned", action="store_true",
+                    help="torch.backends.cudnn.benchmark = True (MIOpen searches every conv "
+                         "for its fastest solver on first use; longer warmup), ResNet in "
+                         "both layouts, LeNet with and without the per-step loss.item()")
     a = ap.parse_args()
-    print(json.dumps({"device": torch.cuda.get_device_name(0)}), flush=True)
+    print(json.dumps({"device": torch.cuda.get_device_name(0), "tuned": a.tuned}), flush=True)
+    if a.tuned:
+        torch.backends.cudnn.benchmark = True
+        for b in (a.resnet_batches or "512").split(","):
+            for cl in (True, False):
+                r = run_resnet(int(b), 224, torch.bfloat16, cl, 15, 20)
+                r["cudnn_benchmark"] = True
+                print(json.dumps(r), flush=True)
+        for sync in (True, False):
+            r = run_lenet(32, 50, 500, sync_every_step=sync)
+            r["cudnn_benchmark"] = True
+            print(json.dumps(r), flush=True)
+        return
     if a.resnet_batches:
         for b in a.resnet_batches.split(","):
             print(json.dumps(run_resnet(int(b), 224, torch.bfloat16, True, 5, 20)), flush=True)
