@@ -1546,6 +1546,14 @@ void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom&
     const size_t sm = 2 * 64 * ((128 + 16) + (128 + 16)) * 2 + MAXTAPS * 16;
     set_smem_attr(k, sm);
     k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db);
+  } else if (cfg == 6) {
+    // 64 x 256: the whole K of the s2d stem (4x4 taps x 16 ch) in one tile, so every dY
+    // row is read once instead of once per 128-column K tile
+    dim3 grid((g.Ncols + 63) / 64, (g.K + 255) / 256, S);
+    auto k = igemm_wgrad2_kernel<64, 256, 2, 2>;
+    const size_t sm = 2 * 64 * ((64 + 16) + (256 + 16)) * 2 + MAXTAPS * 16;
+    set_smem_attr(k, sm);
+    k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db);
   } else {
     dim3 grid((g.Ncols + 63) / 64, (g.K + 127) / 128, S);
     auto k = igemm_wgrad2_kernel<64, 128, 2, 2>;

@@ -78,7 +78,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
     cfg 4/5: halo-staged 3x3 unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per
-    block; cfg 2/3: v2 igemm tiles 128x128 / 64x128 (cfg 0/1: v1, kept for A/B).
+    block; cfg 2/3/6: v2 igemm tiles 128x128 / 64x128 / 64x256 (cfg 0/1: v1, kept for A/B).
     S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
     ~2 blocks per CU, each split >= 8 row steps, slab bytes S*cout*K*4."""
     halo = k == 3 and stride == 1 and cin % 64 == 0 and cout % 8 == 0
@@ -96,7 +96,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
         max_split = max(1, M // 512)
     else:
         bm = 128 if cfg in (0, 2) else 64
-        tiles = math.ceil(cout / bm) * math.ceil(K / 128)
+        tiles = math.ceil(cout / bm) * math.ceil(K / (256 if cfg == 6 else 128))
         # >= 8 row steps of 64 per split: the small-K layers (1x1/s2 downsample: K = Cin)
         # have one or two output tiles, so the m-split is their only parallelism
         max_split = max(1, M // 512)

@@ -85,7 +85,10 @@ def init(world_size: int | None = None, rank: int | None = None, master_addr: st
         device_type = os.environ.get("DMLAB_DEVICE") or (
             "cuda" if torch.cuda.is_available() else "cpu")
     if device_type == "cuda":
-        lr = int(os.environ.get("LOCAL_RANK", rk % max(torch.cuda.device_count(), 1)))
+        ndev = max(torch.cuda.device_count(), 1)
+        # more local ranks than GPUs: ranks share devices round-robin (only usable with
+        # gloo, DMLAB_BACKEND=gloo -- RCCL rejects two ranks on one GPU, loudly)
+        lr = int(os.environ.get("LOCAL_RANK", rk)) % ndev
         _DEVICE = torch.device("cuda", lr)
         torch.cuda.set_device(_DEVICE)
     else:

@@ -2,5 +2,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=s5i
-timeout -k 10 900 python -u tools/probe_stock.py --tuned --resnet-batches 512 2> gpurun_out/stock_$t.err | tee gpurun_out/stock_tuned_$t.jsonl || { tail -20 gpurun_out/stock_$t.err; exit 1; }
+t=s5l
+DMLAB_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes 1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29533 tools/bench_allreduce.py --iters 10 --max-mb 16 > gpurun_out/ar_$t.jsonl 2> gpurun_out/ar_$t.err || { tail -30 gpurun_out/ar_$t.err; exit 1; }
+cat gpurun_out/ar_$t.jsonl
