@@ -407,6 +407,20 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
   __syncthreads();
   const long long n8 = a.M * C8;
   const long long stride = (long long)gridDim.x * blockDim.x;
+  // With C8 | blockDim (C <= 2048) a thread's channel chunk never changes across the
+  // grid-stride loop: its 24 coefficients live in registers instead of being re-read
+  // from LDS per element (lanes 8 floats apart: the kernel's LDS bank conflicts).
+  const bool hoist = (blockDim.x % C8) == 0;
+  float ka[8], kb[8], kc[8];
+  if (hoist) {
+    const int c0 = (threadIdx.x & (C8 - 1)) * 8;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ka[j] = cf[c0 + j];
+      kb[j] = cf[C + c0 + j];
+      kc[j] = cf[2 * C + c0 + j];
+    }
+  }
   for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
     BnBwdBatch<MODE, U> bt;
     bt.load(a, i0, stride, n8);
@@ -420,9 +434,14 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
       bt.dz(a, u, i, chunk, C8, sc, sh, d, yv);
       if (DRES) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
       float r[8];
+      if (hoist) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
+        for (int j = 0; j < 8; ++j) r[j] = ka[j] * d[j] + kb[j] * yv[j] + kc[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
+      }
       reinterpret_cast<uint4*>(dy)[i] = pack8(r);
     }
   }
