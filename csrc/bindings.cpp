@@ -192,7 +192,7 @@ void gemm(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor B, c10::opti
                    S > 1 ? part.data_ptr<float>() : nullptr, S, cur_stream());
 }
 
-// ------------------------------------------------------------ xGMI one-shot all-reduce
+// ------------------------------------------------------------ xGMI one-/two-shot all-reduce
 int64_t xgmi_alloc(int64_t bytes) { return (int64_t)(uintptr_t)dm::xgmi_alloc((size_t)bytes); }
 void xgmi_free(int64_t ptr) { dm::xgmi_free((void*)(uintptr_t)ptr); }
 py::bytes xgmi_get_handle(int64_t ptr) {
@@ -207,15 +207,17 @@ int64_t xgmi_open_handle(py::bytes handle) {
 }
 void xgmi_close_handle(int64_t ptr) { dm::xgmi_close_handle((void*)(uintptr_t)ptr); }
 void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int64_t> data,
-                    std::vector<int64_t> flags, int64_t rank, double scale, int64_t epoch,
-                    at::Tensor err, int64_t algo) {
+                    std::vector<int64_t> flags, int64_t rank, double scale, at::Tensor state,
+                    int64_t algo) {
   CHECK_F32(in);
   CHECK_F32(out);
   TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel());
   TORCH_CHECK(in.numel() <= cap, "tensor larger than the shared buffer");
   const int W = data.size();
   TORCH_CHECK(W >= 1 && W <= 8 && (int)flags.size() == W && rank >= 0 && rank < W);
-  TORCH_CHECK(err.scalar_type() == at::kInt && err.is_cuda());
+  // [timeout flag, last published epoch, done-block counter, pad] on the device
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.is_cuda() && state.numel() >= 3 &&
+              state.device() == in.device());
   std::vector<void*> d(W), f(W);
   for (int q = 0; q < W; ++q) {
     d[q] = (void*)(uintptr_t)data[q];
@@ -223,8 +225,8 @@ void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int6
   }
   const DeviceGuard guard(in.device());
   dm::xgmi_allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cap, d.data(),
-                     f.data(), (int)rank, W, (unsigned)epoch, (float)scale, err.data_ptr<int>(),
-                     (int)algo, cur_stream());
+                     f.data(), (int)rank, W, (float)scale,
+                     reinterpret_cast<unsigned*>(state.data_ptr<int>()), (int)algo, cur_stream());
 }
 
 void colsum(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor out, double beta) {

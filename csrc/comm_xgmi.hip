@@ -16,6 +16,12 @@
 //      rank order (bitwise-identical results on every rank) and writes out = scale * sum.
 // Blocks synchronise only with their namesakes on the peers — no grid-wide barrier.
 //
+// The call epoch lives on the DEVICE (state[1]), not in a kernel argument: every block reads
+// epoch = state[1] + 1 on entry, and the last block to leave (a done-counter, state[2])
+// publishes it.  A hipGraph replay therefore advances the epoch (and flips the parity half)
+// exactly like an eager call; a host counter frozen into the captured arguments would replay
+// the same epoch and let the flag waits pass at once.  state[0] is the timeout flag.
+//
 // Two-shot variant (large buckets, e.g. ResNet-18's 25 MB): the one-shot kernel reads W
 // full copies per rank, (W-1)·n remote bytes.  Two-shot splits the message into W rank
 // slices; block b of rank r
@@ -81,6 +87,25 @@ __device__ inline bool xg_wait(const XgmiPtrs& p, int phase, int b, int rank, in
   return ok;
 }
 
+// epoch of this call: one past the last published one (read before this block can finish,
+// so before the last block of the grid can publish)
+__device__ inline unsigned xg_epoch(const unsigned* state) {
+  return __hip_atomic_load(state + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// every block calls this exactly once on every exit path; the last one publishes the epoch
+__device__ inline void xg_finish(unsigned* state, unsigned epoch) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(state + 2, 1u, __ATOMIC_ACQ_REL,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(state + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(state + 1, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 template <int VEC>
 struct XgVec;
 template <>
@@ -105,9 +130,10 @@ template <int VEC>
 __global__ void __launch_bounds__(256) xgmi_allreduce2_kernel(const float* __restrict__ in_,
                                                               float* __restrict__ out_, long long n,
                                                               long long cap, XgmiPtrs p, int rank,
-                                                              int W, unsigned epoch, float scale,
-                                                              int* __restrict__ err) {
+                                                              int W, float scale,
+                                                              unsigned* __restrict__ state) {
   using V = typename XgVec<VEC>::T;
+  const unsigned epoch = xg_epoch(state);
   const V* in = reinterpret_cast<const V*>(in_);
   V* out = reinterpret_cast<V*>(out_);
   const int b = blockIdx.x, G = gridDim.x;
@@ -127,7 +153,8 @@ __global__ void __launch_bounds__(256) xgmi_allreduce2_kernel(const float* __res
   }
   xg_signal(p, 0, b, rank, W, epoch);
   if (!xg_wait(p, 0, b, rank, W, epoch)) {
-    if (threadIdx.x == 0) atomicExch(err, 1);
+    if (threadIdx.x == 0) atomicExch(state, 1u);
+    xg_finish(state, epoch);
     return;
   }
   range(rank, lo, hi);
@@ -140,7 +167,8 @@ __global__ void __launch_bounds__(256) xgmi_allreduce2_kernel(const float* __res
   }
   xg_signal(p, 1, b, rank, W, epoch);
   if (!xg_wait(p, 1, b, rank, W, epoch)) {
-    if (threadIdx.x == 0) atomicExch(err, 1);
+    if (threadIdx.x == 0) atomicExch(state, 1u);
+    xg_finish(state, epoch);
     return;
   }
   for (int q = 0; q < W; ++q) {
@@ -149,14 +177,16 @@ __global__ void __launch_bounds__(256) xgmi_allreduce2_kernel(const float* __res
     range(q, lo, hi);
     for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = src[i];
   }
+  xg_finish(state, epoch);
 }
 
 __global__ void __launch_bounds__(256) xgmi_allreduce_kernel(const float* __restrict__ in,
                                                              float* __restrict__ out, long long n,
                                                              long long cap, XgmiPtrs p, int rank,
-                                                             int W, unsigned epoch, float scale,
-                                                             int* __restrict__ err) {
+                                                             int W, float scale,
+                                                             unsigned* __restrict__ state) {
   const int b = blockIdx.x;
+  const unsigned epoch = xg_epoch(state);
   const long long per = (n + gridDim.x - 1) / gridDim.x;
   const long long lo = b * per, hi = lo + per < n ? lo + per : n;
   const long long half = (long long)(epoch & 1u) * cap;
@@ -166,7 +196,8 @@ __global__ void __launch_bounds__(256) xgmi_allreduce_kernel(const float* __rest
   // >=: a fast peer may already have stored epoch+1 (it then waits for OUR epoch+1 flag,
   // so it cannot reach epoch+2 and overwrite the parity half this call reads)
   if (!xg_wait(p, 0, b, rank, W, epoch)) {
-    if (threadIdx.x == 0) atomicExch(err, 1);
+    if (threadIdx.x == 0) atomicExch(state, 1u);
+    xg_finish(state, epoch);
     return;
   }
   for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) {
@@ -174,6 +205,7 @@ __global__ void __launch_bounds__(256) xgmi_allreduce_kernel(const float* __rest
     for (int q = 0; q < W; ++q) s += p.data[q][half + i];
     out[i] = s * scale;
   }
+  xg_finish(state, epoch);
 }
 
 void* xgmi_alloc(size_t bytes) {
@@ -204,16 +236,16 @@ void* xgmi_open_handle(const void* handle64) {
 void xgmi_close_handle(void* ptr) { DM_CHECK(hipIpcCloseMemHandle(ptr)); }
 
 void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
-                    void* const* flags, int rank, int W, unsigned epoch, float scale, int* err,
-                    int algo, hipStream_t st) {
+                    void* const* flags, int rank, int W, float scale, unsigned* state, int algo,
+                    hipStream_t st) {
   XgmiPtrs p{};
   for (int q = 0; q < W; ++q) {
     p.data[q] = (float*)data[q];
     p.flags[q] = (unsigned*)flags[q];
   }
   if (algo == 0) {
-    xgmi_allreduce_kernel<<<XG_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, epoch, scale,
-                                                     err);
+    xgmi_allreduce_kernel<<<XG_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, scale,
+                                                     state);
     return;
   }
   // two-shot: float4 when every rank's view is 16-B aligned (cap % 4 == 0 keeps the parity
@@ -222,10 +254,10 @@ void xgmi_allreduce(const float* in, float* out, long long n, long long cap, voi
                   ((uintptr_t)out % 16) == 0;
   if (v4)
     xgmi_allreduce2_kernel<4><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n / 4, cap / 4, p, rank, W,
-                                                          epoch, scale, err);
+                                                          scale, state);
   else
-    xgmi_allreduce2_kernel<1><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, epoch,
-                                                          scale, err);
+    xgmi_allreduce2_kernel<1><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, scale,
+                                                          state);
 }
 
 }  // namespace dm

@@ -55,8 +55,8 @@ void xgmi_get_handle(void* ptr, void* handle64);
 void* xgmi_open_handle(const void* handle64);
 void xgmi_close_handle(void* ptr);
 void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
-                    void* const* flags, int rank, int W, unsigned epoch, float scale, int* err,
-                    int algo, hipStream_t st);
+                    void* const* flags, int rank, int W, float scale, unsigned* state, int algo,
+                    hipStream_t st);
 // conv_igemm.hip
 struct ConvGeom;
 struct ConvGeomSet;

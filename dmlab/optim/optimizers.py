@@ -12,7 +12,8 @@ per-tensor path with the same formulas.
 
 ``grad_scale`` multiplies the gradient inside the step — the data-parallel
 1/world_size average is folded in there instead of a separate divide kernel
-(SURVEY K24).
+(SURVEY K24).  It is runtime configuration owned by DDP, so it is not part of
+``state_dict``.
 """
 from __future__ import annotations
 
@@ -45,14 +46,27 @@ class BaseOptimizer:
         self.params = [p for p in params]
         if self.params and isinstance(self.params[0], dict):
             raise TypeError("parameter groups are not supported; pass a parameter iterable")
-        self.lr = lr
+        # one persistent group dict: `for g in opt.param_groups: g["lr"] = x` (the usual LR
+        # schedule idiom) writes straight into the value step() reads
+        self._groups = [{"params": self.params, "lr": lr}]
+        # runtime data-parallel config (DDP.fold_average_into sets 1/ws), NOT optimiser
+        # state: it is neither saved nor restored, so a resume on another world size
+        # (or without DDP) does not inherit a stale 1/N factor
         self.grad_scale = 1.0
         self.flat = _flat_of(self.params)
         self.step_count = 0
 
     @property
-    def param_groups(self):  # minimal torch.optim compatibility (LR schedulers, logging)
-        return [{"params": self.params, "lr": self.lr}]
+    def lr(self):
+        return self._groups[0]["lr"]
+
+    @lr.setter
+    def lr(self, v):
+        self._groups[0]["lr"] = v
+
+    @property
+    def param_groups(self):  # one group: enough for manual LR schedules and logging
+        return self._groups
 
     def step(self):
         raise NotImplementedError
@@ -80,7 +94,7 @@ class BaseOptimizer:
         return {}
 
     def state_dict(self):
-        sd = {"lr": self.lr, "step_count": self.step_count, "grad_scale": self.grad_scale}
+        sd = {"lr": self.lr, "step_count": self.step_count}
         sd.update({k: v.detach().clone() for k, v in self._state_tensors().items()
                    if v is not None})
         return sd
@@ -88,7 +102,7 @@ class BaseOptimizer:
     def load_state_dict(self, sd):
         self.lr = sd["lr"]
         self.step_count = sd.get("step_count", 0)
-        self.grad_scale = sd.get("grad_scale", self.grad_scale)
+        # a "grad_scale" key written by older checkpoints is ignored on purpose (see __init__)
         for k, t in self._state_tensors().items():
             if t is not None and k in sd:
                 with torch.no_grad():

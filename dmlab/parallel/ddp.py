@@ -283,6 +283,8 @@ class DistributedDataParallel(nn.Module):
             if self.program is None:
                 self._final_queued = False
             return
+        if self._xgmi is not None:
+            self._xgmi.poll()  # a timed-out peer raises here (asynchronously, no sync)
         if self._native is not None:
             self._native.finalize()
             if self.program is None:

@@ -24,26 +24,31 @@ from dmlab.nn.program import Program
 from . import env
 
 
-def _tp():
+def _tp(group=None):
+    """(degree, index) of this rank in the tensor-parallel group: the shard geometry must
+    match the group the partial results are reduced over (a TP subgroup of a larger job
+    shards by its own size and rank, not the global ones)."""
+    if group is not None and dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
     return env.get_world_size(), env.get_rank()
 
 
 def _all_reduce(t, group=None):
-    if env.get_world_size() > 1:
+    if _tp(group)[0] > 1:
         dist.all_reduce(t, group=group)
     return t
 
 
 class ColumnParallelLinear(Linear):
     def __init__(self, fin, fout, bias=True, relu=False, group=None):
-        ws, _ = _tp()
+        ws, _ = _tp(group)
         assert fout % ws == 0, "output features must divide the TP degree"
         super().__init__(fin, fout // ws, bias=bias, relu=relu)
         self.full_out = fout
         self.group = group
 
     def load_from_full(self, w, b=None):
-        ws, r = _tp()
+        ws, r = _tp(self.group)
         n = self.fout
         with torch.no_grad():
             self.weight.copy_(w[r * n:(r + 1) * n])
@@ -61,7 +66,7 @@ class RowParallelLinear(Linear):
     """Input features are sharded; the bias is replicated and added after the sum."""
 
     def __init__(self, fin, fout, bias=True, relu=False, group=None):
-        ws, _ = _tp()
+        ws, _ = _tp(group)
         assert fin % ws == 0, "input features must divide the TP degree"
         super().__init__(fin // ws, fout, bias=False, relu=False)
         self.full_in = fin
@@ -70,7 +75,7 @@ class RowParallelLinear(Linear):
         self.rbias = nn.Parameter(torch.zeros(fout)) if bias else None
 
     def load_from_full(self, w, b=None):
-        ws, r = _tp()
+        ws, r = _tp(self.group)
         n = self.fin
         with torch.no_grad():
             self.weight.copy_(w[:, r * n:(r + 1) * n])

@@ -10,7 +10,11 @@ slice in, flag every peer, wait for every peer's flag, sum the W slices in rank 
 rank sums ITS slice from all W buffers) then all-gather of the reduced slices, two flag
 phases, 2(W-1)/W of the bytes per rank over all W-1 links at once.  Waits are bounded: a
 missing peer raises
-:class:`RuntimeError` on :meth:`check` instead of hanging the GPU.
+:class:`RuntimeError` on :meth:`check` (synchronous) or :meth:`poll` (asynchronous: DDP
+calls it at the end of every backward; it never blocks) instead of hanging the GPU.
+
+The call epoch (flag value and parity half) is a device-side counter the kernel advances
+itself, so a captured hipGraph replays correctly: each replay is a new epoch.
 
 Requirements: one process per GPU on one node (or several processes sharing one GPU, as
 the tests do), ``HSA_ENABLE_IPC_MODE_LEGACY=0`` (dmabuf IPC), fp32 contiguous tensors of
@@ -59,8 +63,12 @@ class XGMIAllReduce:
                 bases.append(p)
         self._data = bases
         self._flags = [b + 8 * self.cap for b in bases]
-        self._err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self._epoch = 0
+        # [timeout flag, last published epoch, done-block counter, pad] (device side)
+        self._state = torch.zeros(4, dtype=torch.int32, device=self.device)
+        self._calls = 0
+        # asynchronous error poll: a pinned copy of the flag plus the event that completes it
+        self._err_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._err_event = None
         dist.barrier(group=group)
 
     def _algo(self, n: int, algo: str | None) -> int:
@@ -77,15 +85,40 @@ class XGMIAllReduce:
         if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() > self.cap:
             raise ValueError("xGMI all-reduce: fp32 contiguous tensor of <= cap elements")
         out = t if out is None else out
-        self._epoch += 1
+        self._calls += 1
         lib().xgmi_allreduce(t, out, self.cap, self._data, self._flags, self.rank, float(scale),
-                             self._epoch, self._err, self._algo(t.numel(), algo))
+                             self._state, self._algo(t.numel(), algo))
         return out
+
+    @property
+    def epoch(self) -> int:
+        """Calls completed on the device so far (synchronises)."""
+        return int(self._state[1].item())
+
+    def _raise(self):
+        raise RuntimeError("xGMI all-reduce: a peer never arrived (timed out); this rank's "
+                           "bucket kept its local gradient, so the replicas have diverged")
 
     def check(self):
         """Raise if any call so far timed out waiting for a peer (synchronises)."""
-        if int(self._err.item()):
-            raise RuntimeError("xGMI all-reduce: a peer never arrived (timed out)")
+        if int(self._state[0].item()):
+            self._raise()
+
+    def poll(self):
+        """Non-blocking error check on the current stream: raises if an earlier poll's copy of
+        the timeout flag has landed and is set, then queues the next copy.  Never
+        synchronises; skipped while a hipGraph is being captured."""
+        if torch.cuda.is_current_stream_capturing():
+            return
+        ev = self._err_event
+        if ev is not None:
+            if not ev.query():
+                return  # the previous copy is still in flight: look again next time
+            if int(self._err_host[0]):
+                self._raise()
+        self._err_host.copy_(self._state[:1], non_blocking=True)
+        self._err_event = torch.cuda.Event()
+        self._err_event.record()
 
     def close(self):
         L = lib()

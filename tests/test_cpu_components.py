@@ -240,6 +240,23 @@ def test_program_to_refits_flat_buffer():
         assert p._dm_flat is m.flat
 
 
+def test_param_groups_lr_is_persistent():
+    """`for g in opt.param_groups: g["lr"] = x` (manual LR schedule) reaches step()."""
+    m, _ = _lenet_pair()
+    o = SGD(m.parameters(), lr=0.1)
+    for grp in o.param_groups:
+        grp["lr"] = 0.0
+    assert o.lr == 0.0
+    before = [p.detach().clone() for p in m.parameters()]
+    o.zero_grad()
+    _loss(m, 0).backward()
+    o.step()
+    for a, b in zip(before, m.parameters()):
+        torch.testing.assert_close(a, b)
+    o.lr = 0.3
+    assert o.param_groups[0]["lr"] == 0.3
+
+
 def test_checkpoint_roundtrip(tmp_path):
     from dmlab.utils import checkpoint
 

@@ -211,3 +211,41 @@ def _native_vs_python_reducer(rank, ws, path):
 
 def test_native_reducer_matches_python():
     run_dist(_native_vs_python_reducer, 2, None)
+
+
+def _resume_other_world_size(rank, ws, path):
+    """A checkpoint written by a DDP run (1/ws folded into the optimiser) resumed by a
+    single process: the resumed optimiser must not inherit the 1/ws gradient scale."""
+    import os
+
+    from dmlab.models import Net
+    from dmlab.optim import SGD
+    from dmlab.parallel import DDP
+    from dmlab.utils import checkpoint
+
+    torch.manual_seed(0)
+    model = Net()
+    ddp = DDP(model)
+    opt = ddp.fold_average_into(SGD(model.parameters(), lr=0.1, momentum=0.9))
+    assert opt.grad_scale == 1.0 / ws
+    g = torch.Generator().manual_seed(5)
+    X, Y = torch.rand(4, 1, 28, 28, generator=g), torch.randint(0, 10, (4,), generator=g)
+    opt.zero_grad()
+    F.cross_entropy(ddp(X), Y).backward()
+    opt.step()
+    ck = os.path.join(path, "ck.pt")
+    checkpoint.save(ck, ddp, opt)
+    if rank == 0:
+        assert "grad_scale" not in torch.load(ck, weights_only=True)["optimizer"]
+
+
+def test_checkpoint_resume_on_another_world_size(tmp_path):
+    from dmlab.models import Net
+    from dmlab.optim import SGD
+    from dmlab.utils import checkpoint
+
+    run_dist(_resume_other_world_size, 2, str(tmp_path))
+    b = Net()
+    ob = SGD(b.parameters(), lr=0.5, momentum=0.9)
+    checkpoint.load(tmp_path / "ck.pt", b, ob)
+    assert ob.grad_scale == 1.0 and ob.lr == 0.1 and ob.step_count == 1

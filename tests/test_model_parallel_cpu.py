@@ -95,6 +95,31 @@ def test_tensor_parallel_head_matches_full_model(ws):
     run_dist(_tp, ws, None)
 
 
+def _tp_subgroups(rank, ws, _):
+    """TP degree 2 inside a 4-rank job (two TP groups {0,1}, {2,3}): shards follow the
+    subgroup's size and rank, not the global ones (a global-rank shard would be wrong)."""
+    import torch.distributed as dist
+
+    from dmlab.models import Net
+    from dmlab.parallel.tensor_parallel import TPLeNet
+
+    groups = [dist.new_group([0, 1]), dist.new_group([2, 3])]
+    grp = groups[rank // 2]
+    g = torch.Generator().manual_seed(11)
+    X = torch.rand(4, 1, 28, 28, generator=g)
+    torch.manual_seed(0)
+    full = Net()
+    tp = TPLeNet(group=grp).load_from_full(full)
+    assert tp.fc1.weight.shape[0] == 60 and tp.fc2.weight.shape[1] == 60
+    n, r = 60, rank % 2
+    torch.testing.assert_close(tp.fc1.weight, full.fc1.weight[r * n:(r + 1) * n])
+    torch.testing.assert_close(tp(X), full(X), rtol=1e-5, atol=1e-6)
+
+
+def test_tensor_parallel_subgroups():
+    run_dist(_tp_subgroups, 4, None)
+
+
 def test_rpc_reference_model_trains(tmp_path):
     env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "3",

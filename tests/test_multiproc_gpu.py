@@ -61,6 +61,31 @@ def _entry(rank, ws, port, kind, q):
                 err = max(err, ((out - ref_v).abs().max() / ref_v.abs().max().clamp_min(1)).item())
             ar.check()
             ar.close()
+        elif kind == "xgmi_graph":
+            # the all-reduce captured into a hipGraph and replayed: the epoch (flag value and
+            # parity half) lives on the device, so every replay is a fresh, correct call
+            from dmlab.parallel.xgmi import XGMIAllReduce
+
+            ar = XGMIAllReduce(cap=4096)
+            n = 4000
+            src = torch.zeros(n, device=dev)
+            dst = torch.zeros(n, device=dev)
+            ar(src, out=dst)  # eager call before capture (epoch 1)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                ar(src, out=dst, scale=0.5)
+            err = 0.0
+            base = torch.arange(n, device=dev, dtype=torch.float32)
+            for it in range(6):
+                src.copy_(base * (rank + 1) + it)
+                graph.replay()
+                want = 0.5 * (base * (ws * (ws + 1) // 2) + ws * it)
+                err = max(err, ((dst - want).abs().max() / want.abs().max()).item())
+            assert ar.epoch == 7, ar.epoch  # 1 eager + 6 replays (capture does not run it)
+            ar.check()
+            ar.poll()
+            ar.close()
         elif kind in ("ddp_resnet", "ddp_resnet_xgmi2"):
             # ResNet-18 (bf16 native kernels, conv weight gradients on the side stream):
             # the DDP-averaged gradient == the mean of the two per-shard gradients computed
@@ -135,7 +160,7 @@ def _entry(rank, ws, port, kind, q):
 
 
 @pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "ddp_resnet", "ddp_resnet_xgmi2", "pipeline",
-                                  "xgmi"])
+                                  "xgmi", "xgmi_graph"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 
