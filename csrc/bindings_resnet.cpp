@@ -85,6 +85,15 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
     TORCH_CHECK(pre_shift.has_value(), "pre_scale needs pre_shift");
     need_f32(*pre_scale, "pre_scale", x.size(3));
     need_f32(*pre_shift, "pre_shift", x.size(3));
+    if (cfg == 50 || cfg == 51) {
+      if (dm::conv_h5_supported(g, (int)cfg)) {
+        dm::conv_h5(bp(x), bp(wpack), bp(y), ap, sp, g, (int)cfg, cur_stream(), fp(*pre_scale),
+                    fp(*pre_shift));
+        return;
+      }
+      TORCH_CHECK(cfg == 50, "cfg 51 needs a single-chunk 3x3/s1 geometry");
+      cfg = 41;  // same 256-row tile: the stats slab rows still match
+    }
     TORCH_CHECK(dm::halo_cfg((int)cfg, bn, waves) && dm::conv_halo_supported(g),
                 "fused pre-BN needs a halo-kernel cfg and a unit-stride 3x3 geometry");
     dm::conv_halo(bp(x), bp(wpack), bp(y), ap, sp, g, bn, waves, cur_stream(), fp(*pre_scale),
@@ -117,7 +126,8 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
                    c10::optional<at::Tensor> bnb_y, c10::optional<at::Tensor> bnb_out,
                    c10::optional<at::Tensor> bnb_mean, c10::optional<at::Tensor> bnb_invstd,
                    c10::optional<at::Tensor> bnb_scale, c10::optional<at::Tensor> bnb_shift,
-                   int64_t bnb_mode, c10::optional<at::Tensor> bnb_slab) {
+                   int64_t bnb_mode, c10::optional<at::Tensor> bnb_slab,
+                   c10::optional<at::Tensor> bnb_mask) {
   // add: tensor added to the result (may alias dx for in-place accumulation)
   need_bf16_nhwc(dy, "dy");
   need_bf16_nhwc(dx, "dx");
@@ -151,7 +161,7 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
   if (bnb_rows > 0) {
     need_bf16_nhwc(*bnb_y, "bnb_y");
     TORCH_CHECK(bnb_y->sizes() == dx.sizes(), "bnb_y: the BN input, shaped like dx");
-    TORCH_CHECK(bnb_mode >= 0 && bnb_mode <= 2, "bnb_mode: 0, 1 or 2");
+    TORCH_CHECK(bnb_mode >= 0 && bnb_mode <= 4 && bnb_mode != 3, "bnb_mode: 0, 1, 2 or 4");
     TORCH_CHECK(bnb_slab.has_value(), "bnb_slab required");
     need_f32(*bnb_slab, "bnb_slab", bnb_rows * 2 * Cin);
     need_f32(*bnb_mean, "bnb_mean", Cin);
@@ -165,6 +175,12 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
       need_bf16_nhwc(*bnb_out, "bnb_out");
       TORCH_CHECK(bnb_out->sizes() == dx.sizes());
       bnb.out = bp(*bnb_out);
+    }
+    if (bnb_mode == 4) {
+      TORCH_CHECK(bnb_mask.has_value() && bnb_mask->is_cuda() && bnb_mask->scalar_type() == at::kByte &&
+                  bnb_mask->is_contiguous() && bnb_mask->numel() == dx.numel() / 8,
+                  "bnb_mode 4 needs the uint8 1-bit mask of the BN output");
+      bnb.mask = (const unsigned char*)bnb_mask->data_ptr();
     }
     if (bnb_mode == 2) {
       need_f32(*bnb_scale, "bnb_scale", Cin);
@@ -388,6 +404,53 @@ int64_t bn_bwd_work(int64_t M, int64_t C) { return (int64_t)dm::bn_bwd_groups(M,
 // mode: 0 no ReLU, 1 mask from `out`, 2 mask from y*scale+shift, 3 (stem) dz gathered
 // from the following max-pool's gradient (pdy, pidx; pool K/S/P) with mask from y, 4 mask
 // from the 1-bit (out > 0) mask that bn_apply wrote in the forward.
+// Stem backward without the full-resolution dy: BN-backward coefficients from the pooled-
+// domain sums (pre_slab, bn_bwd_reduce_masked), then the fused gather + apply + s2d weight
+// gradient (conv_stem.hip) into slab, then the fixed-order reduce into dw [Cout][Cin][7][7].
+bool stem_bwd_fused_supported(at::Tensor y, at::Tensor xs) {
+  return y.dim() == 4 && xs.dim() == 4 && y.size(0) == xs.size(0) && y.size(1) == xs.size(1) &&
+         y.size(2) == xs.size(2) &&
+         dm::stem_wgrad_fused_supported(y.size(0), y.size(1), y.size(2), y.size(3), xs.size(3));
+}
+
+int64_t stem_bwd_slab_floats(int64_t N, int64_t H) {
+  return (int64_t)dm::stem_wgrad_fused_blocks((int)N, (int)H) * 64 * 256;
+}
+
+void stem_bwd_fused(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma,
+                    at::Tensor dgamma, at::Tensor dbeta, double gbeta, at::Tensor scale,
+                    at::Tensor shift, at::Tensor pdy, at::Tensor pidx, at::Tensor pre_slab,
+                    int64_t pre_rows, at::Tensor xs, int64_t Cin, at::Tensor dw, double wbeta,
+                    at::Tensor work, at::Tensor slab) {
+  need_bf16_nhwc(y, "y");
+  need_bf16_nhwc(xs, "xs");
+  need_bf16_nhwc(pdy, "pdy");
+  TORCH_CHECK(stem_bwd_fused_supported(y, xs), "stem_bwd_fused: unsupported shape");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  TORCH_CHECK(pdy.size(0) == N && pdy.size(1) == H / 2 && pdy.size(2) == W / 2 && pdy.size(3) == C,
+              "pdy must be the 3x3/s2/p1 pooled gradient");
+  TORCH_CHECK(pidx.is_cuda() && pidx.scalar_type() == at::kByte && pidx.is_contiguous() &&
+              pidx.numel() == pdy.numel());
+  const long long M = (long long)N * H * W;
+  need_f32(work, "work", bn_bwd_work(M, C));
+  need_f32(pre_slab, "pre_slab", pre_rows * 2 * C);
+  need_f32(scale, "scale", C);
+  need_f32(shift, "shift", C);
+  need_f32(dw, "dw", (int64_t)C * Cin * 49);
+  const int S = dm::stem_wgrad_fused_blocks(N, H);
+  need_f32(slab, "slab", (int64_t)S * 64 * 256);
+  const DeviceGuard guard(y.device());
+  auto st = cur_stream();
+  // mode 3, dy = nullptr: finalize only; with pre_part the coefficients land at work[0, 3C)
+  dm::bn_backward(nullptr, nullptr, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
+                  (float)gbeta, M, C, 3, fp(scale), fp(shift), bp(pdy),
+                  (const uint8_t*)pidx.data_ptr(), H, W, H / 2, W / 2, 3, 2, 1, nullptr, nullptr,
+                  fp(work), st, fp(pre_slab), (int)pre_rows, nullptr);
+  dm::stem_wgrad_fused(bp(xs), bp(y), bp(pdy), (const uint8_t*)pidx.data_ptr(), fp(work),
+                       fp(scale), fp(shift), fp(slab), N, H, W, S, st);
+  dm::wgrad_reduce_s2d(fp(slab), S, C, (int)Cin, xs.size(3), fp(dw), (float)wbeta, st);
+}
+
 void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, at::Tensor y,
                  at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
                  at::Tensor dbeta, double gbeta, int64_t mode, c10::optional<at::Tensor> scale,
@@ -558,7 +621,8 @@ void register_resnet(pybind11::module_& m) {
         py::arg("bnb_y") = py::none(), py::arg("bnb_out") = py::none(),
         py::arg("bnb_mean") = py::none(), py::arg("bnb_invstd") = py::none(),
         py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(),
-        py::arg("bnb_mode") = 0, py::arg("bnb_slab") = py::none());
+        py::arg("bnb_mode") = 0, py::arg("bnb_slab") = py::none(),
+        py::arg("bnb_mask") = py::none());
   m.def("dgrad_bnb_rows", &dgrad_bnb_rows);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
@@ -575,6 +639,13 @@ void register_resnet(pybind11::module_& m) {
   m.def("bn_apply", &bn_apply, py::arg("y"), py::arg("res"), py::arg("scale"), py::arg("shift"),
         py::arg("out"), py::arg("relu"), py::arg("mask") = py::none());
   m.def("bn_bwd_work", &bn_bwd_work);
+  m.def("stem_bwd_fused_supported", &stem_bwd_fused_supported);
+  m.def("stem_bwd_slab_floats", &stem_bwd_slab_floats);
+  m.def("stem_bwd_fused", &stem_bwd_fused, py::arg("y"), py::arg("mean"), py::arg("invstd"),
+        py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("scale"),
+        py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("pre_slab"), py::arg("pre_rows"),
+        py::arg("xs"), py::arg("Cin"), py::arg("dw"), py::arg("wbeta"), py::arg("work"),
+        py::arg("slab"));
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
         py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none());
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("y"), py::arg("scale"), py::arg("shift"),

@@ -1004,6 +1004,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   }
   bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C, (double)M, gamma,
                                                         mean, invstd, dgamma, dbeta, gbeta, coef);
+  if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;

@@ -30,7 +30,8 @@ struct ConvGeom {
 //     Σ dz,  Σ dz·(y - mean)·invstd       dz = dout masked by the BN's ReLU
 // into the stats slab rows (the layout of the forward statistics), so the BN backward
 // needs no separate reduction pass over dout and y.  mode: 0 no ReLU, 1 mask out > 0
-// (block output with residual), 2 mask y*sc + sh > 0.  y == nullptr: disabled.
+// (block output with residual), 2 mask y*sc + sh > 0, 4 the forward's 1-bit (out > 0) mask
+// (bit j of byte i: channel j of 8-channel chunk i).  y == nullptr: disabled.
 struct BnBwdEpi {
   const unsigned short* y;
   const unsigned short* out;
@@ -39,6 +40,7 @@ struct BnBwdEpi {
   const float* sc;
   const float* sh;
   int mode;
+  const unsigned char* mask;
 };
 
 // several geometries for one launch (selected by blockIdx.z)

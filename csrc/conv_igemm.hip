@@ -1474,6 +1474,17 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
   // 36 / 37: 256-pixel halo tile (2 x 2 waves of 128 x BN/2), BN 128 / 64
   // 38 / 39: 256-pixel halo tile with 4 x 2 waves of 64 x BN/2, BN 128 / 64
+  if (cfg == 60) {  // s2d stem kernel; fallback keeps its 256-row tile (stats rows)
+    if (!bnb && !ADD && stem_conv_supported(g)) return stem_conv(X, Wp, Y, stats, g, st);
+    return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+  }
+  if (cfg == 50 || cfg == 51) {
+    if (conv_h5_supported(g, cfg)) return conv_h5(X, Wp, Y, ADD, stats, g, cfg, st, nullptr, nullptr, bnb);
+    // 50 falls back to the register-staged halo tile with the same 256-row tile (41), so
+    // the stats slab rows (igemm_fwd_rowtile) still match; 51 has no 512-row fallback
+    if (cfg == 51) throw std::runtime_error("igemm_fwd: cfg 51 needs a single-chunk 3x3/s1 shape");
+    cfg = 41;
+  }
   int bn, waves;
   if (halo_cfg(cfg, bn, waves)) {
     if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st, nullptr, nullptr, bnb);
@@ -1518,7 +1529,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { if (cfg == 50 || cfg == 51) return conv_h5_rowtile(cfg); if (cfg == 60) return 256; return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -1,0 +1,455 @@
+// Stem convolution on the space-to-depth input (4x4/s1 taps over 16 channels), gfx950.
+//
+// The ResNet stem (7x7/s2 over RGB) runs as a 4x4/s1 conv over the s2d-packed input
+// [N][112][112][16] (conv_igemm.hip pack_input_s2d): M = N*112*112 output pixels, 64 output
+// channels, K = 16 taps x 16 channels = 256.  The generic implicit-GEMM tiles stage one
+// (4-tap, 16-channel) K-slice of the im2col matrix per step, so every input pixel is fetched
+// 16 times and the weight tile is re-staged 4 times per 128 output pixels.  Here:
+//
+//  * a block owns 256 consecutive output pixels and stages, ONCE, (a) the whole packed weight
+//    matrix [64][256] (32 KB, L2-resident across blocks) and (b) the input halo: the flattened
+//    pixel rows r0-2 .. r1+1 that all 16 taps of the 256 pixels touch (<= 7 x 112 pixels x 32 B);
+//  * each tap is exactly one v_mfma_f32_32x32x16_bf16 k-step (16 channels): per tap a wave
+//    reads its 2 A fragments from the halo at row offset dy*W + dx (out-of-image taps read a
+//    zero row = the conv's zero padding) and 2 B fragments from the resident weights;
+//  * 4 waves x (64 px x 64 ch), 2 x 2 MFMA blocks each, 64 MFMAs per wave, then the shared
+//    tile epilogue (BN statistics from the fp32 tile + coalesced bf16 stores).
+//
+// Bank layout: a weight row is 512 B (32 16-B chunks), so the 16-B chunk index is XORed with
+// (row & 15): the 32 lanes of a B-fragment read (32 rows, same k) hit 16 distinct slots per
+// 16-lane group.  A halo pixel is 32 B (two 16-B halves); its halves are swapped when
+// (pixel >> 3) & 1, so 16 consecutive pixels reading the same half cover all 16 slots.
+#include "common.h"
+#include "conv_geom.h"
+#include "igemm_common.h"
+#include "kernels.h"
+
+namespace dm {
+
+namespace {
+constexpr int SBM = 256;        // output pixels per block
+constexpr int SC = 16;          // input channels (s2d: 4 x RGB padded to 16)
+constexpr int SCO = 64;         // output channels
+constexpr int SK = 256;         // K = 16 taps x 16 channels
+constexpr int SHP = 8 * 112;    // halo pixel capacity (W = 112: <= 4 + 3 rows; smaller W: more rows)
+constexpr unsigned SOOB = 0x80000000u;
+
+__device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ (row & 15); }
+__device__ __forceinline__ int hswz(int pix, int half) { return half ^ ((pix >> 3) & 1); }
+
+__global__ void __launch_bounds__(256, 2) stem_conv_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
+    float* __restrict__ stats, ConvGeom g, unsigned xbytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem);  // [64][256]
+  bf16_t* Hs = Ws + SCO * SK;                     // [SHP + 1][16], last pixel = zeros
+  int4* taps = reinterpret_cast<int4*>(Hs + (SHP + 1) * SC);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const long long m0 = (long long)blockIdx.x * SBM;
+  const int ntaps = g.nth * g.ntw;
+  const int NHW = g.N * g.H * g.W;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
+    taps[tid] = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * SC,
+                          dy * g.W + dx);
+  }
+  if (tid < 2) *reinterpret_cast<uint4*>(Hs + SHP * SC + tid * 8) = make_uint4(0, 0, 0, 0);
+
+  // halo: flattened rows r0 + dymin .. r1 + dymax (the tap grid's row span)
+  const int dymin = g.dys > 0 ? g.dy0 : g.dy0 + (g.nth - 1) * g.dys;
+  const int dymax = g.dys > 0 ? g.dy0 + (g.nth - 1) * g.dys : g.dy0;
+  const int r0 = (int)fdiv((unsigned)m0, g.wg_mul, g.wg_shr);
+  const long long mlast = (m0 + SBM - 1 < g.M) ? m0 + SBM - 1 : g.M - 1;
+  const int r1 = (int)fdiv((unsigned)mlast, g.wg_mul, g.wg_shr);
+  const int hbase = (r0 + dymin) * g.W;
+  const int hp = (r1 - r0 + 1 + dymax - dymin) * g.W;
+
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  // stage the weights (64 x 32 chunks = 8 per thread) and the halo (2 chunks per pixel)
+  {
+    uint4 wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, row = e >> 5, ch = e & 31;
+      wv[i] = *reinterpret_cast<const uint4*>(Wp + row * SK + ch * 8);
+    }
+    constexpr int HI = (2 * SHP + 255) / 256;
+    uint4 hv[HI];
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int e = tid + 256 * i, pix = e >> 1, half = e & 1;
+      const int gp = hbase + pix;
+      const bool ok = pix < hp && (unsigned)gp < (unsigned)NHW;
+      const unsigned off = ok ? ((unsigned)gp * SC + half * 8) * 2u : SOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      hv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, row = e >> 5, ch = e & 31;
+      *reinterpret_cast<uint4*>(Ws + row * SK + wswz(row, ch) * 8) = wv[i];
+    }
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int e = tid + 256 * i, pix = e >> 1, half = e & 1;
+      if (pix < SHP) *reinterpret_cast<uint4*>(Hs + pix * SC + hswz(pix, half) * 8) = hv[i];
+    }
+  }
+  // per-lane A rows: halo pixel of the zero-offset tap and the pixel coordinates
+  int a_h[2], a_x[2], a_y[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long long m = m0 + wid * 64 + i * 32 + (lane & 31);
+    const unsigned r = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+    a_x[i] = (int)((unsigned)m - r * (unsigned)g.W);
+    const unsigned n = fdiv(r, g.hg_mul, g.hg_shr);
+    a_y[i] = (m < g.M) ? (int)(r - n * (unsigned)g.H) : -(1 << 28);
+    a_h[i] = (int)(m - hbase);
+  }
+  __syncthreads();
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int h = lane >> 5;  // k half: channels 8h..8h+7 of the tap
+  auto frags = [&](int t, bf16x8 (&af)[2], bf16x8 (&bf)[2]) {
+    const int4 tp = taps[t];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bool ok = (unsigned)(a_x[i] + tp.y) < (unsigned)g.W &&
+                      (unsigned)(a_y[i] + tp.x) < (unsigned)g.H;
+      const int pix = ok ? a_h[i] + tp.w : SHP;
+      af[i] = *reinterpret_cast<const bf16x8*>(Hs + pix * SC + hswz(pix, h) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = j * 32 + (lane & 31);
+      bf[j] = *reinterpret_cast<const bf16x8*>(Ws + row * SK + wswz(row, (tp.z >> 3) + h) * 8);
+    }
+  };
+  // 16 taps, fragments of tap t+1 read while tap t's MFMAs issue (static register sets)
+  bf16x8 a0[2], b0[2], a1[2], b1[2];
+  auto mma = [&](const bf16x8 (&af)[2], const bf16x8 (&bf)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  };
+  frags(0, a0, b0);
+#pragma unroll
+  for (int t = 0; t < 16; t += 2) {
+    frags(t + 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a0, b0);
+    if (t + 2 < 16) frags(t + 2, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(a1, b1);
+  }
+  __syncthreads();  // the epilogue reuses the staging LDS
+  mfma_tile_epilogue<SBM, SCO, 4, 1, true, 1>(acc, smem, m0, 0, blockIdx.x, stats, g, Y, nullptr);
+}
+
+// ------------------------------------------------------------------ fused stem backward
+// Weight gradient of the s2d stem with the stem's BatchNorm backward applied on the fly:
+//
+//   dW[co][tap*16 + c] = Σ_m dy[m][co] · xs[m + off(tap)][c]
+//   dy = a·dz + b·y + cc      dz = max-pool gradient gathered at its argmax pixels, masked
+//                              by relu(y·sc + sh) (3x3/s2/p1 pool over even H, W)
+//
+// The unfused path writes dy at full resolution (bn_bwd_apply_quad: read y + pooled grad +
+// codes, write dy) and the wgrad re-reads it; here each block walks image row PAIRS
+// (2 x W pixels = the W/2 pooling quads of one pooled row band), gathers dz for every quad
+// exactly as bn_bwd_apply_quad does (4 pixels share their 4 candidate windows), writes the
+// bf16 dy tile straight into LDS (bit-identical to the unfused dy), stages the 5 input rows
+// the 4x4 taps touch, and reduces over the pair's pixels with v_mfma_f32_16x16x32_bf16 from
+// transposed LDS reads (ds_read_b64_tr_b16), as wgrad_halo.hip.  dy never reaches memory.
+// 8 waves: wave w owns kernel row w & 3 (4 taps) x output channels 32*(w >> 2) .. +31 x 16
+// input channels; one quad item (4 pixels x 8 channels) per thread.  The next row pair's
+// loads are in flight while the current one computes.  One block per CU (512 threads hold
+// the staging registers of a whole row pair); blocks own contiguous ranges of row pairs and
+// write fp32 slabs [block][64][256] (fixed-order reduce after).
+struct StemBwdArgs {
+  const bf16_t* xs;     // [N][H][W][16] s2d input
+  const bf16_t* y;      // [N][H][W][64] raw stem conv output
+  const bf16_t* pdy;    // [N][H/2][W/2][64] max-pool output gradient
+  const uint8_t* pidx;  // argmax codes (kh*3 + kw), same shape
+  const float* coef;    // [3][64] a, b, cc of dy = a·dz + b·y + cc
+  const float* sc;      // forward BN scale / shift (ReLU mask)
+  const float* sh;
+  float* slab;          // [gridDim.x][64][256]
+  int N, H, W;
+  int spb;              // row pairs per block
+};
+
+__device__ __forceinline__ void s_unpack8(const uint4& v, float f[8]) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    f[2 * k] = bf2f((bf16_t)(w[k] & 0xffff));
+    f[2 * k + 1] = bf2f((bf16_t)(w[k] >> 16));
+  }
+}
+
+typedef short s4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ s4v tr_read4(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)p);
+}
+
+constexpr int FW = 112;        // widest row supported (ResNet stem at 224: 112)
+constexpr int FDP = 80;        // dY tile pitch (elements, 160 B rows: conflict-free tr reads)
+constexpr int FR = 2 * FW;     // pixel rows per row pair
+constexpr int FXH = 5 * FW;    // input halo pixels (rows y0-2 .. y0+2)
+
+__global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Ds = reinterpret_cast<bf16_t*>(smem);  // [FR][FDP] dy tile
+  bf16_t* Xs = Ds + FR * FDP;                     // [FXH + 1][16] input halo, last = zeros
+  float* cf = reinterpret_cast<float*>(Xs + (FXH + 1) * SC);  // [5][64] a, b, cc, sc, sh
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int W = a.W, H = a.H, W2 = W >> 1, H2 = H >> 1;
+  const int R = 2 * W, nks = (R + 31) >> 5;
+  const long long total = (long long)a.N * H2;
+  const long long s0 = (long long)blockIdx.x * a.spb;
+  const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
+
+  for (int i = tid; i < FR * FDP / 8; i += 512)
+    reinterpret_cast<uint4*>(Ds)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
+  if (tid < 2) *reinterpret_cast<uint4*>(Xs + FXH * SC + tid * 8) = make_uint4(0, 0, 0, 0);
+  for (int c = tid; c < 64; c += 512) {
+    cf[c] = a.coef[c];
+    cf[64 + c] = a.coef[64 + c];
+    cf[128 + c] = a.coef[128 + c];
+    cf[192 + c] = a.sc[c];
+    cf[256 + c] = a.sh[c];
+  }
+
+  // staging roles: quad item tid (< W2 * 8): quad qb = tid >> 3, channel chunk tid & 7
+  const int chunk = tid & 7, c0 = chunk * 8;
+  const int nitems = W2 * 8;
+  uint4 qy[1][4], qg[1][4];
+  uint2 qi[1][4];
+  bool qok[1][4];
+  constexpr int XI = (2 * FXH + 511) / 512;
+  uint4 xv[XI];
+  auto load = [&](long long s) {
+    const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
+#pragma unroll
+    for (int u = 0; u < 1; ++u) {
+      const int it = tid;
+      if (it >= nitems) continue;
+      const int qb = it >> 3;
+      const long long pix0 = ((long long)n * H + 2 * qa) * W + 2 * qb;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        qy[u][p] = reinterpret_cast<const uint4*>(a.y)[(pix0 + (p >> 1) * W + (p & 1)) * 8 + chunk];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int oh = qa + (w >> 1), ow = qb + (w & 1);
+        qok[u][w] = oh < H2 && ow < W2;
+        const long long o = (((long long)n * H2 + (qok[u][w] ? oh : qa)) * W2 + (qok[u][w] ? ow : qb)) * 8 + chunk;
+        qi[u][w] = reinterpret_cast<const uint2*>(a.pidx)[o];
+        qg[u][w] = reinterpret_cast<const uint4*>(a.pdy)[o];
+      }
+    }
+    const int y0 = 2 * qa;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
+      const int hr = pix / W, x = pix - hr * W;
+      const int yy = y0 - 2 + hr;
+      xv[i] = make_uint4(0, 0, 0, 0);
+      if (pix < 5 * W && yy >= 0 && yy < H)
+        xv[i] = *reinterpret_cast<const uint4*>(a.xs + (((long long)n * H + yy) * W + x) * SC + half * 8);
+    }
+  };
+  // gather dz per quad (bn_bwd_apply_quad's terms, same order), dy to LDS; halo to LDS
+  auto store = [&]() {
+    float ca[8], cb[8], cc[8], ms[8], mh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ca[j] = cf[c0 + j];
+      cb[j] = cf[64 + c0 + j];
+      cc[j] = cf[128 + c0 + j];
+      ms[j] = cf[192 + c0 + j];
+      mh[j] = cf[256 + c0 + j];
+    }
+#pragma unroll
+    for (int u = 0; u < 1; ++u) {
+      const int it = tid;
+      if (it >= nitems) continue;
+      const int qb = it >> 3;
+      float d[4][8];
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[p][j] = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (!qok[u][w]) continue;
+        const int wa = w >> 1, wb = w & 1;
+        float gg[8];
+        s_unpack8(qg[u][w], gg);
+        const uint32_t aw[2] = {qi[u][w].x, qi[u][w].y};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const int ddy = p >> 1, ddx = p & 1;
+          if (wa == 1 && ddy == 0) continue;
+          if (wb == 1 && ddx == 0) continue;
+          const unsigned code = (unsigned)((ddy ? (wa ? 0 : 2) : 1) * 3 + (ddx ? (wb ? 0 : 2) : 1));
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[p][j] += gg[j];
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        float yv[8];
+        s_unpack8(qy[u][p], yv);
+        uint32_t o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float r2[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int j = 2 * k + e;
+            const float dz = (yv[j] * ms[j] + mh[j]) > 0.f ? d[p][j] : 0.f;
+            r2[e] = ca[j] * dz + cb[j] * yv[j] + cc[j];
+          }
+          o[k] = pack_bf2(r2[0], r2[1]);
+        }
+        const int lp = (p >> 1) * W + 2 * qb + (p & 1);
+        *reinterpret_cast<uint4*>(Ds + lp * FDP + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
+      if (pix < 5 * W) *reinterpret_cast<uint4*>(Xs + pix * SC + half * 8) = xv[i];
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // transposed-read roles: rows grp*4 + q (+16) of a 32-row k-step, column quad p
+  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int rbase = grp * 4 + q;
+  const int th = wid & 3;          // kernel row of this wave: dy = th - 2
+  const int cob = (wid >> 2) * 32;  // first output channel of this wave
+
+  if (s0 < s1) load(s0);
+  __syncthreads();  // zeroed tiles, coefficients
+  for (long long s = s0; s < s1; ++s) {
+    store();
+    __syncthreads();
+    const int qa = (int)(s % H2);
+    if (s + 1 < s1) load(s + 1);
+    const int y0 = 2 * qa;
+    for (int ks = 0; ks < nks; ++ks) {
+      int rlo[2], okrow[2], xr[2], rr[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = ks * 32 + rbase + 16 * u;
+        rlo[u] = r;
+        rr[u] = r >= W ? 1 : 0;
+        xr[u] = r - rr[u] * W;
+        okrow[u] = r < R && (unsigned)(y0 + rr[u] + th - 2) < (unsigned)H;
+      }
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const s4v lo = tr_read4(Ds + rlo[0] * FDP + cob + i * 16 + 4 * pp);
+        const s4v hi = tr_read4(Ds + rlo[1] * FDP + cob + i * 16 + 4 * pp);
+        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int tw = 0; tw < 4; ++tw) {
+        const bf16_t* src[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int xx = xr[u] + tw - 2;
+          const bool ok = okrow[u] && (unsigned)xx < (unsigned)W;
+          src[u] = ok ? Xs + ((rr[u] + th) * W + xx) * SC + 4 * pp : Xs + FXH * SC + 4 * pp;
+        }
+        const s4v lo = tr_read4(src[0]);
+        const s4v hi = tr_read4(src[1]);
+        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][tw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][tw], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // every wave done with the tiles before the next store
+  }
+  // slab[b][co][tap*16 + c]; 16x16 C map: col = lane & 15 (channel), row = (lane>>4)*4 + r (co)
+  float* out = a.slab + (long long)blockIdx.x * 64 * SK;
+  const int c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int tw = 0; tw < 4; ++tw)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cob + i * 16 + (lane >> 4) * 4 + r;
+        out[(long long)co * SK + (th * 4 + tw) * SC + c] = acc[i][tw][r];
+      }
+}
+}  // namespace
+
+bool stem_conv_supported(const ConvGeom& g) {
+  if (g.C != SC || g.Ncols != SCO || g.wK != SK || g.nth * g.ntw != 16) return false;
+  if (g.isy != 1 || g.isx != 1 || g.Hg != g.H || g.Wg != g.W || g.OC != SCO) return false;
+  if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31)) return false;
+  const int span = (g.nth - 1) * (g.dys < 0 ? -g.dys : g.dys);
+  // worst-case halo over blocks: a 256-pixel run starting at the last pixel of a row
+  const int rows = (g.W - 1 + SBM - 1) / g.W + 1 + span;
+  return rows * g.W <= SHP && (g.dxs == 1 || g.dxs == -1);
+}
+
+bool stem_wgrad_fused_supported(int N, int H, int W, int C, int Cpad) {
+  return C == 64 && Cpad == SC && H % 2 == 0 && W % 2 == 0 && W <= FW && H >= 2 &&
+         (long long)N * H * W * 64 < (1LL << 31);
+}
+
+int stem_wgrad_fused_blocks(int N, int H) {
+  const long long pairs = (long long)N * (H / 2);
+  // one block per CU; each block's slab is 64 KB
+  long long b = pairs < 256 ? pairs : 256;
+  const long long spb = (pairs + b - 1) / b;
+  return (int)((pairs + spb - 1) / spb);
+}
+
+void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
+                      const float* coef, const float* sc, const float* sh, float* slab, int N,
+                      int H, int W, int S, hipStream_t st) {
+  const long long pairs = (long long)N * (H / 2);
+  StemBwdArgs a{xs, y, pdy, pidx, coef, sc, sh, slab, N, H, W, (int)((pairs + S - 1) / S)};
+  const size_t sm = (size_t)FR * FDP * 2 + (size_t)(FXH + 1) * SC * 2 + 5 * 64 * 4;
+  set_smem_attr(stem_wgrad_fused_kernel, sm);
+  stem_wgrad_fused_kernel<<<S, 512, sm, st>>>(a);
+  DM_CHECK(hipGetLastError());
+}
+
+void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const ConvGeom& g,
+               hipStream_t st) {
+  const size_t main = (size_t)SCO * SK * 2 + (size_t)(SHP + 1) * SC * 2 + MAXTAPS * 16;
+  const size_t epi = (size_t)SBM * (SCO + 4) * 4;
+  const size_t sm = main > epi ? main : epi;
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  set_smem_attr(stem_conv_kernel, sm);
+  // each wave's column of the MFMA epilogue needs rows >= M zeroed for the stats: the A rows
+  // of pixels past M are never valid (a_y poisoned), so their accumulators stay 0
+  stem_conv_kernel<<<(unsigned)((g.M + SBM - 1) / SBM), 256, sm, st>>>(X, Wp, Y, stats, g, xb);
+  DM_CHECK(hipGetLastError());
+}
+
+}  // namespace dm

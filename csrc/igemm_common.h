@@ -63,6 +63,7 @@ using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 // Rows >= g.M must hold zeros when stats are requested.  Requires (BM/PASSES)*(BN+4)*4 B of
 // LDS: with PASSES > 1 the tile is staged one band of BM/PASSES rows (whole wave rows) at a time.
 //  * optional BN-backward sums (bnb.y set; stats then receives Σdz, Σdz·x̂ — see BnBwdEpi)
+// LDS for the BN-backward combine: NT*16 + 2*BN*SPL floats (within the staging tile size)
 template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1>
 __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / WM / (MF32 ? 32 : 16)][BN / WN / (MF32 ? 32 : 16)],
                                                    unsigned char* smem, long long m0, int n0,
@@ -141,8 +142,22 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       bsh[j] = okc && bnb.mode == 2 ? bnb.sh[bcol + j] : 0.f;
     }
   }
-#pragma unroll
-  for (int pb = 0; pb < PASSES; ++pb) {
+  constexpr int ITERS = RPB * CPR / NT;
+  static_assert(ITERS * NT == RPB * CPR, "rows per band divisible by the block");
+  const int cc = tid % CPR;
+  const int col = n0 + cc * 8;
+  // output offset of row `row` of band pb (and whether it is a real output)
+  auto row_off = [&](int pb, int row, long long& o, bool& ok) {
+    const long long m = m0 + pb * RPB + row;
+    ok = m < g.M && col < g.Ncols;
+    const long long mm = ok ? m : m0;
+    const unsigned t = fdiv((unsigned)mm, g.wg_mul, g.wg_shr);
+    const int x = (int)((unsigned)mm - t * (unsigned)g.Wg);
+    const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+    const int y = (int)(t - n * (unsigned)g.Hg);
+    o = (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+  };
+  auto stage_band = [&](int pb) {
     if (PASSES > 1) __syncthreads();  // previous band's LDS reads done
     if (wm * TM >= pb * RPB && wm * TM < (pb + 1) * RPB) {
 #pragma unroll
@@ -154,58 +169,82 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
             cs[(wm * TM - pb * RPB + i * FM + frow(r)) * LDC + wn * TN + j * FM + fcol] = acc[i][j][r];
     }
     __syncthreads();
-    // rows in groups of UNR: every global load of a group (ADD, and y / out for the
-    // BN-backward sums) is issued before its first store, so they overlap
-    constexpr int ITERS = RPB * CPR / NT;
-    static_assert(ITERS * NT == RPB * CPR, "rows per band divisible by the block");
+  };
+  auto tile_vals = [&](int row, const uint4& a, float (&v)[8]) {
+    const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
+    const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
+    v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
+    v[4] = v1.x; v[5] = v1.y; v[6] = v1.z; v[7] = v1.w;
+    if (ADD) {
+      const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
+        v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+      }
+    }
+  };
+  if (!bwd) {
+    // plain store phase: the ADD loads of ALL bands are issued before the first accumulator
+    // goes to LDS, so their latency overlaps the staging instead of being exposed per row
+    // group (the main loop's staging registers are dead here: no rise in the kernel's peak)
+    constexpr int NLD = PASSES * ITERS;
+    long long o[NLD];
+    bool ok[NLD];
+    uint4 av[NLD];
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {
+      row_off(k / ITERS, (tid + (k % ITERS) * NT) / CPR, o[k], ok[k]);
+      av[k] = make_uint4(0, 0, 0, 0);
+      if (ADD && ok[k]) av[k] = *reinterpret_cast<const uint4*>(ADD + o[k]);
+    }
+#pragma unroll
+    for (int pb = 0; pb < PASSES; ++pb) {
+      stage_band(pb);
+#pragma unroll
+      for (int i = 0; i < ITERS; ++i) {
+        const int k = pb * ITERS + i;
+        if (!ok[k]) continue;
+        float v[8];
+        tile_vals((tid + i * NT) / CPR, av[k], v);
+        *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                                         pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+      }
+    }
+  } else {
+    // BN-backward sums: rows in groups of UNR, every load of a group (ADD, y, and the ReLU
+    // mask source) issued before its first store
     constexpr int UNR = ITERS < 4 ? ITERS : 4;
     static_assert(ITERS % UNR == 0, "row groups");
-    const int cc = tid % CPR;
-    const int col = n0 + cc * 8;
 #pragma unroll
-    for (int i0 = 0; i0 < ITERS; i0 += UNR) {
-      long long o[UNR];
-      bool ok[UNR];
-      uint4 av[UNR], yv[UNR], ov[UNR];
+    for (int pb = 0; pb < PASSES; ++pb) {
+      stage_band(pb);
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        const int row = (tid + (i0 + u) * NT) / CPR;
-        const long long m = m0 + pb * RPB + row;
-        ok[u] = m < g.M && col < g.Ncols;
-        const long long mm = ok[u] ? m : m0;
-        const unsigned t = fdiv((unsigned)mm, g.wg_mul, g.wg_shr);
-        const int x = (int)((unsigned)mm - t * (unsigned)g.Wg);
-        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
-        const int y = (int)(t - n * (unsigned)g.Hg);
-        o[u] = (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
-        av[u] = yv[u] = ov[u] = make_uint4(0, 0, 0, 0);
-        if (ok[u]) {
-          if (ADD) av[u] = *reinterpret_cast<const uint4*>(ADD + o[u]);
-          if (bwd) {
+      for (int i0 = 0; i0 < ITERS; i0 += UNR) {
+        long long o[UNR];
+        bool ok[UNR];
+        uint4 av[UNR], yv[UNR], ov[UNR];
+        uint32_t mk[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          row_off(pb, (tid + (i0 + u) * NT) / CPR, o[u], ok[u]);
+          av[u] = yv[u] = ov[u] = make_uint4(0, 0, 0, 0);
+          mk[u] = 0;
+          if (ok[u]) {
+            if (ADD) av[u] = *reinterpret_cast<const uint4*>(ADD + o[u]);
             yv[u] = *reinterpret_cast<const uint4*>(bnb.y + o[u]);
             if (bnb.mode == 1) ov[u] = *reinterpret_cast<const uint4*>(bnb.out + o[u]);
+            if (bnb.mode == 4) mk[u] = bnb.mask[o[u] >> 3];
           }
         }
-      }
 #pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        if (!ok[u]) continue;
-        const int row = (tid + (i0 + u) * NT) / CPR;
-        const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
-        const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
-        float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        if (ADD) {
-          const uint32_t aw[4] = {av[u].x, av[u].y, av[u].z, av[u].w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
-            v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
-          }
-        }
-        const uint4 packed = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                        pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
-        *reinterpret_cast<uint4*>(Y + o[u]) = packed;
-        if (bwd) {
+        for (int u = 0; u < UNR; ++u) {
+          if (!ok[u]) continue;
+          float v[8];
+          tile_vals((tid + (i0 + u) * NT) / CPR, av[u], v);
+          const uint4 packed = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                          pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+          *reinterpret_cast<uint4*>(Y + o[u]) = packed;
           // sums over the values as stored (bf16), exactly what a separate pass would read
           const uint32_t pw[4] = {packed.x, packed.y, packed.z, packed.w};
           const uint32_t yw[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
@@ -217,6 +256,7 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
             const float yf = bf2f((bf16_t)(yw[j >> 1] >> sh16));
             if (bnb.mode == 1) d = bf2f((bf16_t)(ow[j >> 1] >> sh16)) > 0.f ? d : 0.f;
             else if (bnb.mode == 2) d = yf * bsc[j] + bsh[j] > 0.f ? d : 0.f;
+            else if (bnb.mode == 4) d = (mk[u] >> j) & 1u ? d : 0.f;
             bs_[j] += d;
             bq_[j] += d * (yf - bmu[j]) * bis[j];
           }
@@ -234,18 +274,28 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       rb[tid * 16 + 8 + j] = bq_[j];
     }
     __syncthreads();
+    // two levels, both in a fixed order: SPL threads per column each sum RL/SPL rows, then
+    // one thread per column sums the SPL partials (a serial RL-long LDS chain per column was
+    // the epilogue's tail)
     constexpr int RL = NT / CPR;
-    for (int c = tid; c < BN; c += NT) {
+    constexpr int SPL = (NT / (2 * BN)) < 1 ? 1 : ((NT / (2 * BN)) > RL ? RL : (NT / (2 * BN)));
+    static_assert(RL % SPL == 0, "combine split");
+    float* rp = rb + NT * 16;  // [2 * BN][SPL] partials
+    for (int e = tid; e < 2 * BN * SPL; e += NT) {
+      const int cq = e / SPL, part = e % SPL;
+      const int c = cq >> 1, which = cq & 1;
       const int grp = c >> 3, j = c & 7;
-      float a0 = 0.f, a1 = 0.f;
-      for (int r = 0; r < RL; ++r) {
-        a0 += rb[(r * CPR + grp) * 16 + j];
-        a1 += rb[(r * CPR + grp) * 16 + 8 + j];
-      }
-      if (n0 + c < g.Ncols) {
-        stats[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = a0;
-        stats[((long long)stat_row * 2 + 1) * g.Ncols + n0 + c] = a1;
-      }
+      float a = 0.f;
+      for (int r = part * (RL / SPL); r < (part + 1) * (RL / SPL); ++r)
+        a += rb[(r * CPR + grp) * 16 + which * 8 + j];
+      rp[e] = a;
+    }
+    __syncthreads();
+    for (int cq = tid; cq < 2 * BN; cq += NT) {
+      const int c = cq >> 1, which = cq & 1;
+      float a = 0.f;
+      for (int part = 0; part < SPL; ++part) a += rp[cq * SPL + part];
+      if (n0 + c < g.Ncols) stats[((long long)stat_row * 2 + which) * g.Ncols + n0 + c] = a;
     }
   }
 }

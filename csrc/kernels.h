@@ -65,6 +65,22 @@ bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb = nullptr);
+// conv_stem.hip: s2d stem (16 channels, 16 taps, 64 outputs) with resident weights (cfg 60)
+bool stem_conv_supported(const ConvGeom& g);
+void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const ConvGeom& g,
+               hipStream_t st);
+// fused stem BN backward (quad max-pool gather) + s2d weight gradient -> slabs [S][64][256]
+bool stem_wgrad_fused_supported(int N, int H, int W, int C, int Cpad);
+int stem_wgrad_fused_blocks(int N, int H);
+void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
+                      const float* coef, const float* sc, const float* sh, float* slab, int N,
+                      int H, int W, int S, hipStream_t st);
+// conv_h5.hip: LDS-DMA halo conv (cfg 50: 256 px x 128 ch, 51: 512 px x 64 ch single chunk)
+bool conv_h5_supported(const ConvGeom& g, int cfg);
+int conv_h5_rowtile(int cfg);
+void conv_h5(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+             const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
+             const float* pre_sh = nullptr, const BnBwdEpi* bnb = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,

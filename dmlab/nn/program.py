@@ -319,7 +319,10 @@ class Program(nn.Module):
         dev = torch.cuda.current_device()
         st = self._side_streams.get(dev)
         if st is None:
-            st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
+            # DMLAB_WGRAD_PRIO: stream priority of the side stream (lower = higher priority);
+            # the weight gradients have slack until the end of backward, the main chain does not
+            prio = int(os.environ.get("DMLAB_WGRAD_PRIO", "0"))
+            st = self._side_streams[dev] = torch.cuda.Stream(device=dev, priority=prio)
         return st
 
     def prepare_native(self, x):

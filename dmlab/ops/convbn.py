@@ -44,6 +44,7 @@ def _cpad(c):
 #     v3 tiles 15 / 13 / 11 by the block-count rule below; 256-row tiles lose
 #     (one workgroup per CU exposes the staging latency).
 TILE_CFG = (15, 13, 11)
+_STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
 
 
 def pick_cfg(M, ncols, k=0, stride=0, cin=0):
@@ -227,9 +228,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     if wf is None:
         wf, _ = packed_weights(layer, need_wd=train and not first)
     y = empty_nhwc(N, OH, OW, cout, x)
-    # s2d stem: the 128x64 v3 tile with two K-tiles of register prefetch (16) runs 382 vs
-    # 336 TFLOP/s for the single-prefetch tile (13) at batch 512 (profiles/conv_stem_s2d_r1s4.jsonl)
-    cfg = 16 if s2d else pick_cfg(M, cout, k, s, C)
+    # s2d stem: the resident-weight stem kernel (60, csrc/conv_stem.hip) stages the weights
+    # and the input halo once per 256 pixels (the v3 128x64 tile, 16, re-stages one 4-tap
+    # K-slice per step: 382 TFLOP/s at batch 512, profiles/conv_stem_s2d_r1s4.jsonl)
+    cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
         if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43):
@@ -295,6 +297,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
 # e.g. layer1 dgrad 84 -> 139 us.  Kept for A/B runs: DMLAB_FUSE_BN_BWD=1.
 _FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
 
+# Stem backward: BN-backward apply fused into the s2d weight gradient (DMLAB_FUSED_STEM=0:
+# the separate quad apply pass + igemm wgrad, kept for A/B runs)
+_FUSED_STEM = os.environ.get("DMLAB_FUSED_STEM", "1") == "1"
+
 # Weight gradients of convs with at least this many output channels go to the Program's
 # side stream (DMLAB_WGRAD_STREAM_MIN_COUT; 0 = all).
 _SIDE_MIN_COUT = int(os.environ.get("DMLAB_WGRAD_STREAM_MIN_COUT", "0"))
@@ -306,11 +312,16 @@ def bnb_spec(layer, ctx):
     or None when that BN's backward cannot use them (stem pool gather, eval mode)."""
     if getattr(layer, "pool_k", 0) or ctx.get("mean") is None or "y" not in ctx:
         return None
-    mode = 1 if ctx["has_res"] else (2 if layer.relu else 0)
+    if ctx["has_res"]:
+        # ReLU mask of a residual BN: the forward's 1-bit mask (4) or the saved output (1)
+        mode = 4 if ctx.get("mask") is not None else 1
+    else:
+        mode = 2 if layer.relu else 0
     return dict(bnb_y=ctx["y"], bnb_out=ctx.get("out") if mode == 1 else None,
                 bnb_mean=ctx["mean"], bnb_invstd=ctx["invstd"],
                 bnb_scale=ctx["scale"] if mode == 2 else None,
-                bnb_shift=ctx["shift"] if mode == 2 else None, bnb_mode=mode)
+                bnb_shift=ctx["shift"] if mode == 2 else None, bnb_mode=mode,
+                bnb_mask=ctx.get("mask") if mode == 4 else None)
 
 
 def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=None):
@@ -330,8 +341,6 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     k, s, p = (4, 1, 2) if s2d else (layer.k, layer.stride, layer.padding)
     acc = 1.0 if layer.accumulate else 0.0
     dout = dout.contiguous()
-    dy = empty_nhwc(N, OH, OW, cout, y)
-    dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
     pre_sums = {}
     zs = ctx.pop("dz_stats", None)
@@ -347,6 +356,19 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
         rows = L.bn_bwd_reduce_masked(dout, ctx["yarg"], ctx["mean"], ctx["invstd"], ctx["scale"],
                                       ctx["shift"], part)
         pre_sums = dict(pre_slab=part, pre_rows=rows)
+    if (pool and _FUSED_STEM and s2d and pre_sums and ctx["first"] and not ctx["has_res"]
+            and L.stem_bwd_fused_supported(y, x)):
+        # stem: BN-backward apply fused into the s2d weight gradient -- the full-resolution
+        # dy is never written (csrc/conv_stem.hip stem_wgrad_fused_kernel)
+        slab = torch.empty(L.stem_bwd_slab_floats(N, OH), device=y.device, dtype=torch.float32)
+        L.stem_bwd_fused(y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
+                         layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
+                         ctx["scale"], ctx["shift"], dout, ctx["idx"], pre_sums["pre_slab"],
+                         pre_sums["pre_rows"], x, layer.cin, layer.grad_slot("weight"), acc,
+                         work, slab)
+        return None
+    dy = empty_nhwc(N, OH, OW, cout, y)
+    dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     if pool:
         mode = 3       # dz gathered from the max-pool gradient, ReLU mask from y
     elif not layer.relu:

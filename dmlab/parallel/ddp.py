@@ -17,9 +17,11 @@ task3/dist_utils.py:40-46).  Here:
   the 1/ws factor is either folded into the fused optimiser (``fold_average_into``,
   zero extra passes) or applied per bucket.
 * Bucket size: on MI355X a ring all-reduce is bound by one xGMI link per GPU
-  (~153 GB/s of the 7), so buckets are sized large (default 25 MB fp32; ResNet-18
-  = 2 buckets) to amortise RCCL launch latency; the first bucket is capped
-  smaller (``first_bucket_mb``) so communication starts early in backward.
+  (~153 GB/s of the 7), so buckets are sized large (default 25 MB fp32) to amortise
+  RCCL launch latency; the first bucket is capped smaller (``first_bucket_mb``) so
+  communication starts early in backward, and the LAST one too (``last_bucket_mb``):
+  it can only launch when backward's final layers are done, so all of it is exposed —
+  only the first layers' few gradients should wait for the end of backward.
 * Optional bf16 gradient communication (``comm_dtype=torch.bfloat16``) halves
   the bytes on the links.
 * ``small_allreduce="xgmi"``: buckets of at most ``small_cap_mb`` go through the
@@ -60,7 +62,8 @@ class _Bucket:
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, bucket_cap_mb: float = 25.0,
-                 first_bucket_mb: float = 4.0, comm_dtype=None, broadcast_init: bool = True,
+                 first_bucket_mb: float = 4.0, last_bucket_mb: float = 2.0, comm_dtype=None,
+                 broadcast_init: bool = True,
                  process_group=None, average: bool = True, small_allreduce: str | None = None,
                  small_cap_mb: float = 4.0, native: bool | None = None, xgmi_algo: str = "auto"):
         super().__init__()
@@ -72,6 +75,7 @@ class DistributedDataParallel(nn.Module):
         self._use_avg = avg_supported() if self.ws > 1 else False
         self._fold = False  # 1/ws folded into the optimiser
         self.program = module if hasattr(module, "register_grad_hook") else None
+        self._last_mb = last_bucket_mb
         if broadcast_init and self.ws > 1:
             init_parameters(module)
         if self.program is not None:
@@ -140,7 +144,7 @@ class DistributedDataParallel(nn.Module):
         self._py_launched = v
 
     # ------------------------------------------------------------------ layout
-    def _make_buckets(self, sizes, cap, first):
+    def _make_buckets(self, sizes, cap, first, last_cap=None):
         """sizes: per-param padded (offset, numel) in flat order -> buckets of ids."""
         buckets, cur, lo, acc = [], [], None, 0
         limit = first
@@ -154,6 +158,22 @@ class DistributedDataParallel(nn.Module):
                 cur, lo, limit = [], None, cap
         if cur:
             buckets.append(_Bucket(lo, sizes[cur[-1]][2], cur))
+        # the LAST bucket launches when backward's final layers are done, so all of it is
+        # exposed communication: cap it (split at a parameter boundary) so only the first
+        # layers' few gradients wait for the end of backward
+        last = buckets[-1] if buckets else None
+        limit_last = last_cap
+        if last is not None and limit_last and len(last.params) > 1 and \
+                last.hi - last.lo > limit_last:
+            keep = list(last.params)
+            split = len(keep)
+            while split > 1 and sizes[keep[-1]][2] - sizes[keep[split - 1]][0] <= limit_last:
+                split -= 1
+            split = max(split, 1)
+            if split < len(keep):
+                head, tl = keep[:split], keep[split:]
+                buckets[-1] = _Bucket(last.lo, sizes[tl[0]][0], head)
+                buckets.append(_Bucket(sizes[tl[0]][0], last.hi, tl))
         return buckets
 
     def _setup_program(self, cap_mb, first_mb):
@@ -166,7 +186,8 @@ class DistributedDataParallel(nn.Module):
             end = flat.offsets[i + 1] if i + 1 < len(flat.params) else flat.numel
             sizes.append((off, p.numel(), end))
         el = 4
-        self.buckets = self._make_buckets(sizes, cap_mb * 2**20 / el, first_mb * 2**20 / el)
+        self.buckets = self._make_buckets(sizes, cap_mb * 2**20 / el, first_mb * 2**20 / el,
+                                          self._last_mb * 2**20 / el)
         self._bucket_of = {}
         for b in self.buckets:
             for i in b.params:
@@ -191,7 +212,8 @@ class DistributedDataParallel(nn.Module):
         sizes = [(offs[i], p.numel(), offs[i + 1] if i + 1 < len(params) else off)
                  for i, p in enumerate(params)]
         el = self.grad_buf.element_size()
-        self.buckets = self._make_buckets(sizes, cap_mb * 2**20 / el, first_mb * 2**20 / el)
+        self.buckets = self._make_buckets(sizes, cap_mb * 2**20 / el, first_mb * 2**20 / el,
+                                          self._last_mb * 2**20 / el)
         self._bucket_of = {}
         for b in self.buckets:
             for i in b.params:

@@ -69,6 +69,43 @@ def test_conv_fwd_halo(dev, geom, cfg):
     _check_fwd(dev, geom, cfg)
 
 
+def _h5_skip(cfg, cin_gemm):
+    # cfg 51 (512-pixel, single 64-channel chunk) has no fallback for other channel counts
+    if cfg == 51 and cin_gemm != 64:
+        pytest.skip("cfg 51 needs a single 64-channel chunk")
+
+
+H5_GEOMS = HALO_GEOMS + [GEOMS[0], GEOMS[3], (4, 56, 64, 64, 3, 1, 1), (2, 7, 512, 512, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geom", H5_GEOMS)
+@pytest.mark.parametrize("cfg", [50, 51])
+def test_conv_fwd_h5(dev, geom, cfg):
+    """LDS-DMA halo kernel (conv_h5.hip): 256 x 128 and 512 x 64 tiles, 1x1 and 3x3 taps,
+    several chunks (double-buffered halo), blocks crossing images, partial last block."""
+    _h5_skip(cfg, geom[2])
+    _check_fwd(dev, geom, cfg)
+
+
+@pytest.mark.parametrize("geom", H5_GEOMS)
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("cfg", [50, 51])
+def test_conv_dgrad_h5(dev, geom, accumulate, cfg):
+    _h5_skip(cfg, geom[3])
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    wb = w.bfloat16().float()
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wb, dy.float(), s, p)
+    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    base = dx.clone()
+    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, cfg)
+    if accumulate:
+        ref = ref + _nchw(base).float()
+    assert _rel(_nchw(dx), ref) < 6e-3
+
+
 def _check_fwd(dev, geom, cfg):
     N, H, Cin, Cout, k, s, p = geom
     if cfg in (0, 3, 6, 9, 12, 15, 18, 26, 34, 36, 38) and Cout % 128:
@@ -255,9 +292,11 @@ def test_maxpool_avgpool(dev):
     assert _rel(dxa, ref) < 5e-3
 
 
-@pytest.mark.parametrize("H", [32, 224])
-def test_stem_space_to_depth(dev, H):
-    """7x7/s2/p3 stem == 4x4/s1 conv over the space-to-depth packed input."""
+@pytest.mark.parametrize("H", [32, 224, 18])
+@pytest.mark.parametrize("fcfg", [16, 60])
+def test_stem_space_to_depth(dev, H, fcfg):
+    """7x7/s2/p3 stem == 4x4/s1 conv over the space-to-depth packed input (cfg 60: the
+    resident-weight stem kernel, csrc/conv_stem.hip; H=18: a partial last block)."""
     N, C, Co = 2, 3, 64
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.randn(N, C, H, H, device=dev, generator=g).bfloat16()
@@ -268,8 +307,14 @@ def test_stem_space_to_depth(dev, H):
     lib().pack_weights_s2d(w.contiguous(), wf)
     ref = F.conv2d(x.float(), w.bfloat16().float(), None, 2, 3)
     y = torch.empty(N, H // 2, H // 2, Co, device=dev, dtype=torch.bfloat16)
-    lib().conv_fwd(xs, wf, y, None, None, 4, 4, 1, 2, pick_cfg(N * (H // 2) ** 2, Co))
+    M = N * (H // 2) ** 2
+    T = lib().conv_stats_rows(M, fcfg)
+    stats = torch.empty(T * 2 * Co, device=dev)
+    lib().conv_fwd(xs, wf, y, stats, None, 4, 4, 1, 2, fcfg)
     assert _rel(_nchw(y), ref) < 6e-3
+    st = stats.view(T, 2, Co).sum(0)
+    torch.testing.assert_close(st[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
+    torch.testing.assert_close(st[1], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
     dy = torch.randn_like(ref).bfloat16()
     dref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), 2, 3)
     for S, cfg in ((1, 3), (4, 3)):
@@ -371,11 +416,12 @@ def test_bn_stats_finalize_slab_rows(dev, T):
     torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-6)
 
 
-@pytest.mark.parametrize("geom", [g for g in HALO_GEOMS if g[4] == 3])
-@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43])
+@pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3])
+@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 50, 51])
 def test_conv_fwd_prebn(dev, geom, cfg):
     """Halo conv consuming relu(y*scale + shift) of a RAW previous-conv output (fused
     BN-apply + ReLU in the staging); zero padding stays zero after the BN."""
+    _h5_skip(cfg, geom[2])
     N, H, Cin, Cout, k, s, p = geom
     g = torch.Generator(device=dev).manual_seed(2)
     y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
@@ -443,9 +489,9 @@ def test_pack_weights_tiled_matches_per_layer(dev):
 @pytest.mark.parametrize("geom", [(3, 14, 128, 128, 3, 1, 1), (2, 14, 64, 128, 3, 2, 1),
                                   (2, 15, 64, 128, 3, 2, 1), (2, 9, 64, 64, 1, 2, 0),
                                   (2, 7, 128, 256, 3, 1, 1)])
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 4])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 42, 43])
+@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 41, 42, 43, 50])
 def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     """The dgrad epilogue's BN-backward sums (Σdz, Σdz·x̂ of the BN whose input gradient dx
     is) equal the sums over the stored dx; the BN backward run from them equals the
@@ -453,6 +499,8 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     if s == 2 and cfg not in (15, 16):
         pytest.skip("stride-2 dgrad runs on the v3 tiles")
+    if cfg == 50 and Cin % 128:
+        pytest.skip("cfg 50: 128-wide column tile")
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
     OH = (H + 2 * p - k) // s + 1
     g = torch.Generator(device=dev).manual_seed(9)
@@ -464,19 +512,23 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     invstd = torch.rand(Cin, **f) + 0.5
     sc, sh = torch.randn(Cin, **f), torch.randn(Cin, **f)
     dx = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    # the forward's 1-bit ReLU mask of `out` (bit j of byte i: channel j of chunk i)
+    bits = (out.reshape(-1, 8) > 0).to(torch.int32) << torch.arange(8, device=dev, dtype=torch.int32)
+    mask = bits.sum(1).to(torch.uint8)
     L = lib()
     rows = L.dgrad_bnb_rows(N, H, H, s, cfg)
     slab = torch.full((max(rows, 1) * 2 * Cin,), float("nan"), **f)
     r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx if accumulate else None, cfg,
                      bnb_y=y, bnb_out=out, bnb_mean=mean, bnb_invstd=invstd, bnb_scale=sc,
-                     bnb_shift=sh, bnb_mode=mode, bnb_slab=slab)
+                     bnb_shift=sh, bnb_mode=mode, bnb_slab=slab,
+                     bnb_mask=mask if mode == 4 else None)
     if k == 1 and s == 2 and accumulate:
         assert r == 0  # tap-less parity classes keep old values: not fusable
         return
     assert r == rows > 0
     d = dx.float().reshape(-1, Cin)
     yf = y.float().reshape(-1, Cin)
-    if mode == 1:
+    if mode in (1, 4):
         d = torch.where(out.float().reshape(-1, Cin) > 0, d, torch.zeros_like(d))
     elif mode == 2:
         d = torch.where(yf * sc + sh > 0, d, torch.zeros_like(d))
@@ -495,7 +547,7 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
         kw = dict(pre_slab=slab, pre_rows=r) if pre else {}
         L.bn_backward(dx, out if mode == 1 else None, y, mean, invstd, gamma, dg, db, 0.0, mode,
                       sc if mode == 2 else None, sh if mode == 2 else None, None, None, 3, 2, 1,
-                      dyy, None, work, **kw)
+                      dyy, None, work, mask=mask if mode == 4 else None, **kw)
         res.append((dyy.float(), dg, db))
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-4, atol=1e-3)

@@ -69,3 +69,32 @@ def test_resnet18_eval_mode(dev):
         with torch.autocast("cuda", dtype=torch.bfloat16):
             auto = b(x)
         assert _rel(a(x), ref) < 1.5 * _rel(auto, ref) + 0.02
+
+
+@pytest.mark.parametrize("res", [64, 224])
+def test_fused_stem_backward_matches_unfused(dev, res):
+    """The stem's BN-backward apply fused into the s2d weight gradient (conv_stem.hip) gives
+    the same stem gradients as the separate quad-apply pass + igemm wgrad (same bf16 dy,
+    fp32 sums in another order), and every other gradient bit-for-bit."""
+    import dmlab.ops.convbn as cb
+
+    torch.manual_seed(3)
+    a = ResNet18(num_classes=10).to(dev)
+    x = torch.rand(4, 3, res, res, device=dev)
+    y = torch.randint(0, 10, (4,), device=dev)
+    grads = []
+    old = cb._FUSED_STEM
+    try:
+        for fused in (False, True):
+            cb._FUSED_STEM = fused
+            a.flat.grad.zero_()
+            cross_entropy(a(x), y).backward()
+            torch.cuda.synchronize()
+            grads.append({n: p.grad.detach().clone() for n, p in a.named_parameters()})
+    finally:
+        cb._FUSED_STEM = old
+    for n in grads[0]:
+        if n.startswith("stem."):
+            assert _rel(grads[1][n], grads[0][n]) < 2e-3, n
+        else:
+            torch.testing.assert_close(grads[1][n], grads[0][n], rtol=0, atol=0, msg=n)
