@@ -37,6 +37,15 @@ int ilog2(int v) {
   return l;
 }
 
+// persistent per-layer ticket counter of the one-launch BN finalizes (int32, zero between
+// launches; the kernel's last block resets it)
+unsigned* counter_ptr(const c10::optional<at::Tensor>& c, const at::Tensor& like) {
+  if (!c.has_value()) return nullptr;
+  TORCH_CHECK(c->scalar_type() == at::kInt && c->is_contiguous() && c->numel() >= 1 &&
+              c->device() == like.device(), "counter: int32 tensor on the device");
+  return reinterpret_cast<unsigned*>(c->data_ptr<int>());
+}
+
 dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride, int pad, int OH,
                       int OW) {
   dm::ConvGeom g{};
@@ -85,6 +94,14 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
     TORCH_CHECK(pre_shift.has_value(), "pre_scale needs pre_shift");
     need_f32(*pre_scale, "pre_scale", x.size(3));
     need_f32(*pre_shift, "pre_shift", x.size(3));
+    if (cfg == 70) {
+      if (dm::conv_l1_supported(g)) {
+        dm::conv_l1(bp(x), bp(wpack), bp(y), ap, sp, g, cur_stream(), fp(*pre_scale),
+                    fp(*pre_shift));
+        return;
+      }
+      cfg = 39;  // same 256-row tile
+    }
     if (cfg == 50 || cfg == 51) {
       if (dm::conv_h5_supported(g, (int)cfg)) {
         dm::conv_h5(bp(x), bp(wpack), bp(y), ap, sp, g, (int)cfg, cur_stream(), fp(*pre_scale),
@@ -352,7 +369,7 @@ void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gam
                        c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
                        double momentum, double eps, at::Tensor scale, at::Tensor shift,
                        at::Tensor mean, at::Tensor invstd, at::Tensor work,
-                       c10::optional<at::Tensor> num_batches) {
+                       c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> counter) {
   const int C = gamma.numel();
   need_f32(stats, "stats", T * 2 * C);
   long long* nb = nullptr;  // BatchNorm num_batches_tracked, incremented in the finalize kernel
@@ -367,7 +384,7 @@ void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gam
   dm::bn_stats_finalize(fp(stats), T, C, count, fp(gamma), fp(beta),
                         rmean.has_value() ? fp(*rmean) : nullptr, rvar.has_value() ? fp(*rvar) : nullptr,
                         momentum, eps, fp(scale), fp(shift), fp(mean), fp(invstd), fp(work), nb,
-                        cur_stream());
+                        cur_stream(), counter_ptr(counter, stats));
 }
 
 void bn_eval_coeffs(at::Tensor gamma, at::Tensor beta, at::Tensor rmean, at::Tensor rvar, double eps,
@@ -451,6 +468,70 @@ void stem_bwd_fused(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor
   dm::wgrad_reduce_s2d(fp(slab), S, C, (int)Cin, xs.size(3), fp(dw), (float)wbeta, st);
 }
 
+// Split stem backward (the pipelined alternative to stem_bwd_fused): coefficients once,
+// then per batch slice the quad apply (dy) and the s2d weight gradient into its own slabs,
+// then one fixed-order reduce of all slabs.
+void stem_bwd_coef(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma,
+                   at::Tensor dgamma, at::Tensor dbeta, double gbeta, at::Tensor scale,
+                   at::Tensor shift, at::Tensor pdy, at::Tensor pidx, at::Tensor pre_slab,
+                   int64_t pre_rows, at::Tensor work) {
+  need_bf16_nhwc(y, "y");
+  need_bf16_nhwc(pdy, "pdy");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  const long long M = (long long)N * H * W;
+  need_f32(work, "work", bn_bwd_work(M, C));
+  need_f32(pre_slab, "pre_slab", pre_rows * 2 * C);
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && pdy.size(1) == H / 2 && pdy.size(2) == W / 2);
+  const DeviceGuard guard(y.device());
+  dm::bn_backward(nullptr, nullptr, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
+                  (float)gbeta, M, C, 3, fp(scale), fp(shift), bp(pdy),
+                  (const uint8_t*)pidx.data_ptr(), H, W, H / 2, W / 2, 3, 2, 1, nullptr, nullptr,
+                  fp(work), cur_stream(), fp(pre_slab), (int)pre_rows, nullptr);
+}
+
+void bn_bwd_apply_quad(at::Tensor y, at::Tensor pdy, at::Tensor pidx, at::Tensor coef,
+                       at::Tensor scale, at::Tensor shift, at::Tensor dy) {
+  need_bf16_nhwc(y, "y");
+  need_bf16_nhwc(pdy, "pdy");
+  need_bf16_nhwc(dy, "dy");
+  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  TORCH_CHECK(dy.sizes() == y.sizes() && H % 2 == 0 && W % 2 == 0);
+  TORCH_CHECK(pdy.size(0) == N && pdy.size(1) == H / 2 && pdy.size(2) == W / 2 && pdy.size(3) == C);
+  TORCH_CHECK(pidx.is_cuda() && pidx.scalar_type() == at::kByte && pidx.is_contiguous() &&
+              pidx.numel() == pdy.numel());
+  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0);
+  need_f32(coef, "coef", 3 * C);
+  need_f32(scale, "scale", C);
+  need_f32(shift, "shift", C);
+  const DeviceGuard guard(y.device());
+  dm::bn_bwd_apply_quad(bp(y), bp(pdy), (const uint8_t*)pidx.data_ptr(), fp(coef), fp(scale),
+                        fp(shift), bp(dy), N, H, W, C, cur_stream());
+}
+
+int64_t stem_wgrad_blocks(int64_t N, int64_t H) { return dm::stem_wgrad_fused_blocks((int)N, (int)H); }
+
+// s2d stem weight-gradient slabs [S][64][256] of one batch slice (no reduce)
+void stem_wgrad_dy(at::Tensor xs, at::Tensor dy, at::Tensor slab, int64_t S) {
+  need_bf16_nhwc(xs, "xs");
+  need_bf16_nhwc(dy, "dy");
+  TORCH_CHECK(dm::stem_wgrad_fused_supported(dy.size(0), dy.size(1), dy.size(2), dy.size(3), xs.size(3)) &&
+              xs.size(0) == dy.size(0) && xs.size(1) == dy.size(1) && xs.size(2) == dy.size(2),
+              "stem_wgrad_dy: unsupported shape");
+  need_f32(slab, "slab", S * 64 * 256);
+  const DeviceGuard guard(xs.device());
+  dm::stem_wgrad_dy(bp(xs), bp(dy), fp(slab), dy.size(0), dy.size(1), dy.size(2), (int)S,
+                    cur_stream());
+}
+
+void wgrad_reduce_s2d(at::Tensor slab, int64_t S, int64_t Cout, int64_t Cin, int64_t Cp,
+                      at::Tensor dw, double beta) {
+  need_f32(slab, "slab", S * Cout * 16 * Cp);
+  need_f32(dw, "dw", Cout * Cin * 49);
+  const DeviceGuard guard(slab.device());
+  dm::wgrad_reduce_s2d(fp(slab), (int)S, (int)Cout, (int)Cin, (int)Cp, fp(dw), (float)beta,
+                       cur_stream());
+}
+
 void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, at::Tensor y,
                  at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
                  at::Tensor dbeta, double gbeta, int64_t mode, c10::optional<at::Tensor> scale,
@@ -458,7 +539,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
                  c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P, at::Tensor dy,
                  c10::optional<at::Tensor> dres, at::Tensor work,
                  c10::optional<at::Tensor> pre_slab, int64_t pre_rows,
-                 c10::optional<at::Tensor> mask) {
+                 c10::optional<at::Tensor> mask, c10::optional<at::Tensor> counter) {
   need_bf16_nhwc(y, "y");
   need_bf16_nhwc(dy, "dy");
   TORCH_CHECK(dy.sizes() == y.sizes());
@@ -519,7 +600,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
                   (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
                   OW, K, S, P, bp(dy), drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
-                  (int)pre_rows, mp);
+                  (int)pre_rows, mp, counter_ptr(counter, y));
 }
 
 void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,
@@ -634,7 +715,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("bn_stats_finalize", &bn_stats_finalize, py::arg("stats"), py::arg("T"), py::arg("count"),
         py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),
-        py::arg("work"), py::arg("num_batches") = py::none());
+        py::arg("work"), py::arg("num_batches") = py::none(), py::arg("counter") = py::none());
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply, py::arg("y"), py::arg("res"), py::arg("scale"), py::arg("shift"),
         py::arg("out"), py::arg("relu"), py::arg("mask") = py::none());
@@ -646,8 +727,14 @@ void register_resnet(pybind11::module_& m) {
         py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("pre_slab"), py::arg("pre_rows"),
         py::arg("xs"), py::arg("Cin"), py::arg("dw"), py::arg("wbeta"), py::arg("work"),
         py::arg("slab"));
+  m.def("stem_bwd_coef", &stem_bwd_coef);
+  m.def("bn_bwd_apply_quad", &bn_bwd_apply_quad);
+  m.def("stem_wgrad_blocks", &stem_wgrad_blocks);
+  m.def("stem_wgrad_dy", &stem_wgrad_dy);
+  m.def("wgrad_reduce_s2d", &wgrad_reduce_s2d);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
-        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none());
+        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none(),
+        py::arg("counter") = py::none());
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("out"), py::arg("idx"), py::arg("K"), py::arg("S"), py::arg("P"),
         py::arg("yarg") = py::none());

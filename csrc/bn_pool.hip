@@ -83,31 +83,123 @@ __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G
 // level-1 groups for a [T][2C] slab: none when the finalize block can sum it directly
 static inline int colsum_groups(int T) { return T <= 256 ? 0 : min(256, (T + 31) / 32); }
 
-// stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
-// grid ceil(C/16) x 256 threads
-__global__ void __launch_bounds__(256) bn_finalize_kernel(
-    const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
-    float momentum, float eps, float* __restrict__ scale, float* __restrict__ shift,
-    float* __restrict__ mean_out, float* __restrict__ invstd_out, long long* num_batches) {
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
-  if (num_batches && blockIdx.x == 0 && threadIdx.x == 0) *num_batches += 1;
-  double s, q;
-  block_sum2(part, G, C, c, s, q);
-  if (threadIdx.x >= FIN_CH || c >= C) return;
+// Per-channel finalize math shared by the separate and the fused (last-block) finalizes.
+struct FinFwd {
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  float momentum, eps;
+  float* scale;
+  float* shift;
+  float* mean_out;
+  float* invstd_out;
+  long long* num_batches;
+};
+struct FinBwd {
+  const float* gamma;
+  const float* mean;
+  const float* invstd;
+  float* dgamma;
+  float* dbeta;
+  float gbeta;
+  float* coef;
+};
+
+__device__ __forceinline__ void fin_fwd_channel(const FinFwd& f, int c, double s, double q,
+                                                double count) {
   const double mean = s / count;
   double var = q / count - mean * mean;
   if (var < 0) var = 0;
-  const float invstd = (float)(1.0 / sqrt(var + eps));
-  const float sc = gamma[c] * invstd;
-  scale[c] = sc;
-  shift[c] = beta[c] - (float)mean * sc;
-  mean_out[c] = (float)mean;
-  invstd_out[c] = invstd;
-  if (rmean) {
+  const float invstd = (float)(1.0 / sqrt(var + f.eps));
+  const float sc = f.gamma[c] * invstd;
+  f.scale[c] = sc;
+  f.shift[c] = f.beta[c] - (float)mean * sc;
+  f.mean_out[c] = (float)mean;
+  f.invstd_out[c] = invstd;
+  if (f.rmean) {
     const double unbiased = count > 1 ? var * count / (count - 1) : var;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * (float)mean;
+    f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * (float)unbiased;
+  }
+}
+
+__device__ __forceinline__ void fin_bwd_channel(const FinBwd& f, int c, int C, double s, double q,
+                                                double count) {
+  f.dbeta[c] = (f.gbeta != 0.f ? f.gbeta * f.dbeta[c] : 0.f) + (float)s;
+  f.dgamma[c] = (f.gbeta != 0.f ? f.gbeta * f.dgamma[c] : 0.f) + (float)q;
+  const float a = f.gamma[c] * f.invstd[c];
+  const float inv_m = (float)(1.0 / count);
+  const float b = -a * f.invstd[c] * (float)q * inv_m;
+  const float cc = -a * (float)s * inv_m - b * f.mean[c];
+  f.coef[c] = a;
+  f.coef[C + c] = b;
+  f.coef[2 * C + c] = cc;
+}
+
+// stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
+// grid ceil(C/16) x 256 threads
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int G,
+                                                          int C, double count, FinFwd f) {
+  const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
+  if (f.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *f.num_batches += 1;
+  double s, q;
+  block_sum2(part, G, C, c, s, q);
+  if (threadIdx.x >= FIN_CH || c >= C) return;
+  fin_fwd_channel(f, c, s, q, count);
+}
+
+// One launch instead of slab_colsum + finalize: the blocks of the first-level column sums
+// publish their [G][W] rows (agent-scope release + a ticket counter); the last block to
+// arrive acquires them and runs the finalize for every channel (the rows are few: G <= 256).
+// Same partial rows and summation order as the two-launch path (bit-identical results).
+// ctr: a counter owned by the caller (one per BN layer and direction), 0 between launches;
+// the last block resets it.
+template <bool BWD>
+__global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __restrict__ in, int T,
+                                                              int C, float* __restrict__ out,
+                                                              unsigned* __restrict__ ctr,
+                                                              double count, FinFwd ff, FinBwd fb) {
+  const int W = 2 * C;
+  const int G = gridDim.y, gi = blockIdx.y;
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const int R = (T + G - 1) / G;
+  const int r0 = gi * R, r1 = min(T, r0 + R);
+  __shared__ double red[4][64];
+  __shared__ int last;
+  red[rl][threadIdx.x & 63] = col < W ? sum_rows8(in + col, r0 + rl, r1, 4, W) : 0.0;
+  __syncthreads();
+  if (rl == 0 && col < W)
+    out[(long long)gi * W + col] = (float)(red[0][threadIdx.x] + red[1][threadIdx.x] +
+                                           red[2][threadIdx.x] + red[3][threadIdx.x]);
+  // publish (cdna guide, Guideline 16 counter form): stores retired, one agent release, ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned n = gridDim.x * gridDim.y;
+    last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!BWD && ff.num_batches) *ff.num_batches += 1;
+  }
+  __syncthreads();
+  for (int c0 = 0; c0 < C; c0 += FIN_CH) {
+    const int c = c0 + (threadIdx.x % FIN_CH);
+    double s, q;
+    block_sum2(out, G, C, c, s, q);
+    if (threadIdx.x < FIN_CH && c < C) {
+      if (BWD) fin_bwd_channel(fb, c, C, s, q, count);
+      else fin_fwd_channel(ff, c, s, q, count);
+    }
+    __syncthreads();  // block_sum2's shared rows are reused by the next channel group
   }
 }
 
@@ -369,23 +461,14 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
 
 // finalize: Σ over G partials -> dgamma, dbeta (written with beta-accumulate into grad
 // slots) and the affine dy coefficients a, b, c.  grid ceil(C/16) x 256 threads.
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
-    const float* __restrict__ part, int G, int C, double count, const float* __restrict__ gamma,
-    const float* __restrict__ mean, const float* __restrict__ invstd, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, float gbeta, float* __restrict__ coef) {
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part,
+                                                              int G, int C, double count,
+                                                              FinBwd f) {
   const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
   double s, q;
   block_sum2(part, G, C, c, s, q);
   if (threadIdx.x >= FIN_CH || c >= C) return;
-  dbeta[c] = (gbeta != 0.f ? gbeta * dbeta[c] : 0.f) + (float)s;
-  dgamma[c] = (gbeta != 0.f ? gbeta * dgamma[c] : 0.f) + (float)q;
-  const float a = gamma[c] * invstd[c];
-  const float inv_m = (float)(1.0 / count);
-  const float b = -a * invstd[c] * (float)q * inv_m;
-  const float cc = -a * (float)s * inv_m - b * mean[c];
-  coef[c] = a;
-  coef[C + c] = b;
-  coef[2 * C + c] = cc;
+  fin_bwd_channel(f, c, C, s, q, count);
 }
 
 // dy = a·dz + b·y + c ; optional dres = dz
@@ -924,17 +1007,21 @@ void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, i
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
                        float* scale, float* shift, float* mean, float* invstd, float* work,
-                       long long* num_batches, hipStream_t st) {
+                       long long* num_batches, hipStream_t st, unsigned* ctr) {
   const int W = 2 * C;
   const int G = colsum_groups(T);
+  const FinFwd f{gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd, num_batches};
+  if (G && ctr) {  // one launch: column sums + last-block finalize
+    colsum_finalize_kernel<false><<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, C, work, ctr,
+                                                                         count, f, FinBwd{});
+    return;
+  }
   const float* fin = stats;
   if (G) {
     slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
     fin = work;
   }
-  bn_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G ? G : T, C, count, gamma, beta, rmean,
-                                                       rvar, momentum, eps, scale, shift, mean,
-                                                       invstd, num_batches);
+  bn_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G ? G : T, C, count, f);
 }
 
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
@@ -973,7 +1060,8 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  float gbeta, long long M, int C, int mode, const float* scale,
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
-                 hipStream_t st, const float* pre_part, int pre_rows, const uint8_t* mask) {
+                 hipStream_t st, const float* pre_part, int pre_rows, const uint8_t* mask,
+                 unsigned* ctr) {
   // pre_part (optional): [pre_rows][2C] partial Σdz, Σdz·x̂ already reduced by the producing
   // dgrad's epilogue (BnBwdEpi) — the reduction pass over dout and y is skipped
   // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
@@ -997,13 +1085,19 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
   const int G2 = colsum_groups(G);
-  const float* fin = part;
-  if (G2) {  // parallel fixed-order pre-reduction so the finalize sums stay short
-    slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
-    fin = part2;
+  const FinBwd fb{gamma, mean, invstd, dgamma, dbeta, gbeta, coef};
+  if (G2 && ctr) {  // one launch: column sums + last-block finalize
+    colsum_finalize_kernel<true><<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(
+        part, G, C, part2, ctr, (double)M, FinFwd{}, fb);
+  } else {
+    const float* fin = part;
+    if (G2) {  // parallel fixed-order pre-reduction so the finalize sums stay short
+      slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
+      fin = part2;
+    }
+    bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C,
+                                                                      (double)M, fb);
   }
-  bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C, (double)M, gamma,
-                                                        mean, invstd, dgamma, dbeta, gbeta, coef);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
@@ -1026,6 +1120,18 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     default: DM_BNB(4, true); break;
   }
 #undef DM_BNB
+}
+
+// The stem's quad apply (dy = a·dz + b·y + c, dz gathered from the 3x3/s2/p1 max-pool
+// gradient) on its own, for coefficients computed earlier (bn_backward with dy == nullptr):
+// lets the caller run it over batch slices and pipeline the weight gradient behind it.
+void bn_bwd_apply_quad(const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx, const float* coef,
+                       const float* scale, const float* shift, bf16_t* dy, int N, int H, int W,
+                       int C, hipStream_t st) {
+  BnBwdArgs a{nullptr, nullptr, y, nullptr, nullptr, scale, shift, pdy, pidx, H, W, H / 2, W / 2,
+              3, 2, 1, (long long)N * H * W, C, nullptr};
+  const long long n8 = a.M * C / 8;
+  bn_bwd_apply_quad_kernel<<<grid_for(n8 / 4, 256, 4096), 256, sizeof(float) * 5 * C, st>>>(a, coef, dy);
 }
 
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,

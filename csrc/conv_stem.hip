@@ -403,6 +403,141 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
         out[(long long)co * SK + (th * 4 + tw) * SC + c] = acc[i][tw][r];
       }
 }
+
+// ------------------------------------------------------------------ stem weight gradient
+// dW[co][tap*16 + c] = Σ_m dy[m][co] · xs[m + off(tap)][c] with dy read from memory (the
+// quad BN-backward apply wrote it).  Same row-pair steps, LDS images and MFMA loop as the
+// fused kernel above; the staging is plain 16-B loads, so a thread's share of a row pair
+// is small (4 dy chunks + 3 halo chunks) and NSET row pairs stay in flight in registers
+// (the fused kernel's quad gathers hold ~50 registers per pair and so stay one pair ahead,
+// which left it bound by memory latency).
+template <int NSET>
+__global__ void __launch_bounds__(512) stem_wgrad_dy_kernel(StemBwdArgs a, const bf16_t* __restrict__ dyp) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Ds = reinterpret_cast<bf16_t*>(smem);  // [FR][FDP] dy tile
+  bf16_t* Xs = Ds + FR * FDP;                     // [FXH + 1][16] input halo, last = zeros
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int W = a.W, H = a.H, H2 = H >> 1;
+  const int R = 2 * W, nks = (R + 31) >> 5;
+  const long long total = (long long)a.N * H2;
+  const long long s0 = (long long)blockIdx.x * a.spb;
+  const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
+  for (int i = tid; i < FR * FDP / 8; i += 512)
+    reinterpret_cast<uint4*>(Ds)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
+  if (tid < 2) *reinterpret_cast<uint4*>(Xs + FXH * SC + tid * 8) = make_uint4(0, 0, 0, 0);
+
+  constexpr int DI = (FR * 8 + 511) / 512;   // dy chunks per thread
+  constexpr int XI = (2 * FXH + 511) / 512;  // halo chunks per thread
+  uint4 dv[NSET][DI], xv[NSET][XI];
+  auto load = [&](long long s, uint4 (&d)[DI], uint4 (&x)[XI]) {
+    const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
+    const long long base = ((long long)n * H + 2 * qa) * W;  // first pixel of the pair
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int e = tid + 512 * i;
+      d[i] = make_uint4(0, 0, 0, 0);
+      if (e < R * 8) d[i] = reinterpret_cast<const uint4*>(dyp)[base * 8 + e];
+    }
+    const int y0 = 2 * qa;
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
+      const int hr = pix / W, xx = pix - hr * W;
+      const int yy = y0 - 2 + hr;
+      x[i] = make_uint4(0, 0, 0, 0);
+      if (pix < 5 * W && yy >= 0 && yy < H)
+        x[i] = *reinterpret_cast<const uint4*>(a.xs + (((long long)n * H + yy) * W + xx) * SC + half * 8);
+    }
+  };
+  auto store = [&](const uint4 (&d)[DI], const uint4 (&x)[XI]) {
+#pragma unroll
+    for (int i = 0; i < DI; ++i) {
+      const int e = tid + 512 * i;
+      if (e < R * 8) *reinterpret_cast<uint4*>(Ds + (e >> 3) * FDP + (e & 7) * 8) = d[i];
+    }
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
+      if (pix < 5 * W) *reinterpret_cast<uint4*>(Xs + pix * SC + half * 8) = x[i];
+    }
+  };
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int rbase = grp * 4 + q;
+  const int th = wid & 3;
+  const int cob = (wid >> 2) * 32;
+  auto compute = [&](long long s) {
+    const int qa = (int)(s % H2);
+    const int y0 = 2 * qa;
+    for (int ks = 0; ks < nks; ++ks) {
+      int rlo[2], okrow[2], xr[2], rr[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = ks * 32 + rbase + 16 * u;
+        rlo[u] = r;
+        rr[u] = r >= W ? 1 : 0;
+        xr[u] = r - rr[u] * W;
+        okrow[u] = r < R && (unsigned)(y0 + rr[u] + th - 2) < (unsigned)H;
+      }
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const s4v lo = tr_read4(Ds + rlo[0] * FDP + cob + i * 16 + 4 * pp);
+        const s4v hi = tr_read4(Ds + rlo[1] * FDP + cob + i * 16 + 4 * pp);
+        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int tw = 0; tw < 4; ++tw) {
+        const bf16_t* src[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int xx = xr[u] + tw - 2;
+          const bool ok = okrow[u] && (unsigned)xx < (unsigned)W;
+          src[u] = ok ? Xs + ((rr[u] + th) * W + xx) * SC + 4 * pp : Xs + FXH * SC + 4 * pp;
+        }
+        const s4v lo = tr_read4(src[0]);
+        const s4v hi = tr_read4(src[1]);
+        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][tw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][tw], 0, 0, 0);
+      }
+    }
+  };
+  // NSET row pairs in flight: set k holds pair s with s % NSET == k (static register sets)
+#pragma unroll
+  for (int k = 0; k < NSET; ++k)
+    if (s0 + k < s1) load(s0 + k, dv[k], xv[k]);
+  __syncthreads();  // zeroed tiles
+  for (long long sb = s0; sb < s1; sb += NSET) {
+#pragma unroll
+    for (int k = 0; k < NSET; ++k) {
+      const long long s = sb + k;
+      if (s >= s1) break;
+      store(dv[k], xv[k]);
+      __syncthreads();
+      if (s + NSET < s1) load(s + NSET, dv[k], xv[k]);
+      compute(s);
+      __syncthreads();
+    }
+  }
+  float* out = a.slab + (long long)blockIdx.x * 64 * SK;
+  const int c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int tw = 0; tw < 4; ++tw)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = cob + i * 16 + (lane >> 4) * 4 + r;
+        out[(long long)co * SK + (th * 4 + tw) * SC + c] = acc[i][tw][r];
+      }
+}
 }  // namespace
 
 bool stem_conv_supported(const ConvGeom& g) {
@@ -436,6 +571,17 @@ void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, cons
   const size_t sm = (size_t)FR * FDP * 2 + (size_t)(FXH + 1) * SC * 2 + 5 * 64 * 4;
   set_smem_attr(stem_wgrad_fused_kernel, sm);
   stem_wgrad_fused_kernel<<<S, 512, sm, st>>>(a);
+  DM_CHECK(hipGetLastError());
+}
+
+void stem_wgrad_dy(const bf16_t* xs, const bf16_t* dy, float* slab, int N, int H, int W, int S,
+                   hipStream_t st) {
+  const long long pairs = (long long)N * (H / 2);
+  StemBwdArgs a{xs, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, slab, N, H, W,
+                (int)((pairs + S - 1) / S)};
+  const size_t sm = (size_t)FR * FDP * 2 + (size_t)(FXH + 1) * SC * 2;
+  set_smem_attr(stem_wgrad_dy_kernel<3>, sm);
+  stem_wgrad_dy_kernel<3><<<S, 512, sm, st>>>(a, dy);
   DM_CHECK(hipGetLastError());
 }
 

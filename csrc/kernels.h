@@ -65,12 +65,23 @@ bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb = nullptr);
+// conv_l1.hip: persistent resident-weight 64->64 3x3/s1 conv (cfg 70)
+bool conv_l1_supported(const ConvGeom& g);
+void conv_l1(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+             const ConvGeom& g, hipStream_t st, const float* pre_sc = nullptr,
+             const float* pre_sh = nullptr);
 // conv_stem.hip: s2d stem (16 channels, 16 taps, 64 outputs) with resident weights (cfg 60)
 bool stem_conv_supported(const ConvGeom& g);
 void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const ConvGeom& g,
                hipStream_t st);
 // fused stem BN backward (quad max-pool gather) + s2d weight gradient -> slabs [S][64][256]
 bool stem_wgrad_fused_supported(int N, int H, int W, int C, int Cpad);
+void bn_bwd_apply_quad(const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx, const float* coef,
+                       const float* scale, const float* shift, bf16_t* dy, int N, int H, int W,
+                       int C, hipStream_t st);
+// same s2d weight gradient from a materialised dy [N][H][W][64] (several row pairs in flight)
+void stem_wgrad_dy(const bf16_t* xs, const bf16_t* dy, float* slab, int N, int H, int W, int S,
+                   hipStream_t st);
 int stem_wgrad_fused_blocks(int N, int H);
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
@@ -106,7 +117,7 @@ void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
                        float* scale, float* shift, float* mean, float* invstd, float* work, long long* num_batches,
-                       hipStream_t st);
+                       hipStream_t st, unsigned* ctr = nullptr);
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                     float eps, int C, float* scale, float* shift, hipStream_t st);
 void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
@@ -118,7 +129,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
                  hipStream_t st, const float* pre_part = nullptr, int pre_rows = 0,
-                 const uint8_t* mask = nullptr);
+                 const uint8_t* mask = nullptr, unsigned* ctr = nullptr);
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
                      int P, hipStream_t st, bf16_t* yarg = nullptr);

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -195,13 +197,34 @@ class BasicBlock(Layer):
 
     def native_fwd(self, x, ctx, train):
         c1, c2, cd = Ctx(), Ctx(), Ctx()
-        idt = x if self.down is None else self.down.native_fwd(x, cd, train)
+        side = self._down_stream() if self.down is not None else None
+        if side is not None:
+            # the projection shortcut (1x1/s2 conv + BN) and c1 both read only x: run the
+            # shortcut on the side stream so its small grids fill c1's tail and vice versa
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                idt = self.down.native_fwd(x, cd, train)
+        else:
+            idt = x if self.down is None else self.down.native_fwd(x, cd, train)
         # c1's BN-apply + ReLU is fused into c2's operand staging: relu(bn1(y1)) is never
         # written (c2's forward and weight-gradient halo kernels normalise y1 on the fly)
         y1 = self.c1.native_fwd(x, c1, train, raw=True)
+        if side is not None:
+            main.wait_stream(side)
+            # tensors the side stream allocated are used (and freed) on the main stream
+            for t in [idt] + [v for v in cd.values() if torch.is_tensor(v)]:
+                t.record_stream(main)
+            x.record_stream(side)
         out = self.c2.native_fwd(y1, c2, train, residual=idt, pre=(c1["scale"], c1["shift"]))
         ctx.update(c1=c1, c2=c2, cd=cd)
         return out
+
+    def _down_stream(self):
+        prog = getattr(self, "_prog", None)
+        if prog is None or os.environ.get("DMLAB_DOWN_STREAM", "1") == "0":
+            return None
+        return prog._side_stream() if prog._native_active else None
 
     def bn_consumer(self, ctx):
         """The ConvBN whose BN backward consumes this block's output gradient first."""

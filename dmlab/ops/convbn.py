@@ -196,6 +196,16 @@ def pack_all(prog, layers):
         object.__setattr__(m, "_wcache", (ver, wf, wd))
 
 
+def _fin_counter(layer, device):
+    """Persistent int32 ticket counters of this layer's one-launch BN finalizes ([0] forward,
+    [1] backward); zero between launches (the finalizing block resets them)."""
+    c = getattr(layer, "_fin_ctr", None)
+    if c is None or c.device != device:
+        c = torch.zeros(2, dtype=torch.int32, device=device)
+        object.__setattr__(layer, "_fin_ctr", c)
+    return c
+
+
 def _materialise(x, pre):
     """relu(x*scale + shift) as a tensor (fallback when a consumer cannot fuse it)."""
     out = empty_nhwc(*x.shape, x)
@@ -252,7 +262,8 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
         work = torch.empty(256 * 2 * cout, **f32)
         L.bn_stats_finalize(stats, T, float(M), layer.bn_weight.detach(), layer.bn_bias.detach(),
                             layer.running_mean, layer.running_var, layer.momentum, layer.eps,
-                            scale, shift, mean, invstd, work, layer.num_batches_tracked)
+                            scale, shift, mean, invstd, work, layer.num_batches_tracked,
+                            counter=_fin_counter(layer, x.device)[0:1] if _FUSED_FIN else None)
     else:
         L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg, **pre_kw)
         L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
@@ -297,9 +308,18 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
 # e.g. layer1 dgrad 84 -> 139 us.  Kept for A/B runs: DMLAB_FUSE_BN_BWD=1.
 _FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
 
-# Stem backward: BN-backward apply fused into the s2d weight gradient (DMLAB_FUSED_STEM=0:
-# the separate quad apply pass + igemm wgrad, kept for A/B runs)
-_FUSED_STEM = os.environ.get("DMLAB_FUSED_STEM", "1") == "1"
+# Stem backward (DMLAB_STEM_BWD): "split" = coefficients once, then per batch slice the quad
+# BN-backward apply and, on the side stream, the s2d weight gradient of that slice
+# (DMLAB_STEM_SPLIT slices); "fused" = the apply computed inside the weight-gradient kernel
+# (dy never written, but its gathers keep only one row pair in flight); "legacy" = one
+# apply pass + the generic igemm weight gradient.  Kept for A/B runs.
+_STEM_BWD = os.environ.get("DMLAB_STEM_BWD", "fused")
+# BN finalizes as one launch (column sums + a last-block finalize, bit-identical) instead of
+# two: opt-in (DMLAB_FUSED_FIN=1).  Measured 6 % SLOWER end to end on MI355X (12.8 vs 12.1
+# ms/step): the last block walks the channel groups serially, where the separate finalize
+# spreads them over C/16 blocks -- the saved launch (~5 us) costs more than it saves
+_FUSED_FIN = os.environ.get("DMLAB_FUSED_FIN", "0") == "1"
+_STEM_SPLIT = int(os.environ.get("DMLAB_STEM_SPLIT", "4"))
 
 # Weight gradients of convs with at least this many output channels go to the Program's
 # side stream (DMLAB_WGRAD_STREAM_MIN_COUT; 0 = all).
@@ -356,8 +376,43 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
         rows = L.bn_bwd_reduce_masked(dout, ctx["yarg"], ctx["mean"], ctx["invstd"], ctx["scale"],
                                       ctx["shift"], part)
         pre_sums = dict(pre_slab=part, pre_rows=rows)
-    if (pool and _FUSED_STEM and s2d and pre_sums and ctx["first"] and not ctx["has_res"]
-            and L.stem_bwd_fused_supported(y, x)):
+    stem_ok = (pool and s2d and pre_sums and ctx["first"] and not ctx["has_res"]
+               and L.stem_bwd_fused_supported(y, x))
+    if stem_ok and _STEM_BWD == "split":
+        # coefficients once; then per batch slice the quad BN-backward apply (main stream)
+        # and the s2d weight gradient of that slice (side stream), so the weight gradient
+        # of slice i overlaps the apply of slice i+1; one fixed-order reduce of all slabs
+        L.stem_bwd_coef(y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
+                        layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
+                        ctx["scale"], ctx["shift"], dout, ctx["idx"], pre_sums["pre_slab"],
+                        pre_sums["pre_rows"], work)
+        coef = work[: 3 * cout]
+        dy = empty_nhwc(N, OH, OW, cout, y)
+        P = max(1, min(_STEM_SPLIT, N))
+        bounds = [N * i // P for i in range(P + 1)]
+        nblk = [L.stem_wgrad_blocks(bounds[i + 1] - bounds[i], OH) for i in range(P)]
+        side = getattr(layer._prog, "_wgrad_stream", None)
+        main = torch.cuda.current_stream()
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            slab = torch.empty(sum(nblk) * 64 * 256, device=y.device, dtype=torch.float32)
+        off = 0
+        for i in range(P):
+            a, b = bounds[i], bounds[i + 1]
+            L.bn_bwd_apply_quad(y[a:b], dout[a:b], ctx["idx"][a:b], coef, ctx["scale"],
+                                ctx["shift"], dy[a:b])
+            if side is not None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                L.stem_wgrad_dy(x[a:b], dy[a:b], slab[off * 16384:(off + nblk[i]) * 16384], nblk[i])
+            off += nblk[i]
+        if side is not None:
+            dy.record_stream(side)
+            x.record_stream(side)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            L.wgrad_reduce_s2d(slab, off, cout, layer.cin, x.shape[3], layer.grad_slot("weight"),
+                               acc)
+        return None
+    if stem_ok and _STEM_BWD == "fused":
         # stem: BN-backward apply fused into the s2d weight gradient -- the full-resolution
         # dy is never written (csrc/conv_stem.hip stem_wgrad_fused_kernel)
         slab = torch.empty(L.stem_bwd_slab_floats(N, OH), device=y.device, dtype=torch.float32)
@@ -383,7 +438,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
-                  getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"), **pre_sums)
+                  getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"),
+                  counter=_fin_counter(layer, y.device)[1:2] if _FUSED_FIN else None, **pre_sums)
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does

@@ -78,6 +78,32 @@ def _h5_skip(cfg, cin_gemm):
 H5_GEOMS = HALO_GEOMS + [GEOMS[0], GEOMS[3], (4, 56, 64, 64, 3, 1, 1), (2, 7, 512, 512, 3, 1, 1)]
 
 
+L1_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 14, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
+            (1, 9, 64, 64, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geom", L1_GEOMS)
+def test_conv_fwd_l1_persistent(dev, geom):
+    """Persistent resident-weight 64->64 kernel (conv_l1.hip, cfg 70): tiles crossing image
+    rows and images, partial last tile, fewer tiles than CUs."""
+    _check_fwd(dev, geom, 70)
+
+
+@pytest.mark.parametrize("geom", L1_GEOMS)
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_dgrad_l1_persistent(dev, geom, accumulate):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w.bfloat16().float(), dy.float(), s, p)
+    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    base = dx.clone()
+    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, 70)
+    if accumulate:
+        ref = ref + _nchw(base).float()
+    assert _rel(_nchw(dx), ref) < 6e-3
+
+
 @pytest.mark.parametrize("geom", H5_GEOMS)
 @pytest.mark.parametrize("cfg", [50, 51])
 def test_conv_fwd_h5(dev, geom, cfg):
@@ -414,10 +440,21 @@ def test_bn_stats_finalize_slab_rows(dev, T):
     var = (qd / M - mu * mu).clamp_min(0)
     torch.testing.assert_close(mean.double(), mu, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-6)
+    # the one-launch finalize (column sums + last-block finalize, ticket counter) is bit-identical,
+    # leaves its counter at 0 and increments num_batches once per call
+    ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+    nb = torch.zeros(1, dtype=torch.int64, device=dev)
+    for rep in range(3):
+        out = [torch.empty(C, **f) for _ in range(4)]
+        lib().bn_stats_finalize(stats.view(-1), T, M, gamma, beta, None, None, 0.1, 1e-5, *out,
+                                torch.empty(512 * C, **f), nb, counter=ctr)
+        for a, b in zip(out, (scale, shift, mean, invstd)):
+            assert torch.equal(a, b)
+        assert int(ctr.item()) == 0 and int(nb.item()) == rep + 1
 
 
-@pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3])
-@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 50, 51])
+@pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3] + L1_GEOMS[1:])
+@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 50, 51, 70])
 def test_conv_fwd_prebn(dev, geom, cfg):
     """Halo conv consuming relu(y*scale + shift) of a RAW previous-conv output (fused
     BN-apply + ReLU in the staging); zero padding stays zero after the BN."""
@@ -549,6 +586,15 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
                       sc if mode == 2 else None, sh if mode == 2 else None, None, None, 3, 2, 1,
                       dyy, None, work, mask=mask if mode == 4 else None, **kw)
         res.append((dyy.float(), dg, db))
+        if not pre:  # the one-launch finalize (ticket counter) is bit-identical
+            ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+            d2, dg2, db2 = torch.empty_like(y), torch.zeros(Cin, **f), torch.zeros(Cin, **f)
+            L.bn_backward(dx, out if mode == 1 else None, y, mean, invstd, gamma, dg2, db2, 0.0,
+                          mode, sc if mode == 2 else None, sh if mode == 2 else None, None, None,
+                          3, 2, 1, d2, None, torch.empty_like(work),
+                          mask=mask if mode == 4 else None, counter=ctr)
+            assert torch.equal(d2, dyy) and torch.equal(dg2, dg) and torch.equal(db2, db)
+            assert int(ctr.item()) == 0
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-4, atol=1e-3)
     assert _rel(res[0][0], res[1][0]) < 1e-3

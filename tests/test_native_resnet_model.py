@@ -72,10 +72,12 @@ def test_resnet18_eval_mode(dev):
 
 
 @pytest.mark.parametrize("res", [64, 224])
-def test_fused_stem_backward_matches_unfused(dev, res):
-    """The stem's BN-backward apply fused into the s2d weight gradient (conv_stem.hip) gives
-    the same stem gradients as the separate quad-apply pass + igemm wgrad (same bf16 dy,
-    fp32 sums in another order), and every other gradient bit-for-bit."""
+@pytest.mark.parametrize("variant", ["fused", "split"])
+def test_fused_stem_backward_matches_unfused(dev, res, variant):
+    """The stem backward variants (conv_stem.hip: the BN-backward apply fused into the s2d
+    weight gradient, or per batch slice apply + pipelined s2d weight gradient) give the same
+    stem gradients as the separate quad-apply pass + igemm wgrad (same bf16 dy, fp32 sums in
+    another order), and every other gradient bit-for-bit."""
     import dmlab.ops.convbn as cb
 
     torch.manual_seed(3)
@@ -83,16 +85,16 @@ def test_fused_stem_backward_matches_unfused(dev, res):
     x = torch.rand(4, 3, res, res, device=dev)
     y = torch.randint(0, 10, (4,), device=dev)
     grads = []
-    old = cb._FUSED_STEM
+    old = cb._STEM_BWD
     try:
-        for fused in (False, True):
-            cb._FUSED_STEM = fused
+        for mode in ("legacy", variant):
+            cb._STEM_BWD = mode
             a.flat.grad.zero_()
             cross_entropy(a(x), y).backward()
             torch.cuda.synchronize()
             grads.append({n: p.grad.detach().clone() for n, p in a.named_parameters()})
     finally:
-        cb._FUSED_STEM = old
+        cb._STEM_BWD = old
     for n in grads[0]:
         if n.startswith("stem."):
             assert _rel(grads[1][n], grads[0][n]) < 2e-3, n
