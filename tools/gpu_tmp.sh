@@ -2,14 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=${1:-fin}
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$t.log 2>&1 || { tail -40 gpurun_out/pytest_$t.log; exit 1; }
-tail -2 gpurun_out/pytest_$t.log
-for f in 1 0 1 0 1 0; do
-DMLAB_FUSED_FIN=$f timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${t}_$f.json 2> gpurun_out/bench_${t}_$f.err || { tail -20 gpurun_out/bench_${t}_$f.err; exit 1; }
-echo "fused_fin $f: $(python -c "import json;d=json.load(open('gpurun_out/bench_${t}_$f.json'));print(d['value'], d['ms_per_step'], d['final_loss'])")"
-done
-for b in 768 1024; do
-timeout -k 10 300 python bench.py --steps 15 --warmup 5 --batch $b > gpurun_out/bench_${t}_b$b.json 2> gpurun_out/bench_${t}_b$b.err || { tail -20 gpurun_out/bench_${t}_b$b.err; exit 1; }
-echo "batch $b: $(python -c "import json;d=json.load(open('gpurun_out/bench_${t}_b$b.json'));print(d['value'], d['ms_per_step'])")"
-done
+t=${1:-bytes}
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${t}_f -o pmc -- python bench.py --steps 3 --warmup 2 > gpurun_out/${t}_f.log 2>&1 && \
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${t}_w -o pmc -- python bench.py --steps 3 --warmup 2 > gpurun_out/${t}_w.log 2>&1
+ls gpurun_out/${t}_f gpurun_out/${t}_w

@@ -1,3 +1,8 @@
+"""Every dispatch of one training step (queue, start offset, duration, grid) from a rocprofv3
+kernel trace, plus per-queue backward sums (profiles/rocprof_resnet18_b512_step_dispatches_r2a.txt).
+
+    python tools/step_timeline.py <kernel_trace.csv>
+"""
 import csv, sys, re
 rows = sorted(((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"], int(r["Grid_Size_X"])//int(r["Workgroup_Size_X"]), int(r["Grid_Size_Y"]), int(r["Grid_Size_Z"])) for r in csv.DictReader(open(sys.argv[1]))), key=lambda t: t[1])
 starts = [i for i, r in enumerate(rows) if "pack_input_s2d" in r[0]]
