@@ -63,6 +63,8 @@ dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride,
   return g;
 }
 
+int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols);
+
 // y = conv(x, w)  (+add) ; stats [T][2][Cout] optional
 void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Tensor> stats,
               c10::optional<at::Tensor> add, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
@@ -82,8 +84,7 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
   auto g = fwd_geom(x, Cout, KH, KW, stride, pad, OH, OW);
   float* sp = nullptr;
   if (stats.has_value()) {
-    const int bm = dm::igemm_fwd_rowtile(cfg);
-    need_f32(*stats, "stats", ((g.M + bm - 1) / bm) * 2 * Cout);
+    need_f32(*stats, "stats", conv_stats_rows(g.M, cfg, Cout) * 2 * Cout);
     sp = fp(*stats);
   }
   const bf* ap = nullptr;
@@ -120,7 +121,10 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
   dm::igemm_fwd(bp(x), bp(wpack), bp(y), ap, sp, g, cfg, cur_stream());
 }
 
-int64_t conv_stats_rows(int64_t M, int64_t cfg) {
+// statistics rows a forward conv of this cfg writes; ncols (output channels) is needed for the
+// cfg-41 tail split (ncols < 0: the plain one-row-per-tile count, no split)
+int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
+  if (cfg == 41 && ncols > 0) return dm::conv_halo41_stats_rows(M, (int)ncols);
   const int bm = dm::igemm_fwd_rowtile(cfg);
   return (M + bm - 1) / bm;
 }
@@ -129,7 +133,7 @@ int64_t conv_stats_rows(int64_t M, int64_t cfg) {
 // Slab rows the BN-backward epilogue of conv_dgrad writes (0: the shape/cfg cannot fuse it).
 int64_t dgrad_bnb_rows(int64_t N, int64_t H, int64_t W, int64_t stride, int64_t cfg) {
   if (cfg < 9) return 0;
-  if (stride == 1) return conv_stats_rows(N * H * W, cfg);
+  if (stride == 1) return conv_stats_rows(N * H * W, cfg, -1);  // fused sums: no tail split
   if (!(cfg == 12 || cfg == 13 || cfg == 15 || cfg == 16)) return 0;
   const long long mmax = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);  // class (0, 0) is largest
   return ((mmax + 127) / 128) * 4;
@@ -696,7 +700,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wpack"), py::arg("y"), py::arg("stats"),
         py::arg("add"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("cfg"), py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
-  m.def("conv_stats_rows", &conv_stats_rows);
+  m.def("conv_stats_rows", &conv_stats_rows, py::arg("M"), py::arg("cfg"), py::arg("ncols") = -1);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("dx"), py::arg("KH"),
         py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("add"), py::arg("cfg"),
         py::arg("bnb_y") = py::none(), py::arg("bnb_out") = py::none(),

@@ -43,8 +43,11 @@ template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb) {
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,
+    long long mbase, int rowbase) {
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
+  // mbase / rowbase: first output pixel and first statistics row of this launch (a launch
+  // may cover only the tail of the pixel range, see conv_halo's tail split)
   // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
   // image taps still read the zero row, i.e. the padding stays zero AFTER the BN.
   constexpr int TM = BMH / WM, TN = BN / WN;
@@ -60,7 +63,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = (long long)blockIdx.x * BMH;
+  const long long m0 = mbase + (long long)blockIdx.x * BMH;
   const int n0 = blockIdx.y * BN;
   const int ntaps = g.nth * g.ntw;
   const int nchunk = g.C / HBK;
@@ -276,7 +279,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       if (s + 1 < S) step(s + 1, rb, rb2);
     }
   }
-  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, blockIdx.x, stats, g, Y, ADD,
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, rowbase + blockIdx.x,
+                                                       stats, g, Y, ADD,
                                                        bnb);
 }
 
@@ -288,20 +292,67 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
 template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
-                 const BnBwdEpi& bnb) {
+                 const BnBwdEpi& bnb, long long mbase = 0, int rowbase = 0, long long mend = -1) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
   const size_t sm = main > epi ? main : epi;
-  dim3 grid((unsigned)((g.M + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
+  if (mend < 0) mend = g.M;
+  dim3 grid((unsigned)((mend - mbase + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
   auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
                   : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
   set_smem_attr(k, sm);
-  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb, mbase,
+                                    rowbase);
+}
+
+// Tail split for the 256-pixel 4x1-wave tile (cfg 41).  Its layer-3/4 grids are just over a
+// whole number of rounds of resident workgroups (1568 / 784 blocks on 512 slots), so the
+// last round runs a handful of blocks while most CUs idle (measured: layer4 at exactly one
+// round 910 vs 792 TFLOP/s at batch 512).  When the last round is under ~60 % full, the
+// pixel rows of that round go to a second launch of 128-pixel tiles (3 workgroups per CU):
+// twice the blocks, each half the work.  Statistics rows: the main tiles first, then the
+// 128-pixel tiles.
+int halo_slots() {
+  if (const char* e = getenv("DMLAB_TAIL_SLOTS"))  // tests: force the split on small shapes
+    if (atoi(e) > 0) return atoi(e);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    DM_CHECK(hipGetDevice(&dev));
+    DM_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  return 2 * cus;  // cfg 41: two 4-wave workgroups per CU
+}
+
+// main M-tiles (256 px) of a cfg-41 launch; == all tiles when no tail split applies
+// Opt-in (DMLAB_TAIL_SPLIT=1, or DMLAB_TAIL_SLOTS for tests): measured slower end to end
+// (12.29 vs 12.08 ms/step; layer3 717 vs 733 TFLOP/s, layer4 773 vs 755): the blocks of a
+// nearly empty last round run faster alone than the model assumes, and the 128-pixel tail
+// tile plus its launch cost more than the idle CUs.
+long long halo41_main_tiles(long long M, int Ncols) {
+  const char* on = getenv("DMLAB_TAIL_SPLIT");
+  const char* sl = getenv("DMLAB_TAIL_SLOTS");
+  if (!((on && atoi(on) == 1) || (sl && atoi(sl) > 0))) return (M + 255) / 256;
+  const long long gx = (M + 255) / 256, gy = (Ncols + 63) / 64;
+  const long long T = gx * gy, slots = halo_slots();
+  if (T <= slots) return gx;
+  const long long tail = T % slots;
+  if (tail == 0 || tail * 10 > slots * 6) return gx;
+  const long long gxm = (T - tail) / gy;  // whole rounds, whole M-tiles
+  return gxm < gx ? gxm : gx;
 }
 }  // namespace
+
+// statistics rows written by a halo launch of this config (256-px tiles, plus the 128-px tail
+// tiles of a cfg-41 tail split)
+long long conv_halo41_stats_rows(long long M, int Ncols) {
+  const long long gxm = halo41_main_tiles(M, Ncols);
+  const long long mend = gxm * 256 < M ? gxm * 256 : M;
+  return gxm + (M - mend + 127) / 128;
+}
 
 bool conv_halo_supported(const ConvGeom& g) {
   if (g.isy != 1 || g.isx != 1 || g.Hg != g.H || g.Wg != g.W) return false;
@@ -355,12 +406,22 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                                   // BN 128 as 64 x 128 per wave spills: not instantiated)
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 31) / 32;
+    // tail split (not with the fused BN-backward sums, whose slab rows are per 256-px tile)
+    const long long gxm = bnbp ? (g.M + 255) / 256 : halo41_main_tiles(g.M, g.Ncols);
+    const long long mend = gxm * 256 < g.M ? gxm * 256 : g.M;
 #define DM_HALO256W41(BN_)                                                                   \
-  if (hr <= 10) launch_halo<BN_, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);                \
-  else if (hr <= 12) launch_halo<BN_, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
-  else launch_halo<BN_, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+  if (hr <= 10) launch_halo<BN_, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, 0, 0, mend);      \
+  else if (hr <= 12) launch_halo<BN_, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, 0, 0, mend); \
+  else launch_halo<BN_, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, 0, 0, mend);
     DM_HALO256W41(64)
 #undef DM_HALO256W41
+    if (mend < g.M) {  // the tail's pixel rows as 128-pixel tiles (2 x 2 waves of 64 x 32)
+      const int hp = halo_rows_needed(g);
+      const int rb = (int)gxm;
+      if (hp <= 192) launch_halo<64, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, mend, rb);
+      else if (hp <= 256) launch_halo<64, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, mend, rb);
+      else launch_halo<64, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, mend, rb);
+    }
     DM_CHECK(hipGetLastError());
     return;
   }

@@ -93,6 +93,7 @@ void conv_h5(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, fl
              const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
              const float* pre_sh = nullptr, const BnBwdEpi* bnb = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
+long long conv_halo41_stats_rows(long long M, int Ncols);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,

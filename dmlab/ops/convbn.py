@@ -254,7 +254,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     shift = torch.empty(cout, **f32)
     use_batch = layer.training
     if use_batch:
-        T = L.conv_stats_rows(M, cfg)
+        T = L.conv_stats_rows(M, cfg, cout)
         stats = torch.empty(T * 2 * cout, **f32)
         L.conv_fwd(x, wf, y, stats, None, k, k, s, p, cfg, **pre_kw)
         mean = torch.empty(cout, **f32)
@@ -320,6 +320,8 @@ _STEM_BWD = os.environ.get("DMLAB_STEM_BWD", "fused")
 # spreads them over C/16 blocks -- the saved launch (~5 us) costs more than it saves
 _FUSED_FIN = os.environ.get("DMLAB_FUSED_FIN", "0") == "1"
 _STEM_SPLIT = int(os.environ.get("DMLAB_STEM_SPLIT", "4"))
+# weight gradient of the split path: "dy" (stem_wgrad_dy_kernel) or "igemm" (v2 s2d tiles)
+_STEM_WGRAD = os.environ.get("DMLAB_STEM_WGRAD", "dy")
 
 # Weight gradients of convs with at least this many output channels go to the Program's
 # side stream (DMLAB_WGRAD_STREAM_MIN_COUT; 0 = all).
@@ -403,14 +405,25 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
             if side is not None:
                 side.wait_stream(main)
             with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                L.stem_wgrad_dy(x[a:b], dy[a:b], slab[off * 16384:(off + nblk[i]) * 16384], nblk[i])
+                if _STEM_WGRAD == "igemm":
+                    # the generic s2d igemm weight gradient of this slice, accumulated
+                    Mi = (b - a) * OH * OW
+                    wc, Si = _wgrad_plan(Mi, cout, 16 * x.shape[3])
+                    sl = torch.empty(Si * cout * 16 * x.shape[3], device=y.device,
+                                     dtype=torch.float32)
+                    L.conv_wgrad(x[a:b], dy[a:b], layer.grad_slot("weight"), sl, layer.cin, 4, 4,
+                                 1, 2, acc if i == 0 else 1.0, Si, wc, True)
+                else:
+                    L.stem_wgrad_dy(x[a:b], dy[a:b], slab[off * 16384:(off + nblk[i]) * 16384],
+                                    nblk[i])
             off += nblk[i]
         if side is not None:
             dy.record_stream(side)
             x.record_stream(side)
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            L.wgrad_reduce_s2d(slab, off, cout, layer.cin, x.shape[3], layer.grad_slot("weight"),
-                               acc)
+        if _STEM_WGRAD != "igemm":
+            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+                L.wgrad_reduce_s2d(slab, off, cout, layer.cin, x.shape[3],
+                                   layer.grad_slot("weight"), acc)
         return None
     if stem_ok and _STEM_BWD == "fused":
         # stem: BN-backward apply fused into the s2d weight gradient -- the full-resolution

@@ -78,6 +78,49 @@ def _h5_skip(cfg, cin_gemm):
 H5_GEOMS = HALO_GEOMS + [GEOMS[0], GEOMS[3], (4, 56, 64, 64, 3, 1, 1), (2, 7, 512, 512, 3, 1, 1)]
 
 
+@pytest.mark.parametrize("geom", [(6, 14, 256, 256, 3, 1, 1), (14, 7, 128, 512, 3, 1, 1)])
+@pytest.mark.parametrize("pre", [False, True])
+def test_conv_fwd_tail_split(dev, geom, pre, monkeypatch):
+    """cfg 41 with a nearly empty last round moves that round's pixel rows to a launch of
+    128-pixel tiles (DMLAB_TAIL_SLOTS shrinks the slot count so small shapes split): same
+    outputs, and statistics rows = main tiles + tail tiles."""
+    monkeypatch.setenv("DMLAB_TAIL_SLOTS", "16")
+    N, H, Cin, Cout, k, s, p = geom
+    M = N * H * H
+    T = lib().conv_stats_rows(M, 41, Cout)
+    assert T > (M + 255) // 256  # the split applies
+    if pre:
+        g = torch.Generator(device=dev).manual_seed(4)
+        y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+        sc = torch.rand(Cin, device=dev, generator=g) + 0.5
+        sh = torch.randn(Cin, device=dev, generator=g) * 0.5
+        w = torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k)
+        wf = torch.empty(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16)
+        lib().pack_weights(w.contiguous(), wf, None, Cin)
+        a = (y.float() * sc + sh).relu().bfloat16().float()
+        ref = F.conv2d(_nchw(a), w.bfloat16().float(), None, s, p)
+        out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
+        stats = torch.full((T * 2 * Cout,), float("nan"), device=dev)
+        lib().conv_fwd(y, wf, out, stats, None, k, k, s, p, 41, pre_scale=sc, pre_shift=sh)
+    else:
+        x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
+        ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
+        out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
+        stats = torch.full((T * 2 * Cout,), float("nan"), device=dev)
+        lib().conv_fwd(xn, wf, out, stats, None, k, k, s, p, 41)
+    assert _rel(_nchw(out), ref) < 6e-3
+    st = stats.view(T, 2, Cout).sum(0)  # every row written (NaN-filled before)
+    torch.testing.assert_close(st[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
+    torch.testing.assert_close(st[1], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
+    # data gradient through the same split (stride 1: the flipped-tap geometry)
+    x2, w2, xn2, wf2, wd2 = _setup(dev, N, H, Cout, Cin, k, s, p)
+    dy = torch.randn(N, Cin, H, H, device=dev).bfloat16()
+    dref = torch.nn.grad.conv2d_input((N, Cout, H, H), w2.bfloat16().float(), dy.float(), s, p)
+    dx = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
+    lib().conv_dgrad(_nhwc(dy), wd2, dx, k, k, s, p, None, 41)
+    assert _rel(_nchw(dx), dref) < 6e-3
+
+
 L1_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 14, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
             (1, 9, 64, 64, 3, 1, 1)]
 
@@ -141,7 +184,7 @@ def _check_fwd(dev, geom, cfg):
     OH = ref.shape[2]
     y = torch.empty(N, OH, OH, Cout, device=dev, dtype=torch.bfloat16)
     M = N * OH * OH
-    T = lib().conv_stats_rows(M, cfg)
+    T = lib().conv_stats_rows(M, cfg, Cout)
     stats = torch.empty(T * 2 * Cout, device=dev)
     lib().conv_fwd(xn, wf, y, stats, None, k, k, s, p, cfg)
     assert _rel(_nchw(y), ref) < 6e-3
@@ -334,7 +377,7 @@ def test_stem_space_to_depth(dev, H, fcfg):
     ref = F.conv2d(x.float(), w.bfloat16().float(), None, 2, 3)
     y = torch.empty(N, H // 2, H // 2, Co, device=dev, dtype=torch.bfloat16)
     M = N * (H // 2) ** 2
-    T = lib().conv_stats_rows(M, fcfg)
+    T = lib().conv_stats_rows(M, fcfg, Co)
     stats = torch.empty(T * 2 * Co, device=dev)
     lib().conv_fwd(xs, wf, y, stats, None, 4, 4, 1, 2, fcfg)
     assert _rel(_nchw(y), ref) < 6e-3
@@ -471,7 +514,7 @@ def test_conv_fwd_prebn(dev, geom, cfg):
     ref = F.conv2d(_nchw(a), w.bfloat16().float(), None, s, p)
     out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
     M = N * H * H
-    T = lib().conv_stats_rows(M, cfg)
+    T = lib().conv_stats_rows(M, cfg, Cout)
     stats = torch.empty(T * 2 * Cout, device=dev)
     lib().conv_fwd(y, wf, out, stats, None, k, k, s, p, cfg, pre_scale=sc, pre_shift=sh)
     assert _rel(_nchw(out), ref) < 6e-3

@@ -92,7 +92,7 @@ def main():
                 if cfg == 70 and not (C == 64 and Co == 64 and k == 3 and s == 1):
                     continue
                 M = N * OH * OH
-                T = L.conv_stats_rows(M, cfg)
+                T = L.conv_stats_rows(M, cfg, Co)
                 st = torch.empty(T * 2 * Co, device=dev)
                 t = timeit(lambda: L.conv_fwd(x, wf, y, st, None, k, k, s, p, cfg), a.iters)
                 row[f"fwd_c{cfg}_TF"] = round(flops / t / 1e12, 1)

@@ -16,7 +16,7 @@ L = lib()
 x = torch.randn(N, H, H, C, device="cuda").bfloat16()
 wf = (torch.randn(Co, 3, 3, C, device="cuda") * 0.05).bfloat16()
 y = torch.empty(N, H, H, Co, device="cuda", dtype=torch.bfloat16)
-T = L.conv_stats_rows(N * H * H, cfg)
+T = L.conv_stats_rows(N * H * H, cfg, Co)
 st = torch.empty(T * 2 * Co, device="cuda")
 for _ in range(10):
     L.conv_fwd(x, wf, y, st, None, 3, 3, 1, 1, cfg)
