@@ -512,7 +512,7 @@ void bn_bwd_apply_quad(at::Tensor y, at::Tensor pdy, at::Tensor pidx, at::Tensor
                         fp(shift), bp(dy), N, H, W, C, cur_stream());
 }
 
-int64_t stem_wgrad_blocks(int64_t N, int64_t H) { return dm::stem_wgrad_fused_blocks((int)N, (int)H); }
+int64_t stem_wgrad_blocks(int64_t N, int64_t H) { return dm::stem_wgrad_dy_blocks((int)N, (int)H); }
 
 // s2d stem weight-gradient slabs [S][64][256] of one batch slice (no reduce)
 void stem_wgrad_dy(at::Tensor xs, at::Tensor dy, at::Tensor slab, int64_t S) {

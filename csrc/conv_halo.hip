@@ -370,7 +370,8 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
                const float* pre_sh, const BnBwdEpi* bnbp) {
   const BnBwdEpi bnb = bnbp ? *bnbp : BnBwdEpi{};
-  if (waves & 0x100) {  // two-deep weight prefetch (BN 128 only): 4 waves / 128 px, 8 waves / 256 px
+  if (waves & 0x100) {  // two-deep weight prefetch: BN 128 4 waves / 128 px, 8 waves / 256 px;
+                        // BN 64 4 x 1 waves (cfg 44) and 4 x 2 waves (cfg 45) / 256 px
     waves &= 0xff;
     if (bn == 128 && waves == 4) {
       const int hp = halo_rows_needed(g);
@@ -381,8 +382,23 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
       DM_CHECK(hipGetLastError());
       return;
     }
-    if (bn == 128 && waves == 16) {
+    if (bn == 64 && waves == 32) {  // cfg 44: the 4 x 1-wave 64 x 64 tile of cfg 41
+      const int hr = (halo_rows_needed(g, 256) + 31) / 32;
+      if (hr <= 10) launch_halo<64, 10, 4, 1, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      else if (hr <= 12) launch_halo<64, 12, 4, 1, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      else launch_halo<64, 14, 4, 1, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+      DM_CHECK(hipGetLastError());
+      return;
+    }
+    if (waves == 16) {  // BN 128: cfg 43; BN 64: cfg 45 (the 4 x 2-wave tile of cfg 39)
       const int hr = (halo_rows_needed(g, 256) + 63) / 64;
+      if (bn == 64) {
+        if (hr <= 5) launch_halo<64, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+        else if (hr <= 6) launch_halo<64, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+        else launch_halo<64, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+        DM_CHECK(hipGetLastError());
+        return;
+      }
       if (hr <= 5) launch_halo<128, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
       else if (hr <= 6) launch_halo<128, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
       else launch_halo<128, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);

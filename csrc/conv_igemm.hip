@@ -1457,6 +1457,11 @@ bool halo_cfg(int cfg, int& bn, int& waves) {
     waves = (cfg == 42 ? 4 : 16) | 0x100;
     return true;
   }
+  if (cfg == 44 || cfg == 45) {  // 41 / 39 with two weight tiles of register prefetch
+    bn = 64;
+    waves = (cfg == 44 ? 32 : 16) | 0x100;
+    return true;
+  }
   if (!(cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39) || cfg == 41))
     return false;
   bn = (cfg == 20 || cfg == 24 || cfg == 36 || cfg == 38) ? 128 : 64;
@@ -1533,7 +1538,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { if (cfg == 50 || cfg == 51) return conv_h5_rowtile(cfg); if (cfg == 60 || cfg == 70) return 256; return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { if (cfg == 50 || cfg == 51) return conv_h5_rowtile(cfg); if (cfg == 60 || cfg == 70) return 256; return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43 || cfg == 44 || cfg == 45) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -206,22 +206,31 @@ constexpr int FW = 112;        // widest row supported (ResNet stem at 224: 112)
 constexpr int FDP = 80;        // dY tile pitch (elements, 160 B rows: conflict-free tr reads)
 constexpr int FR = 2 * FW;     // pixel rows per row pair
 constexpr int FXH = 5 * FW;    // input halo pixels (rows y0-2 .. y0+2)
+constexpr int FWP = FW + 3;    // padded halo row: 2 zero pixels left, 1 right (x = -2 .. W)
 
+// Per row pair the work is mostly VALU (the quad gather + BN apply of 4 x 8 values per thread
+// and, in the first version, ~60 address instructions per MFMA k-step), so the loop keeps the
+// VALU side lean: the halo rows carry zero pad columns (every 4x4 tap read is in bounds, the
+// zero padding comes from the pads and from the zero rows outside the image), every LDS
+// address of the k-loop is a per-lane base + a compile-time offset, and the global offsets
+// are 32-bit (all tensors < 2^31 elements, checked by stem_wgrad_fused_supported).
 __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ds = reinterpret_cast<bf16_t*>(smem);  // [FR][FDP] dy tile
-  bf16_t* Xs = Ds + FR * FDP;                     // [FXH + 1][16] input halo, last = zeros
-  float* cf = reinterpret_cast<float*>(Xs + (FXH + 1) * SC);  // [5][64] a, b, cc, sc, sh
+  bf16_t* Xs = Ds + FR * FDP;                     // [5][FWP][16] padded input halo
+  float* cf = reinterpret_cast<float*>(Xs + 5 * FWP * SC);  // [5][64] a, b, cc, sc, sh
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int W = a.W, H = a.H, W2 = W >> 1, H2 = H >> 1;
   const int R = 2 * W, nks = (R + 31) >> 5;
+  const int WP = W + 3;
   const long long total = (long long)a.N * H2;
   const long long s0 = (long long)blockIdx.x * a.spb;
   const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
 
   for (int i = tid; i < FR * FDP / 8; i += 512)
     reinterpret_cast<uint4*>(Ds)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
-  if (tid < 2) *reinterpret_cast<uint4*>(Xs + FXH * SC + tid * 8) = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < 5 * FWP * SC / 8; i += 512)
+    reinterpret_cast<uint4*>(Xs)[i] = make_uint4(0, 0, 0, 0);  // pad columns stay zero
   for (int c = tid; c < 64; c += 512) {
     cf[c] = a.coef[c];
     cf[64 + c] = a.coef[64 + c];
@@ -233,106 +242,105 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
   // staging roles: quad item tid (< W2 * 8): quad qb = tid >> 3, channel chunk tid & 7
   const int chunk = tid & 7, c0 = chunk * 8;
   const int nitems = W2 * 8;
-  uint4 qy[1][4], qg[1][4];
-  uint2 qi[1][4];
-  bool qok[1][4];
+  const bool qitem = tid < nitems;
+  const int qb = tid >> 3;
   constexpr int XI = (2 * FXH + 511) / 512;
+  // halo roles: 16-B piece e = tid + 512 i of the 5 x W x 32-B halo -> halo row hr, column x
+  int xh_row[XI], xh_lds[XI];
+#pragma unroll
+  for (int i = 0; i < XI; ++i) {
+    const int e = tid + 512 * i, pix = e >> 1;
+    const int hr = pix / W, x = pix - hr * W;
+    xh_row[i] = pix < 5 * W ? hr : 1 << 20;  // invalid pieces: never in range
+    xh_lds[i] = ((hr * WP + x + 2) * SC + (e & 1) * 8) * 2;
+  }
+  uint4 qy[4], qg[4];
+  uint2 qi[4];
   uint4 xv[XI];
+  unsigned qok = 0;
   auto load = [&](long long s) {
     const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
-#pragma unroll
-    for (int u = 0; u < 1; ++u) {
-      const int it = tid;
-      if (it >= nitems) continue;
-      const int qb = it >> 3;
-      const long long pix0 = ((long long)n * H + 2 * qa) * W + 2 * qb;
+    if (qitem) {
+      const unsigned pix0 = ((unsigned)n * H + 2 * qa) * W + 2 * qb;
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        qy[u][p] = reinterpret_cast<const uint4*>(a.y)[(pix0 + (p >> 1) * W + (p & 1)) * 8 + chunk];
+        qy[p] = reinterpret_cast<const uint4*>(a.y)[(pix0 + (p >> 1) * W + (p & 1)) * 8 + chunk];
+      qok = 0;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const int oh = qa + (w >> 1), ow = qb + (w & 1);
-        qok[u][w] = oh < H2 && ow < W2;
-        const long long o = (((long long)n * H2 + (qok[u][w] ? oh : qa)) * W2 + (qok[u][w] ? ow : qb)) * 8 + chunk;
-        qi[u][w] = reinterpret_cast<const uint2*>(a.pidx)[o];
-        qg[u][w] = reinterpret_cast<const uint4*>(a.pdy)[o];
+        const bool ok = oh < H2 && ow < W2;
+        qok |= ok ? 1u << w : 0u;
+        const unsigned o = (((unsigned)n * H2 + (ok ? oh : qa)) * W2 + (ok ? ow : qb)) * 8 + chunk;
+        qi[w] = reinterpret_cast<const uint2*>(a.pidx)[o];
+        qg[w] = reinterpret_cast<const uint4*>(a.pdy)[o];
       }
     }
-    const int y0 = 2 * qa;
+    const int ylo = 2 - 2 * qa, yhi = H + 2 - 2 * qa;  // halo rows inside the image
+    const bf16_t* xb = a.xs + (((long long)n * H + 2 * qa - 2) * W) * SC;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
-      const int hr = pix / W, x = pix - hr * W;
-      const int yy = y0 - 2 + hr;
       xv[i] = make_uint4(0, 0, 0, 0);
-      if (pix < 5 * W && yy >= 0 && yy < H)
-        xv[i] = *reinterpret_cast<const uint4*>(a.xs + (((long long)n * H + yy) * W + x) * SC + half * 8);
+      if (xh_row[i] >= ylo && xh_row[i] < yhi)
+        xv[i] = *reinterpret_cast<const uint4*>(xb + (tid + 512 * i) * 8);
     }
   };
   // gather dz per quad (bn_bwd_apply_quad's terms, same order), dy to LDS; halo to LDS
   auto store = [&]() {
-    float ca[8], cb[8], cc[8], ms[8], mh[8];
+    if (qitem) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ca[j] = cf[c0 + j];
-      cb[j] = cf[64 + c0 + j];
-      cc[j] = cf[128 + c0 + j];
-      ms[j] = cf[192 + c0 + j];
-      mh[j] = cf[256 + c0 + j];
-    }
+      for (int p = 0; p < 4; ++p) {
+        const int ddy = p >> 1, ddx = p & 1;
+        float d[8];
 #pragma unroll
-    for (int u = 0; u < 1; ++u) {
-      const int it = tid;
-      if (it >= nitems) continue;
-      const int qb = it >> 3;
-      float d[4][8];
+        for (int j = 0; j < 8; ++j) d[j] = 0.f;
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[p][j] = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        if (!qok[u][w]) continue;
-        const int wa = w >> 1, wb = w & 1;
-        float gg[8];
-        s_unpack8(qg[u][w], gg);
-        const uint32_t aw[2] = {qi[u][w].x, qi[u][w].y};
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const int ddy = p >> 1, ddx = p & 1;
+        for (int w = 0; w < 4; ++w) {
+          const int wa = w >> 1, wb = w & 1;
           if (wa == 1 && ddy == 0) continue;
           if (wb == 1 && ddx == 0) continue;
+          if (!(qok & (1u << w))) continue;
+          float gg[8];
+          s_unpack8(qg[w], gg);
+          const uint32_t aw[2] = {qi[w].x, qi[w].y};
           const unsigned code = (unsigned)((ddy ? (wa ? 0 : 2) : 1) * 3 + (ddx ? (wb ? 0 : 2) : 1));
 #pragma unroll
           for (int j = 0; j < 8; ++j)
-            if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[p][j] += gg[j];
+            if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += gg[j];
         }
-      }
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
         float yv[8];
-        s_unpack8(qy[u][p], yv);
+        s_unpack8(qy[p], yv);
         uint32_t o[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float r2[2];
+        for (int h = 0; h < 2; ++h) {
+          const float4 ca = *reinterpret_cast<const float4*>(cf + c0 + 4 * h);
+          const float4 cb = *reinterpret_cast<const float4*>(cf + 64 + c0 + 4 * h);
+          const float4 cc = *reinterpret_cast<const float4*>(cf + 128 + c0 + 4 * h);
+          const float4 ms = *reinterpret_cast<const float4*>(cf + 192 + c0 + 4 * h);
+          const float4 mh = *reinterpret_cast<const float4*>(cf + 256 + c0 + 4 * h);
+          const float av[4] = {ca.x, ca.y, ca.z, ca.w}, bv[4] = {cb.x, cb.y, cb.z, cb.w};
+          const float cv[4] = {cc.x, cc.y, cc.z, cc.w}, sv[4] = {ms.x, ms.y, ms.z, ms.w};
+          const float hv[4] = {mh.x, mh.y, mh.z, mh.w};
 #pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int j = 2 * k + e;
-            const float dz = (yv[j] * ms[j] + mh[j]) > 0.f ? d[p][j] : 0.f;
-            r2[e] = ca[j] * dz + cb[j] * yv[j] + cc[j];
+          for (int k = 0; k < 2; ++k) {
+            float r2[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int jj = 2 * k + e, j = 4 * h + jj;
+              const float dz = (yv[j] * sv[jj] + hv[jj]) > 0.f ? d[j] : 0.f;
+              r2[e] = av[jj] * dz + bv[jj] * yv[j] + cv[jj];
+            }
+            o[2 * h + k] = pack_bf2(r2[0], r2[1]);
           }
-          o[k] = pack_bf2(r2[0], r2[1]);
         }
-        const int lp = (p >> 1) * W + 2 * qb + (p & 1);
+        const int lp = ddy * W + 2 * qb + ddx;
         *reinterpret_cast<uint4*>(Ds + lp * FDP + c0) = make_uint4(o[0], o[1], o[2], o[3]);
       }
     }
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
-      if (pix < 5 * W) *reinterpret_cast<uint4*>(Xs + pix * SC + half * 8) = xv[i];
-    }
+    for (int i = 0; i < XI; ++i)
+      if (xh_row[i] < 5)
+        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(Xs) + xh_lds[i]) = xv[i];
   };
 
   f32x4 acc[2][4];
@@ -345,43 +353,36 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
   const int rbase = grp * 4 + q;
   const int th = wid & 3;          // kernel row of this wave: dy = th - 2
   const int cob = (wid >> 2) * 32;  // first output channel of this wave
+  // per-lane LDS bases: dy rows of k-step ks start at dsb + ks * 32 * FDP; the halo pixel of
+  // row r (pair-local, r < R) and tap column 0 is halo row (r >= W) + th, column r mod W - 2
+  const bf16_t* dsb = Ds + rbase * FDP + cob + 4 * pp;
+  auto xrow = [&](int r) -> const bf16_t* {
+    if (r >= R) r = 0;  // dy rows past the pair are zero: any in-bounds halo pixel will do
+    const int rr = r >= W ? 1 : 0;
+    return Xs + ((rr + th) * WP + (r - rr * W)) * SC + 4 * pp;
+  };
 
   if (s0 < s1) load(s0);
   __syncthreads();  // zeroed tiles, coefficients
   for (long long s = s0; s < s1; ++s) {
     store();
     __syncthreads();
-    const int qa = (int)(s % H2);
     if (s + 1 < s1) load(s + 1);
-    const int y0 = 2 * qa;
     for (int ks = 0; ks < nks; ++ks) {
-      int rlo[2], okrow[2], xr[2], rr[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = ks * 32 + rbase + 16 * u;
-        rlo[u] = r;
-        rr[u] = r >= W ? 1 : 0;
-        xr[u] = r - rr[u] * W;
-        okrow[u] = r < R && (unsigned)(y0 + rr[u] + th - 2) < (unsigned)H;
-      }
+      const bf16_t* dk = dsb + ks * 32 * FDP;
       bf16x8 af[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const s4v lo = tr_read4(Ds + rlo[0] * FDP + cob + i * 16 + 4 * pp);
-        const s4v hi = tr_read4(Ds + rlo[1] * FDP + cob + i * 16 + 4 * pp);
+        const s4v lo = tr_read4(dk + i * 16);
+        const s4v hi = tr_read4(dk + 16 * FDP + i * 16);
         af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
+      const bf16_t* x0 = xrow(ks * 32 + rbase);
+      const bf16_t* x1 = xrow(ks * 32 + rbase + 16);
 #pragma unroll
       for (int tw = 0; tw < 4; ++tw) {
-        const bf16_t* src[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int xx = xr[u] + tw - 2;
-          const bool ok = okrow[u] && (unsigned)xx < (unsigned)W;
-          src[u] = ok ? Xs + ((rr[u] + th) * W + xx) * SC + 4 * pp : Xs + FXH * SC + 4 * pp;
-        }
-        const s4v lo = tr_read4(src[0]);
-        const s4v hi = tr_read4(src[1]);
+        const s4v lo = tr_read4(x0 + tw * SC);
+        const s4v hi = tr_read4(x1 + tw * SC);
         const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -555,20 +556,31 @@ bool stem_wgrad_fused_supported(int N, int H, int W, int C, int Cpad) {
          (long long)N * H * W * 64 < (1LL << 31);
 }
 
-int stem_wgrad_fused_blocks(int N, int H) {
+static int stem_blocks_capped(int N, int H, long long cap) {
   const long long pairs = (long long)N * (H / 2);
-  // one block per CU; each block's slab is 64 KB
-  long long b = pairs < 256 ? pairs : 256;
+  long long b = pairs < cap ? pairs : cap;
   const long long spb = (pairs + b - 1) / b;
   return (int)((pairs + spb - 1) / spb);
 }
+
+// fused kernel: one 512-thread block per CU; each block's slab is 64 KB.
+// DMLAB_STEM_BLOCKS overrides the cap (A/B runs)
+int stem_wgrad_fused_blocks(int N, int H) {
+  long long cap = 256;
+  if (const char* e = getenv("DMLAB_STEM_BLOCKS"))
+    if (atoi(e) > 0) cap = atoi(e);
+  return stem_blocks_capped(N, H, cap);
+}
+
+// stem_wgrad_dy_kernel (174 VGPRs): one block per CU
+int stem_wgrad_dy_blocks(int N, int H) { return stem_blocks_capped(N, H, 256); }
 
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st) {
   const long long pairs = (long long)N * (H / 2);
   StemBwdArgs a{xs, y, pdy, pidx, coef, sc, sh, slab, N, H, W, (int)((pairs + S - 1) / S)};
-  const size_t sm = (size_t)FR * FDP * 2 + (size_t)(FXH + 1) * SC * 2 + 5 * 64 * 4;
+  const size_t sm = (size_t)FR * FDP * 2 + (size_t)5 * FWP * SC * 2 + 5 * 64 * 4;
   set_smem_attr(stem_wgrad_fused_kernel, sm);
   stem_wgrad_fused_kernel<<<S, 512, sm, st>>>(a);
   DM_CHECK(hipGetLastError());

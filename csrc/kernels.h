@@ -83,6 +83,7 @@ void bn_bwd_apply_quad(const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx, 
 void stem_wgrad_dy(const bf16_t* xs, const bf16_t* dy, float* slab, int N, int H, int W, int S,
                    hipStream_t st);
 int stem_wgrad_fused_blocks(int N, int H);
+int stem_wgrad_dy_blocks(int N, int H);
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st);

@@ -45,6 +45,12 @@ def _cpad(c):
 #     (one workgroup per CU exposes the staging latency).
 TILE_CFG = (15, 13, 11)
 _STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
+# 44 / 45: the 41 / 39 halo tiles with two weight tiles of register prefetch (a weight load
+# gets two tap steps of MFMA work to land in instead of one)
+_HALO_PF2 = os.environ.get("DMLAB_HALO_PF2", "0") == "1"
+# per-output-channel override of the unit-stride 3x3 halo cfg, e.g. "64=44,128=44" (A/B runs)
+_HALO_MAP = {int(k): int(v) for k, v in (kv.split("=") for kv in
+             os.environ.get("DMLAB_HALO_MAP", "").split(",") if kv)}
 
 
 def pick_cfg(M, ncols, k=0, stride=0, cin=0):
@@ -63,9 +69,11 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
         #   layer3 (256 ch): 41 852/867, 42 834/840                (b256: 41 722/762)
         #   layer4 (512 ch): 41 856/867, 43 812/820                (b256: 41 822/848)
         #   layer1 (64 ch) : 39 612/683, 41 580/642
+        if ncols in _HALO_MAP:
+            return _HALO_MAP[ncols]
         if ncols >= 256:
-            return 41
-        return 42 if ncols >= 128 else 39
+            return 44 if _HALO_PF2 else 41
+        return 42 if ncols >= 128 else (45 if _HALO_PF2 else 39)
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
         t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
     elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
@@ -244,7 +252,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43):
+        if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43, 44, 45):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)
@@ -464,21 +472,31 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     side = getattr(layer._prog, "_wgrad_stream", None)
     if side is not None and layer.cout < _SIDE_MIN_COUT:
         side = None
-    if side is not None:
-        side.wait_stream(torch.cuda.current_stream())
-        for t in (x, dy) + (tuple(pre) if pre is not None else ()):
-            t.record_stream(side)
-    with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-        slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
-        pre_kw = {}
-        xw = x
-        if pre is not None:
-            if wcfg in (4, 5):
-                pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
-            else:
-                xw = _materialise(x, pre)
-        L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S, wcfg,
-                     s2d, **pre_kw)
+
+    def launch_wgrad():
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            for t in (x, dy) + (tuple(pre) if pre is not None else ()):
+                t.record_stream(side)
+        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
+            slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
+            pre_kw = {}
+            xw = x
+            if pre is not None:
+                if wcfg in (4, 5):
+                    pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
+                else:
+                    xw = _materialise(x, pre)
+            L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S,
+                         wcfg, s2d, **pre_kw)
+
+    deferred = getattr(layer._prog, "_deferred_wgrads", None) if side is not None else None
+    if deferred is not None:
+        # the Program launches it later (Program.backward: DMLAB_DEFER_WGRAD), e.g. next to
+        # the latency-bound stem backward instead of under this block's dgrads
+        deferred.append(launch_wgrad)
+    else:
+        launch_wgrad()
     dx = None
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)

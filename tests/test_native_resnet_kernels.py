@@ -29,7 +29,7 @@ HALO_GEOMS = [
     (3, 14, 256, 256, 3, 1, 1),
     (2, 14, 64, 128, 1, 1, 0),
 ]
-FWD_CFGS = list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39, 41, 42, 43]
+FWD_CFGS = list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39, 41, 42, 43, 44, 45]
 
 
 def _rel(a, b):
@@ -64,7 +64,7 @@ def test_conv_fwd_and_stats(dev, geom, cfg):
 
 
 @pytest.mark.parametrize("geom", HALO_GEOMS)
-@pytest.mark.parametrize("cfg", [12, 20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43])
+@pytest.mark.parametrize("cfg", [12, 20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43, 44, 45])
 def test_conv_fwd_halo(dev, geom, cfg):
     _check_fwd(dev, geom, cfg)
 
@@ -224,7 +224,7 @@ def test_conv_dgrad(dev, geom, accumulate, variant):
 
 @pytest.mark.parametrize("geom", HALO_GEOMS + GEOMS[:2] + GEOMS[3:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39, 41, 42, 43])
+@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39, 41, 42, 43, 44, 45])
 def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
@@ -497,7 +497,7 @@ def test_bn_stats_finalize_slab_rows(dev, T):
 
 
 @pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3] + L1_GEOMS[1:])
-@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 50, 51, 70])
+@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 44, 45, 50, 51, 70])
 def test_conv_fwd_prebn(dev, geom, cfg):
     """Halo conv consuming relu(y*scale + shift) of a RAW previous-conv output (fused
     BN-apply + ReLU in the staging); zero padding stays zero after the BN."""
@@ -571,7 +571,7 @@ def test_pack_weights_tiled_matches_per_layer(dev):
                                   (2, 7, 128, 256, 3, 1, 1)])
 @pytest.mark.parametrize("mode", [0, 1, 2, 4])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 41, 42, 43, 50])
+@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 41, 42, 43, 44, 45, 50])
 def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     """The dgrad epilogue's BN-backward sums (Σdz, Σdz·x̂ of the BN whose input gradient dx
     is) equal the sums over the stored dx; the BN backward run from them equals the

@@ -100,3 +100,42 @@ def test_fused_stem_backward_matches_unfused(dev, res, variant):
             assert _rel(grads[1][n], grads[0][n]) < 2e-3, n
         else:
             torch.testing.assert_close(grads[1][n], grads[0][n], rtol=0, atol=0, msg=n)
+
+
+@pytest.mark.parametrize("defer", [1, 2])
+def test_deferred_wgrads_match(dev, monkeypatch, defer):
+    """DMLAB_DEFER_WGRAD holds the weight gradients of layers 1..d back until the stem's
+    backward: every gradient is bit-identical, and each layer's grad hook (DDP's bucket
+    launch point) still sees its finished weight gradients on the main stream."""
+    torch.manual_seed(5)
+    a = ResNet18(num_classes=10).to(dev)
+    x = torch.rand(8, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    runs = []
+    for d in (0, defer):
+        monkeypatch.setenv("DMLAB_DEFER_WGRAD", str(d))
+        snaps = {}
+
+        def hook(prog, i):
+            # runs on the main stream after the wait for layer i's side-stream wgrads
+            snaps[i] = [p.grad.detach().clone() for p in prog.layers[i].parameters()]
+
+        a._grad_hooks.append(hook)
+        try:
+            a.flat.grad.zero_()
+            cross_entropy(a(x), y).backward()
+            torch.cuda.synchronize()
+        finally:
+            a._grad_hooks.remove(hook)
+        assert sorted(snaps) == list(range(len(a.layers)))
+        runs.append(({n: p.grad.detach().clone() for n, p in a.named_parameters()}, snaps))
+    (g0, s0), (g1, s1) = runs
+    for n in g0:
+        torch.testing.assert_close(g1[n], g0[n], rtol=0, atol=0, msg=n)
+    for i in s0:
+        for u, v in zip(s1[i], s0[i]):
+            torch.testing.assert_close(u, v, rtol=0, atol=0, msg=f"hook {i}")
+        # the hook snapshot is the final gradient
+        for u, p in zip(s1[i], a.layers[i].parameters()):
+            torch.testing.assert_close(u, g1[[n for n, q in a.named_parameters() if q is p][0]],
+                                       rtol=0, atol=0)

@@ -2,16 +2,16 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-t=${1:-tail}
-timeout -k 10 600 python -u -m pytest tests/test_native_resnet_kernels.py tests/test_native_resnet_model.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$t.log 2>&1 || { tail -40 gpurun_out/pytest_$t.log; exit 1; }
-tail -2 gpurun_out/pytest_$t.log
-timeout -k 10 300 python tools/bench_conv.py --batch 512 --iters 20 --cfgs 41 --passes fwd,dgrad --shapes l3_3x3,l4_3x3 > gpurun_out/conv_${t}_on.jsonl 2>&1 && DMLAB_TAIL_SPLIT=0 timeout -k 10 300 python tools/bench_conv.py --batch 512 --iters 20 --cfgs 41 --passes fwd,dgrad --shapes l3_3x3,l4_3x3 > gpurun_out/conv_${t}_off.jsonl 2>&1 && cat gpurun_out/conv_${t}_on.jsonl gpurun_out/conv_${t}_off.jsonl
-for f in 1 0 1 0 1 0; do
-DMLAB_TAIL_SPLIT=$f timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${t}_$f.json 2> gpurun_out/bench_${t}_$f.err || { tail -20 gpurun_out/bench_${t}_$f.err; exit 1; }
-echo "tail_split $f: $(python -c "import json;d=json.load(open('gpurun_out/bench_${t}_$f.json'));print(d['value'], d['ms_per_step'], d['final_loss'])")"
+t=${1:-stem2}
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_native_resnet_model.py -m gpu -k fused_stem > gpurun_out/test_${t}.log 2>&1 && tail -2 gpurun_out/test_${t}.log || { tail -40 gpurun_out/test_${t}.log; exit 1; }
+run() {  # tag, env...
+  local tag=$1; shift
+  env "$@" timeout -k 10 200 python bench.py --steps 80 --warmup 10 > gpurun_out/b_${t}.json 2>gpurun_out/b_${t}.err || exit 1
+  python -c "import json; d=json.load(open('gpurun_out/b_${t}.json')); print('$tag', d['value'], d['ms_per_step'])" | tee -a gpurun_out/bench_$t.txt
+}
+for r in 1 2; do
+  run fused DMLAB_STEM_BWD=fused
+  run split DMLAB_STEM_BWD=split
 done
-for v in "split igemm 4" "fused dy 4" "split igemm 8"; do
-set -- $v
-DMLAB_STEM_BWD=$1 DMLAB_STEM_WGRAD=$2 DMLAB_STEM_SPLIT=$3 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$t.json 2> gpurun_out/bench_$t.err || { tail -20 gpurun_out/bench_$t.err; exit 1; }
-echo "$v: $(python -c "import json;d=json.load(open('gpurun_out/bench_$t.json'));print(d['value'], d['ms_per_step'], d['final_loss'])")"
-done
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$t -o run -- python bench.py --steps 5 --warmup 3 > gpurun_out/prof_$t.log 2>&1 || exit 1
+python tools/prof_summary.py gpurun_out/prof_$t/run_results.db 8 | grep -i -E "stem|total"
