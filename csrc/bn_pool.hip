@@ -740,6 +740,11 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
     }
     reinterpret_cast<uint4*>(out)[i] = pack8(best);
     if (yarg) reinterpret_cast<uint4*>(yarg)[i] = pack8(raw);  // raw is bf16-exact
+    // a window whose max is 0 (every BN value <= 0) passes no gradient: its ReLU mask at
+    // the argmax is 0.  Code 15 (no window position) says so, so the backward gathers need
+    // no mask of their own (the stem's fused weight-gradient kernel relies on this)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) arg[j] = best[j] > 0.f ? arg[j] : 15;
     uint2 a2;
     a2.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
     a2.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);

@@ -258,31 +258,42 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
   uint2 qi[4];
   uint4 xv[XI];
   unsigned qok = 0;
+  const unsigned npix = (unsigned)a.N * H * W, npool = (unsigned)a.N * H2 * W2;
+  const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)(npix * 128u), 0x00020000);
+  const auto rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.pdy, (short)0, (int)(npool * 128u), 0x00020000);
+  const auto ri = __builtin_amdgcn_make_buffer_rsrc((void*)a.pidx, (short)0, (int)(npool * 64u), 0x00020000);
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.xs, (short)0, (int)(npix * 32u), 0x00020000);
+  auto ld16 = [](decltype(ry) r, unsigned off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+  };
   auto load = [&](long long s) {
     const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
     if (qitem) {
       const unsigned pix0 = ((unsigned)n * H + 2 * qa) * W + 2 * qb;
 #pragma unroll
       for (int p = 0; p < 4; ++p)
-        qy[p] = reinterpret_cast<const uint4*>(a.y)[(pix0 + (p >> 1) * W + (p & 1)) * 8 + chunk];
+        qy[p] = ld16(ry, (pix0 + (p >> 1) * W + (p & 1)) * 128u + chunk * 16u);
       qok = 0;
 #pragma unroll
       for (int w = 0; w < 4; ++w) {
         const int oh = qa + (w >> 1), ow = qb + (w & 1);
         const bool ok = oh < H2 && ow < W2;
         qok |= ok ? 1u << w : 0u;
-        const unsigned o = (((unsigned)n * H2 + (ok ? oh : qa)) * W2 + (ok ? ow : qb)) * 8 + chunk;
-        qi[w] = reinterpret_cast<const uint2*>(a.pidx)[o];
-        qg[w] = reinterpret_cast<const uint4*>(a.pdy)[o];
+        const unsigned o = ((unsigned)n * H2 + (ok ? oh : qa)) * W2 + (ok ? ow : qb);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(ri, o * 64u + chunk * 8u, 0, 0);
+        qi[w] = make_uint2(v[0], v[1]);
+        qg[w] = ld16(rg, o * 128u + chunk * 16u);
       }
     }
     const int ylo = 2 - 2 * qa, yhi = H + 2 - 2 * qa;  // halo rows inside the image
-    const bf16_t* xb = a.xs + (((long long)n * H + 2 * qa - 2) * W) * SC;
+    // byte offset of halo row 0 (may be "negative" for the first pair of an image: those
+    // rows are never read)
+    const unsigned xb = ((unsigned)n * H + 2 * qa - 2) * (unsigned)W * 32u;
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       xv[i] = make_uint4(0, 0, 0, 0);
-      if (xh_row[i] >= ylo && xh_row[i] < yhi)
-        xv[i] = *reinterpret_cast<const uint4*>(xb + (tid + 512 * i) * 8);
+      if (xh_row[i] >= ylo && xh_row[i] < yhi) xv[i] = ld16(rx, xb + (tid + 512 * i) * 16u);
     }
   };
   // gather dz per quad (bn_bwd_apply_quad's terms, same order), dy to LDS; halo to LDS
@@ -316,19 +327,17 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
           const float4 ca = *reinterpret_cast<const float4*>(cf + c0 + 4 * h);
           const float4 cb = *reinterpret_cast<const float4*>(cf + 64 + c0 + 4 * h);
           const float4 cc = *reinterpret_cast<const float4*>(cf + 128 + c0 + 4 * h);
-          const float4 ms = *reinterpret_cast<const float4*>(cf + 192 + c0 + 4 * h);
-          const float4 mh = *reinterpret_cast<const float4*>(cf + 256 + c0 + 4 * h);
           const float av[4] = {ca.x, ca.y, ca.z, ca.w}, bv[4] = {cb.x, cb.y, cb.z, cb.w};
-          const float cv[4] = {cc.x, cc.y, cc.z, cc.w}, sv[4] = {ms.x, ms.y, ms.z, ms.w};
-          const float hv[4] = {mh.x, mh.y, mh.z, mh.w};
+          const float cv[4] = {cc.x, cc.y, cc.z, cc.w};
 #pragma unroll
           for (int k = 0; k < 2; ++k) {
             float r2[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
               const int jj = 2 * k + e, j = 4 * h + jj;
-              const float dz = (yv[j] * sv[jj] + hv[jj]) > 0.f ? d[j] : 0.f;
-              r2[e] = av[jj] * dz + bv[jj] * yv[j] + cv[jj];
+              // no ReLU mask: a masked window's code is 15 (bn_relu_maxpool_kernel), so its
+              // gradient was never gathered into d
+              r2[e] = av[jj] * d[j] + bv[jj] * yv[j] + cv[jj];
             }
             o[2 * h + k] = pack_bf2(r2[0], r2[1]);
           }
