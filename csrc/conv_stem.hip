@@ -414,6 +414,259 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
       }
 }
 
+// ------------------------------------------------------------------ warp-specialised variant
+// Same result as stem_wgrad_fused_kernel, but the VALU-heavy dy construction (quad gather +
+// BN apply, ~70 % of that kernel's cycles) and the MFMA reduction no longer alternate in
+// every wave.  Waves 0-3 (producers) build the dy tile of pair s+1 while waves 4-7
+// (consumers) reduce pair s; the tiles (dy and the input halo) are double-buffered in LDS
+// and one barrier per pair hands them over.  Waves w and w+4 share a SIMD (a workgroup's
+// waves go to the SIMDs cyclically), so every SIMD runs one producer beside one consumer.
+//   producers: two quad items per thread (A, B); A's loads for pair s+2 are issued right
+//              after A's tile is written and land while B's tile is built (and vice versa)
+//   consumers: wave 4 + t owns kernel row t, all 64 output channels x 4 taps x 16 channels
+//              (16 accumulators); they also stage the next pair's halo into LDS
+__global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Ds0 = reinterpret_cast<bf16_t*>(smem);  // [2][FR][FDP] dy tiles
+  bf16_t* Xs0 = Ds0 + 2 * FR * FDP;               // [2][5][FWP][16] padded halos
+  float* cf = reinterpret_cast<float*>(Xs0 + 2 * 5 * FWP * SC);  // [3][64] a, b, cc
+  constexpr int DSZ = FR * FDP, XSZ = 5 * FWP * SC;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int W = a.W, H = a.H, W2 = W >> 1, H2 = H >> 1;
+  const int R = 2 * W, nks = (R + 31) >> 5;
+  const int WP = W + 3;
+  const long long total = (long long)a.N * H2;
+  const long long s0 = (long long)blockIdx.x * a.spb;
+  const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
+  const int np = s1 > s0 ? (int)(s1 - s0) : 0;
+
+  for (int i = tid; i < 2 * DSZ / 8; i += 512)
+    reinterpret_cast<uint4*>(Ds0)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
+  for (int i = tid; i < 2 * XSZ / 8; i += 512)
+    reinterpret_cast<uint4*>(Xs0)[i] = make_uint4(0, 0, 0, 0);  // pad columns stay zero
+  for (int c = tid; c < 64; c += 512) {
+    cf[c] = a.coef[c];
+    cf[64 + c] = a.coef[64 + c];
+    cf[128 + c] = a.coef[128 + c];
+  }
+  const unsigned npix = (unsigned)a.N * H * W, npool = (unsigned)a.N * H2 * W2;
+  __syncthreads();
+
+  if (wid < 4) {
+    // ---------------------------------------------------------------- producers
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)(npix * 128u), 0x00020000);
+    const auto rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.pdy, (short)0, (int)(npool * 128u), 0x00020000);
+    const auto ri = __builtin_amdgcn_make_buffer_rsrc((void*)a.pidx, (short)0, (int)(npool * 64u), 0x00020000);
+    const int nitems = W2 * 8;
+    struct Item {
+      uint4 qy[4], qg[4];
+      uint2 qi[4];
+      unsigned ok;
+    };
+    auto ld16 = [](decltype(ry) r, unsigned off) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+      return make_uint4(v[0], v[1], v[2], v[3]);
+    };
+    auto load = [&](Item& I, int it, long long s) {
+      if (it >= nitems) return;
+      const int chunk = it & 7, qb = it >> 3;
+      const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
+      const unsigned pix0 = ((unsigned)n * H + 2 * qa) * W + 2 * qb;
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+        I.qy[p] = ld16(ry, (pix0 + (p >> 1) * W + (p & 1)) * 128u + chunk * 16u);
+      I.ok = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int oh = qa + (w >> 1), ow = qb + (w & 1);
+        const bool ok = oh < H2 && ow < W2;
+        I.ok |= ok ? 1u << w : 0u;
+        const unsigned o = ((unsigned)n * H2 + (ok ? oh : qa)) * W2 + (ok ? ow : qb);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(ri, o * 64u + chunk * 8u, 0, 0);
+        I.qi[w] = make_uint2(v[0], v[1]);
+        I.qg[w] = ld16(rg, o * 128u + chunk * 16u);
+      }
+    };
+    // dz gathered from the pooled gradient (masked windows carry code 15), dy = a dz + b y + cc
+    auto store = [&](const Item& I, int it, bf16_t* Ds) {
+      if (it >= nitems) return;
+      const int chunk = it & 7, qb = it >> 3, c0 = chunk * 8;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int ddy = p >> 1, ddx = p & 1;
+        float d[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          const int wa = w >> 1, wb = w & 1;
+          if (wa == 1 && ddy == 0) continue;
+          if (wb == 1 && ddx == 0) continue;
+          if (!(I.ok & (1u << w))) continue;
+          float gg[8];
+          s_unpack8(I.qg[w], gg);
+          const uint32_t aw[2] = {I.qi[w].x, I.qi[w].y};
+          const unsigned code = (unsigned)((ddy ? (wa ? 0 : 2) : 1) * 3 + (ddx ? (wb ? 0 : 2) : 1));
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += gg[j];
+        }
+        float yv[8];
+        s_unpack8(I.qy[p], yv);
+        uint32_t o[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 ca = *reinterpret_cast<const float4*>(cf + c0 + 4 * h);
+          const float4 cb = *reinterpret_cast<const float4*>(cf + 64 + c0 + 4 * h);
+          const float4 cc = *reinterpret_cast<const float4*>(cf + 128 + c0 + 4 * h);
+          const float av[4] = {ca.x, ca.y, ca.z, ca.w}, bv[4] = {cb.x, cb.y, cb.z, cb.w};
+          const float cv[4] = {cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int j0 = 4 * h + 2 * k;
+            o[2 * h + k] = pack_bf2(av[2 * k] * d[j0] + bv[2 * k] * yv[j0] + cv[2 * k],
+                                    av[2 * k + 1] * d[j0 + 1] + bv[2 * k + 1] * yv[j0 + 1] + cv[2 * k + 1]);
+          }
+        }
+        const int lp = ddy * W + 2 * qb + ddx;
+        *reinterpret_cast<uint4*>(Ds + lp * FDP + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    };
+    const int itA = tid, itB = tid + 256;
+    Item A, B;
+    if (np > 0) {
+      load(A, itA, s0);
+      load(B, itB, s0);
+      store(A, itA, Ds0);
+      if (np > 1) load(A, itA, s0 + 1);
+      store(B, itB, Ds0);
+      if (np > 1) load(B, itB, s0 + 1);
+    }
+    __syncthreads();
+    for (int i = 0; i < np; ++i) {
+      bf16_t* Dn = Ds0 + ((i + 1) & 1) * DSZ;
+      if (i + 1 < np) {
+        store(A, itA, Dn);
+        if (i + 2 < np) load(A, itA, s0 + i + 2);
+        store(B, itB, Dn);
+        if (i + 2 < np) load(B, itB, s0 + i + 2);
+      }
+      __syncthreads();
+    }
+    return;
+  }
+  // ------------------------------------------------------------------ consumers
+  const int ct = tid - 256;  // 0..255
+  const int th = wid - 4;    // kernel row of this wave: dy = th - 2
+  const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.xs, (short)0, (int)(npix * 32u), 0x00020000);
+  constexpr int XC = (2 * FXH + 255) / 256;  // halo pieces per consumer thread
+  int xh_row[XC], xh_lds[XC];
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int e = ct + 256 * i, pix = e >> 1;
+    const int hr = pix / W, x = pix - hr * W;
+    xh_row[i] = pix < 5 * W ? hr : 1 << 20;
+    xh_lds[i] = ((hr * WP + x + 2) * SC + (e & 1) * 8) * 2;
+  }
+  uint4 xv[XC];
+  auto xload = [&](long long s) {
+    const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
+    const int ylo = 2 - 2 * qa, yhi = H + 2 - 2 * qa;
+    const unsigned xb = ((unsigned)n * H + 2 * qa - 2) * (unsigned)W * 32u;
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      xv[i] = make_uint4(0, 0, 0, 0);
+      if (xh_row[i] >= ylo && xh_row[i] < yhi) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rx, xb + (ct + 256 * i) * 16u, 0, 0);
+        xv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  auto xstore = [&](bf16_t* Xs) {
+#pragma unroll
+    for (int i = 0; i < XC; ++i)
+      if (xh_row[i] < 5)
+        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(Xs) + xh_lds[i]) = xv[i];
+  };
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int rbase = grp * 4 + q;
+  auto xrow = [&](const bf16_t* Xs, int r) -> const bf16_t* {
+    if (r >= R) r = 0;  // dy rows past the pair are zero: any in-bounds halo pixel will do
+    const int rr = r >= W ? 1 : 0;
+    return Xs + ((rr + th) * WP + (r - rr * W)) * SC + 4 * pp;
+  };
+  struct Frag {
+    bf16x8 af[4], bf[4];
+  };
+  auto frag = [&](Frag& F, const bf16_t* Ds, const bf16_t* Xs, int ks) {
+    const bf16_t* dk = Ds + (ks * 32 + rbase) * FDP + 4 * pp;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const s4v lo = tr_read4(dk + i * 16);
+      const s4v hi = tr_read4(dk + 16 * FDP + i * 16);
+      F.af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+    const bf16_t* x0 = xrow(Xs, ks * 32 + rbase);
+    const bf16_t* x1 = xrow(Xs, ks * 32 + rbase + 16);
+#pragma unroll
+    for (int tw = 0; tw < 4; ++tw) {
+      const s4v lo = tr_read4(x0 + tw * SC);
+      const s4v hi = tr_read4(x1 + tw * SC);
+      F.bf[tw] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  auto mma = [&](const Frag& F) {
+#pragma unroll
+    for (int tw = 0; tw < 4; ++tw)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc[i][tw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.af[i], F.bf[tw], acc[i][tw], 0, 0, 0);
+  };
+  if (np > 0) {
+    xload(s0);
+    xstore(Xs0);
+    if (np > 1) xload(s0 + 1);
+  }
+  __syncthreads();
+  Frag F0, F1;
+  for (int i = 0; i < np; ++i) {
+    if (i + 1 < np) {
+      xstore(Xs0 + ((i + 1) & 1) * XSZ);  // that buffer was last read in iteration i - 1
+      if (i + 2 < np) xload(s0 + i + 2);
+    }
+    const bf16_t* Ds = Ds0 + (i & 1) * DSZ;
+    const bf16_t* Xs = Xs0 + (i & 1) * XSZ;
+    // k-steps in pairs: the fragments of step ks+1 are read while step ks's MFMAs issue
+    frag(F0, Ds, Xs, 0);
+    for (int ks = 0; ks < nks; ks += 2) {
+      if (ks + 1 < nks) frag(F1, Ds, Xs, ks + 1);
+      mma(F0);
+      if (ks + 1 < nks) {
+        if (ks + 2 < nks) frag(F0, Ds, Xs, ks + 2);
+        mma(F1);
+      }
+    }
+    __syncthreads();
+  }
+  // slab[b][co][tap*16 + c]; 16x16 C map: col = lane & 15 (channel), row = (lane>>4)*4 + r (co)
+  float* out = a.slab + (long long)blockIdx.x * 64 * SK;
+  const int c = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int tw = 0; tw < 4; ++tw)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = i * 16 + (lane >> 4) * 4 + r;
+        out[(long long)co * SK + (th * 4 + tw) * SC + c] = acc[i][tw][r];
+      }
+}
+
 // ------------------------------------------------------------------ stem weight gradient
 // dW[co][tap*16 + c] = Σ_m dy[m][co] · xs[m + off(tap)][c] with dy read from memory (the
 // quad BN-backward apply wrote it).  Same row-pair steps, LDS images and MFMA loop as the
@@ -589,6 +842,15 @@ void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, cons
                       int H, int W, int S, hipStream_t st) {
   const long long pairs = (long long)N * (H / 2);
   StemBwdArgs a{xs, y, pdy, pidx, coef, sc, sh, slab, N, H, W, (int)((pairs + S - 1) / S)};
+  // DMLAB_STEM_WS=0: the single-role kernel (every wave builds dy, then reduces)
+  const char* ws = getenv("DMLAB_STEM_WS");
+  if (!ws || atoi(ws) != 0) {
+    const size_t sm = (size_t)2 * FR * FDP * 2 + (size_t)2 * 5 * FWP * SC * 2 + 3 * 64 * 4;
+    set_smem_attr(stem_wgrad_ws_kernel, sm);
+    stem_wgrad_ws_kernel<<<S, 512, sm, st>>>(a);
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   const size_t sm = (size_t)FR * FDP * 2 + (size_t)5 * FWP * SC * 2 + 5 * 64 * 4;
   set_smem_attr(stem_wgrad_fused_kernel, sm);
   stem_wgrad_fused_kernel<<<S, 512, sm, st>>>(a);
