@@ -417,20 +417,32 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
 // ------------------------------------------------------------------ warp-specialised variant
 // Same result as stem_wgrad_fused_kernel, but the VALU-heavy dy construction (quad gather +
 // BN apply, ~70 % of that kernel's cycles) and the MFMA reduction no longer alternate in
-// every wave.  Waves 0-3 (producers) build the dy tile of pair s+1 while waves 4-7
+// every wave.  Waves 0-7 (producers) build the dy tile of pair s+1 while waves 8-11
 // (consumers) reduce pair s; the tiles (dy and the input halo) are double-buffered in LDS
-// and one barrier per pair hands them over.  Waves w and w+4 share a SIMD (a workgroup's
-// waves go to the SIMDs cyclically), so every SIMD runs one producer beside one consumer.
-//   producers: two quad items per thread (A, B); A's loads for pair s+2 are issued right
-//              after A's tile is written and land while B's tile is built (and vice versa)
-//   consumers: wave 4 + t owns kernel row t, all 64 output channels x 4 taps x 16 channels
-//              (16 accumulators); they also stage the next pair's halo into LDS
-__global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
+// and one barrier per pair hands them over.  Waves w, w+4 and w+8 share a SIMD (a
+// workgroup's waves go to the SIMDs cyclically), so every SIMD runs two producers (one
+// producer alone cannot hide its own VALU / LDS latencies) beside one consumer.  Measured:
+// 4 + 4 waves 478 us, 8 + 4 420, 8 + 8 438 (128-VGPR budget: 1-deep y prefetch).
+//   producers: one quad item per thread; its y rows are loaded two pairs ahead; the pooled
+//              gradient rows come from a 3-slot LDS ring
+//   consumers: wave 8 + t owns kernel row t, all 64 output channels x 4 taps x 16 channels
+//              (16 accumulators); they also stage the next pair's halo and the pooled
+//              gradient rows into LDS
+// DIAG (timing diagnostics only, results wrong): 1 = consumers skip the MFMA k-loop,
+// 2 = producers skip the dy construction (loads still issued), 3 = both
+template <int DIAG>
+__global__ void __launch_bounds__(768) stem_wgrad_ws_kernel(StemBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ds0 = reinterpret_cast<bf16_t*>(smem);  // [2][FR][FDP] dy tiles
   bf16_t* Xs0 = Ds0 + 2 * FR * FDP;               // [2][5][FWP][16] padded halos
-  float* cf = reinterpret_cast<float*>(Xs0 + 2 * 5 * FWP * SC);  // [3][64] a, b, cc
-  constexpr int DSZ = FR * FDP, XSZ = 5 * FWP * SC;
+  // pooled-gradient rows in a PSL-slot ring: pair s reads pooled rows s and s + 1 (global
+  // row index = pair index); the consumers store row s + 3 while pair s + 1 is being built
+  // (loaded one iteration earlier, so a whole iteration covers its latency)
+  constexpr int PSL = 4;
+  bf16_t* Gs = Xs0 + 2 * 5 * FWP * SC;                            // [PSL][FW / 2 * 64] grads
+  uint8_t* Is = reinterpret_cast<uint8_t*>(Gs + PSL * (FW / 2) * 64);  // [PSL][FW / 2 * 64] codes
+  float* cf = reinterpret_cast<float*>(Is + PSL * (FW / 2) * 64);  // [3][64] a, b, cc
+  constexpr int DSZ = FR * FDP, XSZ = 5 * FWP * SC, GSZ = (FW / 2) * 64;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int W = a.W, H = a.H, W2 = W >> 1, H2 = H >> 1;
   const int R = 2 * W, nks = (R + 31) >> 5;
@@ -440,11 +452,11 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
   const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
   const int np = s1 > s0 ? (int)(s1 - s0) : 0;
 
-  for (int i = tid; i < 2 * DSZ / 8; i += 512)
+  for (int i = tid; i < 2 * DSZ / 8; i += 768)
     reinterpret_cast<uint4*>(Ds0)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
-  for (int i = tid; i < 2 * XSZ / 8; i += 512)
+  for (int i = tid; i < 2 * XSZ / 8; i += 768)
     reinterpret_cast<uint4*>(Xs0)[i] = make_uint4(0, 0, 0, 0);  // pad columns stay zero
-  for (int c = tid; c < 64; c += 512) {
+  for (int c = tid; c < 64; c += 768) {
     cf[c] = a.coef[c];
     cf[64 + c] = a.coef[64 + c];
     cf[128 + c] = a.coef[128 + c];
@@ -452,20 +464,12 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
   const unsigned npix = (unsigned)a.N * H * W, npool = (unsigned)a.N * H2 * W2;
   __syncthreads();
 
-  if (wid < 4) {
+  if (wid < 8) {
     // ---------------------------------------------------------------- producers
     const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)(npix * 128u), 0x00020000);
-    const auto rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.pdy, (short)0, (int)(npool * 128u), 0x00020000);
-    const auto ri = __builtin_amdgcn_make_buffer_rsrc((void*)a.pidx, (short)0, (int)(npool * 64u), 0x00020000);
     const int nitems = W2 * 8;
     struct Item {
-      uint4 qy[4], qg[4];
-      uint2 qi[4];
-      unsigned ok;
-    };
-    auto ld16 = [](decltype(ry) r, unsigned off) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-      return make_uint4(v[0], v[1], v[2], v[3]);
+      uint4 qy[4];
     };
     auto load = [&](Item& I, int it, long long s) {
       if (it >= nitems) return;
@@ -473,24 +477,36 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
       const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
       const unsigned pix0 = ((unsigned)n * H + 2 * qa) * W + 2 * qb;
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        I.qy[p] = ld16(ry, (pix0 + (p >> 1) * W + (p & 1)) * 128u + chunk * 16u);
-      I.ok = 0;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int oh = qa + (w >> 1), ow = qb + (w & 1);
-        const bool ok = oh < H2 && ow < W2;
-        I.ok |= ok ? 1u << w : 0u;
-        const unsigned o = ((unsigned)n * H2 + (ok ? oh : qa)) * W2 + (ok ? ow : qb);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(ri, o * 64u + chunk * 8u, 0, 0);
-        I.qi[w] = make_uint2(v[0], v[1]);
-        I.qg[w] = ld16(rg, o * 128u + chunk * 16u);
+      for (int p = 0; p < 4; ++p) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(
+            ry, (pix0 + (p >> 1) * W + (p & 1)) * 128u + chunk * 16u, 0, 0);
+        I.qy[p] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     };
     // dz gathered from the pooled gradient (masked windows carry code 15), dy = a dz + b y + cc
-    auto store = [&](const Item& I, int it, bf16_t* Ds) {
+    auto store = [&](const Item& I, int it, long long s, bf16_t* Ds) {
       if (it >= nitems) return;
+      if (DIAG & 2) {
+        // keep the loads live without the gather / apply
+        const int lp = 2 * (it >> 3);
+        *reinterpret_cast<uint4*>(Ds + lp * FDP + (it & 7) * 8) =
+            make_uint4(I.qy[0].x ^ I.qy[1].x ^ I.qy[2].x ^ I.qy[3].x, 0, 0, 0);
+        return;
+      }
       const int chunk = it & 7, qb = it >> 3, c0 = chunk * 8;
+      const int qa = (int)(s % H2);
+      // the quad's 4 windows: pooled rows s (+1), columns qb (+1); masked off the image
+      uint4 qg[4];
+      uint2 qi[4];
+      unsigned ok = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int wa = w >> 1, wb = w & 1;
+        ok |= (qa + wa < H2 && qb + wb < W2) ? 1u << w : 0u;
+        const int slot = (int)((s + wa) % PSL), col = qb + wb < W2 ? qb + wb : qb;
+        qg[w] = *reinterpret_cast<const uint4*>(Gs + slot * GSZ + col * 64 + c0);
+        qi[w] = *reinterpret_cast<const uint2*>(Is + slot * GSZ + col * 64 + c0);
+      }
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
         const int ddy = p >> 1, ddx = p & 1;
@@ -502,10 +518,10 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
           const int wa = w >> 1, wb = w & 1;
           if (wa == 1 && ddy == 0) continue;
           if (wb == 1 && ddx == 0) continue;
-          if (!(I.ok & (1u << w))) continue;
+          if (!(ok & (1u << w))) continue;
           float gg[8];
-          s_unpack8(I.qg[w], gg);
-          const uint32_t aw[2] = {I.qi[w].x, I.qi[w].y};
+          s_unpack8(qg[w], gg);
+          const uint32_t aw[2] = {qi[w].x, qi[w].y};
           const unsigned code = (unsigned)((ddy ? (wa ? 0 : 2) : 1) * 3 + (ddx ? (wb ? 0 : 2) : 1));
 #pragma unroll
           for (int j = 0; j < 8; ++j)
@@ -532,32 +548,36 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
         *reinterpret_cast<uint4*>(Ds + lp * FDP + c0) = make_uint4(o[0], o[1], o[2], o[3]);
       }
     };
-    const int itA = tid, itB = tid + 256;
-    Item A, B;
+    // one quad item per producer thread; y of pair s sits in register set (s - s0) & 1 and is
+    // loaded two pairs ahead
+    const int it = tid;
+    Item A0, A1;
+    if (np > 0) load(A0, it, s0);
+    if (np > 1) load(A1, it, s0 + 1);
+    __syncthreads();  // pooled rows s0 .. s0 + 2 staged
     if (np > 0) {
-      load(A, itA, s0);
-      load(B, itB, s0);
-      store(A, itA, Ds0);
-      if (np > 1) load(A, itA, s0 + 1);
-      store(B, itB, Ds0);
-      if (np > 1) load(B, itB, s0 + 1);
+      store(A0, it, s0, Ds0);
+      if (np > 2) load(A0, it, s0 + 2);
     }
     __syncthreads();
-    for (int i = 0; i < np; ++i) {
-      bf16_t* Dn = Ds0 + ((i + 1) & 1) * DSZ;
+    auto step = [&](int i, Item& A) {
       if (i + 1 < np) {
-        store(A, itA, Dn);
-        if (i + 2 < np) load(A, itA, s0 + i + 2);
-        store(B, itB, Dn);
-        if (i + 2 < np) load(B, itB, s0 + i + 2);
+        bf16_t* Dn = Ds0 + ((i + 1) & 1) * DSZ;
+        const long long sn = s0 + i + 1;
+        store(A, it, sn, Dn);
+        if (i + 3 < np) load(A, it, sn + 2);
       }
       __syncthreads();
+    };
+    for (int i = 0; i < np; i += 2) {
+      step(i, A1);
+      if (i + 1 < np) step(i + 1, A0);
     }
     return;
   }
   // ------------------------------------------------------------------ consumers
-  const int ct = tid - 256;  // 0..255
-  const int th = wid - 4;    // kernel row of this wave: dy = th - 2
+  const int ct = tid - 512;  // 0..255
+  const int th = wid - 8;    // kernel row of this wave: dy = th - 2
   const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.xs, (short)0, (int)(npix * 32u), 0x00020000);
   constexpr int XC = (2 * FXH + 255) / 256;  // halo pieces per consumer thread
   int xh_row[XC], xh_lds[XC];
@@ -569,6 +589,36 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
     xh_lds[i] = ((hr * WP + x + 2) * SC + (e & 1) * 8) * 2;
   }
   uint4 xv[XC];
+  // pooled row r (global index; rows past the tensor read as zeros): 448 16-B grad pieces and
+  // 448 8-B code pieces, two of each per consumer thread
+  const auto rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.pdy, (short)0, (int)(npool * 128u), 0x00020000);
+  const auto ri = __builtin_amdgcn_make_buffer_rsrc((void*)a.pidx, (short)0, (int)(npool * 64u), 0x00020000);
+  const int npc = W2 * 8;  // pieces per pooled row
+  uint4 pg[2];
+  uint2 pi[2];
+  auto pload = [&](long long r) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = ct + 256 * u;
+      const unsigned off = (unsigned)r * (unsigned)npc + (unsigned)e;  // piece index
+      const bool ok = e < npc && r < total;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rg, ok ? off * 16u : 0x80000000u, 0, 0);
+      pg[u] = make_uint4(v[0], v[1], v[2], v[3]);
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(ri, ok ? off * 8u : 0x80000000u, 0, 0);
+      pi[u] = make_uint2(w[0], w[1]);
+    }
+  };
+  auto pstore = [&](long long r) {
+    const int slot = (int)(r % PSL);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int e = ct + 256 * u;
+      if (e < npc) {
+        *reinterpret_cast<uint4*>(Gs + slot * GSZ + e * 8) = pg[u];
+        *reinterpret_cast<uint2*>(Is + slot * GSZ + e * 8) = pi[u];
+      }
+    }
+  };
   auto xload = [&](long long s) {
     const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
     const int ylo = 2 - 2 * qa, yhi = H + 2 - 2 * qa;
@@ -628,28 +678,38 @@ __global__ void __launch_bounds__(512) stem_wgrad_ws_kernel(StemBwdArgs a) {
         acc[i][tw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(F.af[i], F.bf[tw], acc[i][tw], 0, 0, 0);
   };
   if (np > 0) {
+#pragma unroll 1
+    for (int r = 0; r < 3; ++r) {
+      pload(s0 + r);
+      pstore(s0 + r);
+    }
+    if (np > 2) pload(s0 + 3);
+  }
+  __syncthreads();  // pooled rows s0 .. s0 + 2 staged
+  if (np > 0) {
     xload(s0);
     xstore(Xs0);
     if (np > 1) xload(s0 + 1);
   }
   __syncthreads();
-  Frag F0, F1;
+  Frag F0;
   for (int i = 0; i < np; ++i) {
+    // pooled row s0 + i + 3 (loaded one iteration ago) goes to the slot of row s0 + i - 1,
+    // last read in iteration i - 2; the producers of iteration i + 1 read it.  Row s0 + i + 4
+    // is loaded now and stored next iteration.
+    if (i + 2 < np) pstore(s0 + i + 3);
+    if (i + 3 < np) pload(s0 + i + 4);
     if (i + 1 < np) {
       xstore(Xs0 + ((i + 1) & 1) * XSZ);  // that buffer was last read in iteration i - 1
       if (i + 2 < np) xload(s0 + i + 2);
     }
     const bf16_t* Ds = Ds0 + (i & 1) * DSZ;
     const bf16_t* Xs = Xs0 + (i & 1) * XSZ;
-    // k-steps in pairs: the fragments of step ks+1 are read while step ks's MFMAs issue
-    frag(F0, Ds, Xs, 0);
-    for (int ks = 0; ks < nks; ks += 2) {
-      if (ks + 1 < nks) frag(F1, Ds, Xs, ks + 1);
+    // one fragment set (the registers go to the producers' share); the two producer waves
+    // on this SIMD cover the LDS latency
+    for (int ks = 0; ks < ((DIAG & 1) ? 0 : nks); ++ks) {
+      frag(F0, Ds, Xs, ks);
       mma(F0);
-      if (ks + 1 < nks) {
-        if (ks + 2 < nks) frag(F0, Ds, Xs, ks + 2);
-        mma(F1);
-      }
     }
     __syncthreads();
   }
@@ -845,9 +905,14 @@ void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, cons
   // DMLAB_STEM_WS=0: the single-role kernel (every wave builds dy, then reduces)
   const char* ws = getenv("DMLAB_STEM_WS");
   if (!ws || atoi(ws) != 0) {
-    const size_t sm = (size_t)2 * FR * FDP * 2 + (size_t)2 * 5 * FWP * SC * 2 + 3 * 64 * 4;
-    set_smem_attr(stem_wgrad_ws_kernel, sm);
-    stem_wgrad_ws_kernel<<<S, 512, sm, st>>>(a);
+    const size_t sm = (size_t)2 * FR * FDP * 2 + (size_t)2 * 5 * FWP * SC * 2 +
+                      (size_t)4 * (FW / 2) * 64 * 3 + 3 * 64 * 4;
+    const char* dg = getenv("DMLAB_STEM_DIAG");
+    const int diag = dg ? atoi(dg) : 0;
+    auto k = diag == 1 ? stem_wgrad_ws_kernel<1> : diag == 2 ? stem_wgrad_ws_kernel<2>
+           : diag == 3 ? stem_wgrad_ws_kernel<3> : stem_wgrad_ws_kernel<0>;
+    set_smem_attr(k, sm);
+    k<<<S, 768, sm, st>>>(a);
     DM_CHECK(hipGetLastError());
     return;
   }
