@@ -44,7 +44,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,
-    long long mbase, int rowbase) {
+    long long mbase, int rowbase, int diag, int xcd, int mtiles) {
+  // diag (DMLAB_HALO_DIAG, timing diagnostics only; results wrong when set): bit 0 drops the
+  // MFMA phase, bit 1 the per-step weight loads, bit 2 the epilogue, bit 3 the per-step barriers
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
   // mbase / rowbase: first output pixel and first statistics row of this launch (a launch
   // may cover only the tail of the pixel range, see conv_halo's tail split)
@@ -63,8 +65,18 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = mbase + (long long)blockIdx.x * BMH;
-  const int n0 = blockIdx.y * BN;
+  // block -> (M tile, N tile).  xcd > 0 (1-D grid): the N tiles of one M tile are
+  // consecutive blocks on the same XCD (blocks go to the XCDs round-robin, b % 8), so the
+  // input halo the N tiles share is fetched into that XCD's L2 once, not once per N tile
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (xcd) {
+    const int b = blockIdx.x, j = b >> 3;
+    by = j % xcd;
+    bx = (j / xcd) * 8 + (b & 7);
+    if (bx >= mtiles) return;  // padding of the M tiles to a multiple of 8
+  }
+  const long long m0 = mbase + (long long)bx * BMH;
+  const int n0 = by * BN;
   const int ntaps = g.nth * g.ntw;
   const int nchunk = g.C / HBK;
   const int HW = g.H * g.W;
@@ -141,6 +153,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
     }
   };
   auto load_b_into = [&](uint4 (&dst)[BR], int cc, int t) {
+    if (diag & 2) return;
     const unsigned kb = (unsigned)(taps[t].z + cc * HBK + chunk * 8) * 2u;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
@@ -169,6 +182,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto compute = [&](int buf, int t) {
+    if (diag & 1) return;
     const int4 tp = taps[t];
     int hrow[RM];
 #pragma unroll
@@ -223,7 +237,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       if (s + 1 < S) load_b(ncc, nt);
       compute(s & 1, t);
       if (s + 1 < S) store_b((s + 1) & 1);
-      __syncthreads();
+      if (!(diag & 8)) __syncthreads();
       if (ncc != cc && s + 1 < S) {
         store_halo(ncc);  // every wave is past the last tap of chunk cc
         __syncthreads();
@@ -265,7 +279,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       nxt(lc, lt);
       compute(s & 1, t);
       if (s + 1 < S) store_b_from(rnext, (s + 1) & 1);
-      __syncthreads();
+      if (!(diag & 8)) __syncthreads();
       if (ncc != cc && s + 1 < S) {
         store_halo(ncc);
         __syncthreads();
@@ -279,7 +293,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       if (s + 1 < S) step(s + 1, rb, rb2);
     }
   }
-  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, rowbase + blockIdx.x,
+  if (diag & 4) return;
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, rowbase + bx,
                                                        stats, g, Y, ADD,
                                                        bnb);
 }
@@ -304,8 +319,20 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
                   : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
   set_smem_attr(k, sm);
+  static const int diag = getenv("DMLAB_HALO_DIAG") ? atoi(getenv("DMLAB_HALO_DIAG")) : 0;
+  // measured (tools/bench_conv.py, batch 512, one call): layer3 fwd 845 -> 880 TF/s, dgrad
+  // 859 -> 892; layer2 / layer4 +2-7 %; 11.60 vs 11.62 ms/step.  DMLAB_HALO_XCD=0: 2-D grid
+  static const int xcd_on = getenv("DMLAB_HALO_XCD") ? atoi(getenv("DMLAB_HALO_XCD")) : 1;
+  if (xcd_on && grid.y > 1) {
+    // 1-D grid over the M tiles (padded to a multiple of 8) x N tiles
+    const unsigned mt8 = (grid.x + 7) / 8 * 8, ntiles = grid.y;
+    k<<<dim3(mt8 * ntiles), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc,
+                                                   pre_sh, bnb, mbase, rowbase, diag,
+                                                   (int)ntiles, (int)grid.x);
+    return;
+  }
   k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb, mbase,
-                                    rowbase);
+                                    rowbase, diag, 0, (int)grid.x);
 }
 
 // Tail split for the 256-pixel 4x1-wave tile (cfg 41).  Its layer-3/4 grids are just over a
