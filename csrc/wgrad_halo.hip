@@ -49,7 +49,7 @@ template <int HRN, int NTY, bool PRE>
 __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int xy, int gx, int nz) {
   // pre_sc/pre_sh (optional): X is the previous conv's raw output; the operand is
   // relu(x*sc + sh) applied while staging (out-of-image taps read the zero row)
   constexpr int HROWS_MAX = HRN * 32;  // halo rows a buffer holds (8 chunks per row)
@@ -60,10 +60,21 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
 
   constexpr int NT = 3 * NTY;  // taps per block
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int co0 = blockIdx.x * WBM;
-  const int cc0 = (blockIdx.y / (3 / NTY)) * WBC;
-  const int dy_lo = -1 + (int)(blockIdx.y % (3 / NTY)) * NTY;  // first kernel row of the block
-  const long long mb = (long long)blockIdx.z * mchunk;
+  // block -> (co tile bx, channel/row tile by, m slice bz).  xy > 0 (1-D grid): the xy tiles
+  // of one m slice are consecutive blocks on one XCD (blocks go to the XCDs round-robin), so
+  // the slice's dY rows and input halo are fetched into that XCD's L2 once
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (xy) {
+    const int b = blockIdx.x, j = b >> 3, t = j % xy;
+    bz = (j / xy) * 8 + (b & 7);
+    if (bz >= nz) return;  // padding of the m slices to a multiple of 8
+    bx = t % gx;
+    by = t / gx;
+  }
+  const int co0 = bx * WBM;
+  const int cc0 = (by / (3 / NTY)) * WBC;
+  const int dy_lo = -1 + (int)(by % (3 / NTY)) * NTY;  // first kernel row of the block
+  const long long mb = (long long)bz * mchunk;
   const long long me = min(g.M, mb + mchunk);
   const int W = g.W, H = g.H;
   const int hrows = WBK + 2 + (NTY - 1) * W;  // pixels m0 + dy_lo*W - 1 ... m0 + (dy_hi)*W + 64
@@ -173,7 +184,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     __syncthreads();
   }
   // slab[z][co][tap*C + c]; 16x16 C map: col = lane & 15 (channel), row = (lane>>4)*4 + r (co)
-  float* out = slab + (long long)blockIdx.z * g.Ncols * g.K;
+  float* out = slab + (long long)bz * g.Ncols * g.K;
   const int c = cc0 + wid * 16 + (lane & 15);
   const int t0 = (dy_lo + 1) * 3;  // global tap index of the block's first tap
 #pragma unroll
@@ -197,7 +208,18 @@ void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const Con
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
   auto k = pre_sc ? wgrad_halo_kernel<HRN, NTY, true> : wgrad_halo_kernel<HRN, NTY, false>;
   set_smem_attr(k, sm);
-  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh);
+  // XCD-grouped order for the 9-tap tiles (DMLAB_WGRAD_XCD=0: plain 3-D grid).  Measured
+  // (tools/bench_conv.py, one call): 9-tap layer2 +2-4 %, layer3/4 within 1 %, step 11.55 vs
+  // 11.57 ms; the 3-tap tiles lose (layer1 526 -> 475 TF/s) and keep the 3-D grid
+  static const int xcd_on = getenv("DMLAB_WGRAD_XCD") ? atoi(getenv("DMLAB_WGRAD_XCD")) : 1;
+  const int xy = (int)(grid.x * grid.y);
+  if (xcd_on && NTY == 3 && xy > 1 && S > 1) {
+    const unsigned z8 = (unsigned)((S + 7) / 8 * 8);
+    k<<<dim3(z8 * xy), 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, xy,
+                                       (int)grid.x, S);
+    return;
+  }
+  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, 0, (int)grid.x, S);
 }
 }  // namespace
 
