@@ -254,6 +254,15 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
       dm::geom_finalize(g);
       set.g[ng++] = g;
     }
+  // cfg 80: all four classes of a 3x3/s2 dgrad in one block over one staged dY halo
+  // (csrc/dgrad_s2.hip); shapes it does not cover take the v3 128x64 parity-class tile
+  if (cfg == 80) {
+    if (!bnbp && dm::dgrad_s2_supported(set, ng)) {
+      dm::dgrad_s2(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, st);
+      return 0;
+    }
+    cfg = Cin % 128 == 0 ? 15 : 13;
+  }
   // all parity classes in one launch (blockIdx.z = class) when the tile supports it
   if (bnbp) {
     // slab rows of absent classes, or of row tiles past a smaller class's M (odd sizes),

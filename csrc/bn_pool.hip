@@ -752,6 +752,88 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
   }
 }
 
+// The stem's 3x3/s2/p1 case of bn_relu_maxpool_kernel: a thread owns two horizontally
+// adjacent pooled outputs (they share one input column: 15 loads instead of 18) and issues
+// all 15 16-B loads before any compare (the generic kernel's guarded loop keeps only a few
+// in flight).  Same scan order and strict '>' (first max wins), same codes and yarg.
+__global__ void __launch_bounds__(256) bn_relu_maxpool3s2_kernel(
+    const bf16_t* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    bf16_t* __restrict__ out, uint8_t* __restrict__ idx, bf16_t* __restrict__ yarg, int N, int H,
+    int W, int C, int OH, int OW) {
+  extern __shared__ float ss[];  // [2][C]
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    ss[c] = scale[c];
+    ss[C + c] = shift[c];
+  }
+  __syncthreads();
+  const unsigned C8 = (unsigned)(C >> 3), OWP = (unsigned)((OW + 1) >> 1);
+  const unsigned total = (unsigned)N * (unsigned)OH * OWP * C8;  // < 2^31 (host check)
+  const unsigned stride = gridDim.x * blockDim.x;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int c8 = (int)(i % C8);
+    unsigned t = i / C8;
+    const int owp = (int)(t % OWP);
+    t /= OWP;
+    const int oh = (int)(t % (unsigned)OH);
+    const int n = (int)(t / (unsigned)OH);
+    const int c0 = c8 * 8, ow0 = owp * 2;
+    const bool two = ow0 + 1 < OW;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sc[j] = ss[c0 + j];
+      sh[j] = ss[C + c0 + j];
+    }
+    // rows 2oh-1..2oh+1, columns 2ow0-1..2ow0+3; an out-of-image tap loads the (always
+    // valid) window centre and is skipped in the compare
+    const unsigned ctr = (((unsigned)n * H + 2 * oh) * W + 2 * ow0) * C + c0;
+    uint4 v[3][5];
+    bool ok[3][5];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = 2 * oh - 1 + kh;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const int iw = 2 * ow0 - 1 + q;
+        ok[kh][q] = (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W && (q < 3 || two);
+        const unsigned off = ok[kh][q] ? (((unsigned)n * H + ih) * W + iw) * C + c0 : ctr;
+        v[kh][q] = *reinterpret_cast<const uint4*>(y + off);
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      if (o == 1 && !two) break;
+      float best[8], raw[8];
+      int arg[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { best[j] = -INFINITY; arg[j] = 0; raw[j] = 0.f; }
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw) {
+          const int q = 2 * o + kw;
+          if (!ok[kh][q]) continue;
+          float f[8];
+          unpack8(v[kh][q], f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float val = fmaxf(f[j] * sc[j] + sh[j], 0.f);
+            if (val > best[j]) { best[j] = val; arg[j] = kh * 3 + kw; raw[j] = f[j]; }
+          }
+        }
+      const unsigned oi = (((unsigned)n * OH + oh) * OW + ow0 + o) * C8 + c8;
+      reinterpret_cast<uint4*>(out)[oi] = pack8(best);
+      if (yarg) reinterpret_cast<uint4*>(yarg)[oi] = pack8(raw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) arg[j] = best[j] > 0.f ? arg[j] : 15;
+      uint2 a2;
+      a2.x = arg[0] | (arg[1] << 8) | (arg[2] << 16) | (arg[3] << 24);
+      a2.y = arg[4] | (arg[5] << 8) | (arg[6] << 16) | (arg[7] << 24);
+      reinterpret_cast<uint2*>(idx)[oi] = a2;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ max pool (NHWC)
 // out[n,oh,ow,c] = max window; idx = argmax position in window (0..K*K-1), first max wins
 __global__ void __launch_bounds__(256) maxpool_fwd_kernel(const bf16_t* __restrict__ x,
@@ -1143,6 +1225,14 @@ void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
                      int P, hipStream_t st, bf16_t* yarg) {
   const long long total = (long long)N * OH * OW * (C / 8);
+  static const bool generic = getenv("DMLAB_POOL_GENERIC") && atoi(getenv("DMLAB_POOL_GENERIC"));
+  if (!generic && K == 3 && S == 2 && P == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 &&
+      (long long)N * H * W * C < (1LL << 31)) {
+    const long long pairs = (long long)N * OH * ((OW + 1) / 2) * (C / 8);
+    bn_relu_maxpool3s2_kernel<<<grid_for(pairs, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
+        y, scale, shift, out, idx, yarg, N, H, W, C, OH, OW);
+    return;
+  }
   bn_relu_maxpool_kernel<<<grid_for(total, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
       y, scale, shift, out, idx, yarg, N, H, W, C, OH, OW, K, S, P);
 }

@@ -100,6 +100,10 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const ConvGeom& g, int bn, int waves, hipStream_t st,
                const float* pre_sc = nullptr, const float* pre_sh = nullptr,
                const BnBwdEpi* bnb = nullptr);
+// dgrad_s2.hip: stride-2 3x3 data gradient, all four parity classes per block (cfg 80)
+bool dgrad_s2_supported(const ConvGeomSet& set, int ng);
+void dgrad_s2(const bf16_t* dY, const bf16_t* Wd, bf16_t* dX, const bf16_t* ADD,
+              const ConvGeomSet& set, hipStream_t st);
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,

@@ -53,6 +53,21 @@ _HALO_MAP = {int(k): int(v) for k, v in (kv.split("=") for kv in
              os.environ.get("DMLAB_HALO_MAP", "").split(",") if kv)}
 
 
+# cfg 80: stride-2 3x3 data gradient with the four parity classes of a dY tile in one block
+# (csrc/dgrad_s2.hip).  Opt-in (DMLAB_DGRAD_S2=1): at batch 512 it ties the per-class igemm
+# tiles on layer2/3 (373 vs 374, 452-473 vs 473 TFLOP/s) and loses on layer4 (515 vs 588),
+# end to end 43.98/44.01k vs 43.86/44.04k img/s (profiles/dgrad_s2_r2c.txt)
+_DGRAD_S2 = os.environ.get("DMLAB_DGRAD_S2", "0") == "1"
+
+
+def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
+    """Kernel config of a data-gradient GEMM (dX has M pixels of ``cin`` channels)."""
+    if (_DGRAD_S2 and not _FUSE_BN_BWD and k == 3 and stride == 2 and cin % 64 == 0
+            and cout % 64 == 0 and H % 2 == 0 and W % 2 == 0):
+        return 80
+    return pick_cfg(M, cin, k, stride, cout)
+
+
 def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     """Kernel config for a forward-style conv GEMM with M output pixels and ncols
     output channels.  ``k``/``stride``/``cin`` (kernel size, tap stride, input
@@ -501,7 +516,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)
         N_, H, W, Cin = x.shape
-        cfg = pick_cfg(N_ * H * W, Cin, k, s, cout)
+        cfg = dgrad_cfg(N_ * H * W, Cin, k, s, cout, H, W)
         bkw = {}
         spec = bnb_spec(*consumer) if (consumer is not None and _FUSE_BN_BWD) else None
         if spec is not None:

@@ -240,6 +240,32 @@ def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
     assert _rel(_nchw(dx), ref) < 6e-3
 
 
+S2_GEOMS = [  # stride-2 3x3 dgrad, all parity classes per block (cfg 80)
+    (2, 56, 64, 128, 3, 2, 1),   # layer2: dY 28x28, a block spans 5 dY rows
+    (3, 28, 128, 256, 3, 2, 1),  # layer3: 2 N tiles (XCD-ordered 1-D grid), 4 chunks
+    (5, 14, 256, 512, 3, 2, 1),  # layer4: dY 7x7, blocks cross images, partial last block
+    (2, 16, 64, 64, 3, 2, 1),
+    (2, 9, 64, 128, 3, 2, 1),    # odd input: class grids differ -> per-class igemm fallback
+]
+
+
+@pytest.mark.parametrize("geom", S2_GEOMS)
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_dgrad_s2_classes(dev, geom, accumulate):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    wb = w.bfloat16().float()
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wb, dy.float(), s, p)
+    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    base = dx.clone()
+    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, 80)
+    if accumulate:
+        ref = ref + _nchw(base).float()
+    assert _rel(_nchw(dx), ref) < 6e-3
+
+
 @pytest.mark.parametrize("geom", GEOMS)
 def test_conv_wgrad(dev, geom):
     N, H, Cin, Cout, k, s, p = geom
@@ -410,6 +436,38 @@ def test_stem_s2d_packing_layouts(dev, layout, H):
             sub = x[:, :, dy::2, dx::2].permute(0, 2, 3, 1)
             ref[..., (dy * 2 + dx) * 3:(dy * 2 + dx) * 3 + 3] = sub
     assert torch.equal(xs.float(), ref.bfloat16().float())
+
+
+@pytest.mark.parametrize("H,W,C", [(18, 18, 64), (17, 17, 64), (56, 56, 32), (9, 14, 64)])
+def test_bn_relu_maxpool_3x3s2_codes(dev, H, W, C):
+    """The 3x3/s2 fused stem tail (two pooled outputs per thread) against torch: pooled
+    values, argmax window codes (first max wins, 15 = window passes no gradient) and y at
+    the argmax."""
+    torch.manual_seed(1)
+    N = 3
+    y = (torch.randn(N, H, W, C, device=dev) * 1.5).bfloat16()
+    scale = torch.rand(C, device=dev) + 0.5
+    shift = torch.randn(C, device=dev) * 0.5
+    z = (y.float() * scale + shift).relu().permute(0, 3, 1, 2)
+    ref, ind = F.max_pool2d(z, 3, 2, 1, return_indices=True)
+    OH, OW = ref.shape[2], ref.shape[3]
+    out = torch.empty(N, OH, OW, C, device=dev, dtype=torch.bfloat16)
+    idx = torch.empty(N, OH, OW, C, device=dev, dtype=torch.uint8)
+    yarg = torch.empty_like(out)
+    lib().bn_relu_maxpool(y, scale, shift, out, idx, 3, 2, 1, yarg=yarg)
+    torch.testing.assert_close(_nchw(out).float(), ref.bfloat16().float(), rtol=0, atol=0)
+    # torch's flat argmax -> (kh, kw) of the window at (2*oh - 1, 2*ow - 1)
+    ih, iw = ind // W, ind % W
+    oh = torch.arange(OH, device=dev).view(1, 1, OH, 1)
+    ow = torch.arange(OW, device=dev).view(1, 1, 1, OW)
+    code = (ih - (2 * oh - 1)) * 3 + (iw - (2 * ow - 1))
+    code = torch.where(ref > 0, code, torch.full_like(code, 15))
+    mism = (_nchw(idx).long() != code).float().mean().item()
+    assert mism < 1e-3  # ties decided differently by fma rounding only
+    yr = y.permute(0, 3, 1, 2).reshape(N, C, -1)
+    yref = torch.gather(yr, 2, ind.reshape(N, C, -1)).view_as(ref)
+    sel = (ref > 0) & (_nchw(idx).long() == code)
+    assert torch.equal(_nchw(yarg)[sel], yref[sel])
 
 
 @pytest.mark.parametrize("H,C", [(18, 64), (17, 64), (56, 32)])
