@@ -46,7 +46,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,
     long long mbase, int rowbase, int diag, int xcd, int mtiles) {
   // diag (DMLAB_HALO_DIAG, timing diagnostics only; results wrong when set): bit 0 drops the
-  // MFMA phase, bit 1 the per-step weight loads, bit 2 the epilogue, bit 3 the per-step barriers
+  // MFMA phase, bit 1 the per-step weight loads, bit 2 the epilogue, bit 3 the per-step
+  // barriers, bit 4 the epilogue's global stores, bit 5 its BN statistics
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
   // mbase / rowbase: first output pixel and first statistics row of this launch (a launch
   // may cover only the tail of the pixel range, see conv_halo's tail split)
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
   if (diag & 4) return;
   mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, rowbase + bx,
                                                        stats, g, Y, ADD,
-                                                       bnb);
+                                                       bnb, diag);
 }
 
 int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
