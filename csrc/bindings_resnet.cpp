@@ -37,12 +37,12 @@ int ilog2(int v) {
   return l;
 }
 
-// persistent per-layer ticket counter of the one-launch BN finalizes (int32, zero between
-// launches; the kernel's last block resets it)
-unsigned* counter_ptr(const c10::optional<at::Tensor>& c, const at::Tensor& like) {
+// persistent per-layer ticket counters of the one-launch BN finalizes (int32, one per
+// 32-channel group, zero between launches; each group's last block resets its own)
+unsigned* counter_ptr(const c10::optional<at::Tensor>& c, const at::Tensor& like, int64_t C) {
   if (!c.has_value()) return nullptr;
-  TORCH_CHECK(c->scalar_type() == at::kInt && c->is_contiguous() && c->numel() >= 1 &&
-              c->device() == like.device(), "counter: int32 tensor on the device");
+  TORCH_CHECK(c->scalar_type() == at::kInt && c->is_contiguous() && c->numel() >= (C + 31) / 32 &&
+              c->device() == like.device(), "counter: int32 tensor on the device, ceil(C/32) long");
   return reinterpret_cast<unsigned*>(c->data_ptr<int>());
 }
 
@@ -397,7 +397,7 @@ void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gam
   dm::bn_stats_finalize(fp(stats), T, C, count, fp(gamma), fp(beta),
                         rmean.has_value() ? fp(*rmean) : nullptr, rvar.has_value() ? fp(*rvar) : nullptr,
                         momentum, eps, fp(scale), fp(shift), fp(mean), fp(invstd), fp(work), nb,
-                        cur_stream(), counter_ptr(counter, stats));
+                        cur_stream(), counter_ptr(counter, stats, C));
 }
 
 void bn_eval_coeffs(at::Tensor gamma, at::Tensor beta, at::Tensor rmean, at::Tensor rvar, double eps,
@@ -613,7 +613,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
                   (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
                   OW, K, S, P, bp(dy), drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
-                  (int)pre_rows, mp, counter_ptr(counter, y));
+                  (int)pre_rows, mp, counter_ptr(counter, y, C));
 }
 
 void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,

@@ -203,6 +203,62 @@ __global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __res
   }
 }
 
+// One launch with the finalize spread over channel groups: block (x, y) sums rows of group y
+// for the 32 channels [32x, 32x + 32) -- both moments, columns c and C + c -- and the last
+// block to arrive FOR ITS CHANNEL GROUP (ticket ctr[x]) finalizes those 32 channels.  The
+// tails of different groups run in parallel (colsum_finalize_kernel's single last block walks
+// every channel serially: 6 % slower end to end).  Same first-level rows and summation order
+// as slab_colsum_kernel, same second level as block_sum2: bit-identical to the two launches.
+// ctr: ceil(C/32) counters owned by the caller, 0 between launches (each group's last block
+// resets its own).
+template <bool BWD>
+__global__ void __launch_bounds__(256) colsum_finalize_grouped_kernel(
+    const float* __restrict__ in, int T, int C, float* __restrict__ out, unsigned* __restrict__ ctr,
+    double count, FinFwd ff, FinBwd fb) {
+  const int W = 2 * C;
+  const int G = gridDim.y, gi = blockIdx.y;
+  const int j = threadIdx.x & 63;
+  const int c = blockIdx.x * 32 + (j & 31);
+  const int col = (j >> 5) * C + c;
+  const bool okc = c < C;
+  const int rl = threadIdx.x >> 6;
+  const int R = (T + G - 1) / G;
+  const int r0 = gi * R, r1 = min(T, r0 + R);
+  __shared__ double red[4][64];
+  __shared__ int last;
+  red[rl][j] = okc ? sum_rows8(in + col, r0 + rl, r1, 4, W) : 0.0;
+  __syncthreads();
+  if (rl == 0 && okc)
+    out[(long long)gi * W + col] = (float)(red[0][j] + red[1][j] + red[2][j] + red[3][j]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ctr + blockIdx.x, 1u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(ctr + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!BWD && ff.num_batches && blockIdx.x == 0) *ff.num_batches += 1;
+  }
+  __syncthreads();
+  for (int c0 = blockIdx.x * 32; c0 < blockIdx.x * 32 + 32 && c0 < C; c0 += FIN_CH) {
+    const int cc = c0 + (threadIdx.x % FIN_CH);
+    double sm, q;
+    block_sum2(out, G, C, cc, sm, q);
+    if (threadIdx.x < FIN_CH && cc < C) {
+      if (BWD) fin_bwd_channel(fb, cc, C, sm, q, count);
+      else fin_fwd_channel(ff, cc, sm, q, count);
+    }
+    __syncthreads();
+  }
+}
+
 // eval mode: scale/shift from running stats
 __global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                       const float* __restrict__ rmean, const float* __restrict__ rvar,
@@ -1098,9 +1154,9 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
   const int W = 2 * C;
   const int G = colsum_groups(T);
   const FinFwd f{gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd, num_batches};
-  if (G && ctr) {  // one launch: column sums + last-block finalize
-    colsum_finalize_kernel<false><<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, C, work, ctr,
-                                                                         count, f, FinBwd{});
+  if (G && ctr) {  // one launch: column sums + per-channel-group last-block finalize
+    colsum_finalize_grouped_kernel<false><<<dim3((C + 31) / 32, G), 256, 0, st>>>(
+        stats, T, C, work, ctr, count, f, FinBwd{});
     return;
   }
   const float* fin = stats;
@@ -1173,8 +1229,8 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   }
   const int G2 = colsum_groups(G);
   const FinBwd fb{gamma, mean, invstd, dgamma, dbeta, gbeta, coef};
-  if (G2 && ctr) {  // one launch: column sums + last-block finalize
-    colsum_finalize_kernel<true><<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(
+  if (G2 && ctr) {  // one launch: column sums + per-channel-group last-block finalize
+    colsum_finalize_grouped_kernel<true><<<dim3((C + 31) / 32, G2), 256, 0, st>>>(
         part, G, C, part2, ctr, (double)M, FinFwd{}, fb);
   } else {
     const float* fin = part;

@@ -219,14 +219,18 @@ def pack_all(prog, layers):
         object.__setattr__(m, "_wcache", (ver, wf, wd))
 
 
-def _fin_counter(layer, device):
-    """Persistent int32 ticket counters of this layer's one-launch BN finalizes ([0] forward,
-    [1] backward); zero between launches (the finalizing block resets them)."""
+_FIN_GROUPS = 32  # ticket counters per direction: one per 32-channel group, C <= 1024
+
+
+def _fin_counter(layer, device, bwd=False):
+    """Persistent int32 ticket counters of this layer's one-launch BN finalizes (forward and
+    backward, one per 32-channel group each); zero between launches (each group's
+    finalizing block resets its own)."""
     c = getattr(layer, "_fin_ctr", None)
     if c is None or c.device != device:
-        c = torch.zeros(2, dtype=torch.int32, device=device)
+        c = torch.zeros(2 * _FIN_GROUPS, dtype=torch.int32, device=device)
         object.__setattr__(layer, "_fin_ctr", c)
-    return c
+    return c[_FIN_GROUPS:] if bwd else c[:_FIN_GROUPS]
 
 
 def _materialise(x, pre):
@@ -286,7 +290,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
         L.bn_stats_finalize(stats, T, float(M), layer.bn_weight.detach(), layer.bn_bias.detach(),
                             layer.running_mean, layer.running_var, layer.momentum, layer.eps,
                             scale, shift, mean, invstd, work, layer.num_batches_tracked,
-                            counter=_fin_counter(layer, x.device)[0:1] if _FUSED_FIN else None)
+                            counter=_fin_counter(layer, x.device) if _FUSED_FIN else None)
     else:
         L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg, **pre_kw)
         L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
@@ -338,9 +342,11 @@ _FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
 # apply pass + the generic igemm weight gradient.  Kept for A/B runs.
 _STEM_BWD = os.environ.get("DMLAB_STEM_BWD", "fused")
 # BN finalizes as one launch (column sums + a last-block finalize, bit-identical) instead of
-# two: opt-in (DMLAB_FUSED_FIN=1).  Measured 6 % SLOWER end to end on MI355X (12.8 vs 12.1
-# ms/step): the last block walks the channel groups serially, where the separate finalize
-# spreads them over C/16 blocks -- the saved launch (~5 us) costs more than it saves
+# two: opt-in (DMLAB_FUSED_FIN=1).  With one last block for all channels it measured 6 %
+# slower end to end (12.8 vs 12.1 ms/step: that block walked every channel group serially);
+# with one last block per 32-channel group it is 0.8 % slower (43.0-43.1k vs 43.35-43.6k
+# img/s, profiles/bn_finalize_grouped_r2c.txt) -- the saved launch does not pay for the
+# ticket fences and the serial tail
 _FUSED_FIN = os.environ.get("DMLAB_FUSED_FIN", "0") == "1"
 _STEM_SPLIT = int(os.environ.get("DMLAB_STEM_SPLIT", "4"))
 # weight gradient of the split path: "dy" (stem_wgrad_dy_kernel) or "igemm" (v2 s2d tiles)
@@ -475,7 +481,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
                   getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"),
-                  counter=_fin_counter(layer, y.device)[1:2] if _FUSED_FIN else None, **pre_sums)
+                  counter=_fin_counter(layer, y.device, bwd=True) if _FUSED_FIN else None, **pre_sums)
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does

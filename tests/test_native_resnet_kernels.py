@@ -524,9 +524,10 @@ def test_fused_bn_relu_maxpool_and_gather_backward(dev, H, C):
 
 
 @pytest.mark.parametrize("T", [1, 100, 129, 6272])
-def test_bn_stats_finalize_slab_rows(dev, T):
+@pytest.mark.parametrize("C", [64, 80, 512])
+def test_bn_stats_finalize_slab_rows(dev, T, C):
     """Σ over a [T][2][C] per-tile statistics slab (direct and two-level reductions)."""
-    C, M = 64, 1000.0
+    M = 1000.0
     f = dict(device=dev, dtype=torch.float32)
     g = torch.Generator(device=dev).manual_seed(3)
     s = torch.rand(T, C, device=dev, generator=g) * 2.0
@@ -541,9 +542,9 @@ def test_bn_stats_finalize_slab_rows(dev, T):
     var = (qd / M - mu * mu).clamp_min(0)
     torch.testing.assert_close(mean.double(), mu, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-6)
-    # the one-launch finalize (column sums + last-block finalize, ticket counter) is bit-identical,
-    # leaves its counter at 0 and increments num_batches once per call
-    ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+    # the one-launch finalize (column sums + per-channel-group last-block finalize, ticket
+    # counters) is bit-identical, leaves its counters at 0 and increments num_batches once per call
+    ctr = torch.zeros(32, dtype=torch.int32, device=dev)  # one per 32-channel group
     nb = torch.zeros(1, dtype=torch.int64, device=dev)
     for rep in range(3):
         out = [torch.empty(C, **f) for _ in range(4)]
@@ -551,7 +552,7 @@ def test_bn_stats_finalize_slab_rows(dev, T):
                                 torch.empty(512 * C, **f), nb, counter=ctr)
         for a, b in zip(out, (scale, shift, mean, invstd)):
             assert torch.equal(a, b)
-        assert int(ctr.item()) == 0 and int(nb.item()) == rep + 1
+        assert int(ctr.abs().sum().item()) == 0 and int(nb.item()) == rep + 1
 
 
 @pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3] + L1_GEOMS[1:])
@@ -688,14 +689,14 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
                       dyy, None, work, mask=mask if mode == 4 else None, **kw)
         res.append((dyy.float(), dg, db))
         if not pre:  # the one-launch finalize (ticket counter) is bit-identical
-            ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+            ctr = torch.zeros(32, dtype=torch.int32, device=dev)  # one per 32-channel group
             d2, dg2, db2 = torch.empty_like(y), torch.zeros(Cin, **f), torch.zeros(Cin, **f)
             L.bn_backward(dx, out if mode == 1 else None, y, mean, invstd, gamma, dg2, db2, 0.0,
                           mode, sc if mode == 2 else None, sh if mode == 2 else None, None, None,
                           3, 2, 1, d2, None, torch.empty_like(work),
                           mask=mask if mode == 4 else None, counter=ctr)
             assert torch.equal(d2, dyy) and torch.equal(dg2, dg) and torch.equal(db2, db)
-            assert int(ctr.item()) == 0
+            assert int(ctr.abs().sum().item()) == 0
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-4, atol=1e-3)
     assert _rel(res[0][0], res[1][0]) < 1e-3
