@@ -240,6 +240,51 @@ def _materialise(x, pre):
     return out
 
 
+def _input_key(x):
+    return (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), x.dtype)
+
+
+def request_input_prefetch(layer, x):
+    """Ask the stem's backward to space-to-depth pack ``x`` (the NEXT step's input batch)
+    on the side stream while the stem weight gradient runs: that kernel is latency-bound
+    and alone on the GPU (one workgroup per CU), so the memory-bound packing (~100 us at
+    batch 512) overlaps it instead of opening the next step's forward.  The next forward
+    uses the packed batch if ``x`` is unchanged (same storage, version, shape)."""
+    if use_s2d(layer, x) and x.is_cuda:
+        object.__setattr__(layer, "_prefetch_req", x)
+
+
+def _launch_input_prefetch(layer, main):
+    x = getattr(layer, "_prefetch_req", None)
+    side = getattr(layer._prog, "_wgrad_stream", None)
+    if x is None or side is None:
+        return
+    object.__setattr__(layer, "_prefetch_req", None)
+    side.wait_stream(main)  # starts at this point of the backward, next to the stem wgrad
+    with torch.cuda.stream(side):
+        Nn, Cc, Hh, Ww = x.shape
+        xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
+        lib().pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
+        ev = torch.cuda.Event()
+        ev.record(side)
+    x.record_stream(side)
+    object.__setattr__(layer, "_prefetched", (_input_key(x), xs, ev))
+
+
+def _take_prefetched(layer, x):
+    pf = getattr(layer, "_prefetched", None)
+    if pf is None:
+        return None
+    object.__setattr__(layer, "_prefetched", None)
+    key, xs, ev = pf
+    if key != _input_key(x):
+        return None
+    cur = torch.cuda.current_stream()
+    cur.wait_event(ev)
+    xs.record_stream(cur)  # allocated on the side stream, consumed (and freed) on this one
+    return xs
+
+
 def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     L = lib()
     first = not (x.dim() == 4 and getattr(x, "_dm_nhwc", False))
@@ -247,8 +292,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     if s2d:
         # stem as a 4x4/s1 conv over the space-to-depth input (pad 2 top/left, 1 bottom/right)
         Nn, Cc, Hh, Ww = x.shape
-        xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
-        L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
+        xs = _take_prefetched(layer, x) if x.is_cuda else None
+        if xs is None:
+            xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
+            L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
         x = xs
         k, s, p = 4, 1, 2
         OH, OW = Hh // 2, Ww // 2
@@ -457,6 +504,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     if stem_ok and _STEM_BWD == "fused":
         # stem: BN-backward apply fused into the s2d weight gradient -- the full-resolution
         # dy is never written (csrc/conv_stem.hip stem_wgrad_fused_kernel)
+        _launch_input_prefetch(layer, torch.cuda.current_stream())
         slab = torch.empty(L.stem_bwd_slab_floats(N, OH), device=y.device, dtype=torch.float32)
         L.stem_bwd_fused(y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
                          layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
