@@ -156,6 +156,144 @@ __global__ void __launch_bounds__(256, 2) stem_conv_kernel(
   mfma_tile_epilogue<SBM, SCO, 4, 1, true, 1>(acc, smem, m0, 0, blockIdx.x, stats, g, Y, nullptr);
 }
 
+// Persistent variant: two workgroups per CU loop over the 256-pixel tiles.  The 32 KB weight
+// matrix is staged ONCE per workgroup (the per-tile kernel re-reads it from L2 for every one
+// of the 25088 tiles at batch 512: as many bytes as the conv writes), and the input halo of
+// tile i+1 is loaded into registers while tile i runs its MFMAs and epilogue.  The epilogue
+// stages the fp32 tile in two 128-row bands in the LDS after the weights (the halo's space),
+// so weights + halo/epilogue still fit two workgroups per CU.
+__device__ __forceinline__ void stem_tile_geom(const ConvGeom& g, long long m0, int dymin, int dymax,
+                                               int& hbase, int& hp) {
+  const int r0 = (int)fdiv((unsigned)m0, g.wg_mul, g.wg_shr);
+  const long long mlast = (m0 + SBM - 1 < g.M) ? m0 + SBM - 1 : g.M - 1;
+  const int r1 = (int)fdiv((unsigned)mlast, g.wg_mul, g.wg_shr);
+  hbase = (r0 + dymin) * g.W;
+  hp = (r1 - r0 + 1 + dymax - dymin) * g.W;
+}
+
+__global__ void __launch_bounds__(256, 2) stem_conv_pers_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
+    float* __restrict__ stats, ConvGeom g, unsigned xbytes, int ntiles) {
+  constexpr int HI = (2 * SHP + 255) / 256;
+  constexpr size_t RBYTES = (size_t)(SHP + 1) * SC * 2 > (size_t)128 * (SCO + 4) * 4
+                                ? (size_t)(SHP + 1) * SC * 2
+                                : (size_t)128 * (SCO + 4) * 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem);                        // [64][256]
+  unsigned char* R = smem + SCO * SK * 2;                              // halo | epilogue band
+  bf16_t* Hs = reinterpret_cast<bf16_t*>(R);                           // [SHP + 1][16]
+  int4* taps = reinterpret_cast<int4*>(R + RBYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntaps = g.nth * g.ntw;
+  const int NHW = g.N * g.H * g.W;
+  if (tid < ntaps) {
+    const int th = tid / g.ntw, tw = tid % g.ntw;
+    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
+    taps[tid] = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * SC,
+                          dy * g.W + dx);
+  }
+  const int dymin = g.dys > 0 ? g.dy0 : g.dy0 + (g.nth - 1) * g.dys;
+  const int dymax = g.dys > 0 ? g.dy0 + (g.nth - 1) * g.dys : g.dy0;
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  uint4 hv[HI];
+  auto load_halo = [&](int tile) {
+    int hbase, hp;
+    stem_tile_geom(g, (long long)tile * SBM, dymin, dymax, hbase, hp);
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int e = tid + 256 * i, pix = e >> 1, half = e & 1;
+      const int gp = hbase + pix;
+      const bool ok = pix < hp && (unsigned)gp < (unsigned)NHW;
+      const unsigned off = ok ? ((unsigned)gp * SC + half * 8) * 2u : SOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      hv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  int tile = blockIdx.x;
+  {
+    uint4 wv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, row = e >> 5, ch = e & 31;
+      wv[i] = *reinterpret_cast<const uint4*>(Wp + row * SK + ch * 8);
+    }
+    load_halo(tile);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = tid + 256 * i, row = e >> 5, ch = e & 31;
+      *reinterpret_cast<uint4*>(Ws + row * SK + wswz(row, ch) * 8) = wv[i];
+    }
+  }
+  const int h = lane >> 5;  // k half: channels 8h..8h+7 of the tap
+  for (; tile < ntiles; tile += gridDim.x) {
+    const long long m0 = (long long)tile * SBM;
+    int hbase, hp;
+    stem_tile_geom(g, m0, dymin, dymax, hbase, hp);
+    __syncthreads();  // the previous tile's epilogue has finished reading the LDS band
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int e = tid + 256 * i, pix = e >> 1, half = e & 1;
+      if (pix < SHP) *reinterpret_cast<uint4*>(Hs + pix * SC + hswz(pix, half) * 8) = hv[i];
+    }
+    if (tid < 2) *reinterpret_cast<uint4*>(Hs + SHP * SC + tid * 8) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load_halo(tile + gridDim.x);  // lands during this tile
+    int a_h[2], a_x[2], a_y[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long m = m0 + wid * 64 + i * 32 + (lane & 31);
+      const unsigned r = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      a_x[i] = (int)((unsigned)m - r * (unsigned)g.W);
+      const unsigned n = fdiv(r, g.hg_mul, g.hg_shr);
+      a_y[i] = (m < g.M) ? (int)(r - n * (unsigned)g.H) : -(1 << 28);
+      a_h[i] = (int)(m - hbase);
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    auto frags = [&](int t, bf16x8 (&af)[2], bf16x8 (&bf)[2]) {
+      const int4 tp = taps[t];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = (unsigned)(a_x[i] + tp.y) < (unsigned)g.W &&
+                        (unsigned)(a_y[i] + tp.x) < (unsigned)g.H;
+        const int pix = ok ? a_h[i] + tp.w : SHP;
+        af[i] = *reinterpret_cast<const bf16x8*>(Hs + pix * SC + hswz(pix, h) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = j * 32 + (lane & 31);
+        bf[j] = *reinterpret_cast<const bf16x8*>(Ws + row * SK + wswz(row, (tp.z >> 3) + h) * 8);
+      }
+    };
+    bf16x8 a0[2], b0[2], a1[2], b1[2];
+    auto mma = [&](const bf16x8 (&af)[2], const bf16x8 (&bf)[2]) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    };
+    frags(0, a0, b0);
+#pragma unroll
+    for (int t = 0; t < 16; t += 2) {
+      frags(t + 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a0, b0);
+      if (t + 2 < 16) frags(t + 2, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(a1, b1);
+    }
+    __syncthreads();  // the epilogue band overwrites the halo
+    mfma_tile_epilogue<SBM, SCO, 4, 1, true, 2>(acc, R, m0, 0, tile, stats, g, Y, nullptr);
+  }
+}
+
 // ------------------------------------------------------------------ fused stem backward
 // Weight gradient of the s2d stem with the stem's BatchNorm backward applied on the fly:
 //
@@ -939,10 +1077,28 @@ void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const
   const size_t epi = (size_t)SBM * (SCO + 4) * 4;
   const size_t sm = main > epi ? main : epi;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const int ntiles = (int)((g.M + SBM - 1) / SBM);
+  // DMLAB_STEM_PERSIST=0: one workgroup per tile (A/B runs)
+  static const bool pers = !getenv("DMLAB_STEM_PERSIST") || atoi(getenv("DMLAB_STEM_PERSIST"));
+  if (pers) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      DM_CHECK(hipGetDevice(&dev));
+      DM_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const size_t hal = (size_t)(SHP + 1) * SC * 2, band = (size_t)128 * (SCO + 4) * 4;
+    const size_t smp = (size_t)SCO * SK * 2 + (hal > band ? hal : band) + MAXTAPS * 16;
+    set_smem_attr(stem_conv_pers_kernel, smp);
+    const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
+    stem_conv_pers_kernel<<<grid, 256, smp, st>>>(X, Wp, Y, stats, g, xb, ntiles);
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   set_smem_attr(stem_conv_kernel, sm);
   // each wave's column of the MFMA epilogue needs rows >= M zeroed for the stats: the A rows
   // of pixels past M are never valid (a_y poisoned), so their accumulators stay 0
-  stem_conv_kernel<<<(unsigned)((g.M + SBM - 1) / SBM), 256, sm, st>>>(X, Wp, Y, stats, g, xb);
+  stem_conv_kernel<<<(unsigned)ntiles, 256, sm, st>>>(X, Wp, Y, stats, g, xb);
   DM_CHECK(hipGetLastError());
 }
 

@@ -387,12 +387,13 @@ def test_maxpool_avgpool(dev):
     assert _rel(dxa, ref) < 5e-3
 
 
-@pytest.mark.parametrize("H", [32, 224, 18])
+@pytest.mark.parametrize("N,H", [(2, 32), (2, 224), (2, 18), (12, 224)])
 @pytest.mark.parametrize("fcfg", [16, 60])
-def test_stem_space_to_depth(dev, H, fcfg):
+def test_stem_space_to_depth(dev, N, H, fcfg):
     """7x7/s2/p3 stem == 4x4/s1 conv over the space-to-depth packed input (cfg 60: the
-    resident-weight stem kernel, csrc/conv_stem.hip; H=18: a partial last block)."""
-    N, C, Co = 2, 3, 64
+    resident-weight stem kernel, csrc/conv_stem.hip; H=18: a partial last block; N=12 at 224:
+    588 tiles, more than the persistent grid, so workgroups loop over several tiles)."""
+    C, Co = 3, 64
     g = torch.Generator(device=dev).manual_seed(3)
     x = torch.randn(N, C, H, H, device=dev, generator=g).bfloat16()
     w = torch.randn(Co, C, 7, 7, device=dev, generator=g) / math.sqrt(C * 49)
