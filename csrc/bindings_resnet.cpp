@@ -148,8 +148,13 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
                    c10::optional<at::Tensor> bnb_mean, c10::optional<at::Tensor> bnb_invstd,
                    c10::optional<at::Tensor> bnb_scale, c10::optional<at::Tensor> bnb_shift,
                    int64_t bnb_mode, c10::optional<at::Tensor> bnb_slab,
-                   c10::optional<at::Tensor> bnb_mask) {
+                   c10::optional<at::Tensor> bnb_mask, c10::optional<at::Tensor> bwd_y,
+                   c10::optional<at::Tensor> bwd_coef, c10::optional<at::Tensor> bwd_scale,
+                   c10::optional<at::Tensor> bwd_shift) {
   // add: tensor added to the result (may alias dx for in-place accumulation)
+  // bwd_* (optional): dy is the UPSTREAM gradient dz of this conv's BatchNorm and the operand
+  // is that BN's backward apply a*dz' + b*y + cc (dz' masked by relu(y*scale + shift) > 0),
+  // computed while staging (cfg 39, stride 1, 64 channels): the apply pass never runs
   need_bf16_nhwc(dy, "dy");
   need_bf16_nhwc(dx, "dx");
   const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), Cout = dy.size(3);
@@ -212,6 +217,19 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
     slabp = fp(*bnb_slab);
   }
   const dm::BnBwdEpi* bnbp = bnb.y ? &bnb : nullptr;
+  dm::BwdPre bpre{};
+  if (bwd_y.has_value()) {
+    need_bf16_nhwc(*bwd_y, "bwd_y");
+    TORCH_CHECK(bwd_y->sizes() == dy.sizes(), "bwd_y: the BN input, shaped like dy");
+    TORCH_CHECK(bwd_coef.has_value() && bwd_scale.has_value() && bwd_shift.has_value(),
+                "bwd_y needs bwd_coef, bwd_scale, bwd_shift");
+    need_f32(*bwd_coef, "bwd_coef", 3 * (int64_t)Cout);
+    need_f32(*bwd_scale, "bwd_scale", Cout);
+    need_f32(*bwd_shift, "bwd_shift", Cout);
+    TORCH_CHECK(stride == 1 && cfg == 39 && Cout == 64 && !bnbp,
+                "BN-backward operand: stride-1 dgrad, cfg 39, 64 channels, no fused sums");
+    bpre = dm::BwdPre{bp(*bwd_y), fp(*bwd_coef), fp(*bwd_scale), fp(*bwd_shift)};
+  }
   dm::ConvGeom base{};
   base.N = N; base.H = OH; base.W = OW; base.C = Cout; base.lgC8 = ilog2(Cout / 8);
   base.OH = H; base.OW = W; base.OC = Cin;
@@ -223,6 +241,12 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
+    if (bpre.y) {
+      TORCH_CHECK(dm::conv_halo_supported(g), "BN-backward operand: not a halo-kernel shape");
+      dm::conv_halo(bp(dy), bp(wd), bp(dx), addp, nullptr, g, 64, 16, st, nullptr, nullptr,
+                    nullptr, &bpre);
+      return 0;
+    }
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, slabp, g, cfg, st, bnbp);
     return bnb_rows;
   }
@@ -285,9 +309,13 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
 void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int64_t Cin,
                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, double beta, int64_t S,
                 int64_t cfg, bool s2d, c10::optional<at::Tensor> pre_scale,
-                c10::optional<at::Tensor> pre_shift) {
+                c10::optional<at::Tensor> pre_shift, c10::optional<at::Tensor> bwd_y,
+                c10::optional<at::Tensor> bwd_coef, c10::optional<at::Tensor> bwd_scale,
+                c10::optional<at::Tensor> bwd_shift) {
   // s2d: x/dy are the space-to-depth stem operands (4x4/s1 conv over 4*Cin channels);
   // dw is the original [Cout][Cin][7][7] gradient
+  // bwd_* (optional): dy is the upstream gradient dz of this conv's BatchNorm; the dY operand
+  // is that BN's backward apply (halo wgrad only, see conv_dgrad)
   need_bf16_nhwc(x, "x");
   need_bf16_nhwc(dy, "dy");
   const int Cout = dy.size(3);
@@ -299,14 +327,32 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   const long long mchunk = ((steps + S - 1) / S) * 64;  // multiple of both kernels' row step
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
-  if (pre_scale.has_value()) {  // x = previous conv's raw output, operand relu(x*sc + sh)
-    TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
-    need_f32(*pre_scale, "pre_scale", x.size(3));
-    need_f32(*pre_shift, "pre_shift", x.size(3));
+  dm::BwdPre dpre{};
+  if (bwd_y.has_value()) {
+    need_bf16_nhwc(*bwd_y, "bwd_y");
+    TORCH_CHECK(bwd_y->sizes() == dy.sizes(), "bwd_y: the BN input, shaped like dy");
+    TORCH_CHECK(bwd_coef.has_value() && bwd_scale.has_value() && bwd_shift.has_value(),
+                "bwd_y needs bwd_coef, bwd_scale, bwd_shift");
+    need_f32(*bwd_coef, "bwd_coef", 3 * (int64_t)Cout);
+    need_f32(*bwd_scale, "bwd_scale", Cout);
+    need_f32(*bwd_shift, "bwd_shift", Cout);
+    TORCH_CHECK(!s2d && (cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
+                "BN-backward dY operand needs the halo wgrad (cfg 4/5) and a 3x3/s1/p1 geometry");
+    dpre = dm::BwdPre{bp(*bwd_y), fp(*bwd_coef), fp(*bwd_scale), fp(*bwd_shift)};
+  }
+  if (pre_scale.has_value() || dpre.y) {
+    const float *psc = nullptr, *psh = nullptr;
+    if (pre_scale.has_value()) {  // x = previous conv's raw output, operand relu(x*sc + sh)
+      TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
+      need_f32(*pre_scale, "pre_scale", x.size(3));
+      need_f32(*pre_shift, "pre_shift", x.size(3));
+      psc = fp(*pre_scale);
+      psh = fp(*pre_shift);
+    }
     TORCH_CHECK((cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
                 "fused pre-BN needs the halo wgrad (cfg 4/5) and a 3x3/s1/p1 geometry");
-    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st,
-                   fp(*pre_scale), fp(*pre_shift));
+    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh,
+                   dpre.y ? &dpre : nullptr);
   } else {
     dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
   }
@@ -549,13 +595,20 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
                  at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
                  at::Tensor dbeta, double gbeta, int64_t mode, c10::optional<at::Tensor> scale,
                  c10::optional<at::Tensor> shift, c10::optional<at::Tensor> pdy,
-                 c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P, at::Tensor dy,
-                 c10::optional<at::Tensor> dres, at::Tensor work,
+                 c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P,
+                 c10::optional<at::Tensor> dy, c10::optional<at::Tensor> dres, at::Tensor work,
                  c10::optional<at::Tensor> pre_slab, int64_t pre_rows,
                  c10::optional<at::Tensor> mask, c10::optional<at::Tensor> counter) {
+  // dy None: reduce + finalize only -- dgamma/dbeta and the coefficients a, b, cc of
+  // dy = a*dz + b*y + cc are left in work (bn_bwd_coef_offset) for a consumer kernel that
+  // applies them while staging its operand (conv_dgrad / conv_wgrad bwd_*)
   need_bf16_nhwc(y, "y");
-  need_bf16_nhwc(dy, "dy");
-  TORCH_CHECK(dy.sizes() == y.sizes());
+  if (dy.has_value()) {
+    need_bf16_nhwc(*dy, "dy");
+    TORCH_CHECK(dy->sizes() == y.sizes());
+  } else {
+    TORCH_CHECK(!dres.has_value() && mode != 3, "dy None: no residual gradient, no pool mode");
+  }
   TORCH_CHECK(mode >= 0 && mode <= 4);
   const int C = y.size(3);
   TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0, "bn_backward: C/8 must divide 256");
@@ -612,7 +665,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   const DeviceGuard guard(y.device());
   dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
                   (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
-                  OW, K, S, P, bp(dy), drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
+                  OW, K, S, P, dy.has_value() ? bp(*dy) : nullptr, drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
                   (int)pre_rows, mp, counter_ptr(counter, y, C));
 }
 
@@ -639,6 +692,11 @@ void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tenso
 }
 
 int64_t bn_bwd_rows(int64_t M, int64_t C) { return dm::bn_bwd_groups(M, C); }
+
+// element offset of the [3][C] backward coefficients in bn_backward's work buffer
+int64_t bn_bwd_coef_offset(int64_t M, int64_t C, bool pre_sums) {
+  return pre_sums ? 0 : (int64_t)dm::bn_bwd_groups(M, C) * 2 * C;
+}
 
 // Σdz, Σdz·x̂ partials of (dout masked by y*scale+shift > 0) -> part [rows][2C]; returns rows
 int64_t bn_bwd_reduce_masked(at::Tensor dout, at::Tensor y, at::Tensor mean, at::Tensor invstd,
@@ -716,12 +774,16 @@ void register_resnet(pybind11::module_& m) {
         py::arg("bnb_mean") = py::none(), py::arg("bnb_invstd") = py::none(),
         py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(),
         py::arg("bnb_mode") = 0, py::arg("bnb_slab") = py::none(),
-        py::arg("bnb_mask") = py::none());
+        py::arg("bnb_mask") = py::none(), py::arg("bwd_y") = py::none(),
+        py::arg("bwd_coef") = py::none(), py::arg("bwd_scale") = py::none(),
+        py::arg("bwd_shift") = py::none());
   m.def("dgrad_bnb_rows", &dgrad_bnb_rows);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),
-        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
+        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none(),
+        py::arg("bwd_y") = py::none(), py::arg("bwd_coef") = py::none(),
+        py::arg("bwd_scale") = py::none(), py::arg("bwd_shift") = py::none());
   m.def("pack_weights", &pack_weights);
   m.def("pack_weights_multi", &pack_weights_multi);
   m.def("pack_weights_tiled", &pack_weights_tiled);
@@ -752,6 +814,7 @@ void register_resnet(pybind11::module_& m) {
         py::arg("out"), py::arg("idx"), py::arg("K"), py::arg("S"), py::arg("P"),
         py::arg("yarg") = py::none());
   m.def("bn_bwd_rows", &bn_bwd_rows);
+  m.def("bn_bwd_coef_offset", &bn_bwd_coef_offset);
   m.def("bn_bwd_reduce_masked", &bn_bwd_reduce_masked);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

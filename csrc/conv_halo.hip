@@ -39,12 +39,16 @@ constexpr unsigned OOB = 0x80000000u;
 // 8-wave BN-64 tiles must stay <= 128 VGPRs to keep two workgroups (4 waves) per SIMD
 // PF: weight-tile register prefetch depth (1: the tile of step s+1 is loaded during step s;
 // 2: the tile of step s+2, so a load has two steps of MFMA work to land in)
-template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
+// PRE: 0 = X as stored; 1 = X is a conv's raw output y, operand relu(y*sc + sh) (forward BN +
+// ReLU of the previous layer); 2 = X is an upstream gradient dz, operand the BN-backward apply
+// a*dz' + b*y + cc with y = bpre.y (a dgrad consuming its BN's backward without the apply
+// pass; single 64-channel chunk only: the next chunk's halo is never prefetched)
+template <int BN, int HR, int WM, int WN, int BMH, int PRE, int PF>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,
-    long long mbase, int rowbase, int diag, int xcd, int mtiles) {
+    long long mbase, int rowbase, int diag, int xcd, int mtiles, BwdPre bpre) {
   // diag (DMLAB_HALO_DIAG, timing diagnostics only; results wrong when set): bit 0 drops the
   // MFMA phase, bit 1 the per-step weight loads, bit 2 the epilogue, bit 3 the per-step
   // barriers, bit 4 the epilogue's global stores, bit 5 its BN statistics
@@ -121,6 +125,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
   __syncthreads();
 
   uint4 rh[HR], rb[BR];
+  uint4 ry[PRE == 2 ? HR : 1];
+  const auto rsy = __builtin_amdgcn_make_buffer_rsrc((void*)bpre.y, (short)0, (int)xbytes, 0x00020000);
   auto load_halo = [&](int cc) {
     const unsigned cb = (unsigned)(cc * HBK + chunk * 8) * 2u;
 #pragma unroll
@@ -131,15 +137,34 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       const unsigned off = ok ? (unsigned)gp * (unsigned)g.C * 2u + cb : OOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
       rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
+      if constexpr (PRE == 2) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsy, off, 0, 0);
+        ry[j] = make_uint4(w[0], w[1], w[2], w[3]);
+      }
     }
   };
   auto store_halo = [&](int cc) {
+    if constexpr (PRE == 2) {
+      // out-of-range rows loaded zeros for both operands: a*0 + b*0 + cc != 0, so they are
+      // stored as zeros explicitly (the conv's zero padding of dy)
+      PreBnBwd pb;
+      pb.load(bpre.coef, bpre.scale, bpre.shift, g.C, cc * HBK + chunk * 8);
+#pragma unroll
+      for (int j = 0; j < HR; ++j) {
+        const int hh = (tid >> 3) + RPP * j;
+        const int gp = hbase + hh;
+        const bool ok = hh < hp && (unsigned)gp < (unsigned)NHW;
+        *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) =
+            ok ? pb.apply(rh[j], ry[j]) : make_uint4(0, 0, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
       const int hh = (tid >> 3) + RPP * j;
       *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) = rh[j];
     }
-    if constexpr (PRE) {
+    if constexpr (PRE == 1) {
       // normalise in place once the staging registers are dead (each thread rewrites
       // only its own chunks: program order suffices, no barrier), so the fused BN costs
       // no registers across the tap loop
@@ -227,7 +252,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
     store_halo(0);
     store_b(0);
     __syncthreads();
-    if (nchunk > 1) load_halo(1);
+    if constexpr (PRE != 2) {
+      if (nchunk > 1) load_halo(1);
+    }
     int cc = 0, t = 0;
     for (int s = 0; s < S; ++s) {
       int nt = t + 1, ncc = cc;
@@ -239,10 +266,12 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       compute(s & 1, t);
       if (s + 1 < S) store_b((s + 1) & 1);
       if (!(diag & 8)) __syncthreads();
-      if (ncc != cc && s + 1 < S) {
-        store_halo(ncc);  // every wave is past the last tap of chunk cc
-        __syncthreads();
-        if (ncc + 1 < nchunk) load_halo(ncc + 1);
+      if constexpr (PRE != 2) {
+        if (ncc != cc && s + 1 < S) {
+          store_halo(ncc);  // every wave is past the last tap of chunk cc
+          __syncthreads();
+          if (ncc + 1 < nchunk) load_halo(ncc + 1);
+        }
       }
       t = nt;
       cc = ncc;
@@ -267,7 +296,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
     if (S > 1) load_b_into(rb2, lc, lt);  // tile 1
     nxt(lc, lt);
     __syncthreads();
-    if (nchunk > 1) load_halo(1);
+    if constexpr (PRE != 2) {
+      if (nchunk > 1) load_halo(1);
+    }
     int cc = 0, t = 0;
     auto step = [&](int s, uint4 (&rnext)[BR], uint4 (&rfree)[BR]) {
       // rnext holds tile s+1; rfree receives tile s+2
@@ -281,10 +312,12 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 :
       compute(s & 1, t);
       if (s + 1 < S) store_b_from(rnext, (s + 1) & 1);
       if (!(diag & 8)) __syncthreads();
-      if (ncc != cc && s + 1 < S) {
-        store_halo(ncc);
-        __syncthreads();
-        if (ncc + 1 < nchunk) load_halo(ncc + 1);
+      if constexpr (PRE != 2) {
+        if (ncc != cc && s + 1 < S) {
+          store_halo(ncc);
+          __syncthreads();
+          if (ncc + 1 < nchunk) load_halo(ncc + 1);
+        }
       }
       t = nt;
       cc = ncc;
@@ -308,7 +341,8 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
 template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
-                 const BnBwdEpi& bnb, long long mbase = 0, int rowbase = 0, long long mend = -1) {
+                 const BnBwdEpi& bnb, long long mbase = 0, int rowbase = 0, long long mend = -1,
+                 const BwdPre* bpre = nullptr) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
@@ -317,8 +351,19 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   dim3 grid((unsigned)((mend - mbase + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
-                  : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
+  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, 1, PF>
+                  : conv_halo_kernel<BN, HR, WM, WN, BMH, 0, PF>;
+  BwdPre bp{};
+  if (bpre) {
+    // the BN-backward-apply operand: the 8-wave 256 x 64 tile (cfg 39) over one chunk only
+    if constexpr (BN == 64 && WM == 4 && WN == 2 && BMH == 256 && PF == 1) {
+      DM_CHECK(g.C == HBK ? hipSuccess : hipErrorInvalidValue);
+      k = conv_halo_kernel<BN, HR, WM, WN, BMH, 2, PF>;
+      bp = *bpre;
+    } else {
+      DM_CHECK(hipErrorInvalidValue);
+    }
+  }
   set_smem_attr(k, sm);
   static const int diag = getenv("DMLAB_HALO_DIAG") ? atoi(getenv("DMLAB_HALO_DIAG")) : 0;
   // measured (tools/bench_conv.py, batch 512, one call): layer3 fwd 845 -> 880 TF/s, dgrad
@@ -329,11 +374,11 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
     const unsigned mt8 = (grid.x + 7) / 8 * 8, ntiles = grid.y;
     k<<<dim3(mt8 * ntiles), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc,
                                                    pre_sh, bnb, mbase, rowbase, diag,
-                                                   (int)ntiles, (int)grid.x);
+                                                   (int)ntiles, (int)grid.x, bp);
     return;
   }
   k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb, mbase,
-                                    rowbase, diag, 0, (int)grid.x);
+                                    rowbase, diag, 0, (int)grid.x, bp);
 }
 
 // Tail split for the 256-pixel 4x1-wave tile (cfg 41).  Its layer-3/4 grids are just over a
@@ -396,8 +441,17 @@ bool conv_halo_supported(const ConvGeom& g) {
 
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
-               const float* pre_sh, const BnBwdEpi* bnbp) {
+               const float* pre_sh, const BnBwdEpi* bnbp, const BwdPre* bpre) {
   const BnBwdEpi bnb = bnbp ? *bnbp : BnBwdEpi{};
+  if (bpre) {  // BN-backward apply on load: cfg 39 (256 px, 4 x 2 waves, BN 64), one chunk
+    DM_CHECK(bn == 64 && waves == 16 && g.C == HBK && !pre_sc ? hipSuccess : hipErrorInvalidValue);
+    const int hr = (halo_rows_needed(g, 256) + 63) / 64;
+    if (hr <= 5) launch_halo<64, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, bnb, 0, 0, -1, bpre);
+    else if (hr <= 6) launch_halo<64, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, bnb, 0, 0, -1, bpre);
+    else launch_halo<64, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, bnb, 0, 0, -1, bpre);
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   if (waves & 0x100) {  // two-deep weight prefetch: BN 128 4 waves / 128 px, 8 waves / 256 px;
                         // BN 64 4 x 1 waves (cfg 44) and 4 x 2 waves (cfg 45) / 256 px
     waves &= 0xff;

@@ -61,6 +61,7 @@ void xgmi_allreduce(const float* in, float* out, long long n, long long cap, voi
 struct ConvGeom;
 struct ConvGeomSet;
 struct BnBwdEpi;
+struct BwdPre;
 bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
@@ -99,7 +100,7 @@ bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,
                const float* pre_sc = nullptr, const float* pre_sh = nullptr,
-               const BnBwdEpi* bnb = nullptr);
+               const BnBwdEpi* bnb = nullptr, const BwdPre* bpre = nullptr);
 // dgrad_s2.hip: stride-2 3x3 data gradient, all four parity classes per block (cfg 80)
 bool dgrad_s2_supported(const ConvGeomSet& set, int ng);
 void dgrad_s2(const bf16_t* dY, const bf16_t* Wd, bf16_t* dX, const bf16_t* ADD,
@@ -107,7 +108,7 @@ void dgrad_s2(const bf16_t* dY, const bf16_t* Wd, bf16_t* dX, const bf16_t* ADD,
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
-                const float* pre_sh = nullptr);
+                const float* pre_sh = nullptr, const BwdPre* dpre = nullptr);
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
                         hipStream_t st);
 void pack_weights_tiled(const long long* desc, const int* tprefix, int nl, int ntiles,

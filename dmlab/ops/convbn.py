@@ -396,6 +396,13 @@ _STEM_BWD = os.environ.get("DMLAB_STEM_BWD", "fused")
 # ticket fences and the serial tail
 _FUSED_FIN = os.environ.get("DMLAB_FUSED_FIN", "0") == "1"
 _STEM_SPLIT = int(os.environ.get("DMLAB_STEM_SPLIT", "4"))
+# BN-backward apply fused into the consumers' operand staging for the 64-channel 3x3 convs
+# whose BN has no residual (layer-1 c1): opt-in (DMLAB_BN_BWD_ON_LOAD=1).  Measured 1.2 %
+# slower end to end (43.15-43.19k vs 43.55-43.80k img/s): the fused dgrad takes 560 us vs
+# 360 + 115 (apply pass) because its single-chunk halo prologue now loads dz AND y and runs
+# the apply before any MFMA, and the fused weight gradient grows 333 -> 446 us
+# (profiles/bn_bwd_on_load_r2c.txt)
+_BN_BWD_ON_LOAD = os.environ.get("DMLAB_BN_BWD_ON_LOAD", "0") == "1"
 # weight gradient of the split path: "dy" (stem_wgrad_dy_kernel) or "igemm" (v2 s2d tiles)
 _STEM_WGRAD = os.environ.get("DMLAB_STEM_WGRAD", "dy")
 
@@ -512,8 +519,6 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                          pre_sums["pre_rows"], x, layer.cin, layer.grad_slot("weight"), acc,
                          work, slab)
         return None
-    dy = empty_nhwc(N, OH, OW, cout, y)
-    dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     if pool:
         mode = 3       # dz gathered from the max-pool gradient, ReLU mask from y
     elif not layer.relu:
@@ -523,6 +528,17 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
         mode = 4 if ctx.get("mask") is not None else 1
     else:
         mode = 2       # mask recomputed from y (no `out` read)
+    C = x.shape[3]
+    K = k * k * C
+    wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
+    # BN-backward apply on load: this conv's dgrad and weight gradient stage
+    # a*dz' + b*y + cc straight from (dout, y), so dy is never written (saves the apply pass)
+    bwd_on_load = (_BN_BWD_ON_LOAD and mode == 2 and not s2d and k == 3 and s == 1
+                   and cout == 64 and C == 64 and wcfg in (4, 5) and need_dx
+                   and not ctx["first"] and not _FUSE_BN_BWD
+                   and dgrad_cfg(M, C, k, s, cout, OH, OW) == 39)
+    dy = None if bwd_on_load else empty_nhwc(N, OH, OW, cout, y)
+    dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
                   layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
@@ -530,13 +546,16 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
                   getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"),
                   counter=_fin_counter(layer, y.device, bwd=True) if _FUSED_FIN else None, **pre_sums)
+    bwd_kw = {}
+    if bwd_on_load:
+        off = L.bn_bwd_coef_offset(M, cout, bool(pre_sums))
+        bwd_kw = dict(bwd_y=y, bwd_coef=work[off:off + 3 * cout], bwd_scale=ctx["scale"],
+                      bwd_shift=ctx["shift"])
+        dy = dout  # the operand the consumers read; the bwd_* terms turn it into dy
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does
     # not hand their memory out again before the wgrad has read them.
-    C = x.shape[3]
-    K = k * k * C
-    wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
     pre = ctx.get("pre")
     side = getattr(layer._prog, "_wgrad_stream", None)
     if side is not None and layer.cout < _SIDE_MIN_COUT:
@@ -545,7 +564,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     def launch_wgrad():
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
-            for t in (x, dy) + (tuple(pre) if pre is not None else ()):
+            for t in (x, dy) + (tuple(pre) if pre is not None else ()) + tuple(bwd_kw.values()):
                 t.record_stream(side)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
@@ -557,7 +576,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                 else:
                     xw = _materialise(x, pre)
             L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S,
-                         wcfg, s2d, **pre_kw)
+                         wcfg, s2d, **pre_kw, **bwd_kw)
 
     deferred = getattr(layer._prog, "_deferred_wgrads", None) if side is not None else None
     if deferred is not None:
@@ -580,10 +599,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                                                       dtype=torch.float32))
         if dx_into is not None:
             dx = dx_into
-            r = L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg, **bkw)
+            r = L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg, **bkw, **bwd_kw)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **bkw)
+            r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **bkw, **bwd_kw)
         if bkw and r:
             consumer[1]["dz_stats"] = (bkw["bnb_slab"], r, dx)
     if ctx["has_res"]:

@@ -701,3 +701,64 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-4, atol=1e-3)
     assert _rel(res[0][0], res[1][0]) < 1e-3
+
+
+BWD_LOAD_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 14, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
+                  (1, 9, 64, 64, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geom", BWD_LOAD_GEOMS)
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_bn_backward_apply_on_load(dev, geom, accumulate):
+    """A conv's dgrad (cfg 39) and halo weight gradient (cfg 4/5) staging the BN-backward
+    apply a*dz' + b*y + cc from (dz, y) == the same kernels fed the dy that the apply pass
+    writes; bn_backward without dy leaves dgamma/dbeta and the coefficients in work."""
+    N, H, Cin, Cout, k, s, p = geom
+    L = lib()
+    f = dict(device=dev, dtype=torch.float32)
+    g = torch.Generator(device=dev).manual_seed(11)
+    M = N * H * H
+    y = (torch.randn(N, H, H, Cout, device=dev, generator=g) * 1.5).bfloat16()
+    dz = torch.randn(N, H, H, Cout, device=dev, generator=g).bfloat16()
+    gamma = torch.rand(Cout, **f) + 0.5
+    beta = torch.randn(Cout, **f) * 0.3
+    yf = y.float().view(M, Cout)
+    stats = torch.stack([yf.sum(0), (yf ** 2).sum(0)]).reshape(-1).contiguous()
+    scale, shift, mean, invstd = (torch.empty(Cout, **f) for _ in range(4))
+    L.bn_stats_finalize(stats, 1, float(M), gamma, beta, None, None, 0.1, 1e-5, scale, shift,
+                        mean, invstd, torch.empty(512 * Cout, **f))
+    # reference: the apply pass writes dy
+    dy = torch.empty_like(y)
+    dg, db = torch.zeros(Cout, **f), torch.zeros(Cout, **f)
+    work = torch.empty(L.bn_bwd_work(M, Cout), **f)
+    L.bn_backward(dz, None, y, mean, invstd, gamma, dg, db, 0.0, 2, scale, shift, None, None,
+                  3, 2, 1, dy, None, work)
+    # coefficients only
+    dg2, db2 = torch.zeros(Cout, **f), torch.zeros(Cout, **f)
+    work2 = torch.empty_like(work)
+    L.bn_backward(dz, None, y, mean, invstd, gamma, dg2, db2, 0.0, 2, scale, shift, None, None,
+                  3, 2, 1, None, None, work2)
+    assert torch.equal(dg2, dg) and torch.equal(db2, db)
+    off = L.bn_bwd_coef_offset(M, Cout, False)
+    bkw = dict(bwd_y=y, bwd_coef=work2[off:off + 3 * Cout], bwd_scale=scale, bwd_shift=shift)
+    # dgrad
+    w = torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k)
+    wd = torch.empty(Cin, k, k, Cout, device=dev, dtype=torch.bfloat16)
+    L.pack_weights(w.contiguous(), torch.empty(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16),
+                   wd, Cin)
+    base = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    dx_ref, dx = base.clone(), base.clone()
+    L.conv_dgrad(dy, wd, dx_ref, k, k, s, p, dx_ref if accumulate else None, 39)
+    L.conv_dgrad(dz, wd, dx, k, k, s, p, dx if accumulate else None, 39, **bkw)
+    torch.testing.assert_close(dx.float(), dx_ref.float(), rtol=1e-2, atol=1e-2)
+    assert _rel(dx, dx_ref) < 1e-3
+    # weight gradient, both halo variants
+    x = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    for cfg in (4, 5):
+        from dmlab.ops.convbn import _wgrad_plan
+        _, S = _wgrad_plan(M, Cout, k * k * Cin, k, s, Cin, force=cfg)
+        slab = torch.empty(S * Cout * k * k * Cin, **f)
+        dw_ref, dw = torch.empty(Cout, Cin, k, k, **f), torch.empty(Cout, Cin, k, k, **f)
+        L.conv_wgrad(x, dy, dw_ref, slab, Cin, k, k, s, p, 0.0, S, cfg, False)
+        L.conv_wgrad(x, dz, dw, slab, Cin, k, k, s, p, 0.0, S, cfg, False, **bkw)
+        assert _rel(dw, dw_ref) < 1e-4, cfg

@@ -177,3 +177,25 @@ def test_input_prefetch_matches(dev):
     torch.testing.assert_close(runs[1][0], runs[0][0], rtol=0, atol=0)
     for n in runs[0][1]:
         torch.testing.assert_close(runs[1][1][n], runs[0][1][n], rtol=0, atol=0, msg=n)
+
+
+def test_bn_backward_apply_on_load_matches(dev, monkeypatch):
+    """Layer-1 c1 with the BN-backward apply fused into its dgrad / weight-gradient operand
+    staging (convbn._BN_BWD_ON_LOAD) trains like the apply-pass path: same losses and
+    gradients up to bf16 rounding of the fused dy."""
+    import dmlab.ops.convbn as cb
+
+    x = torch.rand(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (8,), device=dev)
+    res = []
+    for on in (False, True):
+        monkeypatch.setattr(cb, "_BN_BWD_ON_LOAD", on)
+        torch.manual_seed(7)
+        m = ResNet18(num_classes=10).to(dev)
+        loss = cross_entropy(m(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((loss.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    torch.testing.assert_close(res[1][0], res[0][0], rtol=0, atol=0)
+    for n in res[0][1]:
+        assert _rel(res[1][1][n], res[0][1][n]) < 2e-3, n
