@@ -185,6 +185,12 @@ void gemm(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor B, c10::opti
     const long long tiles = ((M + 63) / 64) * ((N + 63) / 64);
     while (S < 16 && tiles * S < 256 && K / (S * 2) >= 64) S *= 2;
     if (S > 1) part = at::empty({(long long)S * M * N}, A.options().dtype(at::kFloat));
+  } else if (K >= 4 * 64) {
+    // fp32 kernel: its 64-deep LDS stages run serially per block, so a K of >= 4 stages on
+    // few output tiles is split over blocks (one or two stages each) + an ordered reduce
+    const long long tiles = ((M + 63) / 64) * ((N + 63) / 64);
+    while (S < 16 && tiles * S < 256 && K / (S * 2) >= 32) S *= 2;
+    if (S > 1) part = at::empty({(long long)S * M * N}, A.options().dtype(at::kFloat));
   }
   dm::gemm_strided(A.data_ptr(), optp(Amask), is_bf16(A), B.data_ptr(), is_bf16(B), cp, cbf, c32,
                    bias.has_value() ? bias->data_ptr<float>() : nullptr, M, N, K, sam, sak, sbk,

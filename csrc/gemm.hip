@@ -10,8 +10,10 @@
 //   wgrad dW = dYᵀ · X     A=dYᵀ (sam=1, sak=N)     B=X
 // The operands are tiny (LeNet fc 400→120, MLP ≤784×512, ResNet fc 512→1000), so
 // the kernel is latency-oriented: 64×64 tile, 4 waves each owning a 32×32
-// quadrant as 2×2 MFMA 16×16 blocks, BK=16 staged through padded LDS.  Inputs may
-// be fp32 or bf16 (converted on the LDS store; exact fp32 MFMA math either way).
+// quadrant as 2×2 MFMA 16×16 blocks, BK=64 staged through padded LDS (16 independent
+// loads per thread and operand in flight: with BK=16 LeNet's fc1, K=400, was 25 serial
+// load round trips, 59 us for 1.5 MFLOP).  Inputs may be fp32 or bf16 (converted on the
+// LDS store; exact fp32 MFMA math either way).
 // Exact f32 numerics: the MFMA is a k-ordered fmaf chain (guide §3).
 #include "common.h"
 
@@ -24,15 +26,18 @@ template <> __device__ __forceinline__ float ldx<bf16_t>(const bf16_t* p, long l
 }
 
 constexpr int GBM = 64, GBN = 64, GBK = 16;
+constexpr int FBK = 64;  // k per LDS stage of the fp32 kernel
 
 template <typename TA, typename TB, typename TC>
 __global__ void __launch_bounds__(256) gemm_f32mfma_kernel(
     const TA* __restrict__ A, const TA* __restrict__ Amask, const TB* __restrict__ B,
     TC* __restrict__ C, float* __restrict__ C32, const float* __restrict__ bias, int M, int N,
     int K, long long sam, long long sak, long long sbk, long long sbn, long long scm,
-    float alpha, float beta, int relu) {
-  __shared__ float As[GBK][GBM + 4];
-  __shared__ float Bs[GBK][GBN + 4];
+    float alpha, float beta, int relu, float* __restrict__ part, int kchunk) {
+  // split-K (part != nullptr): block z reduces k in [z*kchunk, (z+1)*kchunk) into
+  // part[z][M][N] (alpha applied); gemm_splitk_reduce_kernel sums z in order + epilogue
+  __shared__ float As[FBK][GBM + 4];
+  __shared__ float Bs[FBK][GBN + 4];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int m0 = blockIdx.y * GBM, n0 = blockIdx.x * GBN;
   const int wm = (wid >> 1) * 32, wn = (wid & 1) * 32;
@@ -42,35 +47,55 @@ __global__ void __launch_bounds__(256) gemm_f32mfma_kernel(
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 < K; k0 += GBK) {
-    // stage A tile [GBK][GBM]: 1024 elems / 256 threads = 4 each
+  constexpr int NA = FBK * GBM / 256, NB = FBK * GBN / 256;
+  const int kb = part ? blockIdx.z * kchunk : 0;
+  const int ke = part ? min(K, kb + kchunk) : K;
+  for (int k0 = kb; k0 < ke; k0 += FBK) {
+    // stage A tile [FBK][GBM] and B tile [FBK][GBN]: 16 elements each per thread.  Every
+    // load is issued first (out-of-range elements read element 0 and are zeroed by a select,
+    // no branch), then all LDS stores: a guarded load-then-store per element made the
+    // compiler wait on each load in turn
+    float va[NA], vb[NB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < NA; ++r) {
       const int e = tid + r * 256;
       int mm, kk;
-      if (sak == 1) { mm = e / GBK; kk = e % GBK; }   // k contiguous: walk k fastest
+      if (sak == 1) { mm = e / FBK; kk = e % FBK; }   // k contiguous: walk k fastest
       else { kk = e / GBM; mm = e % GBM; }            // m contiguous
       const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < M && gk < K) {
-        const long long o = (long long)gm * sam + (long long)gk * sak;
-        v = ldx(A, o);
-        if (Amask && !(ldx(Amask, o) > 0.f)) v = 0.f;
-      }
-      As[kk][mm] = v;
+      const bool ok = gm < M && gk < ke;
+      const long long o = ok ? (long long)gm * sam + (long long)gk * sak : 0;
+      float v = ldx(A, o);
+      if (Amask) v = ldx(Amask, o) > 0.f ? v : 0.f;
+      va[r] = ok ? v : 0.f;
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < NB; ++r) {
       const int e = tid + r * 256;
       int nn, kk;
-      if (sbk == 1) { nn = e / GBK; kk = e % GBK; }
+      if (sbk == 1) { nn = e / FBK; kk = e % FBK; }
       else { kk = e / GBN; nn = e % GBN; }
       const int gn = n0 + nn, gk = k0 + kk;
-      Bs[kk][nn] = (gn < N && gk < K) ? ldx(B, (long long)gk * sbk + (long long)gn * sbn) : 0.f;
+      const bool ok = gn < N && gk < ke;
+      const float v = ldx(B, ok ? (long long)gk * sbk + (long long)gn * sbn : 0);
+      vb[r] = ok ? v : 0.f;
+    }
+    if (k0 > kb) __syncthreads();  // the previous tile's MFMA reads are done
+#pragma unroll
+    for (int r = 0; r < NA; ++r) {
+      const int e = tid + r * 256;
+      if (sak == 1) As[e % FBK][e / FBK] = va[r];
+      else As[e / GBM][e % GBM] = va[r];
+    }
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      const int e = tid + r * 256;
+      if (sbk == 1) Bs[e % FBK][e / FBK] = vb[r];
+      else Bs[e / GBN][e % GBN] = vb[r];
     }
     __syncthreads();
 #pragma unroll
-    for (int ks = 0; ks < GBK; ks += 4) {
+    for (int ks = 0; ks < FBK; ks += 4) {
       const int kk = ks + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -82,7 +107,6 @@ __global__ void __launch_bounds__(256) gemm_f32mfma_kernel(
         }
       }
     }
-    __syncthreads();
   }
   // epilogue: C/D map col = lane&15, row = (lane>>4)*4 + r
 #pragma unroll
@@ -95,6 +119,10 @@ __global__ void __launch_bounds__(256) gemm_f32mfma_kernel(
         const int gn = n0 + wn + j * 16 + (lane & 15);
         if (gm < M && gn < N) {
           float v = alpha * acc[i][j][r];
+          if (part) {
+            part[((long long)blockIdx.z * M + gm) * N + gn] = v;
+            continue;
+          }
           const long long o = (long long)gm * scm + gn;
           if (beta != 0.f) v += beta * (C32 ? C32[o] : ldx(C, o));
           if (bias) v += bias[gn];
@@ -134,7 +162,10 @@ __global__ void __launch_bounds__(256) gemm_bf16mfma_kernel(
   const int kb = part ? blockIdx.z * kchunk : 0;
   const int ke = part ? min(K, kb + kchunk) : K;
   for (int k0 = kb; k0 < ke; k0 += BK) {
-    // 64 x 32 elements per operand, 8 per thread, walking the contiguous dimension fastest
+    // 64 x 32 elements per operand, 8 per thread, walking the contiguous dimension fastest.
+    // All 16 loads first (out-of-range elements read element 0, zeroed by a select), then
+    // the LDS stores: a guarded load-then-store per element waited on each load in turn
+    bf16_t va[8], vb[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int e = tid + r * 256;
@@ -142,13 +173,11 @@ __global__ void __launch_bounds__(256) gemm_bf16mfma_kernel(
       if (sak == 1) { mm = e / BK; kk = e % BK; }
       else { kk = e / GBM; mm = e % GBM; }
       const int gm = m0 + mm, gk = k0 + kk;
-      bf16_t v = 0;
-      if (gm < M && gk < ke) {
-        const long long o = (long long)gm * sam + (long long)gk * sak;
-        v = A[o];
-        if (Amask && !(bf2f(Amask[o]) > 0.f)) v = 0;
-      }
-      As[mm][kk] = v;
+      const bool ok = gm < M && gk < ke;
+      const long long o = ok ? (long long)gm * sam + (long long)gk * sak : 0;
+      bf16_t v = A[o];
+      if (Amask) v = bf2f(Amask[o]) > 0.f ? v : (bf16_t)0;
+      va[r] = ok ? v : (bf16_t)0;
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
@@ -157,13 +186,24 @@ __global__ void __launch_bounds__(256) gemm_bf16mfma_kernel(
       if (sbk == 1) { nn = e / BK; kk = e % BK; }
       else { kk = e / GBN; nn = e % GBN; }
       const int gn = n0 + nn, gk = k0 + kk;
-      bf16_t v = 0;
-      if (gn < N && gk < ke) {
-        const long long o = (long long)gk * sbk + (long long)gn * sbn;
-        if constexpr (sizeof(TB) == 4) v = f2bf(B[o]);
-        else v = B[o];
-      }
-      Bs[nn][kk] = v;
+      const bool ok = gn < N && gk < ke;
+      const long long o = ok ? (long long)gk * sbk + (long long)gn * sbn : 0;
+      bf16_t v;
+      if constexpr (sizeof(TB) == 4) v = f2bf(B[o]);
+      else v = B[o];
+      vb[r] = ok ? v : (bf16_t)0;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + r * 256;
+      if (sak == 1) As[e / BK][e % BK] = va[r];
+      else As[e % GBM][e / GBM] = va[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int e = tid + r * 256;
+      if (sbk == 1) Bs[e / BK][e % BK] = vb[r];
+      else Bs[e % GBN][e / GBN] = vb[r];
     }
     __syncthreads();
     const int kq = (lane >> 4) * 8;
@@ -287,10 +327,15 @@ void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, i
     }
     return;
   }
+  // split-K for the fp32 kernel: the caller sized part for S chunks of K (LeNet fc1: 2
+  // output tiles, K = 400 = 7 serial LDS stages -> 7 blocks of one stage each + a reduce)
+  const int kchunk32 = S > 1 ? ((K + S - 1) / S + FBK - 1) / FBK * FBK : K;
+  float* pp32 = S > 1 ? part : nullptr;
+  if (S > 1) grid.z = (K + kchunk32 - 1) / kchunk32;
 #define DM_GEMM(TA, TB, TC)                                                                  \
   gemm_f32mfma_kernel<TA, TB, TC><<<grid, 256, 0, st>>>(                                     \
       (const TA*)A, (const TA*)Amask, (const TB*)B, (TC*)C, C32, bias, M, N, K, sam, sak, sbk, \
-      sbn, scm, alpha, beta, relu)
+      sbn, scm, alpha, beta, relu, pp32, kchunk32)
   if (!a_bf16 && !b_bf16 && !c_bf16) DM_GEMM(float, float, float);
   else if (!a_bf16 && !b_bf16 && c_bf16) DM_GEMM(float, float, bf16_t);
   else if (a_bf16 && !b_bf16 && !c_bf16) DM_GEMM(bf16_t, float, float);
@@ -300,6 +345,15 @@ void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, i
   else if (!a_bf16 && b_bf16 && !c_bf16) DM_GEMM(float, bf16_t, float);
   else DM_GEMM(float, bf16_t, bf16_t);
 #undef DM_GEMM
+  if (S > 1) {
+    const int g = grid_for((long long)M * N, 256, 2048);
+    if (c_bf16)
+      gemm_splitk_reduce_kernel<bf16_t><<<g, 256, 0, st>>>(part, (int)grid.z, M, N, (bf16_t*)C,
+                                                            C32, bias, scm, beta, relu);
+    else
+      gemm_splitk_reduce_kernel<float><<<g, 256, 0, st>>>(part, (int)grid.z, M, N, (float*)C, C32,
+                                                           bias, scm, beta, relu);
+  }
 }
 
 void colsum(const void* A, const void* Amask, int bf16, float* out, int M, int N, float beta,
