@@ -116,11 +116,14 @@ template <typename T, int K>
 __global__ void __launch_bounds__(256) conv_small_bwd_data_kernel(
     const float* __restrict__ dyc, const float* __restrict__ w, T* __restrict__ dx, int Cin,
     int H, int W, int Cout, int OH, int OW, int pad) {
-  // LDS: Cout*K*K weights of this ci, then image b's whole upstream gradient [Cout][OH][OW]
-  // (6.4 KB for LeNet conv2): staged with coalesced loads once, so the 16 x 25 tap loop
-  // reads LDS instead of issuing one dependent L2 load per tap (35 -> ~5 us at batch 32)
+  // LDS: Cout*K*K weights of this ci, then image b's upstream gradient [Cout][OH][OW] with a
+  // zero border of K-1 on every side (18 x 18 per channel for LeNet conv2, 20.7 KB): staged
+  // with coalesced loads once, so the 16 x 25 tap loop reads LDS at compile-time offsets with
+  // no bounds branches (a dependent L2 load per tap: 35 us at batch 32; guarded LDS taps at
+  // 3 waves per CU: 23 us)
   extern __shared__ float ws[];
   float* gs = ws + Cout * K * K;
+  const int PH = OH + 2 * (K - 1), PW = OW + 2 * (K - 1);
   const int bc = blockIdx.y;
   const int b = bc / Cin, ci = bc % Cin;
   for (int i = threadIdx.x; i < Cout * K * K; i += blockDim.x) {
@@ -128,27 +131,31 @@ __global__ void __launch_bounds__(256) conv_small_bwd_data_kernel(
     ws[i] = w[((long long)co * Cin + ci) * K * K + r];
   }
   const float* gb = dyc + (long long)b * Cout * OH * OW;
-  for (int i = threadIdx.x; i < Cout * OH * OW; i += blockDim.x) gs[i] = gb[i];
+  for (int i = threadIdx.x; i < Cout * PH * PW; i += blockDim.x) {
+    const int co = i / (PH * PW), r = i % (PH * PW);
+    const int oh = r / PW - (K - 1), ow = r % PW - (K - 1);
+    gs[i] = (oh >= 0 && oh < OH && ow >= 0 && ow < OW) ? gb[(co * OH + oh) * OW + ow] : 0.f;
+  }
   __syncthreads();
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= H * W) return;
   const int ih = idx / W, iw = idx % W;
-  float acc = 0.f;
+  // tap (kh, kw) reads padded (ih + pad + K-1 - kh, iw + pad + K-1 - kw)
+  const int base = (ih + pad + K - 1) * PW + (iw + pad + K - 1);
+  float part[K];
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) part[kh] = 0.f;
   for (int co = 0; co < Cout; ++co) {
-    const float* g = gs + co * OH * OW;
+    const float* g = gs + co * PH * PW + base;
     const float* wc = ws + co * K * K;
 #pragma unroll
-    for (int kh = 0; kh < K; ++kh) {
-      const int oh = ih + pad - kh;
-      if (oh < 0 || oh >= OH) continue;
+    for (int kh = 0; kh < K; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < K; ++kw) {
-        const int ow = iw + pad - kw;
-        if (ow < 0 || ow >= OW) continue;
-        acc += g[oh * OW + ow] * wc[kh * K + kw];
-      }
-    }
+      for (int kw = 0; kw < K; ++kw) part[kh] += g[-kh * PW - kw] * wc[kh * K + kw];
   }
+  float acc = 0.f;
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) acc += part[kh];
   st(dx, ((long long)b * Cin + ci) * H * W + idx, acc);
 }
 
@@ -281,7 +288,7 @@ static void bwd_impl(const T* x, const float* w, const T* dp, const T* yp, const
                                                                        OH, OW, PH, PW, relu);
   if (dx) {
     dim3 g((H * W + 255) / 256, B * Cin);
-    const size_t sh = sizeof(float) * (Cout * K * K + Cout * OH * OW);
+    const size_t sh = sizeof(float) * (Cout * K * K + Cout * (OH + 2 * (K - 1)) * (OW + 2 * (K - 1)));
     if (K == 5)
       conv_small_bwd_data_kernel<T, 5><<<g, 256, sh, st>>>(dyc, w, dx, Cin, H, W, Cout, OH, OW, pad);
     else
