@@ -488,6 +488,11 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
       return;
     }
   }
+  if (waves == 16 && bn == 64 && !bnbp && conv_halo_pers_ok(g)) {
+    // one 64-channel chunk: the persistent variant prefetches the next tile's halo
+    conv_halo_pers(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    return;
+  }
   if (waves == 16) {  // 256-pixel tile, 4 x 2 waves of 64 x BN/2 (twice the weight reuse per FLOP)
     const int hp2 = halo_rows_needed(g, 256);
     const int hr = (hp2 + 63) / 64;

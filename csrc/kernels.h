@@ -105,6 +105,10 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
 bool dgrad_s2_supported(const ConvGeomSet& set, int ng);
 void dgrad_s2(const bf16_t* dY, const bf16_t* Wd, bf16_t* dX, const bf16_t* ADD,
               const ConvGeomSet& set, hipStream_t st);
+// conv_halo_pers.hip: persistent single-chunk (64 -> 64 channel) halo conv, cfg 39 shape
+bool conv_halo_pers_ok(const ConvGeom& g);
+void conv_halo_pers(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+                    const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st);
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
