@@ -1,6 +1,7 @@
 """NHWC bf16 ResNet kernels (implicit-GEMM conv fwd/dgrad/wgrad, BN, pooling) vs
 PyTorch fp32 references computed on the same bf16-rounded inputs."""
 import math
+from pathlib import Path
 
 import pytest
 import torch
@@ -762,3 +763,62 @@ def test_bn_backward_apply_on_load(dev, geom, accumulate):
         L.conv_wgrad(x, dy, dw_ref, slab, Cin, k, k, s, p, 0.0, S, cfg, False)
         L.conv_wgrad(x, dz, dw, slab, Cin, k, k, s, p, 0.0, S, cfg, False, **bkw)
         assert _rel(dw, dw_ref) < 1e-4, cfg
+
+
+def test_conv_halo_persistent_opt_in(dev, tmp_path):
+    """The opt-in persistent single-chunk halo conv (DMLAB_HALO_PERS=1, read once per process,
+    so checked in a child process): forward with statistics, the fused pre-BN operand and the
+    dgrad equal the per-tile cfg-39 kernel of this process."""
+    import subprocess
+    import sys
+
+    N, H, C = 6, 56, 64  # 6 * 56 * 56 / 256 = 73.5 tiles: a partial last tile
+    g = torch.Generator(device=dev).manual_seed(5)
+    x = torch.randn(N, H, H, C, device=dev, generator=g).bfloat16()
+    w = torch.randn(C, C, 3, 3, device=dev, generator=g) / 24.0
+    sc = torch.rand(C, device=dev, generator=g) + 0.5
+    sh = torch.randn(C, device=dev, generator=g) * 0.3
+    wf = torch.empty(C, 3, 3, C, device=dev, dtype=torch.bfloat16)
+    wd = torch.empty(C, 3, 3, C, device=dev, dtype=torch.bfloat16)
+    lib().pack_weights(w.contiguous(), wf, wd, C)
+    M = N * H * H
+    T = lib().conv_stats_rows(M, 39, C)
+
+    def run():
+        y = torch.empty_like(x)
+        st = torch.empty(T * 2 * C, device=dev)
+        lib().conv_fwd(x, wf, y, st, None, 3, 3, 1, 1, 39)
+        yp = torch.empty_like(x)
+        lib().conv_fwd(x, wf, yp, torch.empty_like(st), None, 3, 3, 1, 1, 39, pre_scale=sc,
+                       pre_shift=sh)
+        dx = torch.empty_like(x)
+        lib().conv_dgrad(x, wd, dx, 3, 3, 1, 1, None, 39)
+        return y, st, yp, dx
+
+    ref = run()
+    path = tmp_path / "ref.pt"
+    torch.save({"x": x.cpu(), "wf": wf.cpu(), "wd": wd.cpu(), "sc": sc.cpu(), "sh": sh.cpu(),
+                "ref": [t.cpu() for t in ref]}, path)
+    code = f"""
+import sys, torch
+sys.path.insert(0, {str(Path(__file__).resolve().parent.parent)!r})
+from dmlab.ops._native import lib
+d = torch.load({str(path)!r}, weights_only=True)
+dev = torch.device("cuda")
+x, wf, wd, sc, sh = (d[k].to(dev) for k in ("x", "wf", "wd", "sc", "sh"))
+C, M = x.shape[3], x.numel() // x.shape[3]
+T = lib().conv_stats_rows(M, 39, C)
+y = torch.empty_like(x); st = torch.empty(T * 2 * C, device=dev)
+lib().conv_fwd(x, wf, y, st, None, 3, 3, 1, 1, 39)
+yp = torch.empty_like(x)
+lib().conv_fwd(x, wf, yp, torch.empty_like(st), None, 3, 3, 1, 1, 39, pre_scale=sc, pre_shift=sh)
+dx = torch.empty_like(x)
+lib().conv_dgrad(x, wd, dx, 3, 3, 1, 1, None, 39)
+for a, b in zip((y, st, yp, dx), d["ref"]):
+    assert torch.equal(a.cpu(), b), "mismatch"
+print("OK")
+"""
+    env = dict(__import__("os").environ, DMLAB_HALO_PERS="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
