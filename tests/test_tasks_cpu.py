@@ -46,6 +46,17 @@ def test_task1_cpu_mlp_sgd(tmp_path):
     assert ls[-1] < ls[0]
 
 
+def test_task1_cpu_mlp_sgd_default_lr_trains(tmp_path):
+    """The logits MLP with the default SGD settings keeps learning (the notebook's lr 0.1,
+    meant for its double-softmax head, diverged to chance on logits)."""
+    out = _run(["-m", "dmlab.tasks.task1", "--device", "cpu", "--synthetic", "--model", "mlp",
+                "--optimizer", "sgd", "--max-steps", "300", "--no-tb"], tmp_path)
+    ls = _losses(out)
+    assert min(ls[-5:]) < 2.0 and ls[-1] < ls[0]
+    acc = float(re.search(r"Test set: Accuracy: \d+/10000 \((\d+\.\d{2})%\)", out).group(1))
+    assert acc > 20.0
+
+
 def test_task2_spawn_allgather_straggler(tmp_path):
     out = _run(["-m", "dmlab.tasks.task2", "--n_devices", "2", "--spawn", "--device", "cpu",
                 "--synthetic", "--train-samples", "2560", "--epochs", "1", "--master_port",
