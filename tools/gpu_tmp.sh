@@ -1,9 +1,9 @@
-# Ad-hoc GPU step (overwritten per experiment): colsum batching check.
+# Ad-hoc GPU step (overwritten per experiment): ResNet eager vs hipGraph re-check.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_native_lenet.py tests/test_native_resnet_model.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_cs.log 2>&1 && \
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_cs -o prof -- python bench.py --steps 7 --warmup 3 > gpurun_out/prof_cs.log 2>&1
-rc=$?
-tail -2 gpurun_out/pytest_cs.log
-exit $rc
+for r in 1 2; do for gph in 0 1; do
+  timeout -k 10 300 python bench.py --steps 30 --warmup 5 --graph $gph > gpurun_out/b.json 2>>gpurun_out/bench_graph.err || exit 1
+  echo "graph=$gph $(cut -c1-170 gpurun_out/b.json)" >> gpurun_out/graph_ab.txt
+done; done
+cat gpurun_out/graph_ab.txt
