@@ -104,9 +104,10 @@ def test_mlp_matches_torch(dev):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_cross_entropy_kernel(dev, dtype):
-    x = (torch.randn(300, 1000, device=dev) * 3).to(dtype).requires_grad_(True)
-    y = torch.randint(0, 1000, (300,), device=dev)
+@pytest.mark.parametrize("B,C", [(300, 1000), (32, 10), (256, 1000), (1, 10)])
+def test_cross_entropy_kernel(dev, dtype, B, C):
+    x = (torch.randn(B, C, device=dev) * 3).to(dtype).requires_grad_(True)
+    y = torch.randint(0, C, (B,), device=dev)
     l1 = cross_entropy(x, y)
     l1.backward(torch.tensor(2.0, device=dev))
     xr = x.detach().float().requires_grad_(True)
