@@ -210,13 +210,20 @@ class BasicBlock(Layer):
         # c1's BN-apply + ReLU is fused into c2's operand staging: relu(bn1(y1)) is never
         # written (c2's forward and weight-gradient halo kernels normalise y1 on the fly)
         y1 = self.c1.native_fwd(x, c1, train, raw=True)
+        residual = idt
         if side is not None:
-            main.wait_stream(side)
-            # tensors the side stream allocated are used (and freed) on the main stream
-            for t in [idt] + [v for v in cd.values() if torch.is_tensor(v)]:
-                t.record_stream(main)
             x.record_stream(side)
-        out = self.c2.native_fwd(y1, c2, train, residual=idt, pre=(c1["scale"], c1["shift"]))
+
+            def residual():
+                # joined only where c2's BN-apply adds the shortcut: c2's conv (which reads
+                # y1, not the shortcut) no longer waits for the side stream (a 10-50 us
+                # main-stream stall per projection block)
+                main.wait_stream(side)
+                # tensors the side stream allocated are used (and freed) on the main stream
+                for t in [idt] + [v for v in cd.values() if torch.is_tensor(v)]:
+                    t.record_stream(main)
+                return idt
+        out = self.c2.native_fwd(y1, c2, train, residual=residual, pre=(c1["scale"], c1["shift"]))
         ctx.update(c1=c1, c2=c2, cd=cd)
         return out
 

@@ -169,14 +169,33 @@ class _ProgramFn(torch.autograd.Function):
         defer = prog._defer_wgrad_layers() if side is not None else 0
         held, held_fns = [], []  # layers whose wgrads are held back, and their launches
 
+        # Hooks registered stream_ok (DDP without a communication-dtype copy) are issued on
+        # the side stream once it has caught up with the main stream: the collective they
+        # launch is then ordered after the layer's weight gradients (side) and its other
+        # parameter gradients (main) without the main stream ever waiting on the side
+        # stream.  Other hooks keep the one-layer-lag scheme (main waits on the wgrad event),
+        # which left 400-460 us of main-stream gaps per ResNet-18 step.
+        side_hooks = side is not None and bool(prog._grad_hooks) and all(
+            id(h) in prog._stream_ok_hooks for h in prog._grad_hooks)
+
+        def run_side_hooks(js):
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                for j in js:
+                    for hook in prog._grad_hooks:
+                        hook(prog, j)
+
         def flush():
             for fn in held_fns:
                 fn()
             held_fns.clear()
             if held and prog._grad_hooks:
-                ev = torch.cuda.Event()
-                ev.record(side)
-                pending.extend((j, ev) for j in held)
+                if side_hooks:
+                    run_side_hooks(list(held))
+                else:
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    pending.extend((j, ev) for j in held)
             held.clear()
 
         try:
@@ -197,6 +216,12 @@ class _ProgramFn(torch.autograd.Function):
                 if side is None:
                     for hook in prog._grad_hooks:
                         hook(prog, i)
+                    continue
+                if side_hooks:
+                    if 0 < i <= defer:
+                        held.append(i)
+                    else:
+                        run_side_hooks([i])
                     continue
                 for j, ev in pending:
                     main.wait_event(ev)
@@ -244,6 +269,7 @@ class Program(nn.Module):
         self._accumulate = False
         self._native_active = False
         self._grad_hooks: list[Callable] = []
+        self._stream_ok_hooks: set[int] = set()  # ids of hooks that may run on the side stream
         self._post_backward_hooks: list[Callable] = []
         self._anchor = torch.zeros(1, requires_grad=True)
         self._wver = None
@@ -316,9 +342,17 @@ class Program(nn.Module):
         return False
 
     # ---------------------------------------------------------------- hooks
-    def register_grad_hook(self, fn):
-        """fn(program, layer_index) after layer i wrote its weight gradients."""
+    def register_grad_hook(self, fn, stream_ok: bool = False):
+        """fn(program, layer_index) after layer i wrote its weight gradients.
+
+        stream_ok: fn only enqueues stream-ordered device work on the current stream (e.g.
+        collectives over the layer's gradient buckets) and keeps no tensor it allocates past
+        the call; with a two-stream backward it is then called with the weight-gradient
+        stream current, once that stream has caught up with the main stream, so the main
+        stream never waits for it."""
         self._grad_hooks.append(fn)
+        if stream_ok:
+            self._stream_ok_hooks.add(id(fn))
 
     def register_post_backward_hook(self, fn):
         self._post_backward_hooks.append(fn)

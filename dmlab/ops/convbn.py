@@ -369,6 +369,8 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     # (the residual is not kept; re-reading `out` would cost 16x the bytes)
     mask = (torch.empty(out.numel() // 8, device=x.device, dtype=torch.uint8)
             if (train and residual is not None and layer.relu) else None)
+    if callable(residual):  # a shortcut computed on another stream: join it here
+        residual = residual()
     L.bn_apply(y, residual, scale, shift, out, layer.relu, mask=mask)
     if train and residual is not None:
         ctx["out"] = out

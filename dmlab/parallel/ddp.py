@@ -195,7 +195,11 @@ class DistributedDataParallel(nn.Module):
         self._bucket_of_index = {i: self._bucket_of[i] for i in range(len(flat.params))
                                  if i in self._bucket_of}
         self._layer_params = [prog.layer_params(i) for i in range(len(prog.layers))]
-        prog.register_grad_hook(self._on_layer_done)
+        if self.ws > 1:  # one rank: nothing to launch per layer (finalize still runs)
+            # stream_ok: the bucket launches only enqueue collectives (or the xGMI kernel) on
+            # the current stream; a bf16 communication copy outlives the call, so it keeps
+            # the main-stream ordering
+            prog.register_grad_hook(self._on_layer_done, stream_ok=self.comm_dtype is None)
         prog.register_post_backward_hook(lambda _p: self._finalize())
 
     def _setup_generic(self, cap_mb, first_mb):

@@ -1,9 +1,10 @@
-# Ad-hoc GPU step (overwritten per experiment): single-block CE.
+# Ad-hoc GPU step (overwritten per experiment): no main-stream waits for DDP hooks / shortcut join.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_native_lenet.py tests/test_graph_capture.py tests/test_tasks_cpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ce.log 2>&1 && \
-for d in fp32 bf16 fp32 bf16; do timeout -k 10 300 python bench.py --model lenet --steps 300 --warmup 30 --dtype $d >> gpurun_out/lenet_ce.jsonl 2>/dev/null || exit 1; done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ns.log 2>&1 && \
+for r in 1 2 3; do timeout -k 10 200 python bench.py --steps 30 --warmup 5 >> gpurun_out/bench_ns.jsonl 2>>gpurun_out/bench_ns.err || exit 1; done && \
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/prof_ns -o prof -- python bench.py --steps 7 --warmup 3 > gpurun_out/prof_ns.log 2>&1
 rc=$?
-tail -2 gpurun_out/pytest_ce.log; cut -c1-160 gpurun_out/lenet_ce.jsonl
+tail -2 gpurun_out/pytest_ns.log; cut -c1-170 gpurun_out/bench_ns.jsonl
 exit $rc
