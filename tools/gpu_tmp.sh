@@ -1,8 +1,14 @@
-# Ad-hoc GPU step (overwritten per experiment): HIP API trace of the ResNet step (host timing).
+# Ad-hoc GPU step (overwritten per experiment): host enqueue time of the ResNet step.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d gpurun_out/prof_api -o prof -- python bench.py --steps 5 --warmup 3 > gpurun_out/prof_api.log 2>&1
+timeout -k 10 300 python tools/host_lead.py --steps 30 --warmup 5 --profile gpurun_out/host2.prof > gpurun_out/host_lead.json 2>&1 && \
+python -c "
+import pstats
+p = pstats.Stats('gpurun_out/host2.prof')
+p.sort_stats('tottime').print_stats(45)
+p.sort_stats('cumtime').print_stats(45)
+" > gpurun_out/host_prof2.txt 2>&1
 rc=$?
-ls gpurun_out/prof_api
+cat gpurun_out/host_lead.json
 exit $rc
