@@ -1,14 +1,10 @@
-# Ad-hoc GPU step (overwritten per experiment): host enqueue time of the ResNet step.
+# Ad-hoc GPU step (overwritten per experiment): CU-masked weight-gradient stream A/B.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/host_lead.py --steps 30 --warmup 5 --profile gpurun_out/host2.prof > gpurun_out/host_lead.json 2>&1 && \
-python -c "
-import pstats
-p = pstats.Stats('gpurun_out/host2.prof')
-p.sort_stats('tottime').print_stats(45)
-p.sort_stats('cumtime').print_stats(45)
-" > gpurun_out/host_prof2.txt 2>&1
-rc=$?
-cat gpurun_out/host_lead.json
-exit $rc
+out=gpurun_out/cumask_ab.jsonl; : > $out
+for m in "" 77777777 7f7f7f7f "" 3f3f3f3f 77777777 7f7f7f7f; do
+  echo "mask=$m" >> $out
+  DMLAB_WGRAD_CUMASK=$m timeout -k 10 200 python bench.py --steps 40 --warmup 8 >> $out 2>> gpurun_out/cumask_ab.err || exit 1
+done
+cat $out | cut -c1-200
