@@ -98,6 +98,13 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     return TILE_CFG[t]
 
 
+# weight-gradient blocks per launch (m-split target): ~2 per CU.  These run on the side
+# stream for the whole kernel and hold LDS the critical-path kernels need.  Measured
+# (profiles/wgrad_blocks_r2c.jsonl, one call): 512 -> 44.2/44.4k img/s, 384 44.2k,
+# 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k
+_WGRAD_BLOCKS = int(os.environ.get("DMLAB_WGRAD_BLOCKS", "512"))
+
+
 def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
@@ -124,7 +131,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
         # >= 8 row steps of 64 per split: the small-K layers (1x1/s2 downsample: K = Cin)
         # have one or two output tiles, so the m-split is their only parallelism
         max_split = max(1, M // 512)
-    S = max(1, min(max_split, math.ceil(512 / tiles)))
+    S = max(1, min(max_split, math.ceil(_WGRAD_BLOCKS / tiles)))
     return cfg, S
 
 

@@ -1,10 +1,10 @@
-# Ad-hoc GPU step (overwritten per experiment): CU-masked weight-gradient stream A/B.
+# Ad-hoc GPU step (overwritten per experiment): weight-gradient m-split target A/B.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-out=gpurun_out/cumask_ab.jsonl; : > $out
-for m in "" 77777777 7f7f7f7f "" 3f3f3f3f 77777777 7f7f7f7f; do
-  echo "mask=$m" >> $out
-  DMLAB_WGRAD_CUMASK=$m timeout -k 10 200 python bench.py --steps 40 --warmup 8 >> $out 2>> gpurun_out/cumask_ab.err || exit 1
+out=gpurun_out/wgrad_blocks_ab.jsonl; : > $out
+for b in 512 256 1024 384 512 768 256 1024; do
+  echo "blocks=$b" >> $out
+  DMLAB_WGRAD_BLOCKS=$b timeout -k 10 200 python bench.py --steps 40 --warmup 8 >> $out 2>> gpurun_out/wgrad_blocks_ab.err || exit 1
 done
-cat $out | cut -c1-200
+cut -c1-120 $out
