@@ -287,7 +287,7 @@ __device__ __forceinline__ uint32_t pos_bits8(const uint4& v) {
   return b;
 }
 
-template <bool RES, bool RELU>
+template <bool RES, bool RELU, int U = 4>  // U: loads of U grid-strided chunks in flight
 __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ y,
                                                        const bf16_t* __restrict__ res,
                                                        const float* __restrict__ scale,
@@ -302,7 +302,6 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   __syncthreads();
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int C8 = C >> 3;
-  constexpr int U = 4;  // loads of U grid-strided chunks in flight before any is consumed
   for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
     uint4 yr[U], rr[U];
 #pragma unroll
@@ -456,9 +455,9 @@ struct BnBwdBatch {
 };
 
 // grid (G); block 256; thread t owns channel chunk t % C8 of the rows ≡ t / C8 (mod 256 / C8)
-template <int MODE>
+template <int MODE, int UU = 4>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* __restrict__ part) {
-  constexpr int U = MODE == 3 ? 2 : 4;
+  constexpr int U = MODE == 3 ? 2 : UU;
   extern __shared__ float red[];  // [256][16] partials, then [2][C] scale/shift
   const int C = a.C, C8 = C >> 3;
   float* sc = red + 256 * 16;
@@ -528,11 +527,11 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 }
 
 // dy = a·dz + b·y + c ; optional dres = dz
-template <int MODE, bool DRES>
+template <int MODE, bool DRES, int UU = 4>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const float* __restrict__ coef,
                                                            bf16_t* __restrict__ dy,
                                                            bf16_t* __restrict__ dres) {
-  constexpr int U = MODE == 3 ? 2 : 4;
+  constexpr int U = MODE == 3 ? 2 : UU;
   extern __shared__ float cf[];  // [3][C] coefficients, [2][C] forward scale/shift
   const int C = a.C, C8 = C >> 3;
   for (int i = threadIdx.x; i < 3 * C; i += blockDim.x) cf[i] = coef[i];
@@ -1186,6 +1185,11 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
   const long long n8 = n / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 2 * C;
+  static const int bnf_u = getenv("DMLAB_BNF_U") ? atoi(getenv("DMLAB_BNF_U")) : 4;
+  if (res && relu && bnf_u == 8) {
+    bn_apply_kernel<true, true, 8><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
+    return;
+  }
   if (res) {
     if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
     else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
@@ -1193,6 +1197,11 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
     if (relu) bn_apply_kernel<false, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
     else bn_apply_kernel<false, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
   }
+}
+
+static int bnr_u() {
+  static const int u = getenv("DMLAB_BNR_U") ? atoi(getenv("DMLAB_BNR_U")) : 4;
+  return u;
 }
 
 int bn_bwd_groups(long long M, int C);
@@ -1229,10 +1238,13 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   if (pre_part) {
   } else if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
   else switch (mode) {
-    case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
+    // DMLAB_BNR_U / DMLAB_BNA_U / DMLAB_BNF_U: 16-B chunks per operand in flight per thread
+    // in the reduce / backward apply / forward apply passes.  8 instead of 4: reduce and
+    // forward apply neutral, backward apply -1.2 % (profiles/bn_loads_in_flight_r2c.jsonl)
+    case 0: if (bnr_u() == 8) bn_bwd_reduce_kernel<0, 8><<<G, 256, shr, st>>>(a, part); else bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
     case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
-    case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
-    case 4: bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part); break;
+    case 2: if (bnr_u() == 8) bn_bwd_reduce_kernel<2, 8><<<G, 256, shr, st>>>(a, part); else bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
+    case 4: if (bnr_u() == 8) bn_bwd_reduce_kernel<4, 8><<<G, 256, shr, st>>>(a, part); else bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part); break;
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
   const int G2 = colsum_groups(G);
@@ -1253,7 +1265,10 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;
-#define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
+  static const int bna_u = getenv("DMLAB_BNA_U") ? atoi(getenv("DMLAB_BNA_U")) : 4;
+#define DM_BNB(MD, D)                                                            \
+  if (bna_u == 8 && MD != 3) bn_bwd_apply_kernel<MD, D, 8><<<grid, 256, sh, st>>>(a, coef, dy, dres); \
+  else bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
   if (quad) {
     bn_bwd_apply_quad_kernel<<<grid_for(n8 / 4, 256, 4096), 256, sh, st>>>(a, coef, dy);
     return;
