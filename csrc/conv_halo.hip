@@ -43,8 +43,11 @@ constexpr unsigned OOB = 0x80000000u;
 // ReLU of the previous layer); 2 = X is an upstream gradient dz, operand the BN-backward apply
 // a*dz' + b*y + cc with y = bpre.y (a dgrad consuming its BN's backward without the apply
 // pass; single 64-channel chunk only: the next chunk's halo is never prefetched)
+#ifndef DM_HALO39_MINB
+#define DM_HALO39_MINB 4
+#endif
 template <int BN, int HR, int WM, int WN, int BMH, int PRE, int PF>
-__global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? 4 : 2) conv_halo_kernel(
+__global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_HALO39_MINB : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,

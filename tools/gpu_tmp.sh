@@ -1,13 +1,19 @@
-# Ad-hoc GPU step (overwritten per experiment): BN pass loads-in-flight A/B.
+# Ad-hoc GPU step (overwritten per experiment): layer-1 halo conv launch-bounds A/B
+# (alt/_C_minb2.so = the extension built with -DDM_HALO39_MINB=2).
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-DMLAB_BNR_U=8 DMLAB_BNA_U=8 DMLAB_BNF_U=8 timeout -k 10 300 python -u -m pytest tests/test_native_resnet_kernels.py tests/test_native_resnet_model.py -m gpu -x -q --timeout 120 --timeout-method thread -k "bn or model or resnet" > gpurun_out/pytest_bnu.log 2>&1 || { tail -20 gpurun_out/pytest_bnu.log; exit 1; }
-tail -1 gpurun_out/pytest_bnu.log
-out=gpurun_out/bnu_ab.jsonl; : > $out
-for cfg in "4 4 4" "8 4 4" "4 8 4" "4 4 8" "8 8 8" "4 4 4" "8 8 8"; do
-  set -- $cfg
-  echo "reduceU=$1 applyU=$2 fwdU=$3" >> $out
-  DMLAB_BNR_U=$1 DMLAB_BNA_U=$2 DMLAB_BNF_U=$3 timeout -k 10 200 python bench.py --steps 40 --warmup 8 >> $out 2>> gpurun_out/bnu_ab.err || exit 1
+so=dmlab/_C.cpython-310-x86_64-linux-gnu.so
+cp $so alt/_C_default.so
+out=gpurun_out/minb_ab.jsonl; : > $out
+for v in default minb2 default minb2 default minb2; do
+  cp alt/_C_$v.so $so
+  echo "variant=$v" >> $out
+  timeout -k 10 200 python bench.py --steps 40 --warmup 8 >> $out 2>> gpurun_out/minb_ab.err || exit 1
 done
+cp alt/_C_minb2.so $so
+timeout -k 10 300 python -u -m pytest tests/test_native_resnet_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -k halo > gpurun_out/pytest_minb.log 2>&1 || { tail -20 gpurun_out/pytest_minb.log; exit 1; }
+tail -1 gpurun_out/pytest_minb.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_minb2 -o prof -- python bench.py --steps 7 --warmup 3 > gpurun_out/prof_minb2.log 2>&1
+cp alt/_C_default.so $so
 cut -c1-120 $out
