@@ -43,6 +43,9 @@ constexpr unsigned OOB = 0x80000000u;
 // ReLU of the previous layer); 2 = X is an upstream gradient dz, operand the BN-backward apply
 // a*dz' + b*y + cc with y = bpre.y (a dgrad consuming its BN's backward without the apply
 // pass; single 64-channel chunk only: the next chunk's halo is never prefetched)
+// waves per SIMD the 8-wave 64-channel tile (cfg 39) is compiled for: 4 = its LDS-bound
+// occupancy (2 workgroups per CU).  Built with 2: 43.9k vs 44.8k img/s
+// (profiles/halo39_launch_bounds_r2c.jsonl)
 #ifndef DM_HALO39_MINB
 #define DM_HALO39_MINB 4
 #endif
