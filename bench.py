@@ -33,11 +33,12 @@ METRIC = "samples/sec (whole node) for task3 DDP CNN at 1/2/4/8 MI355X"
 # cudnn.benchmark = True (MIOpen solver search; LeNet without the per-step loss.item()),
 # profiles/stock_pytorch_rocm_tuned_r1s5.jsonl
 STOCK_PER_GPU = {("resnet18", 256): 16912.7, ("resnet18", 512): 19785.8, ("lenet", 32): 49523.7}
-# per-GPU batch of the headline run: 512 images (a 1.3 ms/step fixed cost -- BN statistic
-# reductions, weight-gradient slab reduces, optimizer, launch floor -- is amortised over
-# twice the work of 256; measured 35.4k -> 39.0k img/s on one MI355X; 288 GB HBM holds it
-# with room to spare)
-RESNET_BATCH = 512
+# per-GPU batch of the headline run: 1024 images.  A ~1.3 ms/step fixed cost (BN statistic
+# reductions, weight-gradient slab reduces, optimizer, launch floor) is amortised over more
+# work: 256 -> 36.7k, 512 -> 44.5k, 768 -> 46.5k, 1024 -> 46.7-46.9k img/s on one MI355X
+# (profiles/batch_sweep_r2c.jsonl); activations take ~60 GB of the 288 GB HBM3E.  The
+# native step matches stock PyTorch's loss at this batch (profiles/batch_numerics_r2c.jsonl).
+RESNET_BATCH = 1024
 
 
 def parse():
