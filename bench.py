@@ -32,12 +32,16 @@ METRIC = "samples/sec (whole node) for task3 DDP CNN at 1/2/4/8 MI355X"
 # default run (profiles/stock_pytorch_rocm_r1.jsonl) and the --tuned run with
 # cudnn.benchmark = True (MIOpen solver search; LeNet without the per-step loss.item()),
 # profiles/stock_pytorch_rocm_tuned_r1s5.jsonl
-STOCK_PER_GPU = {("resnet18", 256): 16912.7, ("resnet18", 512): 19785.8, ("lenet", 32): 49523.7}
+# (1024: default run only, profiles/stock_pytorch_rocm_b1024_r2c.jsonl; the tuned solver
+# search outran gpurun's silence limit)
+STOCK_PER_GPU = {("resnet18", 256): 16912.7, ("resnet18", 512): 19785.8,
+                 ("resnet18", 1024): 18581.2, ("lenet", 32): 49523.7}
 # per-GPU batch of the headline run: 1024 images.  A ~1.3 ms/step fixed cost (BN statistic
 # reductions, weight-gradient slab reduces, optimizer, launch floor) is amortised over more
 # work: 256 -> 36.7k, 512 -> 44.5k, 768 -> 46.5k, 1024 -> 46.7-46.9k img/s on one MI355X
-# (profiles/batch_sweep_r2c.jsonl); activations take ~60 GB of the 288 GB HBM3E.  The
-# native step matches stock PyTorch's loss at this batch (profiles/batch_numerics_r2c.jsonl).
+# (profiles/batch_sweep_r2c.jsonl); twice the 512-image activations, a small part of the
+# 288 GB HBM3E.  The native step matches stock PyTorch's loss at this batch
+# (profiles/batch_numerics_r2c.jsonl).
 RESNET_BATCH = 1024
 
 

@@ -1,17 +1,8 @@
-# Ad-hoc GPU step (overwritten per experiment): native vs stock-torch loss at large per-GPU batch.
+# Ad-hoc GPU step (overwritten per experiment): stock PyTorch-ROCm ResNet-18 at 1024 per GPU.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-out=gpurun_out/batch_numerics.jsonl; : > $out
-for b in 512 1024; do
-  for be in native torch; do
-    for s in 1 4; do
-      timeout -k 10 240 python bench.py --batch $b --backend $be --steps $s --warmup 0 >> $out 2>> gpurun_out/batch_numerics.err || { tail -5 gpurun_out/batch_numerics.err; exit 1; }
-    done
-  done
-done
-python -c "
-import json
-for l in open('$out'):
-    d=json.loads(l); print(d['config']['per_gpu_batch'], d['config']['backend'], d['steps'], d['final_loss'])
-"
+timeout -k 10 500 python -u tools/probe_stock.py --resnet-batches 1024 > gpurun_out/stock_b1024.jsonl 2> gpurun_out/stock_b1024.err
+rc=$?
+cat gpurun_out/stock_b1024.jsonl | cut -c1-200
+exit $rc
