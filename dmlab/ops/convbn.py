@@ -101,7 +101,8 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
 # weight-gradient blocks per launch (m-split target): ~2 per CU.  These run on the side
 # stream for the whole kernel and hold LDS the critical-path kernels need.  Measured
 # (profiles/wgrad_blocks_r2c.jsonl, one call): 512 -> 44.2/44.4k img/s, 384 44.2k,
-# 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k
+# 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k; at 1024 images per GPU 512 -> 46.6k,
+# 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl)
 _WGRAD_BLOCKS = int(os.environ.get("DMLAB_WGRAD_BLOCKS", "512"))
 
 
