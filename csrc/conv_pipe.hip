@@ -1,0 +1,402 @@
+// Pipelined implicit-GEMM convolution ("pipe" kernels, cfg 90/91), gfx950.
+//
+// Round 3 rebuild of the conv main loop around what the register-staged tiles could not do
+// (docs/KERNELS.md "Where the ceiling is"): the v3/halo kernels keep 64x64 per wave, stage
+// every operand through VGPRs and ds_write, and run at 2 workgroups per CU with a barrier per
+// 64-deep K step; their MFMA pipe is busy ~30 % of the time.  Here:
+//
+//  * one 256-pixel x BN-channel tile per workgroup, 4 waves (2 x 2), each wave owning a
+//    128 x BN/2 sub-tile as 4 x BN/64 blocks of v_mfma_f32_32x32x16_bf16 (the 256 fp32
+//    accumulators of the BN = 256 tile live in the AGPR half of the unified register file):
+//    0.5 LDS fragment reads per MFMA (v3: 1.0);
+//  * both operands go global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds): no staging
+//    VGPRs, no ds_write pass.  The A operand is the implicit im2col matrix gathered row by
+//    row — each DMA lane supplies the address of its own output pixel's tap source, padding
+//    taps read 0 through the buffer range check — so one kernel serves every tap geometry
+//    ConvGeom describes (3x3 and 1x1, stride 1 and 2, forward and the data gradient);
+//  * two LDS stages; the ONE barrier of a K step sits after the last fragment reads of the
+//    step (before its last 16-deep substep), so the DMA of tile t+2 is issued right after it
+//    and has a full K step to land while the other stage is consumed; the first fragments of
+//    the next tile are read under the last substep's MFMAs (no read latency at the seam);
+//  * the DMA is issued from inline asm so the compiler's alias-blind LDS-DMA bookkeeping does
+//    not drain the queue before every ds_read (docs/KERNELS.md, conv_h5 notes); the loop
+//    retires it with its own s_waitcnt vmcnt(0) at the barrier.  The loop has no other VMEM
+//    op, so nothing else waits on the queue.
+//  * epilogue: per-column BN statistics straight from the accumulators (no LDS pass), then
+//    each wave stages its own 32-row bands through a private LDS region and stores 16-B bf16
+//    chunks (optional residual add), so no cross-wave barrier and no 2-pass 133 KB image.
+//
+// LDS swizzle: the 16-B chunk c of tile row r lives at slot c ^ ((r >> 1) & 7) (igemm_common.h
+// swz), conflict-free for the 32x32x16 fragment reads; the DMA image is lane-linear (base +
+// 16 * lane), so the swizzle is applied to the SOURCE chunk each lane fetches.
+#include "common.h"
+#include "conv_geom.h"
+#include "igemm_common.h"
+#include "kernels.h"
+
+#include <type_traits>
+
+namespace dm {
+
+namespace {
+constexpr int PBM = 256;   // output pixels per tile
+constexpr int PBK = 64;    // K per step (one 128-B LDS row per tile row)
+constexpr unsigned POOB = 0x80000000u;
+
+typedef int pi32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ pi32x4 prsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  pi32x4 r;
+  r[0] = (int)(unsigned)a;
+  r[1] = (int)(unsigned)(a >> 32) & 0xffff;
+  r[2] = (int)bytes;
+  r[3] = 0x00020000;
+  return r;
+}
+
+// lane l's 16 bytes at buffer byte `off` -> LDS byte lds + 16*l (lds wave-uniform, in an SGPR)
+__device__ __forceinline__ void pdma16(const pi32x4& rs, unsigned lds, unsigned off) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %2, 0 offen lds"
+      :
+      : "v"(off), "s"(lds), "s"(rs)
+      : "memory");
+}
+
+// BN output channels per tile (256 or 128); WM x WN waves, wave tile 256/WM x BN/WN
+template <int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64, 1) conv_pipe_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
+    float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes, int ntN, int mtiles,
+    int xcd) {
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int TM = PBM / WM, TN = BN / WN;  // wave tile
+  constexpr int RM = TM / 32, RN = TN / 32;   // 32x32 blocks per wave
+  constexpr int AI = PBM * 8 / NT;            // A DMA instructions per thread per tile
+  constexpr int BI = BN * 8 / NT;             // B DMA instructions per thread per tile
+  static_assert(AI * NT == PBM * 8 && BI * NT == BN * 8 && RM >= 1 && RN >= 1, "tile");
+  constexpr unsigned ABYTES = PBM * PBK * 2;
+  constexpr unsigned STG = ABYTES + BN * PBK * 2;  // one pipeline stage
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+
+  // block -> (M tile, N tile): the N tiles of one M tile are blocks b, b+8, ... (one XCD)
+  int bx = blockIdx.x, by = 0;
+  if (xcd) {
+    const int b = blockIdx.x, j = b >> 3;
+    by = j % ntN;
+    bx = (j / ntN) * 8 + (b & 7);
+    if (bx >= mtiles) return;
+  } else {
+    bx = blockIdx.x % mtiles;
+    by = blockIdx.x / mtiles;
+  }
+  const int m0 = bx * PBM;
+  const int n0 = by * BN;
+  const int ntaps = g.nth * g.ntw;
+  const int nchunk = g.C / PBK;
+  const int S = ntaps * nchunk;
+
+  const pi32x4 rsx = prsrc(X, xbytes);
+  const pi32x4 rsw = prsrc(Wp, wbytes);
+  const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)smem;
+
+  // ---- DMA lane geometry: instruction j of wave w fills tile rows 8 NW j + 8w + lane/8 ----
+  const int drow = 8 * wid + (lane >> 3);                 // row within an 8 NW-row group
+  const int dch = (lane & 7) ^ ((drow >> 1) & 7);         // logical chunk this lane fetches
+  const unsigned choff = (unsigned)dch * 16u;
+  unsigned abase[AI], amask[AI];
+#pragma unroll
+  for (int j = 0; j < AI; ++j) {
+    const int m = m0 + 8 * NW * j + drow;
+    unsigned base = 0, mk = 0;
+    if (m < g.M) {
+      const unsigned r = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      const int x = (int)((unsigned)m - r * (unsigned)g.Wg);
+      const unsigned n = fdiv(r, g.hg_mul, g.hg_shr);
+      const int y = (int)(r - n * (unsigned)g.Hg);
+      const int iy = y * g.isy, ix = x * g.isx;
+      base = (((unsigned)n * g.H + iy) * g.W + ix) * (unsigned)g.C * 2u + choff;
+      for (int th = 0; th < g.nth; ++th) {
+        const int yy = iy + g.dy0 + th * g.dys;
+        if ((unsigned)yy >= (unsigned)g.H) continue;
+        for (int tw = 0; tw < g.ntw; ++tw) {
+          const int xx = ix + g.dx0 + tw * g.dxs;
+          if ((unsigned)xx < (unsigned)g.W) mk |= 1u << (th * g.ntw + tw);
+        }
+      }
+    }
+    abase[j] = base;
+    amask[j] = mk;
+  }
+  unsigned bbase[BI];
+#pragma unroll
+  for (int j = 0; j < BI; ++j) {
+    const int n = n0 + 8 * NW * j + drow;
+    bbase[j] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u + choff : POOB;
+  }
+
+  // DMA of the next K step (chunk icc, tap ith/itw): prep() computes this thread's source
+  // offsets and advances the counters; one(q, st) issues DMA instruction q into stage st
+  constexpr int ND = AI + BI;
+  int icc = 0, ith = 0, itw = 0;
+  unsigned doff[ND];
+  auto prep = [&]() __attribute__((always_inline)) {
+    const int cc = icc, th = ith, tw = itw;
+    const int t = th * g.ntw + tw;
+    if (++itw == g.ntw) {
+      itw = 0;
+      if (++ith == g.nth) {
+        ith = 0;
+        ++icc;
+      }
+    }
+    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
+    const bool live = cc < nchunk;  // steps past the end load zeros
+    const unsigned tapd = (unsigned)((dy * g.W + dx) * g.C * 2 + cc * PBK * 2);
+    const unsigned wko =
+        (unsigned)((((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C + cc * PBK) * 2);
+#pragma unroll
+    for (int j = 0; j < AI; ++j) doff[j] = live && ((amask[j] >> t) & 1u) ? abase[j] + tapd : POOB;
+#pragma unroll
+    for (int j = 0; j < BI; ++j) doff[AI + j] = live && bbase[j] != POOB ? bbase[j] + wko : POOB;
+  };
+  const unsigned ldsw = lds0 + (unsigned)wid * 1024u;
+  auto one = [&](int q, int st) __attribute__((always_inline)) {
+    if (q < AI)
+      pdma16(rsx, ldsw + (unsigned)st * STG + (unsigned)q * (NW * 1024u), doff[q]);
+    else
+      pdma16(rsw, ldsw + (unsigned)st * STG + ABYTES + (unsigned)(q - AI) * (NW * 1024u), doff[q]);
+  };
+
+  // ---- fragment reads: A rows wm*TM + i*32 + (lane&31), B rows wn*TN + j*32 + (lane&31) ----
+  const int frow_a = wm * TM + (lane & 31);
+  const int frow_b = wn * TN + (lane & 31);
+  const int fsw_a = (frow_a >> 1) & 7, fsw_b = (frow_b >> 1) & 7;  // same for +32k rows
+  const int hsel = lane >> 5;
+  f32x16 acc[RM][RN];
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  constexpr int NMF = RM * RN;  // MFMAs per 16-deep substep
+  constexpr int NRD = RM + RN;  // fragment reads per substep
+  bf16x8 f0[NRD], f1[NRD];      // [0, RM) A fragments, [RM, NRD) B fragments
+  auto rd1 = [&](bf16x8 (&f)[NRD], int r, int st, int ks) __attribute__((always_inline)) {
+    const int ch = ks * 2 + hsel;
+    if (r < RM)
+      f[r] = *reinterpret_cast<const bf16x8*>(smem + st * STG + frow_a * 128 +
+                                              ((ch ^ fsw_a) << 4) + r * 4096);
+    else
+      f[r] = *reinterpret_cast<const bf16x8*>(smem + st * STG + ABYTES + frow_b * 128 +
+                                              ((ch ^ fsw_b) << 4) + (r - RM) * 4096);
+  };
+  auto rdall = [&](bf16x8 (&f)[NRD], int st, int ks) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < NRD; ++r) rd1(f, r, st, ks);
+  };
+  // one 16-deep substep: the MFMAs of fragment set `fc`, interleaved (one MFMA, one read, then
+  // the DMA share) with the reads of the next substep's fragments into `fn` (RD) and the DMA
+  // of the next-but-one K step into stage dst (DMA)
+  constexpr int NQ = NMF > NRD ? (NMF > ND ? NMF : ND) : (NRD > ND ? NRD : ND);
+  auto sub = [&](const bf16x8 (&fc)[NRD], bf16x8 (&fn)[NRD], int rst, int rks, auto RD_, auto DMA_,
+                 int dst) __attribute__((always_inline)) {
+    constexpr bool RD = decltype(RD_)::value, DMA = decltype(DMA_)::value;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q < NMF) {
+        const int i = q / RN, j = q % RN;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fc[i], fc[RM + j], acc[i][j], 0, 0, 0);
+      }
+      if (RD && q < NRD) rd1(fn, q, rst, rks);
+      if (DMA && q < ND) one(q, dst);
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      if (q < NMF) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (RD && q < NRD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+  };
+  auto barrier_vm0 = [&]() __attribute__((always_inline)) { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // ---- prologue: tiles 0 and 1 in flight, tile 0 published, its first fragments read ----
+  prep();
+#pragma unroll
+  for (int q = 0; q < ND; ++q) one(q, 0);
+  if (S > 1) {
+    prep();
+#pragma unroll
+    for (int q = 0; q < ND; ++q) one(q, 1);
+    if constexpr (ND == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if constexpr (ND == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if constexpr (ND == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (ND == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_barrier" ::: "memory");
+  rdall(f0, 0, 0);
+
+  // one K step from stage cur; MODE 2: barrier, next tile's first reads, DMA of step t+2 into
+  // cur; 1: barrier and reads only (t+2 >= S); 0: last step
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  auto step = [&](int cur, auto MODE_) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(MODE_)::value;
+    sub(f0, f1, cur, 1, T_{}, F_{}, 0);
+    sub(f1, f0, cur, 2, T_{}, F_{}, 0);
+    if constexpr (MODE == 2) prep();
+    sub(f0, f1, cur, 3, T_{}, F_{}, 0);
+    if constexpr (MODE > 0) barrier_vm0();  // tile t+1 landed; every wave is done with stage cur
+    sub(f1, f0, cur ^ 1, 0, std::integral_constant<bool, (MODE > 0)>{},
+        std::integral_constant<bool, (MODE == 2)>{}, cur);
+  };
+  using M2 = std::integral_constant<int, 2>;
+  using M0 = std::integral_constant<int, 0>;
+  // steps past the end (t + 2 >= S) issue zero-DMAs into a stage nobody reads again and read
+  // fragments nobody uses: one uniform loop body (the tail copies of the step cost spills)
+  int t = 0;
+  for (; t + 1 < S; t += 2) {
+    step(0, M2{});
+    step(1, M2{});
+  }
+  if (t < S) step(0, M0{});
+
+  // ---- epilogue ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the stage buffers (LDS reused below)
+  float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2] statistics partials
+  if (stats) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j) {
+      float sm = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = acc[i][j][r];
+          sm += v;
+          q += v * v;
+        }
+      sm += __shfl_xor(sm, 32, 64);
+      q += __shfl_xor(q, 32, 64);
+      if (lane < 32) {
+        const int c = wn * TN + j * 32 + lane;
+        red[(wm * BN + c) * 2 + 0] = sm;
+        red[(wm * BN + c) * 2 + 1] = q;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      if (n0 + c < g.Ncols) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          a += red[(w * BN + c) * 2 + 0];
+          b += red[(w * BN + c) * 2 + 1];
+        }
+        stats[((long long)bx * 2 + 0) * g.Ncols + n0 + c] = a;
+        stats[((long long)bx * 2 + 1) * g.Ncols + n0 + c] = b;
+      }
+    }
+    __syncthreads();
+  }
+  // per-wave staging region: 32 rows x (TN + 4) floats
+  constexpr int LDC = TN + 4;
+  float* cs = reinterpret_cast<float*>(smem) + wid * 32 * LDC;
+  constexpr int CPR = TN / 8;            // 16-B output chunks per row
+  constexpr int RPI = 64 / CPR;          // rows per wave instruction
+  const int cq = lane % CPR, rsub = lane / CPR;
+  const int col = n0 + wn * TN + cq * 8;
+  const int fcol = lane & 31;
+#pragma unroll
+  for (int i = 0; i < RM; ++i) {
+    // stage rows wm*128 + i*32 .. +31 of this wave's columns
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        cs[((r & 3) + 8 * (r >> 2) + 4 * hsel) * LDC + j * 32 + fcol] = acc[i][j][r];
+    // (a wave's LDS accesses complete in order: no barrier between its own write and read)
+#pragma unroll
+    for (int it = 0; it < 32 / RPI; ++it) {
+      const int rr = it * RPI + rsub;
+      const int m = m0 + wm * TM + i * 32 + rr;
+      if (m >= g.M || col >= g.Ncols) continue;
+      const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
+      const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+      const int y = (int)(t - n * (unsigned)g.Hg);
+      const long long o =
+          (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+      const float4 v0 = *reinterpret_cast<const float4*>(cs + rr * LDC + cq * 8);
+      const float4 v1 = *reinterpret_cast<const float4*>(cs + rr * LDC + cq * 8 + 4);
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if (ADD) {
+        const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
+        const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
+          v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+        }
+      }
+      *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                                    pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+    }
+  }
+}
+
+template <int BN, int WM, int WN>
+void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+                 const ConvGeom& g, hipStream_t st) {
+  constexpr size_t STG = (size_t)PBM * PBK * 2 + (size_t)BN * PBK * 2;
+  constexpr size_t sm_main = 2 * STG;
+  constexpr size_t sm_epi = (size_t)WM * WN * 32 * (BN / WN + 4) * 4;
+  constexpr size_t sm = sm_main > sm_epi ? sm_main : sm_epi;
+  const int mtiles = (int)((g.M + PBM - 1) / PBM);
+  const int ntN = (g.Ncols + BN - 1) / BN;
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
+  auto k = conv_pipe_kernel<BN, WM, WN>;
+  constexpr int NT = WM * WN * 64;
+  set_smem_attr(k, sm);
+  if (ntN > 1) {
+    const unsigned mt8 = (unsigned)((mtiles + 7) / 8 * 8);
+    k<<<dim3(mt8 * ntN), NT, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, ntN, mtiles, 1);
+  } else {
+    k<<<dim3((unsigned)mtiles), NT, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, 1, mtiles, 0);
+  }
+  DM_CHECK(hipGetLastError());
+}
+}  // namespace
+
+bool conv_pipe_supported(const ConvGeom& g, int cfg) {
+  const int bn = cfg == 90 ? 256 : 128;
+  if (g.C % PBK != 0 || g.nth * g.ntw > 32 || g.Ncols % bn != 0) return false;
+  if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31)) return false;
+  if ((long long)g.Ncols * g.wK * 2 >= (1LL << 31)) return false;
+  if (g.M >= (1LL << 31)) return false;
+  return true;
+}
+
+void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+               const ConvGeom& g, int cfg, hipStream_t st) {
+  // 90: 256 x 256, 8 waves (2 x 4) of 128 x 64; 91: 256 x 128, 8 waves (4 x 2) of 64 x 64;
+  // 92: 256 x 128, 4 waves (2 x 2) of 128 x 64
+  if (cfg == 90) launch_pipe<256, 2, 4>(X, Wp, Y, ADD, stats, g, st);
+  else if (cfg == 91) launch_pipe<128, 4, 2>(X, Wp, Y, ADD, stats, g, st);
+  else launch_pipe<128, 2, 2>(X, Wp, Y, ADD, stats, g, st);
+}
+
+}  // namespace dm

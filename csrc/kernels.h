@@ -94,6 +94,10 @@ int conv_h5_rowtile(int cfg);
 void conv_h5(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
              const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
              const float* pre_sh = nullptr, const BnBwdEpi* bnb = nullptr);
+// conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90: 256 x 256 tile, 91: 256 x 128)
+bool conv_pipe_supported(const ConvGeom& g, int cfg);
+void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+               const ConvGeom& g, int cfg, hipStream_t st);
 bool conv_halo_supported(const ConvGeom& g);
 long long conv_halo41_stats_rows(long long M, int Ncols);
 bool halo_cfg(int cfg, int& bn, int& waves);

@@ -39,7 +39,8 @@ class Reducer {
   Reducer(at::Tensor grad_buf, std::vector<int64_t> bounds, std::vector<int64_t> param_bucket,
           std::vector<std::vector<int64_t>> layer_params,
           c10::intrusive_ptr<c10d::ProcessGroup> pg, bool use_avg, double avg_scale,
-          int64_t comm_code, int64_t small_cap, py::object small_fn)
+          int64_t comm_code, int64_t small_cap, py::object small_fn,
+          c10::optional<at::Tensor> comm_buf)
       : buf_(std::move(grad_buf)), param_bucket_(std::move(param_bucket)),
         layer_params_(std::move(layer_params)), pg_(pg), use_avg_(use_avg),
         avg_scale_(avg_scale), small_cap_(small_cap), small_fn_(std::move(small_fn)) {
@@ -47,6 +48,13 @@ class Reducer {
     TORCH_CHECK(comm_code >= 0 && comm_code <= 2, "comm_code: 0 (native), 1 (bf16), 2 (fp16)");
     if (comm_code == 1) comm_dtype_ = at::kBFloat16;
     if (comm_code == 2) comm_dtype_ = at::kHalf;
+    if (comm_buf.has_value() && comm_buf->defined()) {
+      TORCH_CHECK(comm_dtype_ && comm_buf->scalar_type() == *comm_dtype_ && comm_buf->dim() == 1 &&
+                      comm_buf->is_contiguous() && comm_buf->numel() >= buf_.numel() &&
+                      comm_buf->device() == buf_.device(),
+                  "comm_buf: flat contiguous buffer of the communication dtype, >= grad_buf");
+      comm_flat_ = *comm_buf;
+    }
     TORCH_CHECK(bounds.size() % 2 == 0 && !bounds.empty(), "bounds: [lo0, hi0, lo1, hi1, ...]");
     TORCH_CHECK(buf_.dim() == 1 && buf_.is_contiguous(), "grad_buf: flat contiguous buffer");
     const int64_t nb = (int64_t)bounds.size() / 2;
@@ -147,7 +155,13 @@ class Reducer {
     }
     at::Tensor t = view;
     if (comm_dtype_ && *comm_dtype_ != view.scalar_type()) {
-      comm_[b] = view.to(*comm_dtype_);
+      // persistent buffer: no allocation (graph-capturable, safe on a side stream)
+      if (comm_flat_.defined()) {
+        comm_[b] = comm_flat_.slice(0, buckets_[b].lo, buckets_[b].hi);
+        comm_[b].copy_(view);
+      } else {
+        comm_[b] = view.to(*comm_dtype_);
+      }
       t = comm_[b];
     }
     c10d::AllreduceOptions opts;
@@ -171,6 +185,7 @@ class Reducer {
   c10::optional<at::ScalarType> comm_dtype_;
   int64_t small_cap_;
   py::object small_fn_;
+  at::Tensor comm_flat_;
   bool enabled_ = true;
   int64_t launched_total_ = 0;
   std::vector<bool> launched_, scaled_;
@@ -184,10 +199,11 @@ void register_reducer(pybind11::module_& m) {
   py::class_<Reducer>(m, "Reducer")
       .def(py::init<at::Tensor, std::vector<int64_t>, std::vector<int64_t>,
                     std::vector<std::vector<int64_t>>, c10::intrusive_ptr<c10d::ProcessGroup>,
-                    bool, double, int64_t, int64_t, py::object>(),
+                    bool, double, int64_t, int64_t, py::object, c10::optional<at::Tensor>>(),
            py::arg("grad_buf"), py::arg("bounds"), py::arg("param_bucket"),
            py::arg("layer_params"), py::arg("pg"), py::arg("use_avg"), py::arg("avg_scale"),
-           py::arg("comm_code"), py::arg("small_cap"), py::arg("small_fn"))
+           py::arg("comm_code"), py::arg("small_cap"), py::arg("small_fn"),
+           py::arg("comm_buf") = py::none())
       .def("mark_ready", &Reducer::mark_ready)
       .def("mark_layer", &Reducer::mark_layer)
       .def("finalize", &Reducer::finalize)

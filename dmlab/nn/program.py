@@ -176,7 +176,7 @@ class _ProgramFn(torch.autograd.Function):
         # stream.  Other hooks keep the one-layer-lag scheme (main waits on the wgrad event),
         # which left 400-460 us of main-stream gaps per ResNet-18 step.
         side_hooks = side is not None and bool(prog._grad_hooks) and all(
-            id(h) in prog._stream_ok_hooks for h in prog._grad_hooks)
+            prog._hook_stream_ok.get(h, False) for h in prog._grad_hooks)
 
         def run_side_hooks(js):
             side.wait_stream(main)
@@ -269,7 +269,9 @@ class Program(nn.Module):
         self._accumulate = False
         self._native_active = False
         self._grad_hooks: list[Callable] = []
-        self._stream_ok_hooks: set[int] = set()  # ids of hooks that may run on the side stream
+        # hook -> may run on the side stream (keyed by the hook object itself, not its id: a
+        # removed hook's id could be reused by an unrelated function)
+        self._hook_stream_ok: dict[Callable, bool] = {}
         self._post_backward_hooks: list[Callable] = []
         self._anchor = torch.zeros(1, requires_grad=True)
         self._wver = None
@@ -351,8 +353,12 @@ class Program(nn.Module):
         stream current, once that stream has caught up with the main stream, so the main
         stream never waits for it."""
         self._grad_hooks.append(fn)
-        if stream_ok:
-            self._stream_ok_hooks.add(id(fn))
+        self._hook_stream_ok[fn] = bool(stream_ok)
+
+    def remove_grad_hook(self, fn):
+        self._grad_hooks.remove(fn)
+        if fn not in self._grad_hooks:
+            self._hook_stream_ok.pop(fn, None)
 
     def register_post_backward_hook(self, fn):
         self._post_backward_hooks.append(fn)

@@ -23,7 +23,17 @@ task3/dist_utils.py:40-46).  Here:
   it can only launch when backward's final layers are done, so all of it is exposed —
   only the first layers' few gradients should wait for the end of backward.
 * Optional bf16 gradient communication (``comm_dtype=torch.bfloat16``) halves
-  the bytes on the links.
+  the bytes on the links.  The cast targets a persistent flat communication buffer
+  (allocated once), so the hooks allocate nothing and stay on the side stream.
+* Bucket hooks on the weight-gradient side stream (``side_stream_hooks``, default on;
+  ``DMLAB_DDP_SIDE_HOOKS=0`` or ``side_stream_hooks=False`` keeps the one-layer-lag scheme
+  in which the main stream waits for each layer's weight gradients before its bucket
+  launches).
+* ``broadcast_buffers`` (default on, as torch DDP): rank 0's module buffers (BatchNorm
+  running statistics, ``num_batches_tracked``) are broadcast — coalesced, one collective
+  per dtype — at every training forward (or every ``buffer_sync_every`` forwards), so the
+  running statistics agree on every rank and a rank-0 checkpoint holds what every rank
+  evaluates with.
 * ``small_allreduce="xgmi"``: buckets of at most ``small_cap_mb`` go through the
   one-shot xGMI peer-memory all-reduce (:mod:`dmlab.parallel.xgmi`, one kernel, no ring
   steps) instead of RCCL — the latency-bound case of the labs' LeNet (207 KB of grads).
@@ -65,7 +75,9 @@ class DistributedDataParallel(nn.Module):
                  first_bucket_mb: float = 4.0, last_bucket_mb: float = 2.0, comm_dtype=None,
                  broadcast_init: bool = True,
                  process_group=None, average: bool = True, small_allreduce: str | None = None,
-                 small_cap_mb: float = 4.0, native: bool | None = None, xgmi_algo: str = "auto"):
+                 small_cap_mb: float = 4.0, native: bool | None = None, xgmi_algo: str = "auto",
+                 side_stream_hooks: bool | None = None, broadcast_buffers: bool = True,
+                 buffer_sync_every: int = 1):
         super().__init__()
         self.module = module
         self.ws = env.get_world_size()
@@ -76,6 +88,15 @@ class DistributedDataParallel(nn.Module):
         self._fold = False  # 1/ws folded into the optimiser
         self.program = module if hasattr(module, "register_grad_hook") else None
         self._last_mb = last_bucket_mb
+        if side_stream_hooks is None:
+            import os
+
+            side_stream_hooks = os.environ.get("DMLAB_DDP_SIDE_HOOKS", "1") != "0"
+        self.side_stream_hooks = bool(side_stream_hooks)
+        self.broadcast_buffers = bool(broadcast_buffers)
+        self.buffer_sync_every = max(1, int(buffer_sync_every))
+        self._fwd_count = 0
+        self._buffers = [b for b in module.buffers()] if self.ws > 1 else []
         if broadcast_init and self.ws > 1:
             init_parameters(module)
         if self.program is not None:
@@ -100,6 +121,12 @@ class DistributedDataParallel(nn.Module):
         self._native = None
         if native is None:
             native = self.ws > 1 and _native_reducer_available()
+        # persistent communication buffer of the low-precision gradient copy (no per-step
+        # allocation: graph-capturable, and safe to fill on the side stream)
+        self._comm_flat = None
+        if self.comm_dtype is not None and self.comm_dtype != self.grad_buf.dtype and self.ws > 1:
+            self._comm_flat = torch.empty(self.grad_buf.numel(), dtype=self.comm_dtype,
+                                          device=self.grad_buf.device)
         if native and self.ws > 1:
             self._build_native(small_cap_mb)
 
@@ -133,7 +160,8 @@ class DistributedDataParallel(nn.Module):
         self._native = _C.Reducer(self.grad_buf, bounds, param_bucket, layer_params, pg,
                                   bool(self._use_avg), self._avg_scale(),
                                   code[self.comm_dtype],
-                                  self._xgmi.cap if self._xgmi is not None else 0, small_fn)
+                                  self._xgmi.cap if self._xgmi is not None else 0, small_fn,
+                                  self._comm_flat)
 
     @property
     def buckets_launched(self):
@@ -196,10 +224,9 @@ class DistributedDataParallel(nn.Module):
                                  if i in self._bucket_of}
         self._layer_params = [prog.layer_params(i) for i in range(len(prog.layers))]
         if self.ws > 1:  # one rank: nothing to launch per layer (finalize still runs)
-            # stream_ok: the bucket launches only enqueue collectives (or the xGMI kernel) on
-            # the current stream; a bf16 communication copy outlives the call, so it keeps
-            # the main-stream ordering
-            prog.register_grad_hook(self._on_layer_done, stream_ok=self.comm_dtype is None)
+            # stream_ok: the bucket launches only enqueue collectives (or the xGMI kernel), and
+            # the bf16 cast into the persistent communication buffer, on the current stream
+            prog.register_grad_hook(self._on_layer_done, stream_ok=self.side_stream_hooks)
         prog.register_post_backward_hook(lambda _p: self._finalize())
 
     def _setup_generic(self, cap_mb, first_mb):
@@ -269,8 +296,9 @@ class DistributedDataParallel(nn.Module):
             b.work, b.scaled = True, True
             self.buckets_launched += 1
             return
-        if self.comm_dtype is not None and self.comm_dtype != view.dtype:
-            b.comm_buf = view.to(self.comm_dtype)
+        if self._comm_flat is not None:
+            b.comm_buf = self._comm_flat[b.lo:b.hi]
+            b.comm_buf.copy_(view)
             t = b.comm_buf
         else:
             t = view
@@ -334,8 +362,40 @@ class DistributedDataParallel(nn.Module):
         if self.program is None:
             self._final_queued = False
 
+    def sync_buffers(self):
+        """Broadcast rank 0's module buffers to every rank (coalesced per dtype)."""
+        if self.ws <= 1 or not self._buffers:
+            return
+        from torch.distributed import distributed_c10d as c10d
+
+        pg = self.pg if self.pg is not None else c10d._get_default_group()
+        dist._broadcast_coalesced(pg, self._buffers, 256 * 2**20, 0)
+
     def forward(self, *a, **kw):
+        if self.broadcast_buffers and self._buffers and self.module.training and \
+                torch.is_grad_enabled():
+            if self._fwd_count % self.buffer_sync_every == 0:
+                self.sync_buffers()
+            self._fwd_count += 1
         return self.module(*a, **kw)
+
+    def train(self, mode: bool = True):
+        # entering evaluation: every rank evaluates with rank 0's running statistics (the
+        # last training forward updated each rank's copy from its own batch)
+        if not mode and self.module.training and self.broadcast_buffers:
+            self.sync_buffers()
+        return super().train(mode)
+
+    def check(self):
+        """Raise if the xGMI all-reduce reported a timed-out peer.  The per-step poll in
+        ``_finalize`` sees a timeout one step late (it reads the flag asynchronously, after
+        the optimiser may already have applied that step); call this at the end of training
+        so a timeout in the final steps is not missed."""
+        if self._xgmi is not None:
+            self._xgmi.check()
+
+    def close(self):
+        self.check()
 
     @contextlib.contextmanager
     def no_sync(self):

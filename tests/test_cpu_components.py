@@ -281,3 +281,45 @@ def test_checkpoint_roundtrip(tmp_path):
         o.step()
     for pa, pb in zip(a.parameters(), b.parameters()):
         torch.testing.assert_close(pa, pb)
+
+
+# ---------------------------------------------------------------- DDP bucket layout
+def _sizes(numels, pad=64):
+    out, off = [], 0
+    for n in numels:
+        end = off + (n + pad - 1) // pad * pad
+        out.append((off, n, end))
+        off = end
+    return out
+
+
+@pytest.mark.parametrize("numels,cap,first,last", [
+    ([100, 5000, 70000, 300, 9000, 120000, 64, 64, 200000], 100000, 6000, 20000),
+    ([1000], 100, 10, 10),                       # a single parameter: one bucket
+    ([10, 10, 10], 10**9, 10**9, 10**9),          # everything fits: one bucket
+    ([64] * 40, 640, 128, 256),                   # many small params
+    ([5000, 500000], 1000, 1000, 1000),           # tail param larger than every cap: unsplit
+])
+def test_ddp_make_buckets_invariants(numels, cap, first, last):
+    from dmlab.parallel.ddp import DistributedDataParallel as D
+
+    sizes = _sizes(numels)
+    bks = D._make_buckets(None, sizes, cap, first, last)
+    # contiguous cover of [0, total) in order, boundaries on parameter boundaries
+    assert bks[0].lo == 0 and bks[-1].hi == sizes[-1][2]
+    for a, b in zip(bks, bks[1:]):
+        assert a.hi == b.lo
+    starts = {s[0] for s in sizes} | {sizes[-1][2]}
+    for b in bks:
+        assert b.lo in starts and b.hi in starts
+        assert b.params == sorted(b.params)
+        assert sizes[b.params[0]][0] == b.lo and sizes[b.params[-1]][2] == b.hi
+    # every parameter in exactly one bucket
+    ids = [i for b in bks for i in b.params]
+    assert sorted(ids) == list(range(len(numels))) and len(ids) == len(set(ids))
+    # the last bucket is capped, unless even its final parameter alone exceeds the cap (then
+    # it is left unsplit) or it is the only bucket's single parameter
+    tail = bks[-1]
+    last_alone = sizes[tail.params[-1]][2] - sizes[tail.params[-1]][0]
+    if len(tail.params) > 1 and last_alone <= last:
+        assert tail.hi - tail.lo <= last

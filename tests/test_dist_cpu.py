@@ -1,4 +1,5 @@
 """Multi-process (gloo, CPU) tests of the lab-2/3 communication layer and DDP."""
+import copy
 import tempfile
 
 import pytest
@@ -249,3 +250,90 @@ def test_checkpoint_resume_on_another_world_size(tmp_path):
     ob = SGD(b.parameters(), lr=0.5, momentum=0.9)
     checkpoint.load(tmp_path / "ck.pt", b, ob)
     assert ob.grad_scale == 1.0 and ob.lr == 0.1 and ob.step_count == 1
+
+
+# ---------------------------------------------------------------- eight ranks (one node)
+@pytest.mark.parametrize("ws", [8])
+def test_ddp_matches_single_process_big_batch_ws8(ws):
+    """The full node: 8 gloo ranks (the world size of the driver's scaling run)."""
+    run_dist(_ddp_equivalence, ws, None)
+
+
+def _sampler_disjoint_ws(rank, ws, path):
+    """PartitionSampler shards of the 8 ranks, gathered over the process group: disjoint,
+    covering the (padded) dataset, and reshuffled by set_epoch identically on every rank."""
+    from dmlab.data import PartitionSampler
+
+    ds = list(range(1001))  # not a multiple of 8: padded by wrap-around
+    s = PartitionSampler(ds, ws, rank, seed=5)
+    for epoch in (0, 1):
+        s.set_epoch(epoch)
+        mine = s.indices().to(torch.long)
+        allg = [torch.zeros_like(mine) for _ in range(ws)]
+        dist.all_gather(allg, mine)
+        cat = torch.cat(allg)
+        assert len(mine) == (1001 + ws - 1) // ws
+        assert set(cat.tolist()) == set(range(1001))
+        assert len(cat) - len(set(cat.tolist())) == len(mine) * ws - 1001  # only the pad repeats
+        if epoch == 0:
+            first = cat.clone()
+    assert not torch.equal(first, cat)  # set_epoch reshuffles
+
+
+def test_partition_sampler_disjoint_ws8():
+    run_dist(_sampler_disjoint_ws, 8, None)
+
+
+def _buffers_synced(rank, ws, path):
+    """broadcast_buffers: BatchNorm running statistics agree on every rank after 3 DDP
+    steps with a different batch per rank (rank 0's buffers are broadcast at each training
+    forward and when the model enters evaluation)."""
+    from dmlab.parallel import DDP
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Conv2d(1, 4, 3), torch.nn.BatchNorm2d(4),
+                                torch.nn.ReLU(), torch.nn.Flatten(), torch.nn.Linear(4 * 26 * 26, 10))
+    for sync in (True, False):
+        m = copy.deepcopy(model)
+        ddp = DDP(m, broadcast_buffers=sync)
+        g = torch.Generator().manual_seed(40 + rank)
+        for _ in range(3):
+            x = torch.rand(4, 1, 28, 28, generator=g) * (1 + rank)
+            F.cross_entropy(ddp(x), torch.zeros(4, dtype=torch.long)).backward()
+        ddp.eval()  # entering evaluation syncs the buffers (the last forward updated them locally)
+        bn = m[1]
+        rm = [torch.zeros_like(bn.running_mean) for _ in range(ws)]
+        dist.all_gather(rm, bn.running_mean)
+        same = all(torch.equal(rm[0], r) for r in rm)
+        assert same == sync, (sync, rm)
+
+
+def test_ddp_broadcast_buffers():
+    run_dist(_buffers_synced, 2, None)
+
+
+def _bf16_comm_side_hooks(rank, ws, path):
+    """bf16 gradient communication through the persistent buffer equals the fp32
+    communication within bf16 rounding, with the side-stream (stream_ok) hook path."""
+    from dmlab.models import Net
+    from dmlab.parallel import DDP
+
+    g = torch.Generator().manual_seed(3 + rank)
+    X, Y = torch.rand(6, 1, 28, 28, generator=g), torch.randint(0, 10, (6,), generator=g)
+    grads = []
+    for comm_dtype in (None, torch.bfloat16):
+        torch.manual_seed(0)
+        m = Net()
+        ddp = DDP(m, bucket_cap_mb=0.05, first_bucket_mb=0.01, comm_dtype=comm_dtype)
+        assert all(m._hook_stream_ok.get(h, False) for h in m._grad_hooks)
+        if comm_dtype is not None:
+            assert ddp._comm_flat is not None and ddp._comm_flat.dtype == torch.bfloat16
+        for _ in range(2):  # the persistent buffer is reused across steps
+            m.flat.grad.zero_()
+            F.cross_entropy(ddp(X), Y).backward()
+        grads.append(m.flat.grad.clone())
+    torch.testing.assert_close(grads[1], grads[0], rtol=2e-2, atol=2e-3)
+
+
+def test_ddp_bf16_comm_persistent_buffer():
+    run_dist(_bf16_comm_side_hooks, 2, None)

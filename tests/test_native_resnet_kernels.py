@@ -822,3 +822,42 @@ print("OK")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
+# pipelined LDS-DMA tiles (conv_pipe.hip, cfg 90/91/92): 3x3 and 1x1 taps, stride 1 and 2,
+# odd and even K-step counts (1 step, 9 steps, 32 steps), several N tiles (XCD-grouped 1-D
+# grid), partial last M tile, and channel counts the tile cannot take (falls back)
+PIPE_GEOMS = [
+    (3, 14, 256, 256, 3, 1, 1),
+    (2, 14, 128, 256, 3, 2, 1),
+    (2, 14, 256, 512, 1, 2, 0),
+    (5, 7, 512, 512, 3, 1, 1),
+    (2, 28, 128, 128, 3, 1, 1),
+    (3, 56, 64, 64, 3, 1, 1),
+    (2, 14, 2048, 256, 1, 1, 0),
+    (2, 9, 64, 256, 1, 1, 0),
+    (3, 20, 64, 128, 3, 1, 1),
+]
+
+
+@pytest.mark.parametrize("geom", PIPE_GEOMS)
+@pytest.mark.parametrize("cfg", [90, 91, 92])
+def test_conv_fwd_pipe(dev, geom, cfg):
+    _check_fwd(dev, geom, cfg)
+
+
+@pytest.mark.parametrize("geom", PIPE_GEOMS[:6])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("cfg", [90, 91, 92])
+def test_conv_dgrad_pipe(dev, geom, accumulate, cfg):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    OH = (H + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w.bfloat16().float(), dy.float(), s, p)
+    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+    base = dx.clone()
+    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, cfg)
+    if accumulate:
+        ref = ref + _nchw(base).float()
+    assert _rel(_nchw(dx), ref) < 6e-3

@@ -120,13 +120,13 @@ def test_deferred_wgrads_match(dev, monkeypatch, defer):
             # runs on the main stream after the wait for layer i's side-stream wgrads
             snaps[i] = [p.grad.detach().clone() for p in prog.layers[i].parameters()]
 
-        a._grad_hooks.append(hook)
+        a.register_grad_hook(hook)
         try:
             a.flat.grad.zero_()
             cross_entropy(a(x), y).backward()
             torch.cuda.synchronize()
         finally:
-            a._grad_hooks.remove(hook)
+            a.remove_grad_hook(hook)
         assert sorted(snaps) == list(range(len(a.layers)))
         runs.append(({n: p.grad.detach().clone() for n, p in a.named_parameters()}, snaps))
     (g0, s0), (g1, s1) = runs
