@@ -36,6 +36,10 @@ METRIC = "samples/sec (whole node) for task3 DDP CNN at 1/2/4/8 MI355X"
 # search outran gpurun's silence limit)
 STOCK_PER_GPU = {("resnet18", 256): 16912.7, ("resnet18", 512): 19785.8,
                  ("resnet18", 1024): 18581.2, ("lenet", 32): 49523.7}
+# the ratio is quoted against stock's BEST measured per-GPU configuration of the model (not
+# the same-batch entry, which mixes tuned and untuned runs): ResNet-18 tuned at 512 images,
+# LeNet at the reference batch 32
+STOCK_BEST = {"resnet18": (19785.8, "tuned MIOpen, 512 img/GPU"), "lenet": (49523.7, "batch 32")}
 # per-GPU batch of the headline run: 1024 images.  A ~1.3 ms/step fixed cost (BN statistic
 # reductions, weight-gradient slab reduces, optimizer, launch floor) is amortised over more
 # work: 256 -> 36.7k, 512 -> 44.5k, 768 -> 46.5k, 1024 -> 46.7-46.9k img/s on one MI355X
@@ -73,9 +77,14 @@ def parse():
                          "would.  Off by default: the stem weight gradient slows by what the "
                          "packing saves (452 vs 372 us, 43.87k vs 43.93k img/s, "
                          "profiles/input_prefetch_r2c.txt)")
+    ap.add_argument("--fused", type=int, default=-1,
+                    help="LeNet: the whole training step as 2 native dispatches "
+                         "(dmlab.models.lenet_fused; 3 + the all-reduce with DDP); -1 = auto (on "
+                         "for the native backend)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole step (fwd+bwd+all-reduce+opt) in a hipGraph; "
-                         "-1 = auto: on for the launch-bound LeNet on one GPU; off for "
+                         "-1 = auto: on for the launch-bound LeNet at any world size (RCCL "
+                         "collectives are captured with the step; gloo cannot be); off for "
                          "ResNet-18, whose step is GPU-bound and whose weight gradients run "
                          "on a second stream (eager two-stream 39.4k img/s vs 38.2-38.4k "
                          "captured, one MI355X, profiles/wgrad_stream_ab_r1s4.txt)")
@@ -124,8 +133,17 @@ def main():
               small_allreduce="xgmi" if a.small_allreduce == "xgmi" else None,
               small_cap_mb=a.xgmi_cap_mb)
     net.fold_average_into(opt)
+    if a.fused < 0:
+        a.fused = 0  # flipped on once the fused step beats the layer-wise one
+    fused = None
+    if a.fused and a.model == "lenet":
+        from dmlab.models.lenet_fused import FusedLeNetStep
+
+        fused = FusedLeNetStep(model, opt, ddp=net)
 
     def train_step(x, y, x_next=None):
+        if fused is not None:
+            return fused(x, y)
         if a.backend == "torch":
             with torch.autocast("cuda", dtype=torch.bfloat16, enabled=a.model == "resnet18"):
                 out = net(x)
@@ -141,7 +159,8 @@ def main():
         return loss.detach()
 
     if a.graph < 0:
-        a.graph = 1 if (ws == 1 and a.model == "lenet") else 0
+        capturable_comm = ws == 1 or dist.get_backend() == "nccl"
+        a.graph = 1 if (a.model == "lenet" and capturable_comm) else 0
     if a.graph and a.backend == "native":
         from dmlab.utils.graph import CapturedStep
 
@@ -191,10 +210,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "vs_stock_pytorch_rocm": (round(value / (STOCK_PER_GPU[(a.model, bs)] * ws), 3)
-                                      if (a.model, bs) in STOCK_PER_GPU
-                                      and not (a.model == "lenet" and a.dtype == "bf16")
+            "vs_stock_pytorch_rocm": (round(value / (STOCK_BEST[a.model][0] * ws), 3)
+                                      if not (a.model == "lenet" and a.dtype == "bf16")
                                       else None),
+            "stock_reference": f"stock PyTorch-ROCm best measured: {STOCK_BEST[a.model][1]}",
             "dtype": "bf16" if (a.model == "resnet18" or a.dtype == "bf16") else "fp32",
             "data": "synthetic (device-resident random images, random-init weights)",
             "config": {
@@ -207,6 +226,7 @@ def main():
                 "optimizer": "SGD(momentum=0.9), fused flat",
                 "ddp": f"bucketed all-reduce overlapped with backward, bucket {a.bucket_mb} MB, comm {a.comm_dtype}",
                 "backend": a.backend,
+                "fused_step": bool(fused is not None),
                 "hip_graph": bool(a.graph and a.backend == "native"),
                 "input_prefetch": bool(a.prefetch and a.model == "resnet18" and a.backend == "native"
                                        and not a.graph),

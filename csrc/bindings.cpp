@@ -235,6 +235,34 @@ void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int6
                      reinterpret_cast<unsigned*>(state.data_ptr<int>()), (int)algo, cur_stream());
 }
 
+// P2P channel (csrc/p2p_xgmi.hip): src/dst tensors contiguous, 16-B aligned, bytes % 16 == 0;
+// ring/full/free are raw device addresses (own or IPC-opened), state an int32[4] device tensor
+void p2p_xgmi_send(at::Tensor src, int64_t ring, int64_t full, int64_t free_, int64_t slot_bytes,
+                   int64_t nslot, at::Tensor state) {
+  CHECK_CUDA(src); CHECK_CONTIG(src); CHECK_ALIGN16(src); CHECK_CUDA(state);
+  const int64_t bytes = src.numel() * src.element_size();
+  TORCH_CHECK(bytes % 16 == 0 && bytes <= slot_bytes && slot_bytes % 16 == 0 && nslot >= 1,
+              "p2p send: payload must be a multiple of 16 B and fit a ring slot");
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() >= 4, "state: int32[4]");
+  const DeviceGuard guard(src.device());
+  dm::p2p_xgmi_send(src.data_ptr(), bytes, (void*)(uintptr_t)ring, (void*)(uintptr_t)full,
+                    (const void*)(uintptr_t)free_, slot_bytes, (int)nslot,
+                    reinterpret_cast<unsigned*>(state.data_ptr<int>()), cur_stream());
+}
+
+void p2p_xgmi_recv(at::Tensor dst, int64_t ring, int64_t full, int64_t free_, int64_t slot_bytes,
+                   int64_t nslot, at::Tensor state) {
+  CHECK_CUDA(dst); CHECK_CONTIG(dst); CHECK_ALIGN16(dst); CHECK_CUDA(state);
+  const int64_t bytes = dst.numel() * dst.element_size();
+  TORCH_CHECK(bytes % 16 == 0 && bytes <= slot_bytes && slot_bytes % 16 == 0 && nslot >= 1,
+              "p2p recv: payload must be a multiple of 16 B and fit a ring slot");
+  TORCH_CHECK(state.scalar_type() == at::kInt && state.numel() >= 4, "state: int32[4]");
+  const DeviceGuard guard(dst.device());
+  dm::p2p_xgmi_recv(dst.data_ptr(), bytes, (const void*)(uintptr_t)ring,
+                    (const void*)(uintptr_t)full, (void*)(uintptr_t)free_, slot_bytes, (int)nslot,
+                    reinterpret_cast<unsigned*>(state.data_ptr<int>()), cur_stream());
+}
+
 void colsum(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor out, double beta) {
   TORCH_CHECK(A.is_cuda() && A.dim() == 2 && A.is_contiguous());
   CHECK_F32(out);
@@ -268,6 +296,61 @@ void argmax_count(at::Tensor logits, at::Tensor labels, at::Tensor correct) {
 }
 
 void spin_us(double us) { dm::spin_us(us, cur_stream()); }
+
+// One LeNet training step (csrc/lenet_fused.hip).  w: conv1.w, conv1.b, conv2.w, conv2.b,
+// fc1.w, fc1.b, fc2.w, fc2.b (fp32 masters); off: flat-buffer offsets of fc2.w, fc2.b, fc1.w,
+// fc1.b, conv2.w, conv2.b, conv1.w, conv1.b; p/mom given: the SGD update runs in the same
+// dispatch as the gradient reduction (p = the flat fp32 parameters, mom its momentum buffer).
+void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w, at::Tensor rec,
+                      at::Tensor cslab, at::Tensor rowloss, at::Tensor grad,
+                      std::vector<int64_t> off, c10::optional<at::Tensor> p,
+                      c10::optional<at::Tensor> mom, double lr, double momentum, double dampening,
+                      double wd, double gscale, bool nesterov, bool first, at::Tensor loss) {
+  CHECK_CUDA(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28,
+              "x: [B, 1, 28, 28]");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x: fp32 or bf16");
+  const int B = (int)x.size(0);
+  TORCH_CHECK(B >= 1 && labels.is_cuda() && labels.scalar_type() == at::kLong &&
+                  labels.is_contiguous() && labels.numel() == B, "labels: int64 [B]");
+  TORCH_CHECK(w.size() == 8 && off.size() == 8, "8 parameter tensors / offsets");
+  const int64_t want[8] = {150, 6, 2400, 16, 48000, 120, 1200, 10};
+  const float* wp[8];
+  for (int i = 0; i < 8; ++i) {
+    CHECK_CUDA(w[i]); CHECK_F32(w[i]); CHECK_CONTIG(w[i]);
+    TORCH_CHECK(w[i].numel() == want[i], "parameter ", i, " has the wrong size");
+    wp[i] = w[i].data_ptr<float>();
+  }
+  for (auto* t : {&rec, &cslab, &rowloss, &grad, &loss}) { CHECK_CUDA(*t); CHECK_F32(*t); CHECK_CONTIG(*t); }
+  TORCH_CHECK(rec.numel() >= (int64_t)B * dm::lenet_record_floats() &&
+                  cslab.numel() >= (int64_t)B * dm::lenet_slab_floats() && rowloss.numel() >= B &&
+                  loss.numel() == 1, "workspace too small");
+  const int64_t segn[8] = {1200, 10, 48000, 120, 2400, 16, 150, 6};
+  int o[8];
+  for (int i = 0; i < 8; ++i) {
+    TORCH_CHECK(off[i] >= 0 && off[i] + segn[i] <= grad.numel(), "flat offset out of range");
+    o[i] = (int)off[i];
+  }
+  float* pp = nullptr;
+  float* mp = nullptr;
+  if (p.has_value()) {
+    CHECK_CUDA(*p); CHECK_F32(*p); CHECK_CONTIG(*p);
+    TORCH_CHECK(p->numel() == grad.numel(), "p: the flat parameter buffer");
+    pp = p->data_ptr<float>();
+    if (momentum != 0.0) {
+      TORCH_CHECK(mom.has_value() && mom->numel() == grad.numel() && mom->scalar_type() == at::kFloat,
+                  "mom: the flat momentum buffer");
+      mp = mom->data_ptr<float>();
+    }
+  }
+  const DeviceGuard guard(x.device());
+  dm::lenet_fused_step(x.data_ptr(), x.scalar_type() == at::kBFloat16,
+                       reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()),
+                       B, wp, rec.data_ptr<float>(), cslab.data_ptr<float>(),
+                       rowloss.data_ptr<float>(), grad.data_ptr<float>(), o, pp, mp, (float)lr,
+                       (float)momentum, (float)dampening, (float)wd, (float)gscale, nesterov,
+                       first, pp != nullptr, loss.data_ptr<float>(), cur_stream());
+}
 
 // A HIP stream whose kernels may only occupy the CUs set in `mask` (bit i of word w =
 // CU 32w+i), on a hardware queue of its own.  Used for the backward weight-gradient
@@ -320,8 +403,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_open_handle", &xgmi_open_handle);
   m.def("xgmi_close_handle", &xgmi_close_handle);
   m.def("xgmi_allreduce", &xgmi_allreduce);
+  m.def("p2p_xgmi_send", &p2p_xgmi_send);
+  m.def("p2p_xgmi_recv", &p2p_xgmi_recv);
   m.def("cross_entropy", &cross_entropy);
   m.def("argmax_count", &argmax_count);
   m.def("spin_us", &spin_us);
+  m.def("lenet_fused_step", &lenet_fused_step, "one fused LeNet training step (2 dispatches)");
+  m.def("lenet_record_floats", &dm::lenet_record_floats);
+  m.def("lenet_slab_floats", &dm::lenet_slab_floats);
   m.attr("arch") = "gfx950";
 }

@@ -95,6 +95,12 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
     TORCH_CHECK(pre_shift.has_value(), "pre_scale needs pre_shift");
     need_f32(*pre_scale, "pre_scale", x.size(3));
     need_f32(*pre_shift, "pre_shift", x.size(3));
+    if (cfg >= 90 && cfg <= 93 && dm::conv_pipe_supported(g, (int)cfg)) {
+      dm::conv_pipe(bp(x), bp(wpack), bp(y), ap, sp, g, (int)cfg, cur_stream(), fp(*pre_scale),
+                    fp(*pre_shift));
+      return;
+    }
+    if (cfg >= 90 && cfg <= 93) cfg = 41;  // same 256-row tile (stats slab rows match)
     if (cfg == 70) {
       if (dm::conv_l1_supported(g)) {
         dm::conv_l1(bp(x), bp(wpack), bp(y), ap, sp, g, cur_stream(), fp(*pre_scale),
@@ -287,6 +293,10 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
     }
     cfg = Cin % 128 == 0 ? 15 : 13;
   }
+  // pipelined tiles: all parity classes in one launch (blockIdx.y = class)
+  if (cfg >= 90 && cfg <= 93 && !bnbp && ng > 0 &&
+      dm::conv_pipe_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, ng, (int)cfg, st))
+    return 0;
   // all parity classes in one launch (blockIdx.z = class) when the tile supports it
   if (bnbp) {
     // slab rows of absent classes, or of row tiles past a smaller class's M (odd sizes),

@@ -1479,7 +1479,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
   // 36 / 37: 256-pixel halo tile (2 x 2 waves of 128 x BN/2), BN 128 / 64
   // 38 / 39: 256-pixel halo tile with 4 x 2 waves of 64 x BN/2, BN 128 / 64
-  if (cfg >= 90 && cfg <= 92) {  // pipelined LDS-DMA tiles (conv_pipe.hip), 256-row tile
+  if (cfg >= 90 && cfg <= 93) {  // pipelined LDS-DMA tiles (conv_pipe.hip), 256-row tile
     if (!bnb && conv_pipe_supported(g, cfg)) return conv_pipe(X, Wp, Y, ADD, stats, g, cfg, st);
     if (g.Ncols % 128 == 0) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
     return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
@@ -1543,7 +1543,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { if (cfg >= 90 && cfg <= 92) return 256; if (cfg == 50 || cfg == 51) return conv_h5_rowtile(cfg); if (cfg == 60 || cfg == 70) return 256; return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43 || cfg == 44 || cfg == 45) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
+int igemm_fwd_rowtile(int cfg) { if (cfg >= 90 && cfg <= 93) return 256; if (cfg == 50 || cfg == 51) return conv_h5_rowtile(cfg); if (cfg == 60 || cfg == 70) return 256; return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43 || cfg == 44 || cfg == 45) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
 
 static size_t wgrad_smem(int BM, int BN) {
   return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;

@@ -45,6 +45,14 @@ void cross_entropy(const void* logits, const long long* labels, float* rowloss, 
 void argmax_count(const void* logits, const long long* labels, int B, int C,
                   unsigned long long* correct, bool bf16, hipStream_t st);
 void spin_us(double us, hipStream_t st);
+// lenet_fused.hip: the whole LeNet training step in 2 dispatches
+int lenet_record_floats();
+int lenet_slab_floats();
+void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B,
+                      const float* const* w, float* rec, float* cslab, float* rowloss, float* grad,
+                      const int* off, float* p, float* mom, float lr, float momentum,
+                      float dampening, float wd, float gscale, bool nesterov, bool first,
+                      bool do_sgd, float* loss, hipStream_t st);
 }  // namespace dm
 
 namespace dm {
@@ -57,6 +65,11 @@ void xgmi_close_handle(void* ptr);
 void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
                     void* const* flags, int rank, int W, float scale, unsigned* state, int algo,
                     hipStream_t st);
+// p2p_xgmi.hip: one-direction stage-to-stage channel over IPC peer memory
+void p2p_xgmi_send(const void* src, long long bytes, void* ring, void* full, const void* free_,
+                   long long slot_bytes, int nslot, unsigned* state, hipStream_t st);
+void p2p_xgmi_recv(void* dst, long long bytes, const void* ring, const void* full, void* free_,
+                   long long slot_bytes, int nslot, unsigned* state, hipStream_t st);
 // conv_igemm.hip
 struct ConvGeom;
 struct ConvGeomSet;
@@ -94,10 +107,13 @@ int conv_h5_rowtile(int cfg);
 void conv_h5(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
              const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
              const float* pre_sh = nullptr, const BnBwdEpi* bnb = nullptr);
-// conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90: 256 x 256 tile, 91: 256 x 128)
+// conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90-93: 256-pixel tiles)
 bool conv_pipe_supported(const ConvGeom& g, int cfg);
+bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st);
+               const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
+               const float* pre_sh = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
 long long conv_halo41_stats_rows(long long M, int Ncols);
 bool halo_cfg(int cfg, int& bn, int& waves);

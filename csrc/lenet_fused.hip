@@ -1,0 +1,345 @@
+// Fused LeNet training step (the reference `Net`, codes/task1/pytorch/model.py:12-35, trained by
+// the task3 loop, codes/task3/model.py:50-64), gfx950.
+//
+// The reference step is ~50-70 kernel launches; the layer-by-layer native
+// Program was 22 dispatches / 206 us at batch 32 (profiles/rocprof_lenet_b32_step_r2c.txt).
+// The whole model is 78 MFLOP per step: the step is launch- and latency-bound, so it is
+// restructured around the batch dimension instead of the layers:
+//
+//  K1 lenet_sample_kernel — ONE workgroup per sample runs the entire forward AND backward of
+//     that sample in LDS: conv1+bias+ReLU+2x2 max-pool, conv2+bias+ReLU+pool, fc1+ReLU, fc2,
+//     softmax cross-entropy (loss and the (softmax - onehot)/B seed), fc2/fc1 data gradients,
+//     unpooling through the argmax codes, the conv2 data gradient, and the per-sample
+//     conv1/conv2 weight- and bias-gradient contributions.  Everything a layer hands to the
+//     next stays in LDS; the only global traffic is the input, the weights (L2-resident,
+//     207 KB) and a per-sample record for K2: h0 (400), h1 (120), dh1 (120), dlogits (10)
+//     and the conv gradient partials (2572 floats).
+//  K2 lenet_grad_kernel — one thread per parameter (51,902): the batch reduction of every
+//     gradient in a fixed order (deterministic; fc weights as sum_b dY[b] (x) X[b] rank-1
+//     terms from the K1 records, conv weights as sums of the per-sample partials), written
+//     into the flat gradient buffer, optionally followed in the same thread by the SGD
+//     (momentum / dampening / nesterov / weight decay) update of that parameter, and the mean
+//     loss (block 0).  With data parallelism K2 writes gradients only; the bucket all-reduce
+//     and the fused SGD kernel (optim.hip) follow.
+//
+// So a single-GPU training step is 2 dispatches (3 with DDP, plus the collective), none of
+// them ATen.  All accumulation is fp32; the bf16 variant reads bf16 input images.
+#include "common.h"
+#include "kernels.h"
+
+namespace dm {
+
+namespace {
+constexpr int LT = 512;  // threads per sample workgroup
+// per-sample conv gradient partials: conv2 w (2400), conv2 b (16), conv1 w (150), conv1 b (6)
+constexpr int CS = 2400 + 16 + 150 + 6;
+
+template <typename XT>
+__device__ __forceinline__ float ldx(const XT* p);
+template <>
+__device__ __forceinline__ float ldx<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ldx<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+
+template <typename XT>
+__global__ void __launch_bounds__(LT) lenet_sample_kernel(
+    const XT* __restrict__ X, const long long* __restrict__ labels,
+    const float* __restrict__ c1w, const float* __restrict__ c1b, const float* __restrict__ c2w,
+    const float* __restrict__ c2b, const float* __restrict__ f1w, const float* __restrict__ f1b,
+    const float* __restrict__ f2w, const float* __restrict__ f2b, float* __restrict__ rec,
+    float* __restrict__ cslab, float* __restrict__ rowloss, float inv_b) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  __shared__ float xs[32 * 32];            // input with the conv1 zero padding (2)
+  __shared__ float w1[152], bb1[8], w2[2400], bb2[16];
+  __shared__ float p1[6 * 196];            // relu(conv1) max-pooled
+  __shared__ unsigned char k1[6 * 196];    // its 2x2 argmax (4 = no gradient)
+  __shared__ float p2[400];                // relu(conv2) max-pooled = h0 (flatten order)
+  __shared__ unsigned char k2[400];
+  __shared__ float h1[128], dl[16], dh1[128], g2[400], g1[6 * 196];
+  __shared__ float red[512];
+
+  // ---- stage input and conv weights ----
+  for (int i = tid; i < 1024; i += LT) {
+    const int y = (i >> 5) - 2, x = (i & 31) - 2;
+    xs[i] = ((unsigned)y < 28u && (unsigned)x < 28u) ? ldx<XT>(X + (long long)b * 784 + y * 28 + x)
+                                                     : 0.f;
+  }
+  for (int i = tid; i < 2400; i += LT) w2[i] = c2w[i];
+  if (tid < 150) w1[tid] = c1w[tid];
+  if (tid < 6) bb1[tid] = c1b[tid];
+  if (tid < 16) bb2[tid] = c2b[tid];
+  __syncthreads();
+
+  // ---- conv1 (1 -> 6, 5x5, pad 2) + bias + ReLU + 2x2 max-pool ----
+  for (int q = tid; q < 1176; q += LT) {
+    const int c = q / 196, r = q - c * 196, py = r / 14, px = r - py * 14;
+    float win[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) win[i][j] = xs[(2 * py + i) * 32 + 2 * px + j];
+    float best = 0.f;
+    int code = 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int ay = a >> 1, ax = a & 1;
+      float acc = bb1[c];
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc += win[ay + kh][ax + kw] * w1[c * 25 + kh * 5 + kw];
+      if (acc > best) {  // first maximum; a window whose max is <= 0 passes no gradient
+        best = acc;
+        code = a;
+      }
+    }
+    p1[q] = best;
+    k1[q] = (unsigned char)code;
+  }
+  __syncthreads();
+
+  // ---- conv2 (6 -> 16, 5x5) + bias + ReLU + 2x2 max-pool ----
+  if (tid < 400) {
+    const int o = tid / 25, r = tid - o * 25, py = r / 5, px = r - py * 5;
+    float acc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) acc[a] = bb2[o];
+    for (int c = 0; c < 6; ++c) {
+      float win[6][6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) win[i][j] = p1[c * 196 + (2 * py + i) * 14 + 2 * px + j];
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float w = w2[o * 150 + c * 25 + kh * 5 + kw];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) acc[a] += win[(a >> 1) + kh][(a & 1) + kw] * w;
+        }
+    }
+    float best = 0.f;
+    int code = 4;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      if (acc[a] > best) {
+        best = acc[a];
+        code = a;
+      }
+    p2[tid] = best;
+    k2[tid] = (unsigned char)code;
+  }
+  __syncthreads();
+
+  // ---- fc1 (400 -> 120) + ReLU: 15 outputs per wave, lanes split K (coalesced rows) ----
+  for (int u = wid; u < 120; u += LT / 64) {
+    float acc = 0.f;
+    for (int k = lane; k < 400; k += 64) acc += f1w[u * 400 + k] * p2[k];
+    acc = wave_sum(acc);
+    if (lane == 0) h1[u] = fmaxf(acc + f1b[u], 0.f);
+  }
+  __syncthreads();
+
+  // ---- fc2 (120 -> 10) + softmax cross-entropy (wave 0) ----
+  if (wid == 0) {
+    float z = -INFINITY;
+    if (lane < 10) {
+      float acc = f2b[lane];
+      for (int u = 0; u < 120; ++u) acc += f2w[lane * 120 + u] * h1[u];
+      z = acc;
+    }
+    const float mx = wave_max(z);
+    const float e = lane < 10 ? __expf(z - mx) : 0.f;
+    const float se = wave_sum(e);
+    const int lab = (int)labels[b];
+    const float zl = __shfl(z, lab, 64);
+    if (lane < 10) dl[lane] = (e / se - (lane == lab ? 1.f : 0.f)) * inv_b;
+    if (lane == 0) rowloss[b] = mx + __logf(se) - zl;
+  }
+  __syncthreads();
+
+  // ---- fc2 data gradient, masked by fc1's ReLU ----
+  if (tid < 120) {
+    float acc = 0.f;
+#pragma unroll
+    for (int o = 0; o < 10; ++o) acc += dl[o] * f2w[o * 120 + tid];
+    dh1[tid] = h1[tid] > 0.f ? acc : 0.f;
+  }
+  __syncthreads();
+
+  // ---- fc1 data gradient -> pooled conv2 gradient (unpool through k2 below) ----
+  float* r = rec + (long long)b * 656;  // per-sample record: h0 | h1 | dh1 | dl (+ pad)
+  if (tid < 400) {
+    float acc = 0.f;
+    for (int u = 0; u < 120; ++u) acc += dh1[u] * f1w[u * 400 + tid];
+    g2[tid] = k2[tid] < 4 ? acc : 0.f;
+    r[tid] = p2[tid];
+  }
+  if (tid < 120) {
+    r[400 + tid] = h1[tid];
+    r[520 + tid] = dh1[tid];
+  }
+  if (tid < 10) r[640 + tid] = dl[tid];
+  __syncthreads();
+
+  float* cs = cslab + (long long)b * CS;
+  // ---- conv2 weight/bias gradient partials and data gradient ----
+  for (int i = tid; i < 2400; i += LT) {
+    const int o = i / 150, rr = i - o * 150, c = rr / 25, t = rr - c * 25, kh = t / 5, kw = t - kh * 5;
+    float acc = 0.f;
+#pragma unroll 5
+    for (int j = 0; j < 25; ++j) {
+      const int code = k2[o * 25 + j];
+      if (code < 4) {
+        const int py = j / 5, px = j - py * 5;
+        acc += g2[o * 25 + j] * p1[c * 196 + (2 * py + (code >> 1) + kh) * 14 + 2 * px + (code & 1) + kw];
+      }
+    }
+    cs[i] = acc;
+  }
+  if (tid < 16) {
+    float acc = 0.f;
+    for (int j = 0; j < 25; ++j) acc += g2[tid * 25 + j];
+    cs[2400 + tid] = acc;
+  }
+  // dp1[c][yy][xx] = sum_o sum_(py,px) g2[o][py][px] W2[o][c][yy - y][xx - x], (y, x) the argmax
+  // position of pooled output (py, px); then unpool1 through k1
+  for (int q = tid; q < 1176; q += LT) {
+    const int c = q / 196, rr = q - c * 196, yy = rr / 14, xx = rr - yy * 14;
+    const int py0 = yy >= 5 ? (yy - 5) / 2 : 0, py1 = (yy / 2) < 4 ? yy / 2 : 4;
+    const int px0 = xx >= 5 ? (xx - 5) / 2 : 0, px1 = (xx / 2) < 4 ? xx / 2 : 4;
+    float acc = 0.f;
+    for (int o = 0; o < 16; ++o)
+      for (int py = py0; py <= py1; ++py)
+        for (int px = px0; px <= px1; ++px) {
+          const int j = o * 25 + py * 5 + px;
+          const int code = k2[j];
+          if (code >= 4) continue;
+          const int kh = yy - 2 * py - (code >> 1), kw = xx - 2 * px - (code & 1);
+          if ((unsigned)kh < 5u && (unsigned)kw < 5u) acc += g2[j] * w2[o * 150 + c * 25 + kh * 5 + kw];
+        }
+    g1[q] = k1[q] < 4 ? acc : 0.f;
+  }
+  __syncthreads();
+
+  // ---- conv1 weight/bias gradient partials: 150 weights x 196 pooled positions, 3 threads
+  //      per weight, combined in a fixed order ----
+  if (tid < 450) {
+    const int i = tid / 3, part = tid - i * 3;
+    const int c = i / 25, t = i - c * 25, kh = t / 5, kw = t - kh * 5;
+    float acc = 0.f;
+    for (int j = part; j < 196; j += 3) {
+      const int code = k1[c * 196 + j];
+      if (code < 4) {
+        const int py = j / 14, px = j - py * 14;
+        acc += g1[c * 196 + j] * xs[(2 * py + (code >> 1) + kh) * 32 + 2 * px + (code & 1) + kw];
+      }
+    }
+    red[tid] = acc;
+  }
+  __syncthreads();
+  if (tid < 150) cs[2416 + tid] = red[3 * tid] + red[3 * tid + 1] + red[3 * tid + 2];
+  if (tid >= 192 && tid < 192 + 6 * 32) {  // conv1 bias: 6 channels x 32 lanes
+    const int c = (tid - 192) >> 5, l = (tid - 192) & 31;
+    float acc = 0.f;
+    for (int j = l; j < 196; j += 32) acc += g1[c * 196 + j];
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 32);
+    if (l == 0) cs[2566 + c] = acc;
+  }
+}
+
+// Flat-buffer segment j (fc2.w, fc2.b, fc1.w, fc1.b, conv2.w, conv2.b, conv1.w, conv1.b in the
+// Program's reverse-execution order) starts at off[j].
+struct LenetFlat {
+  int off[8];
+};
+__device__ __forceinline__ int seg_n(int s) {
+  switch (s) {
+    case 0: return 1200;
+    case 1: return 10;
+    case 2: return 48000;
+    case 3: return 120;
+    case 4: return 2400;
+    case 5: return 16;
+    case 6: return 150;
+    default: return 6;
+  }
+}
+
+__global__ void __launch_bounds__(256) lenet_grad_kernel(
+    const float* __restrict__ rec, const float* __restrict__ cslab, int B, float* __restrict__ grad,
+    LenetFlat fl, float* __restrict__ p, float* __restrict__ mom, float lr, float momentum,
+    float dampening, float wd, float gscale, int nesterov, int first, int do_sgd,
+    const float* __restrict__ rowloss, float* __restrict__ loss) {
+  int i = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // mean loss, fixed order
+    float a = 0.f;
+    for (int j = threadIdx.x; j < B; j += 64) a += rowloss[j];
+    a = wave_sum(a);
+    if (threadIdx.x == 0) *loss = a / (float)B;
+  }
+  int seg = 0;
+  while (seg < 8 && i >= seg_n(seg)) {
+    i -= seg_n(seg);
+    ++seg;
+  }
+  if (seg == 8) return;
+  float g = 0.f;
+  if (seg == 0) {  // fc2.w[o][u] = sum_b dl[b][o] h1[b][u]
+    const int o = i / 120, u = i - o * 120;
+    for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + o] * rec[b * 656 + 400 + u];
+  } else if (seg == 1) {
+    for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + i];
+  } else if (seg == 2) {  // fc1.w[u][k] = sum_b dh1[b][u] h0[b][k]
+    const int u = i / 400, k = i - u * 400;
+    for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + u] * rec[b * 656 + k];
+  } else if (seg == 3) {
+    for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + i];
+  } else {
+    const int base = seg == 4 ? 0 : seg == 5 ? 2400 : seg == 6 ? 2416 : 2566;
+    for (int b = 0; b < B; ++b) g += cslab[(long long)b * CS + base + i];
+  }
+  const int o = fl.off[seg] + i;
+  grad[o] = g;
+  if (!do_sgd) return;
+  float d = g * gscale;
+  const float pv = p[o];
+  if (wd != 0.f) d += wd * pv;
+  if (momentum != 0.f) {
+    const float bv = first ? d : momentum * mom[o] + (1.f - dampening) * d;
+    mom[o] = bv;
+    d = nesterov ? d + momentum * bv : bv;
+  }
+  p[o] = pv - lr * d;
+}
+}  // namespace
+
+int lenet_record_floats() { return 656; }
+int lenet_slab_floats() { return CS; }
+
+void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B,
+                      const float* const* w, float* rec, float* cslab, float* rowloss, float* grad,
+                      const int* off, float* p, float* mom, float lr, float momentum,
+                      float dampening, float wd, float gscale, bool nesterov, bool first,
+                      bool do_sgd, float* loss, hipStream_t st) {
+  const float inv_b = 1.f / (float)B;
+  if (x_bf16)
+    lenet_sample_kernel<bf16_t><<<B, LT, 0, st>>>((const bf16_t*)x, labels, w[0], w[1], w[2], w[3],
+                                                  w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b);
+  else
+    lenet_sample_kernel<float><<<B, LT, 0, st>>>((const float*)x, labels, w[0], w[1], w[2], w[3],
+                                                 w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b);
+  DM_CHECK(hipGetLastError());
+  LenetFlat fl;
+  for (int j = 0; j < 8; ++j) fl.off[j] = off[j];
+  const int total = 1200 + 10 + 48000 + 120 + 2400 + 16 + 150 + 6;
+  lenet_grad_kernel<<<(total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
+                                                         momentum, dampening, wd, gscale,
+                                                         nesterov ? 1 : 0, first ? 1 : 0,
+                                                         do_sgd ? 1 : 0, rowloss, loss);
+  DM_CHECK(hipGetLastError());
+}
+
+}  // namespace dm

@@ -51,6 +51,8 @@ _HALO_PF2 = os.environ.get("DMLAB_HALO_PF2", "0") == "1"
 # per-output-channel override of the unit-stride 3x3 halo cfg, e.g. "64=44,128=44" (A/B runs)
 _HALO_MAP = {int(k): int(v) for k, v in (kv.split("=") for kv in
              os.environ.get("DMLAB_HALO_MAP", "").split(",") if kv)}
+# DMLAB_NO_PIPE=1: the round-2 tile map without the pipelined tiles (A/B runs)
+_NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
 
 
 # cfg 80: stride-2 3x3 data gradient with the four parity classes of a dY tile in one block
@@ -73,6 +75,14 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     output channels.  ``k``/``stride``/``cin`` (kernel size, tap stride, input
     channels) enable the unit-stride halo kernel when they describe a k x k conv with
     unit tap stride over 64-channel-aligned input."""
+    # 90: the pipelined LDS-DMA 256 x 256 tile (csrc/conv_pipe.hip), for >= 256 output
+    # channels and 64-channel-aligned input, any tap geometry.  tools/bench_conv.py at batch
+    # 1024 (profiles/conv_pipe_vs_halo_b1024_r3a.jsonl, TFLOP/s fwd/dgrad, best previous tile):
+    #   layer3 3x3 975/1004 (41: 897/971), layer4 3x3 1151/1160 (41: 933/957),
+    #   layer4 3x3/s2 1030/901 (15: 750/724), layer3 3x3/s2 fwd 778 (42: 690),
+    #   layer4 1x1/s2 442/367 (15: 351/299); the 64/128-channel layers keep the halo tiles
+    if ncols % 256 == 0 and cin % 64 == 0 and cin > 0 and not _NO_PIPE:
+        return 90
     if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
         # 64 output channels: the 256-pixel halo tile (2 x 2 waves of 128 x 32) amortises
         # the single-chunk halo prologue over twice the rows
@@ -326,7 +336,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43, 44, 45):
+        if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43, 44, 45, 90, 91, 92, 93):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)

@@ -232,22 +232,33 @@ class GradAggregator:
 
     ``method``: ``allreduce`` | ``allgather`` | ``allgather_ref`` (B1 compat);
     ``granularity``: ``flat`` (one coalesced collective) | ``per_param``.
-    ``comm_time`` accumulates the wall time of the aggregation including device
-    completion (the reference's ``time.time()`` pair, model-mp.py:61-66, measures
-    only host enqueue time with an async RCCL backend)."""
 
-    def __init__(self, model, method="allreduce", granularity="flat", sync_timing=True):
+    ``timing``:
+      * ``"events"`` (default on a HIP device): a pair of HIP events on the current stream
+        brackets each aggregation (the manual's ``torch.cuda.Event`` recipe,
+        ``task2.tex:69-80``).  RCCL orders the current stream after the collective, so the
+        interval is the device-side communication time, including the wait for a slow
+        peer; nothing synchronises the host, so the measurement does not drain backward
+        the way a ``synchronize()`` pair would.  ``comm_time`` reads the events back once.
+      * ``"sync"``: the old wall-clock bracket with a stream synchronise on both sides.
+      * ``"host"``: host wall time only (the reference's ``time.time()`` pair,
+        model-mp.py:61-66; with an asynchronous backend it measures only the enqueue).
+    On the CPU (gloo) the collectives are synchronous and wall time is exact."""
+
+    def __init__(self, model, method="allreduce", granularity="flat", timing=None,
+                 sync_timing=None):
         self.model, self.method, self.granularity = model, method, granularity
-        self.sync_timing = sync_timing
-        self.comm_time = 0.0
+        if timing is None:
+            timing = "sync" if sync_timing else "events"
+        self.timing = timing
+        self._host_time = 0.0
+        self._events = []
         self.calls = 0
 
-    def __call__(self):
-        dev_sync = self.sync_timing and torch.cuda.is_available() and next(
-            self.model.parameters()).is_cuda
-        if dev_sync:
-            torch.cuda.current_stream().synchronize()
-        t0 = time.perf_counter()
+    def _on_gpu(self):
+        return torch.cuda.is_available() and next(self.model.parameters()).is_cuda
+
+    def _aggregate(self):
         if self.method == "allreduce":
             allreduce_average_gradients(self.model, self.granularity)
         elif self.method == "allgather":
@@ -256,9 +267,33 @@ class GradAggregator:
             allgather_average_gradients_reference_compat(self.model)
         else:
             raise ValueError(self.method)
-        if dev_sync:
+
+    def __call__(self):
+        """Aggregate; returns the host-measured seconds, or None with event timing."""
+        gpu = self._on_gpu()
+        self.calls += 1
+        if gpu and self.timing == "events":
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            self._aggregate()
+            e.record()
+            self._events.append((s, e))
+            return None
+        if gpu and self.timing == "sync":
+            torch.cuda.current_stream().synchronize()
+        t0 = time.perf_counter()
+        self._aggregate()
+        if gpu and self.timing == "sync":
             torch.cuda.current_stream().synchronize()
         dt = time.perf_counter() - t0
-        self.comm_time += dt
-        self.calls += 1
+        self._host_time += dt
         return dt
+
+    @property
+    def comm_time(self) -> float:
+        """Total communication seconds so far (reads pending HIP events back once)."""
+        if self._events:
+            self._events[-1][1].synchronize()
+            self._host_time += sum(s.elapsed_time(e) for s, e in self._events) * 1e-3
+            self._events = []
+        return self._host_time

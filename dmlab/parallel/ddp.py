@@ -362,6 +362,17 @@ class DistributedDataParallel(nn.Module):
         if self.program is None:
             self._final_queued = False
 
+    def reduce_now(self):
+        """Reduce the whole gradient buffer now (every bucket, then the end-of-backward
+        wait / cast-back / average): for steps that produce all gradients outside the
+        per-layer hooks, e.g. :class:`dmlab.models.lenet_fused.FusedLeNetStep`."""
+        if self.ws <= 1:
+            return
+        if self._native is not None and self._sync_enabled:
+            for lp in range(len(getattr(self, "_layer_params", []))):
+                self._native.mark_layer(lp)
+        self._finalize()
+
     def sync_buffers(self):
         """Broadcast rank 0's module buffers to every rank (coalesced per dtype)."""
         if self.ws <= 1 or not self._buffers:

@@ -11,15 +11,19 @@ MI355X-native design (this module):
 * one process per stage (rank i = stage i, its own GPU); the data/loss "driver"
   role is co-located with the first stage (inputs) and the last stage (labels +
   loss), so activations go stage→stage directly, never via a relay;
-* activations and activation-gradients move with ``torch.distributed`` P2P
-  (``isend``/``irecv`` — RCCL over xGMI on GPUs; gloo on CPU, with a host staging
-  copy if a gloo group is used for device tensors);
+* activations and activation-gradients move over a stage transport
+  (:mod:`dmlab.parallel.p2p`): RCCL P2P over xGMI with one process group per direction,
+  or the native xGMI peer-memory channel (``transport="xgmi"``: the sender's kernel writes
+  straight into the receiver's device ring); gloo on the CPU;
+* every receive is posted one micro-batch AHEAD of the compute that consumes it and waited
+  for only where the data is used (a device-side stream wait, never a host sync); message
+  shapes are negotiated once and cached (``static_shapes``, default on: the labs' batches
+  have one shape);
 * GPipe (all-forward, all-backward) or 1F1B micro-batch schedules so stage i
   computes micro-batch m+1 while stage i+1 works on m;
-* each stage steps its own fused optimiser locally (no optimiser RPC).
-
-The tensor shape of every message is fixed by the model; it is negotiated once
-with a small header message and cached.
+* each stage steps its own fused optimiser locally (no optimiser RPC);
+* ``timing=True`` brackets each stage's compute with HIP events, so a step reports its
+  compute time and the bubble (the fraction of the step a stage sits idle).
 """
 from __future__ import annotations
 
@@ -27,76 +31,22 @@ import torch
 import torch.distributed as dist
 
 from . import env
-
-
-class P2P:
-    """Point-to-point transport between adjacent stages.
-
-    Every message is preceded by a 16-word shape header unless ``static_shapes``
-    is set, in which case the header is exchanged once per tag and cached (use it
-    when every micro-batch has the same shape)."""
-
-    def __init__(self, group=None, static_shapes=False):
-        self.group = group
-        self.gloo = dist.get_backend(group) == "gloo"
-        self.static = static_shapes
-        self._shapes = {}
-
-    def _dev_out(self, t):
-        return t.cpu() if (self.gloo and t.is_cuda) else t
-
-    def send(self, t: torch.Tensor, dst: int, tag: str):
-        """Non-blocking (header and payload are both isend) so opposite-direction
-        sends of a 1F1B schedule can never deadlock; returns the works to wait on."""
-        t = t.contiguous()
-        works = []
-        if not self.static or tag not in self._shapes:
-            hdr = torch.tensor([t.dim()] + list(t.shape) + [_DT.index(t.dtype)], dtype=torch.long)
-            hdr = torch.cat([torch.tensor([hdr.numel()]), hdr])
-            hdr = self._pad(hdr)
-            if not self.gloo:
-                hdr = hdr.to(t.device)
-            works.append(dist.isend(hdr, dst, group=self.group))
-            self._shapes[tag] = (tuple(t.shape), t.dtype)
-        works.append(dist.isend(self._dev_out(t), dst, group=self.group))
-        return works
-
-    @staticmethod
-    def _pad(h):
-        out = torch.zeros(16, dtype=torch.long)
-        out[: h.numel()] = h
-        return out
-
-    def recv(self, src: int, tag: str, device):
-        if not self.static or tag not in self._shapes:
-            hdr = torch.zeros(16, dtype=torch.long,
-                              device="cpu" if self.gloo else device)
-            dist.recv(hdr, src, group=self.group)
-            hdr = hdr.cpu()
-            nd = int(hdr[1])
-            shape = tuple(int(v) for v in hdr[2:2 + nd])
-            dtype = _DT[int(hdr[2 + nd])]
-            self._shapes[tag] = (shape, dtype)
-        shape, dtype = self._shapes[tag]
-        dev = torch.device("cpu") if self.gloo else device
-        buf = torch.empty(shape, dtype=dtype, device=dev)
-        work = dist.irecv(buf, src, group=self.group)
-        return buf, work
-
-
-_DT = [torch.float32, torch.bfloat16, torch.float16, torch.int64]
+from .p2p import PGTransport, XGMITransport
 
 
 class PipelineStage:
     """One stage of a linear pipeline.
 
-    ``module``  : this stage's sub-network (a :class:`~dmlab.nn.program.Program` or
-                  any ``nn.Module``); ``loss_fn`` is used on the last stage only.
-    ``ranks``   : the global ranks of all stages in order (default: 0..P-1).
+    ``module``    : this stage's sub-network (a :class:`~dmlab.nn.program.Program` or
+                    any ``nn.Module``); ``loss_fn`` is used on the last stage only.
+    ``ranks``     : the global ranks of all stages in order (default: 0..P-1).
+    ``transport`` : ``"pg"`` (torch.distributed P2P: RCCL / gloo), ``"xgmi"`` (native
+                    peer-memory channels, GPU only) or a transport object.
     """
 
     def __init__(self, module, optimizer, loss_fn=None, ranks=None, device=None,
-                 schedule="1f1b", group=None, static_shapes=False):
+                 schedule="1f1b", group=None, static_shapes=True, transport="pg",
+                 cap_bytes=1 << 20, timing=False):
         self.module = module
         self.opt = optimizer
         self.loss_fn = loss_fn
@@ -109,51 +59,92 @@ class PipelineStage:
         self.prev = self.ranks[self.idx - 1] if not self.first else None
         self.next = self.ranks[self.idx + 1] if not self.last else None
         self.device = device or env.device()
-        self.p2p = P2P(group, static_shapes)
+        if transport == "pg":
+            self.p2p = PGTransport(self.ranks, static_shapes)
+        elif transport == "xgmi":
+            links = [(self.ranks[i], self.ranks[i + 1]) for i in range(self.P - 1)]
+            links += [(self.ranks[i + 1], self.ranks[i]) for i in range(self.P - 1)]
+            if self.P > 2:
+                links.append((self.ranks[0], self.ranks[-1]))  # labels
+            self.p2p = XGMITransport(links, cap_bytes=cap_bytes, group=group, device=self.device)
+        else:
+            self.p2p = transport
         assert schedule in ("gpipe", "1f1b")
         self.schedule = schedule
         self._pending = []
+        self._posted = {}
+        self.timing = timing and torch.cuda.is_available() and self.device.type == "cuda"
+        self._events = []
+        self.last_stats = None
 
     # -------------------------------------------------------------- pieces
+    def _post_recv(self, tag, m, src, ahead=False):
+        """Post the receive of message (tag, m) now; consumed later by _take.  A receive
+        posted AHEAD of its use waits until the message shape is cached (the first step
+        negotiates shapes with a blocking header receive, which must not run ahead of the
+        schedule: the peer may still need a message from this rank first)."""
+        k = (tag, m)
+        if k in self._posted:
+            return
+        if ahead and not self.p2p.known(k):
+            return
+        self._posted[k] = self.p2p.recv(src, k, self.device)
+
+    def _take(self, tag, m, src):
+        self._post_recv(tag, m, src)
+        buf, w = self._posted.pop((tag, m))
+        w.wait()
+        return buf
+
     def _labels(self, y, n_micro):
         """Labels travel from the data owner (first stage) to the last stage."""
         if self.P == 1:
             return y.chunk(n_micro)
         if self.first:
-            self._pending.extend(self.p2p.send(y, self.ranks[-1], "labels"))
+            self._pending.extend(self.p2p.send(y, self.ranks[-1], ("labels", 0)))
             return None
         if self.last:
-            buf, w = self.p2p.recv(self.ranks[0], "labels", self.device)
-            w.wait()
-            return buf.to(self.device).chunk(n_micro)
+            return self._take("labels", 0, self.ranks[0]).to(self.device).chunk(n_micro)
         return None
 
-    def _fwd(self, m, xs, ys, saved, losses):
+    def _timed(self, fn):
+        if not self.timing:
+            return fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = fn()
+        e.record()
+        self._events.append((s, e))
+        return out
+
+    def _fwd(self, m, xs, ys, saved, losses, n_micro):
         if self.first:
             inp = xs[m]
         else:
-            buf, w = self.p2p.recv(self.prev, "act", self.device)
-            w.wait()
-            inp = buf.to(self.device).requires_grad_(True)
-        out = self.module(inp)
+            inp = self._take("act", m, self.prev)
+            if m + 1 < n_micro:
+                self._post_recv("act", m + 1, self.prev, ahead=True)  # lands during compute m
+            inp = inp.to(self.device).requires_grad_(True)
+        out = self._timed(lambda: self.module(inp))
         if self.last:
-            loss = self.loss_fn(out, ys[m]) / len(ys)
+            loss = self._timed(lambda: self.loss_fn(out, ys[m]) / len(ys))
             losses.append(loss.detach())
             saved[m] = (inp, loss)
         else:
-            self._pending.extend(self.p2p.send(out.detach(), self.next, "act"))
+            self._pending.extend(self.p2p.send(out.detach(), self.next, ("act", m)))
             saved[m] = (inp, out)
 
-    def _bwd(self, m, saved):
+    def _bwd(self, m, saved, n_micro):
         inp, out = saved.pop(m)
         if self.last:
-            out.backward()
+            self._timed(lambda: out.backward())
         else:
-            buf, w = self.p2p.recv(self.next, "grad", self.device)
-            w.wait()
-            out.backward(buf.to(self.device).to(out.dtype))
+            g = self._take("grad", m, self.next)
+            if m + 1 < n_micro:
+                self._post_recv("grad", m + 1, self.next, ahead=True)
+            self._timed(lambda: out.backward(g.to(self.device).to(out.dtype)))
         if not self.first:
-            self._pending.extend(self.p2p.send(inp.grad, self.prev, "grad"))
+            self._pending.extend(self.p2p.send(inp.grad, self.prev, ("grad", m)))
 
     def _drain(self):
         for w in self._pending:
@@ -165,34 +156,49 @@ class PipelineStage:
         """One optimisation step over ``n_micro`` micro-batches.  ``x``/``y`` are
         needed on the first stage only.  Returns the mean loss on the last stage
         (a 0-d tensor) and None elsewhere."""
+        if self.timing:
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            self._events = []
+            t0.record()
         self.opt.zero_grad()
         xs = x.chunk(n_micro) if self.first else None
         ys = self._labels(y, n_micro) if (self.first or self.last) else None
         saved, losses = {}, []
         if self.schedule == "gpipe" or self.P == 1:
             for m in range(n_micro):
-                self._fwd(m, xs, ys, saved, losses)
+                self._fwd(m, xs, ys, saved, losses, n_micro)
             for m in range(n_micro):
-                self._bwd(m, saved)
+                self._bwd(m, saved, n_micro)
         else:  # 1F1B: warm up (P - idx - 1) forwards, then alternate, then drain
             warm = min(self.P - self.idx - 1, n_micro)
             f = b = 0
             for _ in range(warm):
-                self._fwd(f, xs, ys, saved, losses)
+                self._fwd(f, xs, ys, saved, losses, n_micro)
                 f += 1
             while f < n_micro:
-                self._fwd(f, xs, ys, saved, losses)
+                self._fwd(f, xs, ys, saved, losses, n_micro)
                 f += 1
-                self._bwd(b, saved)
+                self._bwd(b, saved, n_micro)
                 b += 1
             while b < n_micro:
-                self._bwd(b, saved)
+                self._bwd(b, saved, n_micro)
                 b += 1
         self._drain()
         self.opt.step()
+        if self.timing:
+            t1.record()
+            self._step_events = (t0, t1, list(self._events))
         if self.last:
             return torch.stack(losses).sum()
         return None
+
+    def step_stats(self):
+        """(step ms, compute ms, bubble fraction) of the last timed step (synchronises)."""
+        t0, t1, evs = self._step_events
+        t1.synchronize()
+        step = t0.elapsed_time(t1)
+        comp = sum(s.elapsed_time(e) for s, e in evs)
+        return step, comp, max(0.0, 1.0 - comp / step) if step > 0 else 0.0
 
     @torch.no_grad()
     def forward_only(self, x=None):
@@ -200,12 +206,10 @@ class PipelineStage:
         if self.first:
             h = x
         else:
-            buf, w = self.p2p.recv(self.prev, "eval_act", self.device)
-            w.wait()
-            h = buf.to(self.device)
+            h = self._take("eval_act", 0, self.prev).to(self.device)
         out = self.module(h)
         if not self.last:
-            for w in self.p2p.send(out, self.next, "eval_act"):
+            for w in self.p2p.send(out, self.next, ("eval_act", 0)):
                 w.wait()
             return None
         return out

@@ -84,6 +84,8 @@ def train(model, loader, loss_fn, optimizer, num_epochs=2, *, rank=None, aggrega
         torch.cuda.synchronize()
     stats["train_time"] = time.perf_counter() - t0
     stats["steps"] = step
+    if aggregate is not None and hasattr(aggregate, "comm_time"):
+        stats["comm_time"] = aggregate.comm_time  # event-timed aggregators report here
     print_fn("Training Finished!")
     if writer is not None:
         writer.flush()

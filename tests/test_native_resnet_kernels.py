@@ -558,7 +558,7 @@ def test_bn_stats_finalize_slab_rows(dev, T, C):
 
 
 @pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3] + L1_GEOMS[1:])
-@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 44, 45, 50, 51, 70])
+@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 44, 45, 50, 51, 70, 90, 91, 92, 93])
 def test_conv_fwd_prebn(dev, geom, cfg):
     """Halo conv consuming relu(y*scale + shift) of a RAW previous-conv output (fused
     BN-apply + ReLU in the staging); zero padding stays zero after the BN."""
@@ -841,14 +841,14 @@ PIPE_GEOMS = [
 
 
 @pytest.mark.parametrize("geom", PIPE_GEOMS)
-@pytest.mark.parametrize("cfg", [90, 91, 92])
+@pytest.mark.parametrize("cfg", [90, 91, 92, 93])
 def test_conv_fwd_pipe(dev, geom, cfg):
     _check_fwd(dev, geom, cfg)
 
 
 @pytest.mark.parametrize("geom", PIPE_GEOMS[:6])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [90, 91, 92])
+@pytest.mark.parametrize("cfg", [90, 91, 92, 93])
 def test_conv_dgrad_pipe(dev, geom, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
