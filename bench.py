@@ -71,12 +71,6 @@ def parse():
                          "xgmi; above the bucket size every bucket goes there (two-shot)")
     ap.add_argument("--comm-dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--backend", default="native", choices=["native", "torch"])
-    ap.add_argument("--prefetch", type=int, default=0,
-                    help="ResNet-18: pack the next batch's input (space-to-depth, bf16) on the "
-                         "side stream during the stem weight gradient, as a prefetching loader "
-                         "would.  Off by default: the stem weight gradient slows by what the "
-                         "packing saves (452 vs 372 us, 43.87k vs 43.93k img/s, "
-                         "profiles/input_prefetch_r2c.txt)")
     ap.add_argument("--fused", type=int, default=-1,
                     help="LeNet: the whole training step as 2 native dispatches "
                          "(dmlab.models.lenet_fused; 3 + the all-reduce with DDP); -1 = auto (on "
@@ -141,7 +135,7 @@ def main():
 
         fused = FusedLeNetStep(model, opt, ddp=net)
 
-    def train_step(x, y, x_next=None):
+    def train_step(x, y):
         if fused is not None:
             return fused(x, y)
         if a.backend == "torch":
@@ -150,16 +144,15 @@ def main():
             loss = torch.nn.functional.cross_entropy(out.float(), y)
         else:
             loss = cross_entropy(net(x), y)
-            if x_next is not None and a.prefetch:
-                # the next batch's input packing overlaps this step's stem weight gradient
-                model.prefetch(x_next)
         opt.zero_grad()
         loss.backward()
         opt.step()
         return loss.detach()
 
     if a.graph < 0:
-        capturable_comm = ws == 1 or dist.get_backend() == "nccl"
+        # RCCL collectives and the xGMI all-reduce kernel capture with the step; gloo's
+        # host-side collectives cannot (LeNet's 207 KB of gradients fit one xGMI bucket)
+        capturable_comm = ws == 1 or dist.get_backend() == "nccl" or a.small_allreduce == "xgmi"
         a.graph = 1 if (a.model == "lenet" and capturable_comm) else 0
     if a.graph and a.backend == "native":
         from dmlab.utils.graph import CapturedStep
@@ -228,8 +221,6 @@ def main():
                 "backend": a.backend,
                 "fused_step": bool(fused is not None),
                 "hip_graph": bool(a.graph and a.backend == "native"),
-                "input_prefetch": bool(a.prefetch and a.model == "resnet18" and a.backend == "native"
-                                       and not a.graph),
             },
             "final_loss": round(final_loss, 4),
         }

@@ -352,21 +352,6 @@ void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w
                        first, pp != nullptr, loss.data_ptr<float>(), cur_stream());
 }
 
-// A HIP stream whose kernels may only occupy the CUs set in `mask` (bit i of word w =
-// CU 32w+i), on a hardware queue of its own.  Used for the backward weight-gradient
-// stream so that it can never take every CU from the critical-path stream.  The stream
-// lives for the process (returned as a raw handle for torch.cuda.ExternalStream).
-int64_t cumask_stream(int device, std::vector<int64_t> mask) {
-  TORCH_CHECK(!mask.empty(), "empty CU mask");
-  const DeviceGuard guard(at::Device(at::kCUDA, device));
-  std::vector<uint32_t> m(mask.size());
-  for (size_t i = 0; i < mask.size(); ++i) m[i] = (uint32_t)mask[i];
-  hipStream_t st = nullptr;
-  TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()) == hipSuccess,
-              "hipExtStreamCreateWithCUMask failed");
-  return reinterpret_cast<int64_t>(st);
-}
-
 int num_cus(int device) {
   int n = 0;
   TORCH_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess);
@@ -382,7 +367,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_resnet(m);
   register_reducer(m);
   m.doc() = "dmlab native HIP kernels for MI355X (gfx950)";
-  m.def("cumask_stream", &cumask_stream, "CU-masked HIP stream (raw handle)");
   m.def("num_cus", &num_cus);
   m.def("sgd_step", &sgd_step, "fused flat SGD/GD step");
   m.def("adam_step", &adam_step, "fused flat Adam step");

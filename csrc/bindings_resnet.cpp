@@ -37,15 +37,6 @@ int ilog2(int v) {
   return l;
 }
 
-// persistent per-layer ticket counters of the one-launch BN finalizes (int32, one per
-// 32-channel group, zero between launches; each group's last block resets its own)
-unsigned* counter_ptr(const c10::optional<at::Tensor>& c, const at::Tensor& like, int64_t C) {
-  if (!c.has_value()) return nullptr;
-  TORCH_CHECK(c->scalar_type() == at::kInt && c->is_contiguous() && c->numel() >= (C + 31) / 32 &&
-              c->device() == like.device(), "counter: int32 tensor on the device, ceil(C/32) long");
-  return reinterpret_cast<unsigned*>(c->data_ptr<int>());
-}
-
 dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride, int pad, int OH,
                       int OW) {
   dm::ConvGeom g{};
@@ -101,23 +92,6 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
       return;
     }
     if (cfg >= 90 && cfg <= 93) cfg = 41;  // same 256-row tile (stats slab rows match)
-    if (cfg == 70) {
-      if (dm::conv_l1_supported(g)) {
-        dm::conv_l1(bp(x), bp(wpack), bp(y), ap, sp, g, cur_stream(), fp(*pre_scale),
-                    fp(*pre_shift));
-        return;
-      }
-      cfg = 39;  // same 256-row tile
-    }
-    if (cfg == 50 || cfg == 51) {
-      if (dm::conv_h5_supported(g, (int)cfg)) {
-        dm::conv_h5(bp(x), bp(wpack), bp(y), ap, sp, g, (int)cfg, cur_stream(), fp(*pre_scale),
-                    fp(*pre_shift));
-        return;
-      }
-      TORCH_CHECK(cfg == 50, "cfg 51 needs a single-chunk 3x3/s1 geometry");
-      cfg = 41;  // same 256-row tile: the stats slab rows still match
-    }
     TORCH_CHECK(dm::halo_cfg((int)cfg, bn, waves) && dm::conv_halo_supported(g),
                 "fused pre-BN needs a halo-kernel cfg and a unit-stride 3x3 geometry");
     dm::conv_halo(bp(x), bp(wpack), bp(y), ap, sp, g, bn, waves, cur_stream(), fp(*pre_scale),
@@ -127,10 +101,8 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
   dm::igemm_fwd(bp(x), bp(wpack), bp(y), ap, sp, g, cfg, cur_stream());
 }
 
-// statistics rows a forward conv of this cfg writes; ncols (output channels) is needed for the
-// cfg-41 tail split (ncols < 0: the plain one-row-per-tile count, no split)
+// statistics rows a forward conv of this cfg writes (one per row tile); ncols is unused
 int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
-  if (cfg == 41 && ncols > 0) return dm::conv_halo41_stats_rows(M, (int)ncols);
   const int bm = dm::igemm_fwd_rowtile(cfg);
   return (M + bm - 1) / bm;
 }
@@ -139,7 +111,7 @@ int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
 // Slab rows the BN-backward epilogue of conv_dgrad writes (0: the shape/cfg cannot fuse it).
 int64_t dgrad_bnb_rows(int64_t N, int64_t H, int64_t W, int64_t stride, int64_t cfg) {
   if (cfg < 9) return 0;
-  if (stride == 1) return conv_stats_rows(N * H * W, cfg, -1);  // fused sums: no tail split
+  if (stride == 1) return conv_stats_rows(N * H * W, cfg, -1);
   if (!(cfg == 12 || cfg == 13 || cfg == 15 || cfg == 16)) return 0;
   const long long mmax = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);  // class (0, 0) is largest
   return ((mmax + 127) / 128) * 4;
@@ -154,13 +126,8 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
                    c10::optional<at::Tensor> bnb_mean, c10::optional<at::Tensor> bnb_invstd,
                    c10::optional<at::Tensor> bnb_scale, c10::optional<at::Tensor> bnb_shift,
                    int64_t bnb_mode, c10::optional<at::Tensor> bnb_slab,
-                   c10::optional<at::Tensor> bnb_mask, c10::optional<at::Tensor> bwd_y,
-                   c10::optional<at::Tensor> bwd_coef, c10::optional<at::Tensor> bwd_scale,
-                   c10::optional<at::Tensor> bwd_shift) {
+                   c10::optional<at::Tensor> bnb_mask) {
   // add: tensor added to the result (may alias dx for in-place accumulation)
-  // bwd_* (optional): dy is the UPSTREAM gradient dz of this conv's BatchNorm and the operand
-  // is that BN's backward apply a*dz' + b*y + cc (dz' masked by relu(y*scale + shift) > 0),
-  // computed while staging (cfg 39, stride 1, 64 channels): the apply pass never runs
   need_bf16_nhwc(dy, "dy");
   need_bf16_nhwc(dx, "dx");
   const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), Cout = dy.size(3);
@@ -223,19 +190,6 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
     slabp = fp(*bnb_slab);
   }
   const dm::BnBwdEpi* bnbp = bnb.y ? &bnb : nullptr;
-  dm::BwdPre bpre{};
-  if (bwd_y.has_value()) {
-    need_bf16_nhwc(*bwd_y, "bwd_y");
-    TORCH_CHECK(bwd_y->sizes() == dy.sizes(), "bwd_y: the BN input, shaped like dy");
-    TORCH_CHECK(bwd_coef.has_value() && bwd_scale.has_value() && bwd_shift.has_value(),
-                "bwd_y needs bwd_coef, bwd_scale, bwd_shift");
-    need_f32(*bwd_coef, "bwd_coef", 3 * (int64_t)Cout);
-    need_f32(*bwd_scale, "bwd_scale", Cout);
-    need_f32(*bwd_shift, "bwd_shift", Cout);
-    TORCH_CHECK(stride == 1 && cfg == 39 && Cout == 64 && !bnbp,
-                "BN-backward operand: stride-1 dgrad, cfg 39, 64 channels, no fused sums");
-    bpre = dm::BwdPre{bp(*bwd_y), fp(*bwd_coef), fp(*bwd_scale), fp(*bwd_shift)};
-  }
   dm::ConvGeom base{};
   base.N = N; base.H = OH; base.W = OW; base.C = Cout; base.lgC8 = ilog2(Cout / 8);
   base.OH = H; base.OW = W; base.OC = Cin;
@@ -247,12 +201,6 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
-    if (bpre.y) {
-      TORCH_CHECK(dm::conv_halo_supported(g), "BN-backward operand: not a halo-kernel shape");
-      dm::conv_halo(bp(dy), bp(wd), bp(dx), addp, nullptr, g, 64, 16, st, nullptr, nullptr,
-                    nullptr, &bpre);
-      return 0;
-    }
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, slabp, g, cfg, st, bnbp);
     return bnb_rows;
   }
@@ -284,15 +232,6 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
       dm::geom_finalize(g);
       set.g[ng++] = g;
     }
-  // cfg 80: all four classes of a 3x3/s2 dgrad in one block over one staged dY halo
-  // (csrc/dgrad_s2.hip); shapes it does not cover take the v3 128x64 parity-class tile
-  if (cfg == 80) {
-    if (!bnbp && dm::dgrad_s2_supported(set, ng)) {
-      dm::dgrad_s2(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, st);
-      return 0;
-    }
-    cfg = Cin % 128 == 0 ? 15 : 13;
-  }
   // pipelined tiles: all parity classes in one launch (blockIdx.y = class)
   if (cfg >= 90 && cfg <= 93 && !bnbp && ng > 0 &&
       dm::conv_pipe_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, ng, (int)cfg, st))
@@ -319,13 +258,9 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
 void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int64_t Cin,
                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, double beta, int64_t S,
                 int64_t cfg, bool s2d, c10::optional<at::Tensor> pre_scale,
-                c10::optional<at::Tensor> pre_shift, c10::optional<at::Tensor> bwd_y,
-                c10::optional<at::Tensor> bwd_coef, c10::optional<at::Tensor> bwd_scale,
-                c10::optional<at::Tensor> bwd_shift) {
+                c10::optional<at::Tensor> pre_shift) {
   // s2d: x/dy are the space-to-depth stem operands (4x4/s1 conv over 4*Cin channels);
   // dw is the original [Cout][Cin][7][7] gradient
-  // bwd_* (optional): dy is the upstream gradient dz of this conv's BatchNorm; the dY operand
-  // is that BN's backward apply (halo wgrad only, see conv_dgrad)
   need_bf16_nhwc(x, "x");
   need_bf16_nhwc(dy, "dy");
   const int Cout = dy.size(3);
@@ -337,32 +272,15 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   const long long mchunk = ((steps + S - 1) / S) * 64;  // multiple of both kernels' row step
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
-  dm::BwdPre dpre{};
-  if (bwd_y.has_value()) {
-    need_bf16_nhwc(*bwd_y, "bwd_y");
-    TORCH_CHECK(bwd_y->sizes() == dy.sizes(), "bwd_y: the BN input, shaped like dy");
-    TORCH_CHECK(bwd_coef.has_value() && bwd_scale.has_value() && bwd_shift.has_value(),
-                "bwd_y needs bwd_coef, bwd_scale, bwd_shift");
-    need_f32(*bwd_coef, "bwd_coef", 3 * (int64_t)Cout);
-    need_f32(*bwd_scale, "bwd_scale", Cout);
-    need_f32(*bwd_shift, "bwd_shift", Cout);
-    TORCH_CHECK(!s2d && (cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
-                "BN-backward dY operand needs the halo wgrad (cfg 4/5) and a 3x3/s1/p1 geometry");
-    dpre = dm::BwdPre{bp(*bwd_y), fp(*bwd_coef), fp(*bwd_scale), fp(*bwd_shift)};
-  }
-  if (pre_scale.has_value() || dpre.y) {
-    const float *psc = nullptr, *psh = nullptr;
-    if (pre_scale.has_value()) {  // x = previous conv's raw output, operand relu(x*sc + sh)
-      TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
-      need_f32(*pre_scale, "pre_scale", x.size(3));
-      need_f32(*pre_shift, "pre_shift", x.size(3));
-      psc = fp(*pre_scale);
-      psh = fp(*pre_shift);
-    }
+  if (pre_scale.has_value()) {
+    // x = previous conv's raw output, operand relu(x*sc + sh)
+    TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
+    need_f32(*pre_scale, "pre_scale", x.size(3));
+    need_f32(*pre_shift, "pre_shift", x.size(3));
+    const float *psc = fp(*pre_scale), *psh = fp(*pre_shift);
     TORCH_CHECK((cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
                 "fused pre-BN needs the halo wgrad (cfg 4/5) and a 3x3/s1/p1 geometry");
-    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh,
-                   dpre.y ? &dpre : nullptr);
+    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh);
   } else {
     dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
   }
@@ -438,7 +356,7 @@ void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gam
                        c10::optional<at::Tensor> rmean, c10::optional<at::Tensor> rvar,
                        double momentum, double eps, at::Tensor scale, at::Tensor shift,
                        at::Tensor mean, at::Tensor invstd, at::Tensor work,
-                       c10::optional<at::Tensor> num_batches, c10::optional<at::Tensor> counter) {
+                       c10::optional<at::Tensor> num_batches) {
   const int C = gamma.numel();
   need_f32(stats, "stats", T * 2 * C);
   long long* nb = nullptr;  // BatchNorm num_batches_tracked, incremented in the finalize kernel
@@ -453,7 +371,7 @@ void bn_stats_finalize(at::Tensor stats, int64_t T, double count, at::Tensor gam
   dm::bn_stats_finalize(fp(stats), T, C, count, fp(gamma), fp(beta),
                         rmean.has_value() ? fp(*rmean) : nullptr, rvar.has_value() ? fp(*rvar) : nullptr,
                         momentum, eps, fp(scale), fp(shift), fp(mean), fp(invstd), fp(work), nb,
-                        cur_stream(), counter_ptr(counter, stats, C));
+                        cur_stream());
 }
 
 void bn_eval_coeffs(at::Tensor gamma, at::Tensor beta, at::Tensor rmean, at::Tensor rvar, double eps,
@@ -608,7 +526,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
                  c10::optional<at::Tensor> pidx, int64_t K, int64_t S, int64_t P,
                  c10::optional<at::Tensor> dy, c10::optional<at::Tensor> dres, at::Tensor work,
                  c10::optional<at::Tensor> pre_slab, int64_t pre_rows,
-                 c10::optional<at::Tensor> mask, c10::optional<at::Tensor> counter) {
+                 c10::optional<at::Tensor> mask) {
   // dy None: reduce + finalize only -- dgamma/dbeta and the coefficients a, b, cc of
   // dy = a*dz + b*y + cc are left in work (bn_bwd_coef_offset) for a consumer kernel that
   // applies them while staging its operand (conv_dgrad / conv_wgrad bwd_*)
@@ -676,7 +594,7 @@ void bn_backward(c10::optional<at::Tensor> dout, c10::optional<at::Tensor> out, 
   dm::bn_backward(doutp, outp, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
                   (float)gbeta, M, C, (int)mode, scp, shp, pdyp, pidxp, y.size(1), y.size(2), OH,
                   OW, K, S, P, dy.has_value() ? bp(*dy) : nullptr, drp, fp(work), cur_stream(), pre_slab.has_value() ? fp(*pre_slab) : nullptr,
-                  (int)pre_rows, mp, counter_ptr(counter, y, C));
+                  (int)pre_rows, mp);
 }
 
 void bn_relu_maxpool(at::Tensor y, at::Tensor scale, at::Tensor shift, at::Tensor out,
@@ -784,23 +702,19 @@ void register_resnet(pybind11::module_& m) {
         py::arg("bnb_mean") = py::none(), py::arg("bnb_invstd") = py::none(),
         py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(),
         py::arg("bnb_mode") = 0, py::arg("bnb_slab") = py::none(),
-        py::arg("bnb_mask") = py::none(), py::arg("bwd_y") = py::none(),
-        py::arg("bwd_coef") = py::none(), py::arg("bwd_scale") = py::none(),
-        py::arg("bwd_shift") = py::none());
+        py::arg("bnb_mask") = py::none());
   m.def("dgrad_bnb_rows", &dgrad_bnb_rows);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),
-        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none(),
-        py::arg("bwd_y") = py::none(), py::arg("bwd_coef") = py::none(),
-        py::arg("bwd_scale") = py::none(), py::arg("bwd_shift") = py::none());
+        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
   m.def("pack_weights", &pack_weights);
   m.def("pack_weights_multi", &pack_weights_multi);
   m.def("pack_weights_tiled", &pack_weights_tiled);
   m.def("bn_stats_finalize", &bn_stats_finalize, py::arg("stats"), py::arg("T"), py::arg("count"),
         py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("momentum"),
         py::arg("eps"), py::arg("scale"), py::arg("shift"), py::arg("mean"), py::arg("invstd"),
-        py::arg("work"), py::arg("num_batches") = py::none(), py::arg("counter") = py::none());
+        py::arg("work"), py::arg("num_batches") = py::none());
   m.def("bn_eval_coeffs", &bn_eval_coeffs);
   m.def("bn_apply", &bn_apply, py::arg("y"), py::arg("res"), py::arg("scale"), py::arg("shift"),
         py::arg("out"), py::arg("relu"), py::arg("mask") = py::none());
@@ -818,8 +732,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("stem_wgrad_dy", &stem_wgrad_dy);
   m.def("wgrad_reduce_s2d", &wgrad_reduce_s2d);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
-        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none(),
-        py::arg("counter") = py::none());
+        py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none());
   m.def("bn_relu_maxpool", &bn_relu_maxpool, py::arg("y"), py::arg("scale"), py::arg("shift"),
         py::arg("out"), py::arg("idx"), py::arg("K"), py::arg("S"), py::arg("P"),
         py::arg("yarg") = py::none());

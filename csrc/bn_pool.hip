@@ -149,116 +149,6 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   fin_fwd_channel(f, c, s, q, count);
 }
 
-// One launch instead of slab_colsum + finalize: the blocks of the first-level column sums
-// publish their [G][W] rows (agent-scope release + a ticket counter); the last block to
-// arrive acquires them and runs the finalize for every channel (the rows are few: G <= 256).
-// Same partial rows and summation order as the two-launch path (bit-identical results).
-// ctr: a counter owned by the caller (one per BN layer and direction), 0 between launches;
-// the last block resets it.
-template <bool BWD>
-__global__ void __launch_bounds__(256) colsum_finalize_kernel(const float* __restrict__ in, int T,
-                                                              int C, float* __restrict__ out,
-                                                              unsigned* __restrict__ ctr,
-                                                              double count, FinFwd ff, FinBwd fb) {
-  const int W = 2 * C;
-  const int G = gridDim.y, gi = blockIdx.y;
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
-  const int R = (T + G - 1) / G;
-  const int r0 = gi * R, r1 = min(T, r0 + R);
-  __shared__ double red[4][64];
-  __shared__ int last;
-  red[rl][threadIdx.x & 63] = col < W ? sum_rows8(in + col, r0 + rl, r1, 4, W) : 0.0;
-  __syncthreads();
-  if (rl == 0 && col < W)
-    out[(long long)gi * W + col] = (float)(red[0][threadIdx.x] + red[1][threadIdx.x] +
-                                           red[2][threadIdx.x] + red[3][threadIdx.x]);
-  // publish (cdna guide, Guideline 16 counter form): stores retired, one agent release, ticket
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned n = gridDim.x * gridDim.y;
-    last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!BWD && ff.num_batches) *ff.num_batches += 1;
-  }
-  __syncthreads();
-  for (int c0 = 0; c0 < C; c0 += FIN_CH) {
-    const int c = c0 + (threadIdx.x % FIN_CH);
-    double s, q;
-    block_sum2(out, G, C, c, s, q);
-    if (threadIdx.x < FIN_CH && c < C) {
-      if (BWD) fin_bwd_channel(fb, c, C, s, q, count);
-      else fin_fwd_channel(ff, c, s, q, count);
-    }
-    __syncthreads();  // block_sum2's shared rows are reused by the next channel group
-  }
-}
-
-// One launch with the finalize spread over channel groups: block (x, y) sums rows of group y
-// for the 32 channels [32x, 32x + 32) -- both moments, columns c and C + c -- and the last
-// block to arrive FOR ITS CHANNEL GROUP (ticket ctr[x]) finalizes those 32 channels.  The
-// tails of different groups run in parallel (colsum_finalize_kernel's single last block walks
-// every channel serially: 6 % slower end to end).  Same first-level rows and summation order
-// as slab_colsum_kernel, same second level as block_sum2: bit-identical to the two launches.
-// ctr: ceil(C/32) counters owned by the caller, 0 between launches (each group's last block
-// resets its own).
-template <bool BWD>
-__global__ void __launch_bounds__(256) colsum_finalize_grouped_kernel(
-    const float* __restrict__ in, int T, int C, float* __restrict__ out, unsigned* __restrict__ ctr,
-    double count, FinFwd ff, FinBwd fb) {
-  const int W = 2 * C;
-  const int G = gridDim.y, gi = blockIdx.y;
-  const int j = threadIdx.x & 63;
-  const int c = blockIdx.x * 32 + (j & 31);
-  const int col = (j >> 5) * C + c;
-  const bool okc = c < C;
-  const int rl = threadIdx.x >> 6;
-  const int R = (T + G - 1) / G;
-  const int r0 = gi * R, r1 = min(T, r0 + R);
-  __shared__ double red[4][64];
-  __shared__ int last;
-  red[rl][j] = okc ? sum_rows8(in + col, r0 + rl, r1, 4, W) : 0.0;
-  __syncthreads();
-  if (rl == 0 && okc)
-    out[(long long)gi * W + col] = (float)(red[0][j] + red[1][j] + red[2][j] + red[3][j]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(ctr + blockIdx.x, 1u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT) == (unsigned)G - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(ctr + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!BWD && ff.num_batches && blockIdx.x == 0) *ff.num_batches += 1;
-  }
-  __syncthreads();
-  for (int c0 = blockIdx.x * 32; c0 < blockIdx.x * 32 + 32 && c0 < C; c0 += FIN_CH) {
-    const int cc = c0 + (threadIdx.x % FIN_CH);
-    double sm, q;
-    block_sum2(out, G, C, cc, sm, q);
-    if (threadIdx.x < FIN_CH && cc < C) {
-      if (BWD) fin_bwd_channel(fb, cc, C, sm, q, count);
-      else fin_fwd_channel(ff, cc, sm, q, count);
-    }
-    __syncthreads();
-  }
-}
-
 // eval mode: scale/shift from running stats
 __global__ void bn_eval_coeffs_kernel(const float* __restrict__ gamma, const float* __restrict__ beta,
                                       const float* __restrict__ rmean, const float* __restrict__ rvar,
@@ -1157,15 +1047,10 @@ void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, i
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
                        float* scale, float* shift, float* mean, float* invstd, float* work,
-                       long long* num_batches, hipStream_t st, unsigned* ctr) {
+                       long long* num_batches, hipStream_t st) {
   const int W = 2 * C;
   const int G = colsum_groups(T);
   const FinFwd f{gamma, beta, rmean, rvar, momentum, eps, scale, shift, mean, invstd, num_batches};
-  if (G && ctr) {  // one launch: column sums + per-channel-group last-block finalize
-    colsum_finalize_grouped_kernel<false><<<dim3((C + 31) / 32, G), 256, 0, st>>>(
-        stats, T, C, work, ctr, count, f, FinBwd{});
-    return;
-  }
   const float* fin = stats;
   if (G) {
     slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
@@ -1185,11 +1070,6 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
   const long long n8 = n / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 2 * C;
-  static const int bnf_u = getenv("DMLAB_BNF_U") ? atoi(getenv("DMLAB_BNF_U")) : 4;
-  if (res && relu && bnf_u == 8) {
-    bn_apply_kernel<true, true, 8><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
-    return;
-  }
   if (res) {
     if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
     else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
@@ -1197,11 +1077,6 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
     if (relu) bn_apply_kernel<false, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
     else bn_apply_kernel<false, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
   }
-}
-
-static int bnr_u() {
-  static const int u = getenv("DMLAB_BNR_U") ? atoi(getenv("DMLAB_BNR_U")) : 4;
-  return u;
 }
 
 int bn_bwd_groups(long long M, int C);
@@ -1220,8 +1095,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  float gbeta, long long M, int C, int mode, const float* scale,
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
-                 hipStream_t st, const float* pre_part, int pre_rows, const uint8_t* mask,
-                 unsigned* ctr) {
+                 hipStream_t st, const float* pre_part, int pre_rows, const uint8_t* mask) {
   // pre_part (optional): [pre_rows][2C] partial Σdz, Σdz·x̂ already reduced by the producing
   // dgrad's epilogue (BnBwdEpi) — the reduction pass over dout and y is skipped
   // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
@@ -1238,37 +1112,28 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   if (pre_part) {
   } else if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
   else switch (mode) {
-    // DMLAB_BNR_U / DMLAB_BNA_U / DMLAB_BNF_U: 16-B chunks per operand in flight per thread
-    // in the reduce / backward apply / forward apply passes.  8 instead of 4: reduce and
-    // forward apply neutral, backward apply -1.2 % (profiles/bn_loads_in_flight_r2c.jsonl)
-    case 0: if (bnr_u() == 8) bn_bwd_reduce_kernel<0, 8><<<G, 256, shr, st>>>(a, part); else bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
+    // 4 16-B chunks per operand in flight per thread (8 measured neutral for the reduce and
+    // forward apply, -1.2 % for the backward apply: profiles/bn_loads_in_flight_r2c.jsonl)
+    case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
     case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
-    case 2: if (bnr_u() == 8) bn_bwd_reduce_kernel<2, 8><<<G, 256, shr, st>>>(a, part); else bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
-    case 4: if (bnr_u() == 8) bn_bwd_reduce_kernel<4, 8><<<G, 256, shr, st>>>(a, part); else bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part); break;
+    case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
+    case 4: bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part); break;
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
   const int G2 = colsum_groups(G);
   const FinBwd fb{gamma, mean, invstd, dgamma, dbeta, gbeta, coef};
-  if (G2 && ctr) {  // one launch: column sums + per-channel-group last-block finalize
-    colsum_finalize_grouped_kernel<true><<<dim3((C + 31) / 32, G2), 256, 0, st>>>(
-        part, G, C, part2, ctr, (double)M, FinFwd{}, fb);
-  } else {
-    const float* fin = part;
-    if (G2) {  // parallel fixed-order pre-reduction so the finalize sums stay short
-      slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
-      fin = part2;
-    }
-    bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C,
-                                                                      (double)M, fb);
+  const float* fin = part;
+  if (G2) {  // parallel fixed-order pre-reduction so the finalize sums stay short
+    slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
+    fin = part2;
   }
+  bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C,
+                                                                    (double)M, fb);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;
-  static const int bna_u = getenv("DMLAB_BNA_U") ? atoi(getenv("DMLAB_BNA_U")) : 4;
-#define DM_BNB(MD, D)                                                            \
-  if (bna_u == 8 && MD != 3) bn_bwd_apply_kernel<MD, D, 8><<<grid, 256, sh, st>>>(a, coef, dy, dres); \
-  else bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
+#define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
   if (quad) {
     bn_bwd_apply_quad_kernel<<<grid_for(n8 / 4, 256, 4096), 256, sh, st>>>(a, coef, dy);
     return;

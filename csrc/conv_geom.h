@@ -43,17 +43,6 @@ struct BnBwdEpi {
   const unsigned char* mask;
 };
 
-// Operand of a dgrad / weight-gradient kernel given as the upstream gradient dz of the
-// conv's BatchNorm plus that BN's backward coefficients: the kernel stages
-//     dy = a·dz' + b·y + cc,   dz' = dz masked by relu(y·scale + shift) > 0
-// (igemm_common.h PreBnBwd), so the BN-backward apply pass is never run.  y == nullptr: off.
-struct BwdPre {
-  const unsigned short* y;  // the BN's input (the conv's raw output), shaped like dz
-  const float* coef;        // [3][C]: a, b, cc
-  const float* scale;       // forward BN scale / shift (ReLU mask)
-  const float* shift;
-};
-
 // several geometries for one launch (selected by blockIdx.z)
 struct ConvGeomSet {
   ConvGeom g[4];

@@ -40,27 +40,20 @@ constexpr unsigned OOB = 0x80000000u;
 // PF: weight-tile register prefetch depth (1: the tile of step s+1 is loaded during step s;
 // 2: the tile of step s+2, so a load has two steps of MFMA work to land in)
 // PRE: 0 = X as stored; 1 = X is a conv's raw output y, operand relu(y*sc + sh) (forward BN +
-// ReLU of the previous layer); 2 = X is an upstream gradient dz, operand the BN-backward apply
-// a*dz' + b*y + cc with y = bpre.y (a dgrad consuming its BN's backward without the apply
-// pass; single 64-channel chunk only: the next chunk's halo is never prefetched)
+// ReLU of the previous layer)
 // waves per SIMD the 8-wave 64-channel tile (cfg 39) is compiled for: 4 = its LDS-bound
 // occupancy (2 workgroups per CU).  Built with 2: 43.9k vs 44.8k img/s
 // (profiles/halo39_launch_bounds_r2c.jsonl)
 #ifndef DM_HALO39_MINB
 #define DM_HALO39_MINB 4
 #endif
-template <int BN, int HR, int WM, int WN, int BMH, int PRE, int PF>
+template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_HALO39_MINB : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,
-    long long mbase, int rowbase, int diag, int xcd, int mtiles, BwdPre bpre) {
-  // diag (DMLAB_HALO_DIAG, timing diagnostics only; results wrong when set): bit 0 drops the
-  // MFMA phase, bit 1 the per-step weight loads, bit 2 the epilogue, bit 3 the per-step
-  // barriers, bit 4 the epilogue's global stores, bit 5 its BN statistics
+    int xcd, int mtiles) {
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
-  // mbase / rowbase: first output pixel and first statistics row of this launch (a launch
-  // may cover only the tail of the pixel range, see conv_halo's tail split)
   // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
   // image taps still read the zero row, i.e. the padding stays zero AFTER the BN.
   constexpr int TM = BMH / WM, TN = BN / WN;
@@ -86,7 +79,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
     bx = (j / xcd) * 8 + (b & 7);
     if (bx >= mtiles) return;  // padding of the M tiles to a multiple of 8
   }
-  const long long m0 = mbase + (long long)bx * BMH;
+  const long long m0 = (long long)bx * BMH;
   const int n0 = by * BN;
   const int ntaps = g.nth * g.ntw;
   const int nchunk = g.C / HBK;
@@ -131,8 +124,6 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
   __syncthreads();
 
   uint4 rh[HR], rb[BR];
-  uint4 ry[PRE == 2 ? HR : 1];
-  const auto rsy = __builtin_amdgcn_make_buffer_rsrc((void*)bpre.y, (short)0, (int)xbytes, 0x00020000);
   auto load_halo = [&](int cc) {
     const unsigned cb = (unsigned)(cc * HBK + chunk * 8) * 2u;
 #pragma unroll
@@ -143,34 +134,15 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       const unsigned off = ok ? (unsigned)gp * (unsigned)g.C * 2u + cb : OOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
       rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
-      if constexpr (PRE == 2) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsy, off, 0, 0);
-        ry[j] = make_uint4(w[0], w[1], w[2], w[3]);
-      }
     }
   };
   auto store_halo = [&](int cc) {
-    if constexpr (PRE == 2) {
-      // out-of-range rows loaded zeros for both operands: a*0 + b*0 + cc != 0, so they are
-      // stored as zeros explicitly (the conv's zero padding of dy)
-      PreBnBwd pb;
-      pb.load(bpre.coef, bpre.scale, bpre.shift, g.C, cc * HBK + chunk * 8);
-#pragma unroll
-      for (int j = 0; j < HR; ++j) {
-        const int hh = (tid >> 3) + RPP * j;
-        const int gp = hbase + hh;
-        const bool ok = hh < hp && (unsigned)gp < (unsigned)NHW;
-        *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) =
-            ok ? pb.apply(rh[j], ry[j]) : make_uint4(0, 0, 0, 0);
-      }
-      return;
-    }
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
       const int hh = (tid >> 3) + RPP * j;
       *reinterpret_cast<uint4*>(Hs + hh * HBK + swz(hh, chunk) * 8) = rh[j];
     }
-    if constexpr (PRE == 1) {
+    if constexpr (PRE) {
       // normalise in place once the staging registers are dead (each thread rewrites
       // only its own chunks: program order suffices, no barrier), so the fused BN costs
       // no registers across the tap loop
@@ -185,7 +157,6 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
     }
   };
   auto load_b_into = [&](uint4 (&dst)[BR], int cc, int t) {
-    if (diag & 2) return;
     const unsigned kb = (unsigned)(taps[t].z + cc * HBK + chunk * 8) * 2u;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
@@ -214,7 +185,6 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   auto compute = [&](int buf, int t) {
-    if (diag & 1) return;
     const int4 tp = taps[t];
     int hrow[RM];
 #pragma unroll
@@ -258,9 +228,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
     store_halo(0);
     store_b(0);
     __syncthreads();
-    if constexpr (PRE != 2) {
-      if (nchunk > 1) load_halo(1);
-    }
+    if (nchunk > 1) load_halo(1);
     int cc = 0, t = 0;
     for (int s = 0; s < S; ++s) {
       int nt = t + 1, ncc = cc;
@@ -271,13 +239,11 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       if (s + 1 < S) load_b(ncc, nt);
       compute(s & 1, t);
       if (s + 1 < S) store_b((s + 1) & 1);
-      if (!(diag & 8)) __syncthreads();
-      if constexpr (PRE != 2) {
-        if (ncc != cc && s + 1 < S) {
-          store_halo(ncc);  // every wave is past the last tap of chunk cc
-          __syncthreads();
-          if (ncc + 1 < nchunk) load_halo(ncc + 1);
-        }
+      __syncthreads();
+      if (ncc != cc && s + 1 < S) {
+        store_halo(ncc);  // every wave is past the last tap of chunk cc
+        __syncthreads();
+        if (ncc + 1 < nchunk) load_halo(ncc + 1);
       }
       t = nt;
       cc = ncc;
@@ -302,9 +268,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
     if (S > 1) load_b_into(rb2, lc, lt);  // tile 1
     nxt(lc, lt);
     __syncthreads();
-    if constexpr (PRE != 2) {
-      if (nchunk > 1) load_halo(1);
-    }
+    if (nchunk > 1) load_halo(1);
     int cc = 0, t = 0;
     auto step = [&](int s, uint4 (&rnext)[BR], uint4 (&rfree)[BR]) {
       // rnext holds tile s+1; rfree receives tile s+2
@@ -317,13 +281,11 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       nxt(lc, lt);
       compute(s & 1, t);
       if (s + 1 < S) store_b_from(rnext, (s + 1) & 1);
-      if (!(diag & 8)) __syncthreads();
-      if constexpr (PRE != 2) {
-        if (ncc != cc && s + 1 < S) {
-          store_halo(ncc);
-          __syncthreads();
-          if (ncc + 1 < nchunk) load_halo(ncc + 1);
-        }
+      __syncthreads();
+      if (ncc != cc && s + 1 < S) {
+        store_halo(ncc);
+        __syncthreads();
+        if (ncc + 1 < nchunk) load_halo(ncc + 1);
       }
       t = nt;
       cc = ncc;
@@ -333,10 +295,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       if (s + 1 < S) step(s + 1, rb, rb2);
     }
   }
-  if (diag & 4) return;
-  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, rowbase + bx,
-                                                       stats, g, Y, ADD,
-                                                       bnb, diag);
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, bx, stats, g, Y, ADD,
+                                                       bnb);
 }
 
 int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
@@ -347,91 +307,30 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
 template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
-                 const BnBwdEpi& bnb, long long mbase = 0, int rowbase = 0, long long mend = -1,
-                 const BwdPre* bpre = nullptr) {
+                 const BnBwdEpi& bnb) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
   const size_t sm = main > epi ? main : epi;
-  if (mend < 0) mend = g.M;
-  dim3 grid((unsigned)((mend - mbase + BMH - 1) / BMH), (g.Ncols + BN - 1) / BN);
+  const unsigned mt = (unsigned)((g.M + BMH - 1) / BMH), nt = (g.Ncols + BN - 1) / BN;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, 1, PF>
-                  : conv_halo_kernel<BN, HR, WM, WN, BMH, 0, PF>;
-  BwdPre bp{};
-  if (bpre) {
-    // the BN-backward-apply operand: the 8-wave 256 x 64 tile (cfg 39) over one chunk only
-    if constexpr (BN == 64 && WM == 4 && WN == 2 && BMH == 256 && PF == 1) {
-      DM_CHECK(g.C == HBK ? hipSuccess : hipErrorInvalidValue);
-      k = conv_halo_kernel<BN, HR, WM, WN, BMH, 2, PF>;
-      bp = *bpre;
-    } else {
-      DM_CHECK(hipErrorInvalidValue);
-    }
-  }
+  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
+                  : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
   set_smem_attr(k, sm);
-  static const int diag = getenv("DMLAB_HALO_DIAG") ? atoi(getenv("DMLAB_HALO_DIAG")) : 0;
-  // measured (tools/bench_conv.py, batch 512, one call): layer3 fwd 845 -> 880 TF/s, dgrad
-  // 859 -> 892; layer2 / layer4 +2-7 %; 11.60 vs 11.62 ms/step.  DMLAB_HALO_XCD=0: 2-D grid
-  static const int xcd_on = getenv("DMLAB_HALO_XCD") ? atoi(getenv("DMLAB_HALO_XCD")) : 1;
-  if (xcd_on && grid.y > 1) {
-    // 1-D grid over the M tiles (padded to a multiple of 8) x N tiles
-    const unsigned mt8 = (grid.x + 7) / 8 * 8, ntiles = grid.y;
-    k<<<dim3(mt8 * ntiles), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc,
-                                                   pre_sh, bnb, mbase, rowbase, diag,
-                                                   (int)ntiles, (int)grid.x, bp);
+  // XCD-aware 1-D grid over the M tiles (padded to a multiple of 8) x N tiles: the N tiles of
+  // one M tile share an XCD's L2.  Measured (tools/bench_conv.py, batch 512): layer3 fwd
+  // 845 -> 880 TF/s, dgrad 859 -> 892; layer2 / layer4 +2-7 %
+  if (nt > 1) {
+    const unsigned mt8 = (mt + 7) / 8 * 8;
+    k<<<dim3(mt8 * nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
+                                                bnb, (int)nt, (int)mt);
     return;
   }
-  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb, mbase,
-                                    rowbase, diag, 0, (int)grid.x, bp);
-}
-
-// Tail split for the 256-pixel 4x1-wave tile (cfg 41).  Its layer-3/4 grids are just over a
-// whole number of rounds of resident workgroups (1568 / 784 blocks on 512 slots), so the
-// last round runs a handful of blocks while most CUs idle (measured: layer4 at exactly one
-// round 910 vs 792 TFLOP/s at batch 512).  When the last round is under ~60 % full, the
-// pixel rows of that round go to a second launch of 128-pixel tiles (3 workgroups per CU):
-// twice the blocks, each half the work.  Statistics rows: the main tiles first, then the
-// 128-pixel tiles.
-int halo_slots() {
-  if (const char* e = getenv("DMLAB_TAIL_SLOTS"))  // tests: force the split on small shapes
-    if (atoi(e) > 0) return atoi(e);
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    DM_CHECK(hipGetDevice(&dev));
-    DM_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  return 2 * cus;  // cfg 41: two 4-wave workgroups per CU
-}
-
-// main M-tiles (256 px) of a cfg-41 launch; == all tiles when no tail split applies
-// Opt-in (DMLAB_TAIL_SPLIT=1, or DMLAB_TAIL_SLOTS for tests): measured slower end to end
-// (12.29 vs 12.08 ms/step; layer3 717 vs 733 TFLOP/s, layer4 773 vs 755): the blocks of a
-// nearly empty last round run faster alone than the model assumes, and the 128-pixel tail
-// tile plus its launch cost more than the idle CUs.
-long long halo41_main_tiles(long long M, int Ncols) {
-  const char* on = getenv("DMLAB_TAIL_SPLIT");
-  const char* sl = getenv("DMLAB_TAIL_SLOTS");
-  if (!((on && atoi(on) == 1) || (sl && atoi(sl) > 0))) return (M + 255) / 256;
-  const long long gx = (M + 255) / 256, gy = (Ncols + 63) / 64;
-  const long long T = gx * gy, slots = halo_slots();
-  if (T <= slots) return gx;
-  const long long tail = T % slots;
-  if (tail == 0 || tail * 10 > slots * 6) return gx;
-  const long long gxm = (T - tail) / gy;  // whole rounds, whole M-tiles
-  return gxm < gx ? gxm : gx;
+  k<<<dim3(mt, nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb,
+                                            0, (int)mt);
 }
 }  // namespace
-
-// statistics rows written by a halo launch of this config (256-px tiles, plus the 128-px tail
-// tiles of a cfg-41 tail split)
-long long conv_halo41_stats_rows(long long M, int Ncols) {
-  const long long gxm = halo41_main_tiles(M, Ncols);
-  const long long mend = gxm * 256 < M ? gxm * 256 : M;
-  return gxm + (M - mend + 127) / 128;
-}
 
 bool conv_halo_supported(const ConvGeom& g) {
   if (g.isy != 1 || g.isx != 1 || g.Hg != g.H || g.Wg != g.W) return false;
@@ -445,121 +344,35 @@ bool conv_halo_supported(const ConvGeom& g) {
   return halo_rows_needed(g) <= 32 * 12 && halo_rows_needed(g, 256) <= 32 * 14;
 }
 
+// tiles (igemm_fwd's halo cfgs): waves 4 = 128 px as 2 x 2 waves of 64 x BN/2 (cfg 20 / 21;
+// | 0x100: two weight tiles of register prefetch, cfg 42); 16 = 256 px as 4 x 2 waves of
+// 64 x 32 (cfg 39); 32 = 256 px as 4 x 1 waves of 64 x 64 (cfg 41)
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
-               const float* pre_sh, const BnBwdEpi* bnbp, const BwdPre* bpre) {
+               const float* pre_sh, const BnBwdEpi* bnbp) {
   const BnBwdEpi bnb = bnbp ? *bnbp : BnBwdEpi{};
-  if (bpre) {  // BN-backward apply on load: cfg 39 (256 px, 4 x 2 waves, BN 64), one chunk
-    DM_CHECK(bn == 64 && waves == 16 && g.C == HBK && !pre_sc ? hipSuccess : hipErrorInvalidValue);
-    const int hr = (halo_rows_needed(g, 256) + 63) / 64;
-    if (hr <= 5) launch_halo<64, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, bnb, 0, 0, -1, bpre);
-    else if (hr <= 6) launch_halo<64, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, bnb, 0, 0, -1, bpre);
-    else launch_halo<64, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, bnb, 0, 0, -1, bpre);
-    DM_CHECK(hipGetLastError());
-    return;
-  }
-  if (waves & 0x100) {  // two-deep weight prefetch: BN 128 4 waves / 128 px, 8 waves / 256 px;
-                        // BN 64 4 x 1 waves (cfg 44) and 4 x 2 waves (cfg 45) / 256 px
-    waves &= 0xff;
-    if (bn == 128 && waves == 4) {
-      const int hp = halo_rows_needed(g);
-      const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-      if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      DM_CHECK(hipGetLastError());
-      return;
-    }
-    if (bn == 64 && waves == 32) {  // cfg 44: the 4 x 1-wave 64 x 64 tile of cfg 41
-      const int hr = (halo_rows_needed(g, 256) + 31) / 32;
-      if (hr <= 10) launch_halo<64, 10, 4, 1, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      else if (hr <= 12) launch_halo<64, 12, 4, 1, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      else launch_halo<64, 14, 4, 1, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      DM_CHECK(hipGetLastError());
-      return;
-    }
-    if (waves == 16) {  // BN 128: cfg 43; BN 64: cfg 45 (the 4 x 2-wave tile of cfg 39)
-      const int hr = (halo_rows_needed(g, 256) + 63) / 64;
-      if (bn == 64) {
-        if (hr <= 5) launch_halo<64, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-        else if (hr <= 6) launch_halo<64, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-        else launch_halo<64, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-        DM_CHECK(hipGetLastError());
-        return;
-      }
-      if (hr <= 5) launch_halo<128, 5, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      else if (hr <= 6) launch_halo<128, 6, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      else launch_halo<128, 7, 4, 2, 256, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-      DM_CHECK(hipGetLastError());
-      return;
-    }
-  }
-  if (waves == 16 && bn == 64 && !bnbp && conv_halo_pers_ok(g)) {
-    // one 64-channel chunk: the persistent variant prefetches the next tile's halo
-    conv_halo_pers(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
-    return;
-  }
-  if (waves == 16) {  // 256-pixel tile, 4 x 2 waves of 64 x BN/2 (twice the weight reuse per FLOP)
-    const int hp2 = halo_rows_needed(g, 256);
-    const int hr = (hp2 + 63) / 64;
-#define DM_HALO256W8(BN_)                                                                    \
-  if (hr <= 5) launch_halo<BN_, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);                  \
-  else if (hr <= 6) launch_halo<BN_, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);             \
-  else launch_halo<BN_, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    if (bn == 128) { DM_HALO256W8(128) } else { DM_HALO256W8(64) }
-#undef DM_HALO256W8
-    DM_CHECK(hipGetLastError());
-    return;
-  }
-  if (waves == 32 && bn == 64) {  // 256-pixel tile: 4 x 1 waves of 64 x 64 (1 LDS read per MFMA;
-                                  // BN 128 as 64 x 128 per wave spills: not instantiated)
-    const int hp2 = halo_rows_needed(g, 256);
-    const int hr = (hp2 + 31) / 32;
-    // tail split (not with the fused BN-backward sums, whose slab rows are per 256-px tile)
-    const long long gxm = bnbp ? (g.M + 255) / 256 : halo41_main_tiles(g.M, g.Ncols);
-    const long long mend = gxm * 256 < g.M ? gxm * 256 : g.M;
-#define DM_HALO256W41(BN_)                                                                   \
-  if (hr <= 10) launch_halo<BN_, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, 0, 0, mend);      \
-  else if (hr <= 12) launch_halo<BN_, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, 0, 0, mend); \
-  else launch_halo<BN_, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, 0, 0, mend);
-    DM_HALO256W41(64)
-#undef DM_HALO256W41
-    if (mend < g.M) {  // the tail's pixel rows as 128-pixel tiles (2 x 2 waves of 64 x 32)
-      const int hp = halo_rows_needed(g);
-      const int rb = (int)gxm;
-      if (hp <= 192) launch_halo<64, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, mend, rb);
-      else if (hp <= 256) launch_halo<64, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, mend, rb);
-      else launch_halo<64, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb, mend, rb);
-    }
-    DM_CHECK(hipGetLastError());
-    return;
-  }
-  if (waves == 2) {  // 256-pixel tile: 2 x 2 waves of 128 x BN/2 (twice the weight reuse)
-    const int hp2 = halo_rows_needed(g, 256);
-    const int hr = (hp2 + 31) / 32;
-#define DM_HALO256(BN_)                                                                      \
-  if (hr <= 10) launch_halo<BN_, 10, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);                \
-  else if (hr <= 12) launch_halo<BN_, 12, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
-  else launch_halo<BN_, 14, 2, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    if (bn == 128) { DM_HALO256(128) } else { DM_HALO256(64) }
-#undef DM_HALO256
-    DM_CHECK(hipGetLastError());
-    return;
-  }
-  const int hp = halo_rows_needed(g);
-  if (waves == 8) {  // 4 x 2 waves of 32 x BN/2
-    const int hr = hp <= 192 ? 3 : hp <= 256 ? 4 : 6;
-#define DM_HALO8(BN_)                                                            \
-  if (hr == 3) launch_halo<BN_, 3, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
-  else if (hr == 4) launch_halo<BN_, 4, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);      \
-  else launch_halo<BN_, 6, 4, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    if (bn == 128) { DM_HALO8(128) } else { DM_HALO8(64) }
-#undef DM_HALO8
-  } else {  // 2 x 2 waves of 64 x BN/2
+  const int hp = halo_rows_needed(g), hp2 = halo_rows_needed(g, 256);
+  if (waves == (4 | 0x100) && bn == 128) {
     const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-#define DM_HALO4(BN_)                                                            \
-  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);           \
-  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);      \
+    if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+  } else if (waves == 16 && bn == 64) {
+    const int hr = (hp2 + 63) / 64;
+    if (hr <= 5) launch_halo<64, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    else if (hr <= 6) launch_halo<64, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    else launch_halo<64, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+  } else if (waves == 32 && bn == 64) {
+    const int hr = (hp2 + 31) / 32;
+    if (hr <= 10) launch_halo<64, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    else if (hr <= 12) launch_halo<64, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    else launch_halo<64, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+  } else {
+    DM_CHECK(waves == 4 ? hipSuccess : hipErrorInvalidValue);
+    const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
+#define DM_HALO4(BN_)                                                                       \
+  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);      \
+  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb); \
   else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
     if (bn == 128) { DM_HALO4(128) } else { DM_HALO4(64) }
 #undef DM_HALO4

@@ -33,265 +33,12 @@
 #include "kernels.h"
 
 #include <stdexcept>
+#include <string>
 
 #include <type_traits>
 
 namespace dm {
 
-
-// ------------------------------------------------------------------ shared epilogue
-template <int BM, int BN, int WM, int WN>
-__device__ __forceinline__ void igemm_epilogue(
-    f32x4 (&acc)[BM / WM / 16][BN / WN / 16], unsigned char* smem, bf16_t* Y, const bf16_t* ADD,
-    float* __restrict__ stats, const ConvGeom& g, long long m0, int n0) {
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int RM = TM / 16, RN = TN / 16;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  // ---------------- epilogue 1: BN batch statistics (Σ, Σ²) per output channel
-  float* red = reinterpret_cast<float*>(smem);  // reuse LDS (main loop finished)
-  if (stats) {
-    // red layout: [WM][BN][2]
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = acc[i][j][r];
-          s += v;
-          q += v * v;
-        }
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64);
-      q += __shfl_xor(q, 32, 64);
-      if (lane < 16) {
-        const int c = wn * TN + j * 16 + lane;
-        red[(wm * BN + c) * 2 + 0] = s;
-        red[(wm * BN + c) * 2 + 1] = q;
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += 256) {
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s += red[(w * BN + c) * 2 + 0];
-        q += red[(w * BN + c) * 2 + 1];
-      }
-      if (n0 + c < g.Ncols) {
-        stats[((long long)blockIdx.x * 2 + 0) * g.Ncols + n0 + c] = s;
-        stats[((long long)blockIdx.x * 2 + 1) * g.Ncols + n0 + c] = q;
-      }
-    }
-    __syncthreads();
-  }
-
-  // ---------------- epilogue 2: fp32 tile -> LDS -> coalesced 16-B bf16 stores
-  constexpr int LDC = BN + 4;
-  float* cs = reinterpret_cast<float*>(smem);  // [BM][LDC] fp32 (BM*LDC*4 <= LDS budget)
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        const int col = wn * TN + j * 16 + (lane & 15);
-        cs[row * LDC + col] = acc[i][j][r];
-      }
-  __syncthreads();
-  constexpr int CPR = BN / 8;  // 8-wide chunks per row
-  for (int e = tid; e < BM * CPR; e += 256) {
-    const int row = e / CPR, cc = e % CPR;
-    const long long m = m0 + row;
-    const int col = n0 + cc * 8;
-    if (m >= g.M || col >= g.Ncols) continue;
-    const int x = (int)(m % g.Wg);
-    const long long t = m / g.Wg;
-    const int y = (int)(t % g.Hg);
-    const int n = (int)(t / g.Hg);
-    const long long o =
-        (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
-    const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
-    const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
-    float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    if (ADD) {
-      const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
-      const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
-      }
-    }
-    *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                                  pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
-  }
-}
-
-// ------------------------------------------------------------------ forward / dgrad
-template <int BM, int BN, int WM, int WN, bool BUF>
-__global__ void __launch_bounds__(256, 2) igemm_fwd_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
-    const bf16_t* ADD /* may alias Y (in-place accumulate) */, float* __restrict__ stats,
-    ConvGeom g, unsigned xbytes, unsigned wbytes) {
-  constexpr int BK = 64;
-  constexpr int TM = BM / WM, TN = BN / WN;     // wave tile
-  constexpr int RM = TM / 16, RN = TN / 16;     // MFMA blocks per wave
-  constexpr int AR = BM / 32, BR = BN / 32;     // rows per thread to stage (8 chunks per row)
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                 // [2][BM][BK]
-  bf16_t* Bs = As + 2 * BM * BK;                                 // [2][BN][BK]
-  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);        // [MAXTAPS] {dy, dx, wcol, 0}
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int ntaps = g.nth * g.ntw;
-  if (tid < ntaps) {
-    const int th = tid / g.ntw, tw = tid % g.ntw;
-    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs,
-                          ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C, 0);
-  }
-  // rows this thread stages: r = tid/8 + 32*i, chunk = tid%8
-  const int chunk = tid & 7;
-  int a_iy[AR], a_ix[AR];
-  long long a_nb[AR];
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const long long m = m0 + (tid >> 3) + 32 * i;
-    if (m < g.M) {
-      const int x = (int)(m % g.Wg);
-      const long long t = m / g.Wg;
-      const int y = (int)(t % g.Hg);
-      const int n = (int)(t / g.Hg);
-      a_iy[i] = y * g.isy;
-      a_ix[i] = x * g.isx;
-      a_nb[i] = (long long)n * g.H * g.W;
-    } else {
-      a_iy[i] = -(1 << 28);  // never in range
-      a_ix[i] = 0;
-      a_nb[i] = 0;
-    }
-  }
-  __syncthreads();
-
-  uint4 ra[AR], rb[BR];
-  const int nk = (g.K + BK - 1) / BK;
-
-  // BUF: branch-free buffer loads (32-bit offsets; out-of-range chunks read as zero
-  // through the descriptor's range check) instead of predicated 64-bit global loads
-  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
-  const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
-  unsigned b_off[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int n = n0 + (tid >> 3) + 32 * i;
-    b_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : 0x80000000u;
-  }
-  auto load = [&](int kt) {
-    const int kc = kt * (BK / 8) + chunk;           // global 8-element chunk index
-    const int tap = kc >> g.lgC8;
-    const int c0 = (kc & ((1 << g.lgC8) - 1)) * 8;
-    const bool kval = tap < ntaps;
-    int4 tp = make_int4(0, 0, 0, 0);
-    if (kval) tp = taps[tap];
-    if constexpr (BUF) {
-#pragma unroll
-      for (int i = 0; i < AR; ++i) {
-        const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
-        const bool ok = kval && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
-        const unsigned off =
-            ok ? (((unsigned)a_nb[i] + (unsigned)(iy * g.W + ix)) * (unsigned)g.C + (unsigned)c0) * 2u
-               : 0x80000000u;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
-        ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
-      }
-#pragma unroll
-      for (int i = 0; i < BR; ++i) {
-        const unsigned off = (kval && b_off[i] != 0x80000000u)
-                                 ? b_off[i] + (unsigned)(tp.z + c0) * 2u : 0x80000000u;
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0);
-        rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
-      }
-      return;
-    }
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kval && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-        v = *reinterpret_cast<const uint4*>(X + ((a_nb[i] + (long long)iy * g.W + ix) * g.C + c0));
-      ra[i] = v;
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int n = n0 + (tid >> 3) + 32 * i;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (kval && n < g.Ncols)
-        v = *reinterpret_cast<const uint4*>(Wp + (long long)n * g.wK + tp.z + c0);
-      rb[i] = v;
-    }
-  };
-  auto store = [&](int buf) {
-    bf16_t* as = As + buf * BM * BK;
-    bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[i];
-    }
-  };
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  load(0);
-  store(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load(kt + 1);
-    const bf16_t* as = As + buf * BM * BK;
-    const bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[RM], bfr[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int r = wm * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int r = wn * TN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) store(buf ^ 1);
-    __syncthreads();
-  }
-
-  igemm_epilogue<BM, BN, WM, WN>(acc, smem, Y, ADD, stats, g, m0, n0);
-}
 
 // ------------------------------------------------------------------ forward / dgrad, v3
 // Register-staged buffer loads (as igemm_fwd_kernel<...,BUF=true>) with
@@ -315,7 +62,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
   constexpr int NT = WM * WN * 64, RPP = NT / 8;   // threads, staged rows per pass
   constexpr int AR = BM / RPP, BR = BN / RPP;
   static_assert(AR * RPP == BM && BR * RPP == BN, "tile rows must be a multiple of NT/8");
-  static_assert(DEPTH != 3 || (MF32 && AR <= 4 && BR <= 4), "interleaved stores: 4 substeps");
+  static_assert(DEPTH == 1 || DEPTH == 2, "register prefetch depth");
   constexpr unsigned OOB = 0x80000000u;
   typedef typename std::conditional<MF32, f32x16, f32x4>::type accT;
   constexpr int NR = MF32 ? 16 : 4;
@@ -409,68 +156,6 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     }
   };
 
-  // DEPTH == 0: LDS-DMA loader (buffer_load ... lds): no VGPR staging and no ds_write.
-  // Wave-instruction i of wave wid fills rows (i*NW + wid)*8 + lane/8, physical 16-B slot
-  // lane%8 (the LDS destination is lane-linear), so the swizzle is applied to the SOURCE:
-  // the lane fetches logical chunk slot ^ ((row >> 1) & 7).
-  constexpr int NW = WM * WN;
-  constexpr int DAR = DEPTH == 0 ? BM / (NW * 8) : 1, DBR = DEPTH == 0 ? BN / (NW * 8) : 1;
-  int d_y[DAR], d_x[DAR], d_lc[DAR], db_lc[DBR];
-  unsigned d_pix[DAR], db_off[DBR];
-  if constexpr (DEPTH == 0) {
-#pragma unroll
-    for (int i = 0; i < DAR; ++i) {
-      const int r = (i * NW + wid) * 8 + (lane >> 3);
-      d_lc[i] = (lane & 7) ^ ((r >> 1) & 7);
-      const long long m = m0 + r;
-      if (m < g.M) {
-        const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
-        const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
-        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
-        const int y = (int)(t - n * (unsigned)g.Hg);
-        d_y[i] = y * g.isy;
-        d_x[i] = x * g.isx;
-        d_pix[i] = (n * (unsigned)g.H + (unsigned)d_y[i]) * (unsigned)g.W + (unsigned)d_x[i];
-      } else {
-        d_y[i] = -(1 << 28);
-        d_x[i] = 0;
-        d_pix[i] = 0;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < DBR; ++i) {
-      const int r = (i * NW + wid) * 8 + (lane >> 3);
-      db_lc[i] = (lane & 7) ^ ((r >> 1) & 7);
-      const int n = n0 + r;
-      db_off[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
-    }
-  }
-  auto issue = [&](int kt, int buf) {
-    bf16_t* as = As + buf * BM * BK;
-    bf16_t* bs = Bs + buf * BN * BK;
-    const int cmask = (1 << g.lgC8) - 1;
-#pragma unroll
-    for (int i = 0; i < DAR; ++i) {
-      const int kc = kt * (BK / 8) + d_lc[i];
-      const int tap = kc >> g.lgC8;
-      const int4 tp = taps[tap < MAXTAPS ? tap : MAXTAPS - 1];
-      const bool ok = tap < ntaps && (unsigned)(d_y[i] + tp.x) < (unsigned)g.H &&
-                      (unsigned)(d_x[i] + tp.y) < (unsigned)g.W;
-      const unsigned off = ok ? (d_pix[i] + (unsigned)tp.w) * C2 + (unsigned)((kc & cmask) * 16) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsx, (__attribute__((address_space(3))) void*)(as + (i * NW + wid) * 8 * BK), 16, off, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < DBR; ++i) {
-      const int kc = kt * (BK / 8) + db_lc[i];
-      const int tap = kc >> g.lgC8;
-      const int4 tp = taps[tap < MAXTAPS ? tap : MAXTAPS - 1];
-      const unsigned off = (tap < ntaps && db_off[i] != OOB)
-                               ? db_off[i] + (unsigned)tp.z * 2u + (unsigned)((kc & cmask) * 16) : OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsw, (__attribute__((address_space(3))) void*)(bs + (i * NW + wid) * 8 * BK), 16, off, 0, 0, 0);
-    }
-  };
 
   accT acc[RM][RN];
 #pragma unroll
@@ -540,68 +225,15 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
       }
   };
   auto nopost = [](int) {};
-  // part p of a tile's LDS stores: A rows i and B rows i with i % 4 == p
-  auto store_part = [&](int buf, auto S, int part) {
-    bf16_t* as = As + buf * BM * BK;
-    bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      if (i % 4 != part) continue;
-      const int r = (tid >> 3) + RPP * i;
-      *reinterpret_cast<uint4*>(as + r * BK + swz(r, chunk) * 8) = ra[S][i];
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      if (i % 4 != part) continue;
-      const int r = (tid >> 3) + RPP * i;
-      *reinterpret_cast<uint4*>(bs + r * BK + swz(r, chunk) * 8) = rb[S][i];
-    }
-  };
-  if constexpr (DEPTH == 0) {
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int buf = kt & 1;
-      if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-      compute(buf, nopost);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-  } else if constexpr (DEPTH <= 1) {
-    // DEPTH < 0: measurement-only ablations (wrong results): bit 0 drops the in-loop global
-    // loads, bit 1 the LDS stores, bit 2 the barrier (tools/bench_conv.py --cfgs 30..33)
-    constexpr int ABL = DEPTH < 0 ? -DEPTH : 0;
+  if constexpr (DEPTH == 1) {
     load(0, S0{});
     store(0, S0{});
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      if (!(ABL & 1) && kt + 1 < nk) load(kt + 1, S0{});
+      if (kt + 1 < nk) load(kt + 1, S0{});
       compute(buf, nopost);
-      if (!(ABL & 2) && kt + 1 < nk) store(buf ^ 1, S0{});
-      if (!(ABL & 4)) __syncthreads();
-    }
-  } else if constexpr (DEPTH == 3) {
-    // register sets as DEPTH 2, but tile kt+1's LDS stores are spread over the MFMA
-    // substeps of tile kt (its loads landed an iteration ago), not bunched before the barrier
-    load(0, S0{});
-    if (nk > 1) load(1, S1{});
-    store(0, S0{});
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-      if (kt + 2 < nk) load(kt + 2, S0{});
-      const bool st1 = kt + 1 < nk;
-      compute(0, [&](int ks) {
-        if (st1) store_part(1, S1{}, ks);
-      });
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      if (kt + 3 < nk) load(kt + 3, S1{});
-      const bool st0 = kt + 2 < nk;
-      compute(1, [&](int ks) {
-        if (st0) store_part(0, S0{}, ks);
-      });
+      if (kt + 1 < nk) store(buf ^ 1, S0{});
       __syncthreads();
     }
   } else {
@@ -627,297 +259,9 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
                                            stats, g, Y, ADD, gs.bnb);
 }
 
-// ------------------------------------------------------------------ forward / dgrad, LDS-DMA
-// Same GEMM as igemm_fwd_kernel, but both operand tiles are staged with
-// buffer_load_dwordx4 ... lds (LDS-DMA: global -> LDS with no VGPR round trip).
-// Zero padding of the implicit im2col comes for free from the buffer range check:
-// an out-of-image (or K-tail) chunk gets a voffset beyond num_records and the
-// hardware returns zeros.  The LDS image is lane-linear per wave instruction
-// (8 rows x 128 B), so the chunk swizzle is applied to the SOURCE address.
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256, 2) igemm_fwd_dma_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
-    const bf16_t* ADD, float* __restrict__ stats, ConvGeom g, unsigned xbytes,
-    unsigned wbytes) {
-  constexpr int BK = 64;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int RM = TM / 16, RN = TN / 16;
-  constexpr int AR = BM / 32, BR = BN / 32;     // wave-instructions per wave per tile
-  constexpr unsigned OOB = 0x80000000u;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);                 // [2][BM][BK]
-  bf16_t* Bs = As + 2 * BM * BK;                                 // [2][BN][BK]
-  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * BK);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const long long m0 = (long long)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
-  const int ntaps = g.nth * g.ntw;
-  if (tid < ntaps) {
-    const int th = tid / g.ntw, tw = tid % g.ntw;
-    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs,
-                          ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C, 0);
-  }
-  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
-  const auto rsw = __builtin_amdgcn_make_buffer_rsrc((void*)Wp, (short)0, (int)wbytes, 0x00020000);
-  const int pc = lane & 7;                       // physical 16-B chunk this lane fills
-  int a_iy[AR], a_ix[AR], a_lc[AR];
-  unsigned a_nb[AR];                             // (n*H*W) pixel base
-#pragma unroll
-  for (int i = 0; i < AR; ++i) {
-    const int r = (i * 4 + wid) * 8 + (lane >> 3);
-    a_lc[i] = pc ^ ((r >> 1) & 7);
-    const long long m = m0 + r;
-    if (m < g.M) {
-      const int x = (int)(m % g.Wg);
-      const long long t = m / g.Wg;
-      const int y = (int)(t % g.Hg);
-      const int n = (int)(t / g.Hg);
-      a_iy[i] = y * g.isy;
-      a_ix[i] = x * g.isx;
-      a_nb[i] = (unsigned)n * (unsigned)(g.H * g.W);
-    } else {
-      a_iy[i] = -(1 << 28);
-      a_ix[i] = 0;
-      a_nb[i] = 0;
-    }
-  }
-  int b_lc[BR];
-  unsigned b_row[BR];
-#pragma unroll
-  for (int i = 0; i < BR; ++i) {
-    const int r = (i * 4 + wid) * 8 + (lane >> 3);
-    b_lc[i] = pc ^ ((r >> 1) & 7);
-    const int n = n0 + r;
-    b_row[i] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u : OOB;
-  }
-  __syncthreads();
-  const int nk = (g.K + BK - 1) / BK;
-  const int cmask = (1 << g.lgC8) - 1;
-
-  auto issue = [&](int kt, int buf) {
-    bf16_t* as = As + buf * BM * BK;
-    bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int kc = kt * 8 + a_lc[i];
-      const int tap = kc >> g.lgC8;
-      unsigned off = OOB;
-      if (tap < ntaps) {
-        const int4 tp = taps[tap];
-        const int iy = a_iy[i] + tp.x, ix = a_ix[i] + tp.y;
-        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-          off = ((a_nb[i] + (unsigned)(iy * g.W + ix)) * (unsigned)g.C + (unsigned)((kc & cmask) * 8)) * 2u;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsx, (__attribute__((address_space(3))) void*)(as + (i * 4 + wid) * 8 * BK), 16, off, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int kc = kt * 8 + b_lc[i];
-      const int tap = kc >> g.lgC8;
-      unsigned off = OOB;
-      if (tap < ntaps && b_row[i] != OOB)
-        off = b_row[i] + (unsigned)(taps[tap].z + (kc & cmask) * 8) * 2u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rsw, (__attribute__((address_space(3))) void*)(bs + (i * 4 + wid) * 8 * BK), 16, off, 0, 0, 0);
-    }
-  };
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, buf ^ 1);
-    const bf16_t* as = As + buf * BM * BK;
-    const bf16_t* bs = Bs + buf * BN * BK;
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      const int ch = ks * 4 + (lane >> 4);
-      bf16x8 af[RM], bfr[RN];
-#pragma unroll
-      for (int i = 0; i < RM; ++i) {
-        const int r = wm * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(as + r * BK + swz(r, ch) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const int r = wn * TN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bs + r * BK + swz(r, ch) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  igemm_epilogue<BM, BN, WM, WN>(acc, smem, Y, ADD, stats, g, m0, n0);
-}
-
 // ------------------------------------------------------------------ weight gradient
 // grid: (ceil(Ncols/BM), ceil(K/BN), S).  Block reduces m in [s*mchunk, min(M,(s+1)*mchunk)).
 // A = dY (rows m, cols co), B = im2col(X) (rows m, cols k); LDS images [m][cols+PAD].
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(256, 2) igemm_wgrad_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
-    ConvGeom g, long long mchunk) {
-  constexpr int BKM = 32;                  // m rows per K-step (one MFMA k=32)
-  constexpr int PAD = 16;                  // row stride ≡ 32 B (mod 256 B): tr reads conflict-free
-  constexpr int LA = BM + PAD, LB = BN + PAD;
-  constexpr int TM = BM / WM, TN = BN / WN;
-  constexpr int RM = TM / 16, RN = TN / 16;
-  constexpr int ACH = BM / 8, BCH = BN / 8;               // 16-B chunks per row
-  constexpr int AIT = (BKM * ACH + 255) / 256, BIT = (BKM * BCH + 255) / 256;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);           // [2][BKM][LA]
-  bf16_t* Bs = As + 2 * BKM * LA;                         // [2][BKM][LB]
-  int4* taps = reinterpret_cast<int4*>(Bs + 2 * BKM * LB);
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
-  const int co0 = blockIdx.x * BM, k0 = blockIdx.y * BN;
-  const long long mb = (long long)blockIdx.z * mchunk;
-  const long long me = min(g.M, mb + mchunk);
-  const int ntaps = g.nth * g.ntw;
-  if (tid < ntaps) {
-    const int th = tid / g.ntw, tw = tid % g.ntw;
-    taps[tid] = make_int4(g.dy0 + th * g.dys, g.dx0 + tw * g.dxs, 0, 0);
-  }
-  __syncthreads();
-
-  uint4 ra[AIT], rb[BIT];
-  auto load = [&](long long mt) {
-#pragma unroll
-    for (int it = 0; it < AIT; ++it) {
-      const int e = tid + it * 256;
-      const int r = e / ACH, c = e % ACH;
-      const long long m = mt + r;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < BKM * ACH && m < me && co0 + c * 8 < g.Ncols)
-        v = *reinterpret_cast<const uint4*>(DY + m * g.Ncols + co0 + c * 8);
-      ra[it] = v;
-    }
-#pragma unroll
-    for (int it = 0; it < BIT; ++it) {
-      const int e = tid + it * 256;
-      const int r = e / BCH, c = e % BCH;
-      const long long m = mt + r;
-      const int kc = (k0 >> 3) + c;
-      const int tap = kc >> g.lgC8;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < BKM * BCH && m < me && tap < ntaps) {
-        const int c0 = (kc & ((1 << g.lgC8) - 1)) * 8;
-        const int x = (int)(m % g.Wg);
-        const long long t = m / g.Wg;
-        const int y = (int)(t % g.Hg);
-        const int n = (int)(t / g.Hg);
-        const int4 tp = taps[tap];
-        const int iy = y * g.isy + tp.x, ix = x * g.isx + tp.y;
-        if ((unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-          v = *reinterpret_cast<const uint4*>(
-              X + (((long long)n * g.H + iy) * g.W + ix) * g.C + c0);
-      }
-      rb[it] = v;
-    }
-  };
-  auto store = [&](int buf) {
-    bf16_t* as = As + buf * BKM * LA;
-    bf16_t* bs = Bs + buf * BKM * LB;
-#pragma unroll
-    for (int it = 0; it < AIT; ++it) {
-      const int e = tid + it * 256;
-      if (e < BKM * ACH) {
-        const int r = e / ACH, c = e % ACH;
-        *reinterpret_cast<uint4*>(as + r * LA + c * 8) = ra[it];
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < BIT; ++it) {
-      const int e = tid + it * 256;
-      if (e < BKM * BCH) {
-        const int r = e / BCH, c = e % BCH;
-        *reinterpret_cast<uint4*>(bs + r * LB + c * 8) = rb[it];
-      }
-    }
-  };
-
-  f32x4 acc[RM][RN];
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // transpose-read addressing: lane = 16*grp + 4*q + p ; block rows grp*4 + q (+16),
-  // columns col0 + 4p.  Element e<4 of the fragment = m-row 4*grp+e, e>=4: 16+4*grp+e-4
-  // (a k-permutation applied identically to A and B, so the MFMA sum is unchanged).
-  const int grp = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int nsteps = (int)((me - mb + BKM - 1) / BKM);
-  if (nsteps > 0) {
-    load(mb);
-    store(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nsteps) load(mb + (long long)(st + 1) * BKM);
-    const bf16_t* as = As + buf * BKM * LA;
-    const bf16_t* bs = Bs + buf * BKM * LB;
-    bf16x8 af[RM], bfr[RN];
-#pragma unroll
-    for (int i = 0; i < RM; ++i) {
-      const int col = wm * TM + i * 16 + 4 * p;
-      typedef short s4 __attribute__((ext_vector_type(4)));
-      const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4*)(as + (grp * 4 + q) * LA + col));
-      const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4*)(as + (16 + grp * 4 + q) * LA + col));
-      af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int j = 0; j < RN; ++j) {
-      const int col = wn * TN + j * 16 + 4 * p;
-      typedef short s4 __attribute__((ext_vector_type(4)));
-      const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4*)(bs + (grp * 4 + q) * LB + col));
-      const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-          (__attribute__((address_space(3))) s4*)(bs + (16 + grp * 4 + q) * LB + col));
-      bfr[j] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int i = 0; i < RM; ++i)
-#pragma unroll
-      for (int j = 0; j < RN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (st + 1 < nsteps) store(buf ^ 1);
-    __syncthreads();
-  }
-  // slab[s][co][k] (row length K, fp32)
-  float* out = slab + (long long)blockIdx.z * g.Ncols * g.K;
-#pragma unroll
-  for (int i = 0; i < RM; ++i)
-#pragma unroll
-    for (int j = 0; j < RN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        const int k = k0 + wn * TN + j * 16 + (lane & 15);
-        if (co < g.Ncols && k < g.K) out[(long long)co * g.K + k] = acc[i][j][r];
-      }
-}
-
-
 // Weight gradient, v2: 64 m-rows per barrier (two MFMA k-steps), branch-free buffer
 // loads with range-check zero fill, magic-number row decomposition.
 template <int BM, int BN, int WM, int WN>
@@ -1106,44 +450,8 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
 
 // ------------------------------------------------------------------ weight packing
 // fp32 OIHW -> bf16 [Cout][KH][KW][Cpad] (forward) and optionally
-// bf16 [Cin][KH][KW][Cout] (dgrad; transpose only — the flip is in the tap offsets).
-// Tiled through LDS so every global access is a contiguous run: a block owns TC output
-// x 32 input channels x all T taps; reads OIHW rows (32 ci x T floats), writes wf rows
-// (32 ci) and wd rows (TC co).  grid (ceil(Cpad/32), ceil(Cout/TC)), 256 threads,
-// LDS TC x T x 33 floats.  T is a template constant so the index math is shifts/mults.
-template <int T, int TC>
-__global__ void __launch_bounds__(256) pack_weights_kernel(const float* __restrict__ w,
-                                                           bf16_t* __restrict__ wf,
-                                                           bf16_t* __restrict__ wd, int Cout,
-                                                           int Cin, int Cpad) {
-  __shared__ float tile[TC * T * 33];  // [TC co][T][33 ci]  (pitch 33: no bank conflicts)
-  const int ci0 = blockIdx.x * 32, co0 = blockIdx.y * TC;
-  for (int e = threadIdx.x; e < TC * 32 * T; e += 256) {
-    const int co = e / (32 * T), r = e % (32 * T);
-    const int ci = r / T, t = r % T;
-    float v = 0.f;
-    if (co0 + co < Cout && ci0 + ci < Cin) v = w[((long long)(co0 + co) * Cin + ci0 + ci) * T + t];
-    tile[(co * T + t) * 33 + ci] = v;
-  }
-  __syncthreads();
-  // wf[co][t][ci] (ci fastest, padded channels written as zeros)
-  for (int e = threadIdx.x; e < TC * T * 32; e += 256) {
-    const int ci = e % 32, r = e / 32;
-    const int t = r % T, co = r / T;
-    if (co0 + co < Cout && ci0 + ci < Cpad)
-      wf[((long long)(co0 + co) * T + t) * Cpad + ci0 + ci] = f2bf(tile[(co * T + t) * 33 + ci]);
-  }
-  if (!wd) return;
-  // wd[ci][t][co] (co fastest)
-  for (int e = threadIdx.x; e < TC * T * 32; e += 256) {
-    const int co = e % TC, r = e / TC;
-    const int t = r % T, ci = r / T;
-    if (co0 + co < Cout && ci0 + ci < Cin)
-      wd[((long long)(ci0 + ci) * T + t) * Cout + co0 + co] = f2bf(tile[(co * T + t) * 33 + ci]);
-  }
-}
-
-// any other tap count: one element per thread
+// bf16 [Cin][KH][KW][Cout] (dgrad; transpose only — the flip is in the tap offsets),
+// one element per thread
 __global__ void __launch_bounds__(256) pack_weights_any_kernel(const float* __restrict__ w,
                                                                bf16_t* __restrict__ wf,
                                                                bf16_t* __restrict__ wd, int Cout,
@@ -1381,34 +689,6 @@ static size_t fwd_smem(int BM, int BN) {
   return main > epi ? main : epi;
 }
 
-
-template <int BM, int BN, int WM, int WN>
-static void launch_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                       float* stats, const ConvGeom& g, bool dma, bool buf, bool v3, bool mf32,
-                       hipStream_t st, const BnBwdEpi* bnb = nullptr) {
-  const size_t sm = fwd_smem(BM, BN);
-  dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
-  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
-  const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  if (dma) {
-    auto k = igemm_fwd_dma_kernel<BM, BN, WM, WN>;
-    set_smem_attr(k, sm);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
-  } else if (v3) {
-    auto k = mf32 ? igemm_fwd3_kernel<BM, BN, WM, WN, true, 1> : igemm_fwd3_kernel<BM, BN, WM, WN, false, 1>;
-    set_smem_attr(k, sm);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g, bnb), xb, wb);
-  } else if (buf) {
-    auto k = igemm_fwd_kernel<BM, BN, WM, WN, true>;
-    set_smem_attr(k, sm);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
-  } else {
-    auto k = igemm_fwd_kernel<BM, BN, WM, WN, false>;
-    set_smem_attr(k, sm);
-    k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb);
-  }
-}
-
 template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
 static void launch_fwd3_set(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
                             float* stats, const ConvGeomSet& gs, int ng, hipStream_t st) {
@@ -1446,107 +726,66 @@ bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
   }
 }
 
-// halo-kernel configs (conv_halo.hip): 20/21 128-pixel 4 waves, 24/25 128-pixel 8 waves,
-// 36/37 256-pixel 2x2 waves, 38/39 256-pixel 4x2 waves; even = BN 128, odd = BN 64
-// 41 256-pixel 4x1 waves of 64 x 64 (BN 64 only); 42 / 43 = 20 / 38 with two weight tiles
-// of register prefetch (waves bit 8)
+// halo-kernel configs (conv_halo.hip): 20 / 21 = 128-pixel tile of 2 x 2 waves, BN 128 / 64;
+// 42 = 20 with two weight tiles of register prefetch (waves bit 8); 39 = 256-pixel tile of
+// 4 x 2 waves, BN 64; 41 = 256-pixel tile of 4 x 1 waves of 64 x 64
 int igemm_fwd_rowtile(int cfg);
 bool halo_cfg(int cfg, int& bn, int& waves) {
-  if (cfg == 42 || cfg == 43) {
-    bn = 128;
-    waves = (cfg == 42 ? 4 : 16) | 0x100;
-    return true;
+  switch (cfg) {
+    case 20: bn = 128; waves = 4; return true;
+    case 21: bn = 64; waves = 4; return true;
+    case 42: bn = 128; waves = 4 | 0x100; return true;
+    case 39: bn = 64; waves = 16; return true;
+    case 41: bn = 64; waves = 32; return true;
+    default: return false;
   }
-  if (cfg == 44 || cfg == 45) {  // 41 / 39 with two weight tiles of register prefetch
-    bn = 64;
-    waves = (cfg == 44 ? 32 : 16) | 0x100;
-    return true;
-  }
-  if (!(cfg == 20 || cfg == 21 || cfg == 24 || cfg == 25 || (cfg >= 36 && cfg <= 39) || cfg == 41))
-    return false;
-  bn = (cfg == 20 || cfg == 24 || cfg == 36 || cfg == 38) ? 128 : 64;
-  waves = cfg == 41 ? 32 : cfg >= 38 ? 16 : cfg >= 36 ? 2 : cfg >= 24 ? 8 : 4;
-  return true;
 }
 
+// Forward-style conv GEMM (forward, stride-1 dgrad, one dgrad parity class), by cfg:
+//   9 / 10 / 11  v3 tiles 128x128 / 128x64 / 64x64 (2 x 2 waves) on 16x16x32 MFMA
+//   12 / 13 / 14 the same on 32x32x16 MFMA (64x64 as 16x16x32: 14 == 11)
+//   15 / 16 / 17 12 / 13 / 11 with two tiles of register prefetch
+//   20 / 21 / 42 / 39 / 41  halo-staged unit-stride tiles (conv_halo.hip, see halo_cfg)
+//   60           space-to-depth stem kernel (conv_stem.hip)
+//   90 - 93      pipelined LDS-DMA tiles (conv_pipe.hip)
+// Shapes a specialised kernel does not cover fall back to a v3 tile with the same row tile,
+// so the statistics slab rows (igemm_fwd_rowtile) still match.
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb) {
-  // bnb (BN-backward sums in the epilogue) is supported by the v3 (fwd3) and halo kernels
-  if (bnb && cfg < 9) throw std::runtime_error("igemm_fwd: BN-backward epilogue needs cfg >= 9");
-  // v3 with two tiles of register prefetch: 15 = 128x128 mf32, 16 = 128x64 mf32, 17 = 64x64
-  // 16x16; 18 = 8-wave 256x128 mf32 (measured slower: one workgroup per CU)
-  // 20 / 21: halo-staged unit-stride kernel (conv_halo.hip), BN 128 / 64, 4 waves;
-  // 24 / 25: the same with 8 waves; shapes it does not cover fall back to v3 tiles 12 / 13
-  // 36 / 37: 256-pixel halo tile (2 x 2 waves of 128 x BN/2), BN 128 / 64
-  // 38 / 39: 256-pixel halo tile with 4 x 2 waves of 64 x BN/2, BN 128 / 64
-  if (cfg >= 90 && cfg <= 93) {  // pipelined LDS-DMA tiles (conv_pipe.hip), 256-row tile
+  if (cfg >= 90 && cfg <= 93) {
     if (!bnb && conv_pipe_supported(g, cfg)) return conv_pipe(X, Wp, Y, ADD, stats, g, cfg, st);
     if (g.Ncols % 128 == 0) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
     return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
   }
-  if (cfg == 70) {  // persistent resident-weight 64->64 kernel; fallback: same 256-row tile
-    if (!bnb && conv_l1_supported(g)) return conv_l1(X, Wp, Y, ADD, stats, g, st);
-    cfg = 39;
-  }
-  if (cfg == 60) {  // s2d stem kernel; fallback keeps its 256-row tile (stats rows)
+  if (cfg == 60) {
     if (!bnb && !ADD && stem_conv_supported(g)) return stem_conv(X, Wp, Y, stats, g, st);
     return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  }
-  if (cfg == 50 || cfg == 51) {
-    if (conv_h5_supported(g, cfg)) return conv_h5(X, Wp, Y, ADD, stats, g, cfg, st, nullptr, nullptr, bnb);
-    // 50 falls back to the register-staged halo tile with the same 256-row tile (41), so
-    // the stats slab rows (igemm_fwd_rowtile) still match; 51 has no 512-row fallback
-    if (cfg == 51) throw std::runtime_error("igemm_fwd: cfg 51 needs a single-chunk 3x3/s1 shape");
-    cfg = 41;
   }
   int bn, waves;
   if (halo_cfg(cfg, bn, waves)) {
     if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st, nullptr, nullptr, bnb);
-    // fallback keeps the row tile (stats slab rows = igemm_fwd_rowtile(cfg))
     if (igemm_fwd_rowtile(cfg) == 256) {
       if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
       return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
     }
     cfg = bn == 128 ? 12 : 13;
   }
-  if (cfg == 15) return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 16) return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 17) return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 18) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  // 8-wave 128-row tiles (4 waves per SIMD at 2 workgroups per CU): 19 = 128x128 as 4x2
-  // waves of 32x64, 22 = 128x128 as 2x4 waves of 64x32, 23 = 128x64 as 4x2 waves of 32x32
-  if (cfg == 19) return launch_fwd3<128, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  // 34 / 35: v3 with the next tile's LDS stores interleaved into the MFMA substeps
-  if (cfg == 34) return launch_fwd3<128, 128, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 35) return launch_fwd3<128, 64, 2, 2, true, 3>(X, Wp, Y, ADD, stats, g, st, bnb);
-  // 26 / 27 / 28: v3 with the LDS-DMA loader, tiles 128x128 / 128x64 mf32, 64x64 16x16
-  if (cfg == 26) return launch_fwd3<128, 128, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 27) return launch_fwd3<128, 64, 2, 2, true, 0>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 28) return launch_fwd3<64, 64, 2, 2, false, 0>(X, Wp, Y, ADD, stats, g, st, bnb);
-  // 30-33: ablations of tile 12 for measurement only (results are wrong)
-  if (cfg == 30) return launch_fwd3<128, 128, 2, 2, true, -1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 31) return launch_fwd3<128, 128, 2, 2, true, -2>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 32) return launch_fwd3<128, 128, 2, 2, true, -3>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 33) return launch_fwd3<128, 128, 2, 2, true, -7>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 22) return launch_fwd3<128, 128, 2, 4, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  if (cfg == 23) return launch_fwd3<128, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  // cfg % 3: 0 = 128x128 (2x2 waves, 64x64 per wave), 1 = 128x64, 2 = 64x64
-  // cfg / 3: 0 = register-staged global loads, 1 = LDS-DMA (buffer_load ... lds),
-  //          2 = register-staged buffer loads (branch-free zero fill)
-  //          3 = v3 (cheaper addressing) on 16x16x32 MFMA, 4 = v3 on 32x32x16 MFMA
-  const int ld = cfg / 3;
-  const bool dma = ld == 1, buf = ld == 2, v3 = ld >= 3, mf32 = ld == 4;
-  switch (cfg % 3) {
-    case 0: launch_fwd<128, 128, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st, bnb); break;
-    case 1: launch_fwd<128, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st, bnb); break;
-    default: launch_fwd<64, 64, 2, 2>(X, Wp, Y, ADD, stats, g, dma, buf, v3, mf32, st, bnb); break;
+  switch (cfg) {
+    case 9: return launch_fwd3<128, 128, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 10: return launch_fwd3<128, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 11: case 14: return launch_fwd3<64, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 12: return launch_fwd3<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 13: return launch_fwd3<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 15: return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 16: return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 17: return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+    default: throw std::runtime_error("igemm_fwd: unknown cfg " + std::to_string(cfg));
   }
 }
 
-int igemm_fwd_rowtile(int cfg) { if (cfg >= 90 && cfg <= 93) return 256; if (cfg == 50 || cfg == 51) return conv_h5_rowtile(cfg); if (cfg == 60 || cfg == 70) return 256; return ((cfg >= 36 && cfg <= 39) || cfg == 41 || cfg == 43 || cfg == 44 || cfg == 45) ? 256 : cfg == 28 ? 64 : cfg >= 19 ? 128 : cfg == 18 ? 256 : cfg % 3 == 2 ? 64 : 128; }
-
-static size_t wgrad_smem(int BM, int BN) {
-  return (size_t)2 * 32 * ((BM + 16) + (BN + 16)) * 2 + MAXTAPS * 16;
+int igemm_fwd_rowtile(int cfg) {
+  if ((cfg >= 90 && cfg <= 93) || cfg == 60 || cfg == 39 || cfg == 41) return 256;
+  return (cfg == 11 || cfg == 14 || cfg == 17) ? 64 : 128;
 }
 
 void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
@@ -1554,18 +793,14 @@ void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom&
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
   // 4 / 5: halo-staged 3x3 unit-stride kernel (wgrad_halo.hip) with 9 / 3 taps per block;
-  // other shapes fall back to the v2 tiles
+  // other shapes fall back to the v2 tiles: 2 = 128x128, 3 = 64x128, 6 = 64x256
   if (cfg == 4 || cfg == 5) {
     if (wgrad_halo_supported(g)) return wgrad_halo(X, DY, slab, g, S, mchunk, cfg == 4 ? 3 : 1, st);
     cfg = g.Ncols % 128 == 0 ? 2 : 3;
   }
-  if (cfg == 0) {
-    dim3 grid((g.Ncols + 127) / 128, (g.K + 127) / 128, S);
-    igemm_wgrad_kernel<128, 128, 2, 2><<<grid, 256, wgrad_smem(128, 128), st>>>(X, DY, slab, g, mchunk);
-  } else if (cfg == 1) {
-    dim3 grid((g.Ncols + 63) / 64, (g.K + 127) / 128, S);
-    igemm_wgrad_kernel<64, 128, 2, 2><<<grid, 256, wgrad_smem(64, 128), st>>>(X, DY, slab, g, mchunk);
-  } else if (cfg == 2) {
+  if (cfg != 2 && cfg != 3 && cfg != 6)
+    throw std::runtime_error("igemm_wgrad: cfg must be 2, 3, 4, 5 or 6");
+  if (cfg == 2) {
     dim3 grid((g.Ncols + 127) / 128, (g.K + 127) / 128, S);
     auto k = igemm_wgrad2_kernel<128, 128, 2, 2>;
     const size_t sm = 2 * 64 * ((128 + 16) + (128 + 16)) * 2 + MAXTAPS * 16;

@@ -52,48 +52,6 @@ struct PreBN {
   }
 };
 
-// Fused BatchNorm-backward apply of a staged 16-B chunk (8 bf16 channels c0..c0+7):
-//     dy = a[c]·dz' + b[c]·y + cc[c],   dz' = dz masked by relu(y·sc[c] + sh[c]) > 0
-// (the exact terms of bn_bwd_apply_kernel<2>).  Lets the dgrad / weight-gradient kernels of a
-// conv read the upstream gradient dz and the conv's raw output y instead of a materialised
-// dy: the BN-backward apply pass (write dy, read it twice) disappears.  coef = [3][C] (a, b, cc).
-struct PreBnBwd {
-  float a[8], b[8], c[8], sc[8], sh[8];
-  __device__ __forceinline__ void load(const float* __restrict__ coef, const float* __restrict__ scale,
-                                       const float* __restrict__ shift, int C, int c0) {
-    auto ld8 = [](const float* p, float (&d)[8]) {
-      const float4 u = *reinterpret_cast<const float4*>(p);
-      const float4 v = *reinterpret_cast<const float4*>(p + 4);
-      d[0] = u.x; d[1] = u.y; d[2] = u.z; d[3] = u.w;
-      d[4] = v.x; d[5] = v.y; d[6] = v.z; d[7] = v.w;
-    };
-    ld8(coef + c0, a);
-    ld8(coef + C + c0, b);
-    ld8(coef + 2 * C + c0, c);
-    ld8(scale + c0, sc);
-    ld8(shift + c0, sh);
-  }
-  __device__ __forceinline__ uint4 apply(uint4 dz, uint4 y) const {
-    const uint32_t wd[4] = {dz.x, dz.y, dz.z, dz.w};
-    const uint32_t wy[4] = {y.x, y.y, y.z, y.w};
-    uint32_t o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float r[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int j = 2 * q + h;
-        const float yv = bf2f((bf16_t)(h ? wy[q] >> 16 : wy[q] & 0xffff));
-        float d = bf2f((bf16_t)(h ? wd[q] >> 16 : wd[q] & 0xffff));
-        d = (yv * sc[j] + sh[j]) > 0.f ? d : 0.f;
-        r[h] = a[j] * d + b[j] * yv + c[j];
-      }
-      o[q] = pack_bf2(r[0], r[1]);
-    }
-    return make_uint4(o[0], o[1], o[2], o[3]);
-  }
-};
-
 template <bool MF32>
 using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 
@@ -111,12 +69,9 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
                                                    unsigned char* smem, long long m0, int n0,
                                                    int stat_row, float* stats, const ConvGeom& g,
                                                    bf16_t* Y, const bf16_t* ADD,
-                                                   const BnBwdEpi& bnb = BnBwdEpi{},
-                                                   int diag = 0) {
-  // diag (timing diagnostics of the halo kernels, results wrong): bit 4 drops the global
-  // stores of the plain store phase, bit 5 the statistics
+                                                   const BnBwdEpi& bnb = BnBwdEpi{}) {
   const bool bwd = stats && bnb.y;
-  float* fstats = bwd || (diag & 32) ? nullptr : stats;  // forward Σy, Σy² of the fp32 tile
+  float* fstats = bwd ? nullptr : stats;  // forward Σy, Σy² of the fp32 tile
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = MF32 ? 32 : 16;
   constexpr int RM = TM / FM, RN = TN / FM;
@@ -252,10 +207,6 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
         if (!ok[k]) continue;
         float v[8];
         tile_vals((tid + i * NT) / CPR, av[k], v);
-        if (diag & 16) {
-          if (v[0] == 12345.f) Y[o[k]] = 0;  // keeps the staging reads live
-          continue;
-        }
         *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
                                                          pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
       }

@@ -74,16 +74,10 @@ void p2p_xgmi_recv(void* dst, long long bytes, const void* ring, const void* ful
 struct ConvGeom;
 struct ConvGeomSet;
 struct BnBwdEpi;
-struct BwdPre;
 bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb = nullptr);
-// conv_l1.hip: persistent resident-weight 64->64 3x3/s1 conv (cfg 70)
-bool conv_l1_supported(const ConvGeom& g);
-void conv_l1(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-             const ConvGeom& g, hipStream_t st, const float* pre_sc = nullptr,
-             const float* pre_sh = nullptr);
 // conv_stem.hip: s2d stem (16 channels, 16 taps, 64 outputs) with resident weights (cfg 60)
 bool stem_conv_supported(const ConvGeom& g);
 void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const ConvGeom& g,
@@ -101,12 +95,6 @@ int stem_wgrad_dy_blocks(int N, int H);
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st);
-// conv_h5.hip: LDS-DMA halo conv (cfg 50: 256 px x 128 ch, 51: 512 px x 64 ch single chunk)
-bool conv_h5_supported(const ConvGeom& g, int cfg);
-int conv_h5_rowtile(int cfg);
-void conv_h5(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-             const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
-             const float* pre_sh = nullptr, const BnBwdEpi* bnb = nullptr);
 // conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90-93: 256-pixel tiles)
 bool conv_pipe_supported(const ConvGeom& g, int cfg);
 bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
@@ -115,24 +103,15 @@ void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
                const float* pre_sh = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
-long long conv_halo41_stats_rows(long long M, int Ncols);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,
                const float* pre_sc = nullptr, const float* pre_sh = nullptr,
-               const BnBwdEpi* bnb = nullptr, const BwdPre* bpre = nullptr);
-// dgrad_s2.hip: stride-2 3x3 data gradient, all four parity classes per block (cfg 80)
-bool dgrad_s2_supported(const ConvGeomSet& set, int ng);
-void dgrad_s2(const bf16_t* dY, const bf16_t* Wd, bf16_t* dX, const bf16_t* ADD,
-              const ConvGeomSet& set, hipStream_t st);
-// conv_halo_pers.hip: persistent single-chunk (64 -> 64 channel) halo conv, cfg 39 shape
-bool conv_halo_pers_ok(const ConvGeom& g);
-void conv_halo_pers(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                    const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st);
+               const BnBwdEpi* bnb = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
-                const float* pre_sh = nullptr, const BwdPre* dpre = nullptr);
+                const float* pre_sh = nullptr);
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
                         hipStream_t st);
 void pack_weights_tiled(const long long* desc, const int* tprefix, int nl, int ntiles,
@@ -148,7 +127,7 @@ void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,
                        const float* beta, float* rmean, float* rvar, float momentum, float eps,
                        float* scale, float* shift, float* mean, float* invstd, float* work, long long* num_batches,
-                       hipStream_t st, unsigned* ctr = nullptr);
+                       hipStream_t st);
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
                     float eps, int C, float* scale, float* shift, hipStream_t st);
 void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
@@ -160,7 +139,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  const float* shift, const bf16_t* pdy, const uint8_t* pidx, int H, int W,
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
                  hipStream_t st, const float* pre_part = nullptr, int pre_rows = 0,
-                 const uint8_t* mask = nullptr, unsigned* ctr = nullptr);
+                 const uint8_t* mask = nullptr);
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
                      int P, hipStream_t st, bf16_t* yarg = nullptr);

@@ -50,24 +50,29 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     float* __restrict__ cslab, float* __restrict__ rowloss, float inv_b) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   __shared__ float xs[32 * 32];            // input with the conv1 zero padding (2)
-  __shared__ float w1[152], bb1[8], w2[2400], bb2[16];
+  __shared__ float w1[152], bb1[8], w2[2400], bb2[16], fw2[1200], fb2[16];
   __shared__ float p1[6 * 196];            // relu(conv1) max-pooled
-  __shared__ unsigned char k1[6 * 196];    // its 2x2 argmax (4 = no gradient)
+  __shared__ short pos1[6 * 196];          // xs offset of the window's argmax conv output
   __shared__ float p2[400];                // relu(conv2) max-pooled = h0 (flatten order)
-  __shared__ unsigned char k2[400];
-  __shared__ float h1[128], dl[16], dh1[128], g2[400], g1[6 * 196];
-  __shared__ float red[512];
+  __shared__ short pos2[400];              // p1 offset of the argmax conv2 output
+  __shared__ float h1[128], lg[16], dl[16], dh1[128], g2[400], g1[6 * 196];
+  __shared__ float dc2[16 * 18 * 18];      // unpooled conv2 gradient, 4-pixel zero border
+  __shared__ float4 red4[5 * 100];
+  float* red = reinterpret_cast<float*>(red4);
 
-  // ---- stage input and conv weights ----
+  // ---- stage input and the small weights (fc1's 192 KB stream from L2 instead) ----
   for (int i = tid; i < 1024; i += LT) {
     const int y = (i >> 5) - 2, x = (i & 31) - 2;
     xs[i] = ((unsigned)y < 28u && (unsigned)x < 28u) ? ldx<XT>(X + (long long)b * 784 + y * 28 + x)
                                                      : 0.f;
   }
   for (int i = tid; i < 2400; i += LT) w2[i] = c2w[i];
+  for (int i = tid; i < 1200; i += LT) fw2[i] = f2w[i];
+  for (int i = tid; i < 16 * 18 * 18; i += LT) dc2[i] = 0.f;
   if (tid < 150) w1[tid] = c1w[tid];
   if (tid < 6) bb1[tid] = c1b[tid];
   if (tid < 16) bb2[tid] = c2b[tid];
+  if (tid < 10) fb2[tid] = f2b[tid];
   __syncthreads();
 
   // ---- conv1 (1 -> 6, 5x5, pad 2) + bias + ReLU + 2x2 max-pool ----
@@ -79,7 +84,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
 #pragma unroll
       for (int j = 0; j < 6; ++j) win[i][j] = xs[(2 * py + i) * 32 + 2 * px + j];
     float best = 0.f;
-    int code = 4;
+    int code = -1;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int ay = a >> 1, ax = a & 1;
@@ -94,7 +99,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
       }
     }
     p1[q] = best;
-    k1[q] = (unsigned char)code;
+    pos1[q] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 32 + 2 * px + (code & 1));
   }
   __syncthreads();
 
@@ -120,7 +125,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
         }
     }
     float best = 0.f;
-    int code = 4;
+    int code = -1;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
       if (acc[a] > best) {
@@ -128,27 +133,42 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
         code = a;
       }
     p2[tid] = best;
-    k2[tid] = (unsigned char)code;
+    pos2[tid] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 14 + 2 * px + (code & 1));
   }
   __syncthreads();
 
-  // ---- fc1 (400 -> 120) + ReLU: 15 outputs per wave, lanes split K (coalesced rows) ----
-  for (int u = wid; u < 120; u += LT / 64) {
+  // ---- fc1 (400 -> 120) + ReLU: 4 threads per output, each 25 independent float4 loads of
+  //      its quarter row (all in flight together), combined by lane shuffles ----
+  if (tid < 480) {
+    const int u = tid >> 2, part = tid & 3;
+    const float4* wr = reinterpret_cast<const float4*>(f1w + u * 400) + part * 25;
+    const float4* hr = reinterpret_cast<const float4*>(p2) + part * 25;
+    float4 wv[25];
+#pragma unroll
+    for (int j = 0; j < 25; ++j) wv[j] = wr[j];
     float acc = 0.f;
-    for (int k = lane; k < 400; k += 64) acc += f1w[u * 400 + k] * p2[k];
-    acc = wave_sum(acc);
-    if (lane == 0) h1[u] = fmaxf(acc + f1b[u], 0.f);
+#pragma unroll
+    for (int j = 0; j < 25; ++j) {
+      const float4 h = hr[j];
+      acc += wv[j].x * h.x + wv[j].y * h.y + wv[j].z * h.z + wv[j].w * h.w;
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (part == 0) h1[u] = fmaxf(acc + f1b[u], 0.f);
   }
   __syncthreads();
 
-  // ---- fc2 (120 -> 10) + softmax cross-entropy (wave 0) ----
+  // ---- fc2 (120 -> 10) from LDS, one wave per output ----
+  for (int o = wid; o < 10; o += LT / 64) {
+    float acc = lane < 56 ? fw2[o * 120 + lane] * h1[lane] + fw2[o * 120 + 64 + lane] * h1[64 + lane]
+                          : fw2[o * 120 + lane] * h1[lane];
+    acc = wave_sum(acc);
+    if (lane == 0) lg[o] = acc + fb2[o];
+  }
+  __syncthreads();
+  // ---- softmax cross-entropy: loss and the (softmax - onehot) / B seed ----
   if (wid == 0) {
-    float z = -INFINITY;
-    if (lane < 10) {
-      float acc = f2b[lane];
-      for (int u = 0; u < 120; ++u) acc += f2w[lane * 120 + u] * h1[u];
-      z = acc;
-    }
+    const float z = lane < 10 ? lg[lane] : -INFINITY;
     const float mx = wave_max(z);
     const float e = lane < 10 ? __expf(z - mx) : 0.f;
     const float se = wave_sum(e);
@@ -163,17 +183,39 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   if (tid < 120) {
     float acc = 0.f;
 #pragma unroll
-    for (int o = 0; o < 10; ++o) acc += dl[o] * f2w[o * 120 + tid];
+    for (int o = 0; o < 10; ++o) acc += dl[o] * fw2[o * 120 + tid];
     dh1[tid] = h1[tid] > 0.f ? acc : 0.f;
   }
   __syncthreads();
 
-  // ---- fc1 data gradient -> pooled conv2 gradient (unpool through k2 below) ----
+  // ---- fc1 data gradient: thread (k4, u-group of 24) streams coalesced float4 rows ----
+  if (tid < 500) {
+    const int k4 = tid % 100, ug = tid / 100;
+    float4 wv[24];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) wv[j] = reinterpret_cast<const float4*>(f1w + (ug * 24 + j) * 400)[k4];
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      const float d = dh1[ug * 24 + j];
+      a.x += d * wv[j].x;
+      a.y += d * wv[j].y;
+      a.z += d * wv[j].z;
+      a.w += d * wv[j].w;
+    }
+    red4[ug * 100 + k4] = a;
+  }
+  __syncthreads();
   float* r = rec + (long long)b * 656;  // per-sample record: h0 | h1 | dh1 | dl (+ pad)
   if (tid < 400) {
-    float acc = 0.f;
-    for (int u = 0; u < 120; ++u) acc += dh1[u] * f1w[u * 400 + tid];
-    g2[tid] = k2[tid] < 4 ? acc : 0.f;
+    const float d = red[tid] + red[400 + tid] + red[800 + tid] + red[1200 + tid] + red[1600 + tid];
+    const int ps = pos2[tid];
+    const float gv = ps >= 0 ? d : 0.f;
+    g2[tid] = gv;
+    if (ps >= 0) {  // scatter into the unpooled, zero-bordered conv2 gradient
+      const int o = tid / 25, y = ps / 14, x = ps - (ps / 14) * 14;
+      dc2[o * 324 + (y + 4) * 18 + x + 4] = gv;
+    }
     r[tid] = p2[tid];
   }
   if (tid < 120) {
@@ -184,17 +226,15 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __syncthreads();
 
   float* cs = cslab + (long long)b * CS;
-  // ---- conv2 weight/bias gradient partials and data gradient ----
+  // ---- conv2 weight/bias gradient partials over the 25 argmax positions of each channel ----
   for (int i = tid; i < 2400; i += LT) {
     const int o = i / 150, rr = i - o * 150, c = rr / 25, t = rr - c * 25, kh = t / 5, kw = t - kh * 5;
+    const float* pc = p1 + c * 196 + kh * 14 + kw;
     float acc = 0.f;
-#pragma unroll 5
+#pragma unroll
     for (int j = 0; j < 25; ++j) {
-      const int code = k2[o * 25 + j];
-      if (code < 4) {
-        const int py = j / 5, px = j - py * 5;
-        acc += g2[o * 25 + j] * p1[c * 196 + (2 * py + (code >> 1) + kh) * 14 + 2 * px + (code & 1) + kw];
-      }
+      const int ps = pos2[o * 25 + j];
+      acc += g2[o * 25 + j] * pc[ps < 0 ? 0 : ps];
     }
     cs[i] = acc;
   }
@@ -203,23 +243,31 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     for (int j = 0; j < 25; ++j) acc += g2[tid * 25 + j];
     cs[2400 + tid] = acc;
   }
-  // dp1[c][yy][xx] = sum_o sum_(py,px) g2[o][py][px] W2[o][c][yy - y][xx - x], (y, x) the argmax
-  // position of pooled output (py, px); then unpool1 through k1
-  for (int q = tid; q < 1176; q += LT) {
-    const int c = q / 196, rr = q - c * 196, yy = rr / 14, xx = rr - yy * 14;
-    const int py0 = yy >= 5 ? (yy - 5) / 2 : 0, py1 = (yy / 2) < 4 ? yy / 2 : 4;
-    const int px0 = xx >= 5 ? (xx - 5) / 2 : 0, px1 = (xx / 2) < 4 ? xx / 2 : 4;
-    float acc = 0.f;
-    for (int o = 0; o < 16; ++o)
-      for (int py = py0; py <= py1; ++py)
-        for (int px = px0; px <= px1; ++px) {
-          const int j = o * 25 + py * 5 + px;
-          const int code = k2[j];
-          if (code >= 4) continue;
-          const int kh = yy - 2 * py - (code >> 1), kw = xx - 2 * px - (code & 1);
-          if ((unsigned)kh < 5u && (unsigned)kw < 5u) acc += g2[j] * w2[o * 150 + c * 25 + kh * 5 + kw];
+  // ---- conv2 data gradient (full correlation with the flipped kernel over the unpooled
+  //      gradient), 2x2 outputs per thread sharing a 6x6 window, then unpool1 ----
+  if (tid >= 200 && tid < 200 + 294) {
+    const int q = tid - 200, c = q / 49, rr = q - c * 49, by = rr / 7, bx = rr - by * 7;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int o = 0; o < 16; ++o) {
+      float win[6][6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) win[i][j] = dc2[o * 324 + (2 * by + i) * 18 + 2 * bx + j];
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float w = w2[o * 150 + c * 25 + kh * 5 + kw];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) acc[a] += win[(a >> 1) + 4 - kh][(a & 1) + 4 - kw] * w;
         }
-    g1[q] = k1[q] < 4 ? acc : 0.f;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int idx = c * 196 + (2 * by + (a >> 1)) * 14 + 2 * bx + (a & 1);
+      g1[idx] = pos1[idx] >= 0 ? acc[a] : 0.f;
+    }
   }
   __syncthreads();
 
@@ -228,13 +276,12 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   if (tid < 450) {
     const int i = tid / 3, part = tid - i * 3;
     const int c = i / 25, t = i - c * 25, kh = t / 5, kw = t - kh * 5;
+    const float* xc = xs + kh * 32 + kw;
     float acc = 0.f;
+#pragma unroll 4
     for (int j = part; j < 196; j += 3) {
-      const int code = k1[c * 196 + j];
-      if (code < 4) {
-        const int py = j / 14, px = j - py * 14;
-        acc += g1[c * 196 + j] * xs[(2 * py + (code >> 1) + kh) * 32 + 2 * px + (code & 1) + kw];
-      }
+      const int ps = pos1[c * 196 + j];
+      acc += g1[c * 196 + j] * xc[ps < 0 ? 0 : ps];
     }
     red[tid] = acc;
   }
@@ -289,16 +336,19 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
   float g = 0.f;
   if (seg == 0) {  // fc2.w[o][u] = sum_b dl[b][o] h1[b][u]
     const int o = i / 120, u = i - o * 120;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + o] * rec[b * 656 + 400 + u];
   } else if (seg == 1) {
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + i];
   } else if (seg == 2) {  // fc1.w[u][k] = sum_b dh1[b][u] h0[b][k]
     const int u = i / 400, k = i - u * 400;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + u] * rec[b * 656 + k];
   } else if (seg == 3) {
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + i];
   } else {
     const int base = seg == 4 ? 0 : seg == 5 ? 2400 : seg == 6 ? 2416 : 2566;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) g += cslab[(long long)b * CS + base + i];
   }
   const int o = fl.off[seg] + i;

@@ -45,14 +45,11 @@ __device__ __forceinline__ s4 tr_read(const bf16_t* p) {
 
 // NTY = kernel rows (dy values) per block: 3 = all 9 taps share the dY fragments; 1 = one
 // row of 3 taps (smaller halo, 3x more output tiles -> 3x fewer m-splits and slab bytes)
-// DPRE: DY is the upstream gradient dz of the conv's BatchNorm and the dY operand is that
-// BN's backward apply (dpre: y, coefficients; igemm_common.h PreBnBwd) -- no dy tensor
-template <int HRN, int NTY, bool PRE, bool DPRE>
+template <int HRN, int NTY, bool PRE>
 __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int xy, int gx, int nz,
-    BwdPre dpre) {
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int xy, int gx, int nz) {
   // pre_sc/pre_sh (optional): X is the previous conv's raw output; the operand is
   // relu(x*sc + sh) applied while staging (out-of-image taps read the zero row)
   constexpr int HROWS_MAX = HRN * 32;  // halo rows a buffer holds (8 chunks per row)
@@ -88,8 +85,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
   const auto rsd = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, (int)dybytes, 0x00020000);
   const int chunk = tid & 7, row0 = tid >> 3;  // staging: 32 rows x 8 chunks per pass
 
-  const auto rsy = __builtin_amdgcn_make_buffer_rsrc((void*)dpre.y, (short)0, (int)dybytes, 0x00020000);
-  uint4 ra[2], rh[HRN], ry[DPRE ? 2 : 1];
+  uint4 ra[2], rh[HRN];
   auto load = [&](long long m0) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -97,10 +93,6 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
       const unsigned off = m < me ? (unsigned)((m * g.Ncols + co0 + chunk * 8) * 2) : WOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsd, off, 0, 0);
       ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
-      if constexpr (DPRE) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsy, off, 0, 0);
-        ry[i] = make_uint4(w[0], w[1], w[2], w[3]);
-      }
     }
     const long long hb = m0 + dy_lo * W - 1;
 #pragma unroll
@@ -118,20 +110,9 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     if constexpr (PRE) pbn.load(pre_sc, pre_sh, cc0 + chunk * 8);
     bf16_t* as = As + buf * WBK * WPITCH;
     bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
-    if constexpr (DPRE) {
-      PreBnBwd pb;
-      pb.load(dpre.coef, dpre.scale, dpre.shift, g.Ncols, co0 + chunk * 8);
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {  // rows past the slice stay zero (a*0 + b*0 + cc != 0)
-        const bool ok = m0 + row0 + 32 * i < me;
-        *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) =
-            ok ? pb.apply(ra[i], ry[i]) : make_uint4(0, 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
-    }
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
 #pragma unroll
     for (int j = 0; j < HRN; ++j)
       *reinterpret_cast<uint4*>(hs + (row0 + 32 * j) * WPITCH + chunk * 8) =
@@ -220,14 +201,12 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
 template <int HRN, int NTY>
 void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                        long long mchunk, hipStream_t st, const float* pre_sc,
-                       const float* pre_sh, const BwdPre* dpre) {
+                       const float* pre_sh) {
   const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
   dim3 grid((g.Ncols + WBM - 1) / WBM, (g.C / WBC) * (3 / NTY), S);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
-  auto k = pre_sc ? (dpre ? wgrad_halo_kernel<HRN, NTY, true, true> : wgrad_halo_kernel<HRN, NTY, true, false>)
-                  : (dpre ? wgrad_halo_kernel<HRN, NTY, false, true> : wgrad_halo_kernel<HRN, NTY, false, false>);
-  const BwdPre dp = dpre ? *dpre : BwdPre{};
+  auto k = pre_sc ? wgrad_halo_kernel<HRN, NTY, true> : wgrad_halo_kernel<HRN, NTY, false>;
   set_smem_attr(k, sm);
   // XCD-grouped order for the 9-tap tiles (DMLAB_WGRAD_XCD=0: plain 3-D grid).  Measured
   // (tools/bench_conv.py, one call): 9-tap layer2 +2-4 %, layer3/4 within 1 %, step 11.55 vs
@@ -237,10 +216,10 @@ void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const Con
   if (xcd_on && NTY == 3 && xy > 1 && S > 1) {
     const unsigned z8 = (unsigned)((S + 7) / 8 * 8);
     k<<<dim3(z8 * xy), 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, xy,
-                                       (int)grid.x, S, dp);
+                                       (int)grid.x, S);
     return;
   }
-  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, 0, (int)grid.x, S, dp);
+  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, 0, (int)grid.x, S);
 }
 }  // namespace
 
@@ -257,14 +236,14 @@ bool wgrad_halo_supported(const ConvGeom& g) {
 
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc,
-                const float* pre_sh, const BwdPre* dpre) {
+                const float* pre_sh) {
   if (nty == 1) {
-    launch_wgrad_halo<3, 1>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, dpre);  // 66 rows
+    launch_wgrad_halo<3, 1>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);  // 66 rows
   } else {
     const int rows = WBK + 2 * g.W + 2;
-    if (rows <= 96) launch_wgrad_halo<3, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, dpre);
-    else if (rows <= 128) launch_wgrad_halo<4, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, dpre);
-    else launch_wgrad_halo<6, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, dpre);
+    if (rows <= 96) launch_wgrad_halo<3, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);
+    else if (rows <= 128) launch_wgrad_halo<4, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);
+    else launch_wgrad_halo<6, 3>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);
   }
   DM_CHECK(hipGetLastError());
 }

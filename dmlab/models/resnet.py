@@ -42,15 +42,6 @@ class ResNet18(Program):
         # conv weight gradients run on a second stream, overlapping the dgrad/BN chain
         self._uses_side_stream = True
 
-    def prefetch(self, x):
-        """Declare the next step's input batch: its space-to-depth packing then runs on the
-        side stream during this step's stem weight gradient (see
-        :func:`dmlab.ops.convbn.request_input_prefetch`).  A no-op off the native GPU path."""
-        if self._use_native(x) and self.training:
-            from dmlab.ops.convbn import request_input_prefetch
-
-            request_input_prefetch(self.stem, x)
-
     def prepare_native(self, x):
         if self.compute_dtype != torch.bfloat16:
             raise ValueError("the native ResNet path computes in bf16")

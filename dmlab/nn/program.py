@@ -396,19 +396,7 @@ class Program(nn.Module):
             # DMLAB_WGRAD_PRIO: stream priority of the side stream (lower = higher priority);
             # the weight gradients have slack until the end of backward, the main chain does not
             prio = int(os.environ.get("DMLAB_WGRAD_PRIO", "0"))
-            # DMLAB_WGRAD_CUMASK: 32-bit hex pattern repeated over the CUs; the side stream
-            # then runs on its own hardware queue restricted to those CUs.  Off: with masks
-            # 77777777 / 7f7f7f7f / 3f3f3f3f the step fell from 44.3k to 32.2-32.6k img/s
-            # (profiles/wgrad_cumask_r2c.jsonl), so CU contention is not solved this way
-            cm = os.environ.get("DMLAB_WGRAD_CUMASK", "")
-            if cm:
-                from ..ops._native import lib
-                words = (lib().num_cus(dev) + 31) // 32
-                st = torch.cuda.ExternalStream(lib().cumask_stream(dev, [int(cm, 16)] * words),
-                                               device=torch.device("cuda", dev))
-                self._side_streams[dev] = st
-            else:
-                st = self._side_streams[dev] = torch.cuda.Stream(device=dev, priority=prio)
+            st = self._side_streams[dev] = torch.cuda.Stream(device=dev, priority=prio)
         return st
 
     def prepare_native(self, x):

@@ -28,45 +28,23 @@ def _cpad(c):
     return max(8, (c + 7) // 8 * 8)
 
 
-# forward-style kernel configs (csrc/conv_igemm.hip igemm_fwd): tile = cfg % 3
-# (0: 128x128, 1: 128x64, 2: 64x64); loader = cfg // 3 (0: predicated global loads,
-# 1: LDS-DMA, 2: branch-free buffer loads, 3: v3 addressing on 16x16x32 MFMA,
-# 4: v3 on 32x32x16 MFMA); 15-17: v3 with two tiles of register prefetch; 18: 8-wave
-# 256x128; 20/21: halo-staged unit-stride kernel (csrc/conv_halo.hip, BN 128/64).
-# Measured on MI355X (tools/bench_conv.py -> profiles/conv_kernels_r1.jsonl):
-#   * unit-stride 3x3 with >= 128 output channels: halo kernel (20) fastest
-#     (l2/l3/l4: 714/749/787 TFLOP/s fwd vs 661/708/730 for the best igemm tile);
-#   * 64 output channels at 56x56 (one 64-channel chunk): the 256-pixel halo tile with
-#     8 waves (39), 549/663 TFLOP/s fwd/dgrad vs 497/582 for the v3 128x64 tile (16);
-#   * 512 output channels (layer4): the 256-pixel 8-wave halo tile (38), 737/786 vs
-#     697/748 for the 128-pixel one;
-#   * everything else (strided taps, stride-2 dgrad parity classes, 1x1/s2, stem):
-#     v3 tiles 15 / 13 / 11 by the block-count rule below; 256-row tiles lose
-#     (one workgroup per CU exposes the staging latency).
+# forward-style kernel configs (csrc/conv_igemm.hip igemm_fwd): 9-17 v3 igemm tiles
+# (tile = cfg % 3: 0 128x128, 1 128x64, 2 64x64; 12-13 32x32x16 MFMA, 15-17 two tiles of
+# register prefetch); 20/21/39/41/42 halo-staged unit-stride tiles (csrc/conv_halo.hip);
+# 60 the space-to-depth stem (csrc/conv_stem.hip); 90-93 pipelined LDS-DMA tiles
+# (csrc/conv_pipe.hip).  Measured on MI355X (tools/bench_conv.py ->
+# profiles/conv_kernels_r1.jsonl, conv_halo_tiles_b512_r1s4.jsonl):
+#   * strided taps, stride-2 dgrad parity classes below 256 channels, 1x1/s2 below 256
+#     channels: v3 tiles 15 / 13 / 11 by the block-count rule below (256-row tiles lose
+#     there: one workgroup per CU exposes the staging latency).
 TILE_CFG = (15, 13, 11)
 _STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
-# 44 / 45: the 41 / 39 halo tiles with two weight tiles of register prefetch (a weight load
-# gets two tap steps of MFMA work to land in instead of one)
-_HALO_PF2 = os.environ.get("DMLAB_HALO_PF2", "0") == "1"
-# per-output-channel override of the unit-stride 3x3 halo cfg, e.g. "64=44,128=44" (A/B runs)
-_HALO_MAP = {int(k): int(v) for k, v in (kv.split("=") for kv in
-             os.environ.get("DMLAB_HALO_MAP", "").split(",") if kv)}
 # DMLAB_NO_PIPE=1: the round-2 tile map without the pipelined tiles (A/B runs)
 _NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
 
 
-# cfg 80: stride-2 3x3 data gradient with the four parity classes of a dY tile in one block
-# (csrc/dgrad_s2.hip).  Opt-in (DMLAB_DGRAD_S2=1): at batch 512 it ties the per-class igemm
-# tiles on layer2/3 (373 vs 374, 452-473 vs 473 TFLOP/s) and loses on layer4 (515 vs 588),
-# end to end 43.98/44.01k vs 43.86/44.04k img/s (profiles/dgrad_s2_r2c.txt)
-_DGRAD_S2 = os.environ.get("DMLAB_DGRAD_S2", "0") == "1"
-
-
 def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
     """Kernel config of a data-gradient GEMM (dX has M pixels of ``cin`` channels)."""
-    if (_DGRAD_S2 and not _FUSE_BN_BWD and k == 3 and stride == 2 and cin % 64 == 0
-            and cout % 64 == 0 and H % 2 == 0 and W % 2 == 0):
-        return 80
     return pick_cfg(M, cin, k, stride, cout)
 
 
@@ -94,11 +72,9 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0):
         #   layer3 (256 ch): 41 852/867, 42 834/840                (b256: 41 722/762)
         #   layer4 (512 ch): 41 856/867, 43 812/820                (b256: 41 822/848)
         #   layer1 (64 ch) : 39 612/683, 41 580/642
-        if ncols in _HALO_MAP:
-            return _HALO_MAP[ncols]
         if ncols >= 256:
-            return 44 if _HALO_PF2 else 41
-        return 42 if ncols >= 128 else (45 if _HALO_PF2 else 39)
+            return 41
+        return 42 if ncols >= 128 else 39
     if ncols % 128 == 0 and math.ceil(M / 128) * (ncols // 128) >= 192:
         t = 0  # 64x64 per wave beats the narrower tile even at ~1 block per CU
     elif math.ceil(M / 128) * math.ceil(ncols / 64) >= 480:
@@ -120,7 +96,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
     cfg 4/5: halo-staged 3x3 unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per
-    block; cfg 2/3/6: v2 igemm tiles 128x128 / 64x128 / 64x256 (cfg 0/1: v1, kept for A/B).
+    block; cfg 2/3/6: v2 igemm tiles 128x128 / 64x128 / 64x256.
     S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
     ~2 blocks per CU, each split >= 8 row steps, slab bytes S*cout*K*4."""
     halo = k == 3 and stride == 1 and cin % 64 == 0 and cout % 8 == 0
@@ -137,7 +113,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
         tiles = max(1, math.ceil(cout / 64) * (cin // 64) * (1 if cfg == 4 else 3))
         max_split = max(1, M // 512)
     else:
-        bm = 128 if cfg in (0, 2) else 64
+        bm = 128 if cfg == 2 else 64
         tiles = math.ceil(cout / bm) * math.ceil(K / (256 if cfg == 6 else 128))
         # >= 8 row steps of 64 per split: the small-K layers (1x1/s2 downsample: K = Cin)
         # have one or two output tiles, so the m-split is their only parallelism
@@ -237,70 +213,11 @@ def pack_all(prog, layers):
         object.__setattr__(m, "_wcache", (ver, wf, wd))
 
 
-_FIN_GROUPS = 32  # ticket counters per direction: one per 32-channel group, C <= 1024
-
-
-def _fin_counter(layer, device, bwd=False):
-    """Persistent int32 ticket counters of this layer's one-launch BN finalizes (forward and
-    backward, one per 32-channel group each); zero between launches (each group's
-    finalizing block resets its own)."""
-    c = getattr(layer, "_fin_ctr", None)
-    if c is None or c.device != device:
-        c = torch.zeros(2 * _FIN_GROUPS, dtype=torch.int32, device=device)
-        object.__setattr__(layer, "_fin_ctr", c)
-    return c[_FIN_GROUPS:] if bwd else c[:_FIN_GROUPS]
-
-
 def _materialise(x, pre):
     """relu(x*scale + shift) as a tensor (fallback when a consumer cannot fuse it)."""
     out = empty_nhwc(*x.shape, x)
     lib().bn_apply(x, None, pre[0], pre[1], out, True)
     return out
-
-
-def _input_key(x):
-    return (x.data_ptr(), x._version, tuple(x.shape), tuple(x.stride()), x.dtype)
-
-
-def request_input_prefetch(layer, x):
-    """Ask the stem's backward to space-to-depth pack ``x`` (the NEXT step's input batch)
-    on the side stream while the stem weight gradient runs: that kernel is latency-bound
-    and alone on the GPU (one workgroup per CU), so the memory-bound packing (~100 us at
-    batch 512) overlaps it instead of opening the next step's forward.  The next forward
-    uses the packed batch if ``x`` is unchanged (same storage, version, shape)."""
-    if use_s2d(layer, x) and x.is_cuda:
-        object.__setattr__(layer, "_prefetch_req", x)
-
-
-def _launch_input_prefetch(layer, main):
-    x = getattr(layer, "_prefetch_req", None)
-    side = getattr(layer._prog, "_wgrad_stream", None)
-    if x is None or side is None:
-        return
-    object.__setattr__(layer, "_prefetch_req", None)
-    side.wait_stream(main)  # starts at this point of the backward, next to the stem wgrad
-    with torch.cuda.stream(side):
-        Nn, Cc, Hh, Ww = x.shape
-        xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
-        lib().pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
-        ev = torch.cuda.Event()
-        ev.record(side)
-    x.record_stream(side)
-    object.__setattr__(layer, "_prefetched", (_input_key(x), xs, ev))
-
-
-def _take_prefetched(layer, x):
-    pf = getattr(layer, "_prefetched", None)
-    if pf is None:
-        return None
-    object.__setattr__(layer, "_prefetched", None)
-    key, xs, ev = pf
-    if key != _input_key(x):
-        return None
-    cur = torch.cuda.current_stream()
-    cur.wait_event(ev)
-    xs.record_stream(cur)  # allocated on the side stream, consumed (and freed) on this one
-    return xs
 
 
 def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
@@ -310,10 +227,8 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     if s2d:
         # stem as a 4x4/s1 conv over the space-to-depth input (pad 2 top/left, 1 bottom/right)
         Nn, Cc, Hh, Ww = x.shape
-        xs = _take_prefetched(layer, x) if x.is_cuda else None
-        if xs is None:
-            xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
-            L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
+        xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
+        L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
         x = xs
         k, s, p = 4, 1, 2
         OH, OW = Hh // 2, Ww // 2
@@ -336,7 +251,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43, 44, 45, 90, 91, 92, 93):
+        if cfg in (20, 21, 39, 41, 42, 90, 91, 92, 93):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)
@@ -354,8 +269,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
         work = torch.empty(256 * 2 * cout, **f32)
         L.bn_stats_finalize(stats, T, float(M), layer.bn_weight.detach(), layer.bn_bias.detach(),
                             layer.running_mean, layer.running_var, layer.momentum, layer.eps,
-                            scale, shift, mean, invstd, work, layer.num_batches_tracked,
-                            counter=_fin_counter(layer, x.device) if _FUSED_FIN else None)
+                            scale, shift, mean, invstd, work, layer.num_batches_tracked)
     else:
         L.conv_fwd(x, wf, y, None, None, k, k, s, p, cfg, **pre_kw)
         L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
@@ -408,21 +322,7 @@ _FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
 # (dy never written, but its gathers keep only one row pair in flight); "legacy" = one
 # apply pass + the generic igemm weight gradient.  Kept for A/B runs.
 _STEM_BWD = os.environ.get("DMLAB_STEM_BWD", "fused")
-# BN finalizes as one launch (column sums + a last-block finalize, bit-identical) instead of
-# two: opt-in (DMLAB_FUSED_FIN=1).  With one last block for all channels it measured 6 %
-# slower end to end (12.8 vs 12.1 ms/step: that block walked every channel group serially);
-# with one last block per 32-channel group it is 0.8 % slower (43.0-43.1k vs 43.35-43.6k
-# img/s, profiles/bn_finalize_grouped_r2c.txt) -- the saved launch does not pay for the
-# ticket fences and the serial tail
-_FUSED_FIN = os.environ.get("DMLAB_FUSED_FIN", "0") == "1"
 _STEM_SPLIT = int(os.environ.get("DMLAB_STEM_SPLIT", "4"))
-# BN-backward apply fused into the consumers' operand staging for the 64-channel 3x3 convs
-# whose BN has no residual (layer-1 c1): opt-in (DMLAB_BN_BWD_ON_LOAD=1).  Measured 1.2 %
-# slower end to end (43.15-43.19k vs 43.55-43.80k img/s): the fused dgrad takes 560 us vs
-# 360 + 115 (apply pass) because its single-chunk halo prologue now loads dz AND y and runs
-# the apply before any MFMA, and the fused weight gradient grows 333 -> 446 us
-# (profiles/bn_bwd_on_load_r2c.txt)
-_BN_BWD_ON_LOAD = os.environ.get("DMLAB_BN_BWD_ON_LOAD", "0") == "1"
 # weight gradient of the split path: "dy" (stem_wgrad_dy_kernel) or "igemm" (v2 s2d tiles)
 _STEM_WGRAD = os.environ.get("DMLAB_STEM_WGRAD", "dy")
 
@@ -531,7 +431,6 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     if stem_ok and _STEM_BWD == "fused":
         # stem: BN-backward apply fused into the s2d weight gradient -- the full-resolution
         # dy is never written (csrc/conv_stem.hip stem_wgrad_fused_kernel)
-        _launch_input_prefetch(layer, torch.cuda.current_stream())
         slab = torch.empty(L.stem_bwd_slab_floats(N, OH), device=y.device, dtype=torch.float32)
         L.stem_bwd_fused(y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
                          layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
@@ -551,27 +450,14 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     C = x.shape[3]
     K = k * k * C
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
-    # BN-backward apply on load: this conv's dgrad and weight gradient stage
-    # a*dz' + b*y + cc straight from (dout, y), so dy is never written (saves the apply pass)
-    bwd_on_load = (_BN_BWD_ON_LOAD and mode == 2 and not s2d and k == 3 and s == 1
-                   and cout == 64 and C == 64 and wcfg in (4, 5) and need_dx
-                   and not ctx["first"] and not _FUSE_BN_BWD
-                   and dgrad_cfg(M, C, k, s, cout, OH, OW) == 39)
-    dy = None if bwd_on_load else empty_nhwc(N, OH, OW, cout, y)
+    dy = empty_nhwc(N, OH, OW, cout, y)
     dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
                   layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
-                  getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"),
-                  counter=_fin_counter(layer, y.device, bwd=True) if _FUSED_FIN else None, **pre_sums)
-    bwd_kw = {}
-    if bwd_on_load:
-        off = L.bn_bwd_coef_offset(M, cout, bool(pre_sums))
-        bwd_kw = dict(bwd_y=y, bwd_coef=work[off:off + 3 * cout], bwd_scale=ctx["scale"],
-                      bwd_shift=ctx["shift"])
-        dy = dout  # the operand the consumers read; the bwd_* terms turn it into dy
+                  getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"), **pre_sums)
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does
@@ -584,7 +470,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     def launch_wgrad():
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
-            for t in (x, dy) + (tuple(pre) if pre is not None else ()) + tuple(bwd_kw.values()):
+            for t in (x, dy) + (tuple(pre) if pre is not None else ()):
                 t.record_stream(side)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
@@ -596,7 +482,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                 else:
                     xw = _materialise(x, pre)
             L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S,
-                         wcfg, s2d, **pre_kw, **bwd_kw)
+                         wcfg, s2d, **pre_kw)
 
     deferred = getattr(layer._prog, "_deferred_wgrads", None) if side is not None else None
     if deferred is not None:
@@ -619,10 +505,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
                                                       dtype=torch.float32))
         if dx_into is not None:
             dx = dx_into
-            r = L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg, **bkw, **bwd_kw)
+            r = L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg, **bkw)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **bkw, **bwd_kw)
+            r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **bkw)
         if bkw and r:
             consumer[1]["dz_stats"] = (bkw["bnb_slab"], r, dx)
     if ctx["has_res"]:

@@ -75,7 +75,7 @@ class PipelineStage:
         self._posted = {}
         self.timing = timing and torch.cuda.is_available() and self.device.type == "cuda"
         self._events = []
-        self.last_stats = None
+        self.history = []  # (start, end, compute events) of every timed step
 
     # -------------------------------------------------------------- pieces
     def _post_recv(self, tag, m, src, ahead=False):
@@ -188,17 +188,22 @@ class PipelineStage:
         if self.timing:
             t1.record()
             self._step_events = (t0, t1, list(self._events))
+            self.history.append(self._step_events)
         if self.last:
             return torch.stack(losses).sum()
         return None
 
-    def step_stats(self):
-        """(step ms, compute ms, bubble fraction) of the last timed step (synchronises)."""
-        t0, t1, evs = self._step_events
-        t1.synchronize()
-        step = t0.elapsed_time(t1)
-        comp = sum(s.elapsed_time(e) for s, e in evs)
-        return step, comp, max(0.0, 1.0 - comp / step) if step > 0 else 0.0
+    def step_stats(self, skip=None):
+        """(step ms, compute ms, bubble fraction): of the last timed step, or averaged over
+        the timed steps after the first ``skip`` (synchronises once)."""
+        steps = [self._step_events] if skip is None else self.history[skip:]
+        steps[-1][1].synchronize()
+        tot = comp = 0.0
+        for t0, t1, evs in steps:
+            tot += t0.elapsed_time(t1)
+            comp += sum(s.elapsed_time(e) for s, e in evs)
+        n = len(steps)
+        return tot / n, comp / n, (max(0.0, 1.0 - comp / tot) if tot > 0 else 0.0)
 
     @torch.no_grad()
     def forward_only(self, x=None):

@@ -59,6 +59,10 @@ def parse_args(argv=None):
     p.add_argument("--json", default=None)
     p.add_argument("--save", default=None, help="checkpoint path written after training")
     p.add_argument("--resume", default=None, help="checkpoint to load before training")
+    p.add_argument("--image-size", type=int, default=64,
+                   help="ResNet-18 synthetic image side (224 = the BASELINE/ImageNet shape)")
+    p.add_argument("--num-classes", type=int, default=10,
+                   help="ResNet-18 classifier width (1000 = the BASELINE/ImageNet head)")
     return p.parse_args(argv)
 
 
@@ -76,10 +80,13 @@ def main(argv=None):
     else:
         from dmlab.data import synthetic_classification
 
-        model = ResNet18(num_classes=10).to(dev)
+        # --image-size 224 --num-classes 1000: the headline config of bench.py / BASELINE.json
+        # (ResNet-18 on ImageNet-shaped data); the default 64x64 / 10 classes keeps lab runs short
+        model = ResNet18(num_classes=a.num_classes).to(dev)
         n = a.train_samples or 4096
-        train_set = synthetic_classification(n, (3, 64, 64), 10, seed=0)
-        test_set = synthetic_classification(512, (3, 64, 64), 10, seed=7)
+        shape = (3, a.image_size, a.image_size)
+        train_set = synthetic_classification(n, shape, a.num_classes, seed=0)
+        test_set = synthetic_classification(512, shape, a.num_classes, seed=7)
     # seed=rank as the reference passes (task3/model.py:111); the partition
     # strategy needs a shared permutation so it uses seed 0 on every rank.
     seed = rank if a.sampler == "random" else 0

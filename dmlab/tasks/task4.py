@@ -44,9 +44,17 @@ def parse_args(argv=None):
     p.add_argument("--relay", action="store_true")
     p.add_argument("--micro", type=int, default=1, help="micro-batches per step (pipeline)")
     p.add_argument("--schedule", default="1f1b", choices=["1f1b", "gpipe"])
+    p.add_argument("--transport", default="pg", choices=["pg", "xgmi"],
+                   help="pipeline stage transport: torch.distributed P2P (RCCL / gloo) or the "
+                        "native xGMI peer-memory channel (GPU)")
+    p.add_argument("--bench-json", default=None,
+                   help="pipeline: write per-rank step ms, compute ms and bubble fraction "
+                        "(HIP events) to <path>.rank<r>")
     p.add_argument("--batch-size", type=int, default=32)
     p.add_argument("--epochs", type=int, default=2)
     p.add_argument("--lr", type=float, default=0.01)
+    p.add_argument("--momentum", type=float, default=0.0,
+                   help="SGD momentum for every mode (reference: plain SGD, model.py:126)")
     p.add_argument("--data", default="./data")
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--train-samples", type=int, default=None)
@@ -55,10 +63,11 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def _data(a, dev):
+def _data(a, dev, drop_last=False, test_batch=32):
     tr = load_mnist(a.data, True, synthetic=True if a.synthetic else None, n=a.train_samples)
     te = load_mnist(a.data, False, synthetic=True if a.synthetic else None)
-    return DeviceLoader(tr.to(dev), a.batch_size, shuffle=True), DeviceLoader(te.to(dev), 32)
+    return (DeviceLoader(tr.to(dev), a.batch_size, shuffle=True, drop_last=drop_last),
+            DeviceLoader(te.to(dev), test_batch, drop_last=drop_last))
 
 
 def _log(i, epoch, loss_acc, rank=0):
@@ -84,7 +93,7 @@ def run_rpc(a):
         train_loader, test_loader = _data(a, torch.device("cpu"))
         sdev = "cuda" if a.device == "cuda" else "cpu"  # stage owners' GPUs (BASELINE cfg 4)
         model = ParallelNet(1, 10, relay=a.relay, devices=(sdev, sdev))
-        opt = make_distributed_optimizer(model, lr=a.lr)
+        opt = make_distributed_optimizer(model, lr=a.lr, momentum=a.momentum)
         loss_fn = CrossEntropyLoss()
         t0 = time.perf_counter()
         step, acc, losses = 0, 0.0, []
@@ -129,9 +138,12 @@ def run_pipeline(a):
     assert ws == 2, "the LeNet pipeline has 2 stages"
     torch.manual_seed(0)
     module = (SubNetConv(1) if rank == 0 else SubNetFC(10)).to(dev)
-    opt = SGD(module.parameters(), lr=a.lr)
-    stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule)
-    train_loader, test_loader = _data(a, dev) if rank == 0 else (None, None)
+    opt = SGD(module.parameters(), lr=a.lr, momentum=a.momentum)
+    # every batch one shape (drop_last): message shapes are negotiated once and cached
+    stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
+                          transport=a.transport, timing=bool(a.bench_json))
+    train_loader, test_loader = _data(a, dev, drop_last=True, test_batch=16) if rank == 0 \
+        else (None, None)
     nsteps = len(train_loader) if rank == 0 else 0
     nsteps = int(_bcast_scalar(nsteps, dev))
     print("Device {} starts training ...".format(rank))
@@ -157,10 +169,55 @@ def run_pipeline(a):
             break
     if torch.cuda.is_available() and dev.type == "cuda":
         torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
     print("Training Finished!")
-    print("Training time: {}".format(time.perf_counter() - t0))
+    print("Training time: {}".format(dt))
+    if a.bench_json:
+        import json
+
+        warm = min(5, max(0, step - 1))
+        if stage.timing:
+            step_ms, comp_ms, bubble = stage.step_stats(skip=warm)
+        else:  # CPU: wall time only (no device events)
+            warm, step_ms, comp_ms, bubble = 0, 1e3 * dt / max(step, 1), float("nan"), float("nan")
+        res = {"rank": rank, "stage": "conv" if rank == 0 else "fc", "schedule": a.schedule,
+               "n_micro": a.micro, "transport": a.transport, "batch": a.batch_size,
+               "steps_timed": step - warm, "step_ms": round(step_ms, 4),
+               "compute_ms": round(comp_ms, 4), "bubble": round(bubble, 4),
+               "samples_per_s": round(a.batch_size / step_ms * 1e3, 1), "wall_s": round(dt, 3)}
+        with open(f"{a.bench_json}.rank{rank}", "w") as f:
+            json.dump(res, f)
+    if not a.no_test:
+        _pipeline_test(a, stage, test_loader, dev)
+    if a.transport == "xgmi":
+        stage.p2p.check()
     env.barrier()
     env.destroy()
+
+
+def _pipeline_test(a, stage, test_loader, dev):
+    """Test accuracy through the stages: the first stage feeds the batches and sends their
+    labels to the last one, which prints the reference's accuracy line (test batches of 16
+    divide the 10,000 test images, so every message has one shape)."""
+    n = int(_bcast_scalar(len(test_loader) if stage.first else 0, dev))
+    correct = total = 0
+    it = iter(test_loader) if stage.first else None
+    for _ in range(n):
+        if stage.first:
+            x, y = next(it)
+            stage.forward_only(x)
+            for w in stage.p2p.send(y, stage.ranks[-1], ("eval_lbl", 0)):
+                w.wait()
+        elif stage.last:
+            out = stage.forward_only()
+            y = stage._take("eval_lbl", 0, stage.ranks[0]).to(out.device)
+            correct += int((out.argmax(1) == y).sum())
+            total += y.numel()
+        else:
+            stage.forward_only()
+    if stage.last:
+        print('\nTest set: Accuracy: {}/{} ({:.2f}%)\n'.format(correct, total,
+                                                              100 * correct / max(total, 1)))
 
 
 def _bcast_scalar(v, dev):
@@ -180,7 +237,7 @@ def run_tp(a):
     torch.manual_seed(0)
     full = Net()
     model = TPLeNet().load_from_full(full).to(dev)
-    opt = SGD(model.parameters(), lr=a.lr, momentum=0.9)
+    opt = SGD(model.parameters(), lr=a.lr, momentum=a.momentum)
     train_loader, test_loader = _data(a, dev)
     from dmlab.tasks.common import test, train
 

@@ -135,6 +135,80 @@ def _entry(rank, ws, port, kind, q):
                 cross_entropy(ref(X), Y).backward()
                 ropt.step()
             err = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
+        elif kind in ("lenet_fused_ddp", "lenet_fused_ddp_xgmi"):
+            # the fused 2-dispatch LeNet step with DDP (grads -> bucket all-reduce -> fused
+            # SGD) equals one process on the whole batch
+            from dmlab.models.lenet_fused import FusedLeNetStep
+            from dmlab.parallel import DDP
+
+            torch.manual_seed(0)
+            model = Net().to(dev)
+            ddp = DDP(model, small_allreduce="xgmi" if kind.endswith("xgmi") else None)
+            opt = ddp.fold_average_into(SGD(model.parameters(), lr=0.1, momentum=0.9))
+            step = FusedLeNetStep(model, opt, ddp=ddp)
+            for _ in range(3):
+                step(X[rank * 8:(rank + 1) * 8], Y[rank * 8:(rank + 1) * 8])
+                ropt.zero_grad()
+                cross_entropy(ref(X), Y).backward()
+                ropt.step()
+            err = max((a - b).abs().max().item() for a, b in zip(model.parameters(), ref.parameters()))
+        elif kind == "ddp_xgmi_graph":
+            # the whole DDP step (Program backward, bucket hooks, xGMI all-reduce kernel, fused
+            # SGD) captured into a hipGraph at world size 2 == the same step run eagerly,
+            # bit for bit
+            from dmlab.parallel import DDP
+            from dmlab.utils.graph import CapturedStep
+
+            runs = []
+            for captured in (False, True):
+                torch.manual_seed(0)
+                model = Net().to(dev)
+                ddp = DDP(model, small_allreduce="xgmi")
+                opt = ddp.fold_average_into(SGD(model.parameters(), lr=0.1, momentum=0.9))
+                xs, ys = X[rank * 8:(rank + 1) * 8].clone(), Y[rank * 8:(rank + 1) * 8].clone()
+
+                def train_step(x, y):
+                    loss = cross_entropy(ddp(x), y)
+                    opt.zero_grad()
+                    loss.backward()
+                    opt.step()
+                    return loss.detach()
+
+                if captured:
+                    cap = CapturedStep(train_step, [xs, ys], warmup=2, bind_inputs=True)
+                    for _ in range(3):
+                        cap(xs, ys)
+                else:
+                    for _ in range(5):  # the capture warm-up runs 2 eager steps
+                        train_step(xs, ys)
+                torch.cuda.synchronize()
+                ddp.check()
+                runs.append([p.detach().clone() for p in model.parameters()])
+            err = max((a - b).abs().max().item() for a, b in zip(*runs))
+            assert err == 0.0, err
+        elif kind in ("pipeline_xgmi", "pipeline_xgmi_gpipe"):
+            # the native xGMI stage transport (IPC ring, device flags; the two ranks share
+            # the GPU here), prefetched receives, 1F1B / GPipe
+            from dmlab.parallel.pipeline import PipelineStage
+
+            mod = (SubNetConv() if rank == 0 else SubNetFC()).to(dev)
+            sd = {k: v for k, v in ref.state_dict().items()
+                  if k.startswith("conv" if rank == 0 else "fc")}
+            mod.load_state_dict(sd)
+            st = PipelineStage(mod, SGD(mod.parameters(), lr=0.1, momentum=0.9), CrossEntropyLoss(),
+                               device=dev, transport="xgmi", timing=True,
+                               schedule="gpipe" if kind.endswith("gpipe") else "1f1b")
+            for _ in range(3):
+                st.train_step(X if rank == 0 else None, Y if rank == 0 else None, n_micro=4)
+                ropt.zero_grad()
+                cross_entropy(ref(X), Y).backward()
+                ropt.step()
+            step_ms, comp_ms, bubble = st.step_stats()
+            assert 0.0 <= bubble < 1.0 and comp_ms > 0.0
+            st.p2p.check()
+            err = max((p - ref.get_parameter(n)).abs().max().item()
+                      for n, p in mod.named_parameters())
+            st.p2p.close()
         else:
             from dmlab.parallel.pipeline import PipelineStage
 
@@ -160,7 +234,8 @@ def _entry(rank, ws, port, kind, q):
 
 
 @pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "ddp_resnet", "ddp_resnet_xgmi2", "pipeline",
-                                  "xgmi", "xgmi_graph"])
+                                  "xgmi", "xgmi_graph", "lenet_fused_ddp", "lenet_fused_ddp_xgmi",
+                                  "ddp_xgmi_graph", "pipeline_xgmi", "pipeline_xgmi_gpipe"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 
@@ -253,3 +328,31 @@ def test_xgmi_four_ranks_one_gpu():
     for rank, err, tb in res:
         assert tb is None, tb
         assert err < 2e-4, (rank, err)
+
+
+def test_bench_lenet_two_ranks_graph(tmp_path):
+    """bench.py --model lenet at 2 ranks (gloo process group on the shared GPU): with the
+    xGMI all-reduce kernel the whole DDP step (fused LeNet step, all-reduce, SGD) is captured
+    into a hipGraph at world size > 1 (hip_graph: true in the JSON line)."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    port = free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DMLAB_BACKEND="gloo",
+                   OMP_NUM_THREADS="2")
+        procs.append(subprocess.Popen(
+            [sys.executable, str(root / "bench.py"), "--gpus", "2", "--model", "lenet", "--steps",
+             "20", "--warmup", "5", "--small-allreduce", "xgmi", "--fused", "1"], cwd=tmp_path,
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
+    line = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["config"]["hip_graph"] is True
+    assert res["config"]["fused_step"] is True and res["value"] > 0

@@ -1,7 +1,6 @@
 """NHWC bf16 ResNet kernels (implicit-GEMM conv fwd/dgrad/wgrad, BN, pooling) vs
 PyTorch fp32 references computed on the same bf16-rounded inputs."""
 import math
-from pathlib import Path
 
 import pytest
 import torch
@@ -30,7 +29,8 @@ HALO_GEOMS = [
     (3, 14, 256, 256, 3, 1, 1),
     (2, 14, 64, 128, 1, 1, 0),
 ]
-FWD_CFGS = list(range(20)) + [20, 21, 22, 23, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39, 41, 42, 43, 44, 45]
+FWD_CFGS = list(range(9, 18)) + [20, 21, 39, 41, 42]
+HALO_CFGS = [20, 21, 39, 41, 42]
 
 
 def _rel(a, b):
@@ -65,120 +65,14 @@ def test_conv_fwd_and_stats(dev, geom, cfg):
 
 
 @pytest.mark.parametrize("geom", HALO_GEOMS)
-@pytest.mark.parametrize("cfg", [12, 20, 21, 24, 25, 36, 37, 38, 39, 41, 42, 43, 44, 45])
+@pytest.mark.parametrize("cfg", [12] + HALO_CFGS)
 def test_conv_fwd_halo(dev, geom, cfg):
     _check_fwd(dev, geom, cfg)
 
 
-def _h5_skip(cfg, cin_gemm):
-    # cfg 51 (512-pixel, single 64-channel chunk) has no fallback for other channel counts
-    if cfg == 51 and cin_gemm != 64:
-        pytest.skip("cfg 51 needs a single 64-channel chunk")
-
-
-H5_GEOMS = HALO_GEOMS + [GEOMS[0], GEOMS[3], (4, 56, 64, 64, 3, 1, 1), (2, 7, 512, 512, 3, 1, 1)]
-
-
-@pytest.mark.parametrize("geom", [(6, 14, 256, 256, 3, 1, 1), (14, 7, 128, 512, 3, 1, 1)])
-@pytest.mark.parametrize("pre", [False, True])
-def test_conv_fwd_tail_split(dev, geom, pre, monkeypatch):
-    """cfg 41 with a nearly empty last round moves that round's pixel rows to a launch of
-    128-pixel tiles (DMLAB_TAIL_SLOTS shrinks the slot count so small shapes split): same
-    outputs, and statistics rows = main tiles + tail tiles."""
-    monkeypatch.setenv("DMLAB_TAIL_SLOTS", "16")
-    N, H, Cin, Cout, k, s, p = geom
-    M = N * H * H
-    T = lib().conv_stats_rows(M, 41, Cout)
-    assert T > (M + 255) // 256  # the split applies
-    if pre:
-        g = torch.Generator(device=dev).manual_seed(4)
-        y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
-        sc = torch.rand(Cin, device=dev, generator=g) + 0.5
-        sh = torch.randn(Cin, device=dev, generator=g) * 0.5
-        w = torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k)
-        wf = torch.empty(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16)
-        lib().pack_weights(w.contiguous(), wf, None, Cin)
-        a = (y.float() * sc + sh).relu().bfloat16().float()
-        ref = F.conv2d(_nchw(a), w.bfloat16().float(), None, s, p)
-        out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
-        stats = torch.full((T * 2 * Cout,), float("nan"), device=dev)
-        lib().conv_fwd(y, wf, out, stats, None, k, k, s, p, 41, pre_scale=sc, pre_shift=sh)
-    else:
-        x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
-        ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
-        out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
-        stats = torch.full((T * 2 * Cout,), float("nan"), device=dev)
-        lib().conv_fwd(xn, wf, out, stats, None, k, k, s, p, 41)
-    assert _rel(_nchw(out), ref) < 6e-3
-    st = stats.view(T, 2, Cout).sum(0)  # every row written (NaN-filled before)
-    torch.testing.assert_close(st[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
-    torch.testing.assert_close(st[1], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
-    # data gradient through the same split (stride 1: the flipped-tap geometry)
-    x2, w2, xn2, wf2, wd2 = _setup(dev, N, H, Cout, Cin, k, s, p)
-    dy = torch.randn(N, Cin, H, H, device=dev).bfloat16()
-    dref = torch.nn.grad.conv2d_input((N, Cout, H, H), w2.bfloat16().float(), dy.float(), s, p)
-    dx = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
-    lib().conv_dgrad(_nhwc(dy), wd2, dx, k, k, s, p, None, 41)
-    assert _rel(_nchw(dx), dref) < 6e-3
-
-
-L1_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 14, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
-            (1, 9, 64, 64, 3, 1, 1)]
-
-
-@pytest.mark.parametrize("geom", L1_GEOMS)
-def test_conv_fwd_l1_persistent(dev, geom):
-    """Persistent resident-weight 64->64 kernel (conv_l1.hip, cfg 70): tiles crossing image
-    rows and images, partial last tile, fewer tiles than CUs."""
-    _check_fwd(dev, geom, 70)
-
-
-@pytest.mark.parametrize("geom", L1_GEOMS)
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_conv_dgrad_l1_persistent(dev, geom, accumulate):
-    N, H, Cin, Cout, k, s, p = geom
-    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
-    dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
-    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w.bfloat16().float(), dy.float(), s, p)
-    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
-    base = dx.clone()
-    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, 70)
-    if accumulate:
-        ref = ref + _nchw(base).float()
-    assert _rel(_nchw(dx), ref) < 6e-3
-
-
-@pytest.mark.parametrize("geom", H5_GEOMS)
-@pytest.mark.parametrize("cfg", [50, 51])
-def test_conv_fwd_h5(dev, geom, cfg):
-    """LDS-DMA halo kernel (conv_h5.hip): 256 x 128 and 512 x 64 tiles, 1x1 and 3x3 taps,
-    several chunks (double-buffered halo), blocks crossing images, partial last block."""
-    _h5_skip(cfg, geom[2])
-    _check_fwd(dev, geom, cfg)
-
-
-@pytest.mark.parametrize("geom", H5_GEOMS)
-@pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [50, 51])
-def test_conv_dgrad_h5(dev, geom, accumulate, cfg):
-    _h5_skip(cfg, geom[3])
-    N, H, Cin, Cout, k, s, p = geom
-    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
-    wb = w.bfloat16().float()
-    OH = (H + 2 * p - k) // s + 1
-    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
-    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wb, dy.float(), s, p)
-    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
-    base = dx.clone()
-    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, cfg)
-    if accumulate:
-        ref = ref + _nchw(base).float()
-    assert _rel(_nchw(dx), ref) < 6e-3
-
-
 def _check_fwd(dev, geom, cfg):
     N, H, Cin, Cout, k, s, p = geom
-    if cfg in (0, 3, 6, 9, 12, 15, 18, 26, 34, 36, 38) and Cout % 128:
+    if cfg in (9, 12, 15) and Cout % 128:
         pytest.skip("128-wide tile needs Cout % 128 == 0")
     x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p)
     ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
@@ -206,7 +100,7 @@ def test_conv_fwd_add(dev):
 
 @pytest.mark.parametrize("geom", GEOMS[:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("variant", [2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [3, 4, 5])
 def test_conv_dgrad(dev, geom, accumulate, variant):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
@@ -225,7 +119,7 @@ def test_conv_dgrad(dev, geom, accumulate, variant):
 
 @pytest.mark.parametrize("geom", HALO_GEOMS + GEOMS[:2] + GEOMS[3:5])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [20, 21, 24, 25, 26, 27, 28, 34, 35, 36, 37, 38, 39, 41, 42, 43, 44, 45])
+@pytest.mark.parametrize("cfg", HALO_CFGS)
 def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
@@ -236,32 +130,6 @@ def test_conv_dgrad_halo(dev, geom, accumulate, cfg):
     dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
     base = dx.clone()
     lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, cfg)
-    if accumulate:
-        ref = ref + _nchw(base).float()
-    assert _rel(_nchw(dx), ref) < 6e-3
-
-
-S2_GEOMS = [  # stride-2 3x3 dgrad, all parity classes per block (cfg 80)
-    (2, 56, 64, 128, 3, 2, 1),   # layer2: dY 28x28, a block spans 5 dY rows
-    (3, 28, 128, 256, 3, 2, 1),  # layer3: 2 N tiles (XCD-ordered 1-D grid), 4 chunks
-    (5, 14, 256, 512, 3, 2, 1),  # layer4: dY 7x7, blocks cross images, partial last block
-    (2, 16, 64, 64, 3, 2, 1),
-    (2, 9, 64, 128, 3, 2, 1),    # odd input: class grids differ -> per-class igemm fallback
-]
-
-
-@pytest.mark.parametrize("geom", S2_GEOMS)
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_conv_dgrad_s2_classes(dev, geom, accumulate):
-    N, H, Cin, Cout, k, s, p = geom
-    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
-    wb = w.bfloat16().float()
-    OH = (H + 2 * p - k) // s + 1
-    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
-    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), wb, dy.float(), s, p)
-    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
-    base = dx.clone()
-    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, 80)
     if accumulate:
         ref = ref + _nchw(base).float()
     assert _rel(_nchw(dx), ref) < 6e-3
@@ -278,8 +146,8 @@ def test_conv_wgrad(dev, geom):
     for beta in (0.0, 1.0):
         dw = torch.randn_like(w) if beta else torch.empty_like(w)
         base = dw.clone()
-        big = 0 if Cout % 128 == 0 else 1
-        for S, cfg in ((1, big), (3, 1), (1, big + 2), (3, 3)):
+        big = 2 if Cout % 128 == 0 else 3
+        for S, cfg in ((1, big), (3, 3), (2, 6)):
             K = k * k * _cpad(Cin)
             slab = torch.empty(S * Cout * K, device=dev)
             d = dw.clone()
@@ -544,25 +412,28 @@ def test_bn_stats_finalize_slab_rows(dev, T, C):
     var = (qd / M - mu * mu).clamp_min(0)
     torch.testing.assert_close(mean.double(), mu, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(invstd.double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=1e-6)
-    # the one-launch finalize (column sums + per-channel-group last-block finalize, ticket
-    # counters) is bit-identical, leaves its counters at 0 and increments num_batches once per call
-    ctr = torch.zeros(32, dtype=torch.int32, device=dev)  # one per 32-channel group
+    # num_batches_tracked is incremented once per call by the finalize kernel
     nb = torch.zeros(1, dtype=torch.int64, device=dev)
-    for rep in range(3):
+    for rep in range(2):
         out = [torch.empty(C, **f) for _ in range(4)]
         lib().bn_stats_finalize(stats.view(-1), T, M, gamma, beta, None, None, 0.1, 1e-5, *out,
-                                torch.empty(512 * C, **f), nb, counter=ctr)
+                                torch.empty(512 * C, **f), nb)
         for a, b in zip(out, (scale, shift, mean, invstd)):
             assert torch.equal(a, b)
-        assert int(ctr.abs().sum().item()) == 0 and int(nb.item()) == rep + 1
+        assert int(nb.item()) == rep + 1
 
 
-@pytest.mark.parametrize("geom", [g for g in H5_GEOMS if g[4] == 3] + L1_GEOMS[1:])
-@pytest.mark.parametrize("cfg", [20, 21, 38, 39, 41, 42, 43, 44, 45, 50, 51, 70, 90, 91, 92, 93])
+PREBN_GEOMS = [g for g in HALO_GEOMS if g[4] == 3] + [GEOMS[0], GEOMS[3], (4, 56, 64, 64, 3, 1, 1),
+                                                         (2, 7, 512, 512, 3, 1, 1),
+                                                         (2, 14, 64, 64, 3, 1, 1),
+                                                         (5, 7, 64, 64, 3, 1, 1), (1, 9, 64, 64, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geom", PREBN_GEOMS)
+@pytest.mark.parametrize("cfg", HALO_CFGS + [90, 91, 92, 93])
 def test_conv_fwd_prebn(dev, geom, cfg):
     """Halo conv consuming relu(y*scale + shift) of a RAW previous-conv output (fused
     BN-apply + ReLU in the staging); zero padding stays zero after the BN."""
-    _h5_skip(cfg, geom[2])
     N, H, Cin, Cout, k, s, p = geom
     g = torch.Generator(device=dev).manual_seed(2)
     y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
@@ -632,7 +503,7 @@ def test_pack_weights_tiled_matches_per_layer(dev):
                                   (2, 7, 128, 256, 3, 1, 1)])
 @pytest.mark.parametrize("mode", [0, 1, 2, 4])
 @pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 41, 42, 43, 44, 45, 50])
+@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 41, 42])
 def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     """The dgrad epilogue's BN-backward sums (Σdz, Σdz·x̂ of the BN whose input gradient dx
     is) equal the sums over the stored dx; the BN backward run from them equals the
@@ -640,8 +511,6 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
     N, H, Cin, Cout, k, s, p = geom
     if s == 2 and cfg not in (15, 16):
         pytest.skip("stride-2 dgrad runs on the v3 tiles")
-    if cfg == 50 and Cin % 128:
-        pytest.skip("cfg 50: 128-wide column tile")
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
     OH = (H + 2 * p - k) // s + 1
     g = torch.Generator(device=dev).manual_seed(9)
@@ -690,138 +559,9 @@ def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
                       sc if mode == 2 else None, sh if mode == 2 else None, None, None, 3, 2, 1,
                       dyy, None, work, mask=mask if mode == 4 else None, **kw)
         res.append((dyy.float(), dg, db))
-        if not pre:  # the one-launch finalize (ticket counter) is bit-identical
-            ctr = torch.zeros(32, dtype=torch.int32, device=dev)  # one per 32-channel group
-            d2, dg2, db2 = torch.empty_like(y), torch.zeros(Cin, **f), torch.zeros(Cin, **f)
-            L.bn_backward(dx, out if mode == 1 else None, y, mean, invstd, gamma, dg2, db2, 0.0,
-                          mode, sc if mode == 2 else None, sh if mode == 2 else None, None, None,
-                          3, 2, 1, d2, None, torch.empty_like(work),
-                          mask=mask if mode == 4 else None, counter=ctr)
-            assert torch.equal(d2, dyy) and torch.equal(dg2, dg) and torch.equal(db2, db)
-            assert int(ctr.abs().sum().item()) == 0
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-4, atol=1e-3)
     assert _rel(res[0][0], res[1][0]) < 1e-3
-
-
-BWD_LOAD_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 14, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
-                  (1, 9, 64, 64, 3, 1, 1)]
-
-
-@pytest.mark.parametrize("geom", BWD_LOAD_GEOMS)
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_bn_backward_apply_on_load(dev, geom, accumulate):
-    """A conv's dgrad (cfg 39) and halo weight gradient (cfg 4/5) staging the BN-backward
-    apply a*dz' + b*y + cc from (dz, y) == the same kernels fed the dy that the apply pass
-    writes; bn_backward without dy leaves dgamma/dbeta and the coefficients in work."""
-    N, H, Cin, Cout, k, s, p = geom
-    L = lib()
-    f = dict(device=dev, dtype=torch.float32)
-    g = torch.Generator(device=dev).manual_seed(11)
-    M = N * H * H
-    y = (torch.randn(N, H, H, Cout, device=dev, generator=g) * 1.5).bfloat16()
-    dz = torch.randn(N, H, H, Cout, device=dev, generator=g).bfloat16()
-    gamma = torch.rand(Cout, **f) + 0.5
-    beta = torch.randn(Cout, **f) * 0.3
-    yf = y.float().view(M, Cout)
-    stats = torch.stack([yf.sum(0), (yf ** 2).sum(0)]).reshape(-1).contiguous()
-    scale, shift, mean, invstd = (torch.empty(Cout, **f) for _ in range(4))
-    L.bn_stats_finalize(stats, 1, float(M), gamma, beta, None, None, 0.1, 1e-5, scale, shift,
-                        mean, invstd, torch.empty(512 * Cout, **f))
-    # reference: the apply pass writes dy
-    dy = torch.empty_like(y)
-    dg, db = torch.zeros(Cout, **f), torch.zeros(Cout, **f)
-    work = torch.empty(L.bn_bwd_work(M, Cout), **f)
-    L.bn_backward(dz, None, y, mean, invstd, gamma, dg, db, 0.0, 2, scale, shift, None, None,
-                  3, 2, 1, dy, None, work)
-    # coefficients only
-    dg2, db2 = torch.zeros(Cout, **f), torch.zeros(Cout, **f)
-    work2 = torch.empty_like(work)
-    L.bn_backward(dz, None, y, mean, invstd, gamma, dg2, db2, 0.0, 2, scale, shift, None, None,
-                  3, 2, 1, None, None, work2)
-    assert torch.equal(dg2, dg) and torch.equal(db2, db)
-    off = L.bn_bwd_coef_offset(M, Cout, False)
-    bkw = dict(bwd_y=y, bwd_coef=work2[off:off + 3 * Cout], bwd_scale=scale, bwd_shift=shift)
-    # dgrad
-    w = torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k)
-    wd = torch.empty(Cin, k, k, Cout, device=dev, dtype=torch.bfloat16)
-    L.pack_weights(w.contiguous(), torch.empty(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16),
-                   wd, Cin)
-    base = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
-    dx_ref, dx = base.clone(), base.clone()
-    L.conv_dgrad(dy, wd, dx_ref, k, k, s, p, dx_ref if accumulate else None, 39)
-    L.conv_dgrad(dz, wd, dx, k, k, s, p, dx if accumulate else None, 39, **bkw)
-    torch.testing.assert_close(dx.float(), dx_ref.float(), rtol=1e-2, atol=1e-2)
-    assert _rel(dx, dx_ref) < 1e-3
-    # weight gradient, both halo variants
-    x = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
-    for cfg in (4, 5):
-        from dmlab.ops.convbn import _wgrad_plan
-        _, S = _wgrad_plan(M, Cout, k * k * Cin, k, s, Cin, force=cfg)
-        slab = torch.empty(S * Cout * k * k * Cin, **f)
-        dw_ref, dw = torch.empty(Cout, Cin, k, k, **f), torch.empty(Cout, Cin, k, k, **f)
-        L.conv_wgrad(x, dy, dw_ref, slab, Cin, k, k, s, p, 0.0, S, cfg, False)
-        L.conv_wgrad(x, dz, dw, slab, Cin, k, k, s, p, 0.0, S, cfg, False, **bkw)
-        assert _rel(dw, dw_ref) < 1e-4, cfg
-
-
-def test_conv_halo_persistent_opt_in(dev, tmp_path):
-    """The opt-in persistent single-chunk halo conv (DMLAB_HALO_PERS=1, read once per process,
-    so checked in a child process): forward with statistics, the fused pre-BN operand and the
-    dgrad equal the per-tile cfg-39 kernel of this process."""
-    import subprocess
-    import sys
-
-    N, H, C = 6, 56, 64  # 6 * 56 * 56 / 256 = 73.5 tiles: a partial last tile
-    g = torch.Generator(device=dev).manual_seed(5)
-    x = torch.randn(N, H, H, C, device=dev, generator=g).bfloat16()
-    w = torch.randn(C, C, 3, 3, device=dev, generator=g) / 24.0
-    sc = torch.rand(C, device=dev, generator=g) + 0.5
-    sh = torch.randn(C, device=dev, generator=g) * 0.3
-    wf = torch.empty(C, 3, 3, C, device=dev, dtype=torch.bfloat16)
-    wd = torch.empty(C, 3, 3, C, device=dev, dtype=torch.bfloat16)
-    lib().pack_weights(w.contiguous(), wf, wd, C)
-    M = N * H * H
-    T = lib().conv_stats_rows(M, 39, C)
-
-    def run():
-        y = torch.empty_like(x)
-        st = torch.empty(T * 2 * C, device=dev)
-        lib().conv_fwd(x, wf, y, st, None, 3, 3, 1, 1, 39)
-        yp = torch.empty_like(x)
-        lib().conv_fwd(x, wf, yp, torch.empty_like(st), None, 3, 3, 1, 1, 39, pre_scale=sc,
-                       pre_shift=sh)
-        dx = torch.empty_like(x)
-        lib().conv_dgrad(x, wd, dx, 3, 3, 1, 1, None, 39)
-        return y, st, yp, dx
-
-    ref = run()
-    path = tmp_path / "ref.pt"
-    torch.save({"x": x.cpu(), "wf": wf.cpu(), "wd": wd.cpu(), "sc": sc.cpu(), "sh": sh.cpu(),
-                "ref": [t.cpu() for t in ref]}, path)
-    code = f"""
-import sys, torch
-sys.path.insert(0, {str(Path(__file__).resolve().parent.parent)!r})
-from dmlab.ops._native import lib
-d = torch.load({str(path)!r}, weights_only=True)
-dev = torch.device("cuda")
-x, wf, wd, sc, sh = (d[k].to(dev) for k in ("x", "wf", "wd", "sc", "sh"))
-C, M = x.shape[3], x.numel() // x.shape[3]
-T = lib().conv_stats_rows(M, 39, C)
-y = torch.empty_like(x); st = torch.empty(T * 2 * C, device=dev)
-lib().conv_fwd(x, wf, y, st, None, 3, 3, 1, 1, 39)
-yp = torch.empty_like(x)
-lib().conv_fwd(x, wf, yp, torch.empty_like(st), None, 3, 3, 1, 1, 39, pre_scale=sc, pre_shift=sh)
-dx = torch.empty_like(x)
-lib().conv_dgrad(x, wd, dx, 3, 3, 1, 1, None, 39)
-for a, b in zip((y, st, yp, dx), d["ref"]):
-    assert torch.equal(a.cpu(), b), "mismatch"
-print("OK")
-"""
-    env = dict(__import__("os").environ, DMLAB_HALO_PERS="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
-                       timeout=300)
-    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
 
 
 # pipelined LDS-DMA tiles (conv_pipe.hip, cfg 90/91/92): 3x3 and 1x1 taps, stride 1 and 2,

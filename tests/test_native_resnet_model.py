@@ -139,63 +139,3 @@ def test_deferred_wgrads_match(dev, monkeypatch, defer):
         for u, p in zip(s1[i], a.layers[i].parameters()):
             torch.testing.assert_close(u, g1[[n for n, q in a.named_parameters() if q is p][0]],
                                        rtol=0, atol=0)
-
-
-def test_input_prefetch_matches(dev):
-    """ResNet18.prefetch(next_x): the next batch's space-to-depth packing runs on the side
-    stream during the stem backward and the next forward consumes it -- losses and
-    gradients are bit-identical to packing inline; a batch modified after the prefetch
-    (new version) is packed again instead of using the stale copy."""
-    from dmlab.optim import SGD
-
-    xs = [torch.rand(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
-          for _ in range(2)]
-    ys = [torch.randint(0, 10, (8,), device=dev) for _ in range(2)]
-    runs = []
-    for pf in (False, True):
-        torch.manual_seed(6)
-        m = ResNet18(num_classes=10).to(dev)
-        opt = SGD(m.parameters(), lr=0.05, momentum=0.9)
-        losses = []
-        for i in range(4):
-            loss = cross_entropy(m(xs[i % 2]), ys[i % 2])
-            if pf:
-                m.prefetch(xs[(i + 1) % 2])
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-            losses.append(loss.detach())
-        torch.cuda.synchronize()
-        runs.append((torch.stack(losses), {n: p.detach().clone() for n, p in m.named_parameters()}))
-        if pf:
-            assert m.stem._prefetched is not None  # the last prefetch (of xs[0]) is pending
-            xs[0].mul_(0.5)  # version bump: the forward must not use the stale packing
-            out_new = m(xs[0])
-            assert m.stem._prefetched is None
-            out_ref = m(xs[0].clone())
-            torch.testing.assert_close(out_new, out_ref, rtol=0, atol=0)
-    torch.testing.assert_close(runs[1][0], runs[0][0], rtol=0, atol=0)
-    for n in runs[0][1]:
-        torch.testing.assert_close(runs[1][1][n], runs[0][1][n], rtol=0, atol=0, msg=n)
-
-
-def test_bn_backward_apply_on_load_matches(dev, monkeypatch):
-    """Layer-1 c1 with the BN-backward apply fused into its dgrad / weight-gradient operand
-    staging (convbn._BN_BWD_ON_LOAD) trains like the apply-pass path: same losses and
-    gradients up to bf16 rounding of the fused dy."""
-    import dmlab.ops.convbn as cb
-
-    x = torch.rand(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
-    y = torch.randint(0, 10, (8,), device=dev)
-    res = []
-    for on in (False, True):
-        monkeypatch.setattr(cb, "_BN_BWD_ON_LOAD", on)
-        torch.manual_seed(7)
-        m = ResNet18(num_classes=10).to(dev)
-        loss = cross_entropy(m(x), y)
-        loss.backward()
-        torch.cuda.synchronize()
-        res.append((loss.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
-    torch.testing.assert_close(res[1][0], res[0][0], rtol=0, atol=0)
-    for n in res[0][1]:
-        assert _rel(res[1][1][n], res[0][1][n]) < 2e-3, n

@@ -73,3 +73,18 @@ def test_task3_torchrun_random_sampler(tmp_path):
                 "--device", "cpu", "--synthetic", "--train-samples", "2560", "--epochs", "1",
                 "--sampler", "random", "--lr", "0.01"], tmp_path)
     assert "Device: 0 epoch: 1" in out and "Test set: Accuracy" in out
+
+
+def test_task3_resnet18_imagenet_shape(tmp_path):
+    """``--image-size 224 --num-classes 1000``: lab 3 trains the BASELINE ResNet-18 config
+    (ImageNet-shaped input, 1000-way head) under DDP; two ranks, two steps on the CPU."""
+    import json
+
+    js = tmp_path / "r.json"
+    _run(["-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+          "127.0.0.1", "--master-port", str(free_port()), "-m", "dmlab.tasks.task3",
+          "--device", "cpu", "--model", "resnet18", "--image-size", "224", "--num-classes",
+          "1000", "--train-samples", "8", "--batch-size", "2", "--max-steps", "2",
+          "--epochs", "1", "--no-test", "--json", str(js)], tmp_path, timeout=600)
+    r = json.loads(js.read_text())
+    assert r["world_size"] == 2 and r["samples"] > 0
