@@ -166,8 +166,7 @@ def main():
             return captured[i % 2](pool[i % 2], labels[i % 2])
     else:
         def step(i):
-            return train_step(pool[i % 2], labels[i % 2],
-                              pool[(i + 1) % 2] if a.model == "resnet18" else None)
+            return train_step(pool[i % 2], labels[i % 2])
 
     for i in range(a.warmup):
         loss = step(i)

@@ -43,29 +43,6 @@ constexpr int PBM = 256;   // output pixels per tile
 constexpr int PBK = 64;    // K per step (one 128-B LDS row per tile row)
 constexpr unsigned POOB = 0x80000000u;
 
-typedef int pi32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ pi32x4 prsrc(const void* base, unsigned bytes) {
-  const unsigned long long a = (unsigned long long)base;
-  pi32x4 r;
-  r[0] = (int)(unsigned)a;
-  r[1] = (int)(unsigned)(a >> 32) & 0xffff;
-  r[2] = (int)bytes;
-  r[3] = 0x00020000;
-  return r;
-}
-
-// lane l's 16 bytes at buffer byte `off` -> LDS byte lds + 16*l (lds wave-uniform, in an SGPR)
-__device__ __forceinline__ void pdma16(const pi32x4& rs, unsigned lds, unsigned off) {
-  asm volatile(
-      "s_mov_b32 m0, %1\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %0, %2, 0 offen lds"
-      :
-      : "v"(off), "s"(lds), "s"(rs)
-      : "memory");
-}
-
 // BN output channels per tile (256 / 128 / 64); WM x WN waves, wave tile 256/WM x BN/WN;
 // MINW waves per SIMD the register budget is sized for; PRE: the operand is
 // relu(x * pre_sc + pre_sh) of the stored x (the previous conv's raw output): each thread

@@ -23,6 +23,31 @@ __device__ __forceinline__ unsigned fdiv(unsigned n, unsigned mul, unsigned shr)
 // 16- and 32-row fragment reads of both MFMA shapes
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// Buffer resource for LDS-DMA issued from inline asm (range-checked: offsets >= bytes read 0)
+typedef int pi32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ pi32x4 prsrc(const void* base, unsigned bytes) {
+  const unsigned long long a = (unsigned long long)base;
+  pi32x4 r;
+  r[0] = (int)(unsigned)a;
+  r[1] = (int)(unsigned)(a >> 32) & 0xffff;
+  r[2] = (int)bytes;
+  r[3] = 0x00020000;
+  return r;
+}
+
+// LDS-DMA: lane l's 16 bytes at buffer byte `off` -> LDS byte lds + 16*l (lds wave-uniform).
+// Issued from inline asm so the compiler's alias-blind LDS-DMA tracking does not put a
+// vmcnt(0) before every ds_read; the caller retires it with its own s_waitcnt vmcnt.
+__device__ __forceinline__ void pdma16(const pi32x4& rs, unsigned lds, unsigned off) {
+  asm volatile(
+      "s_mov_b32 m0, %1\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %0, %2, 0 offen lds"
+      :
+      : "v"(off), "s"(lds), "s"(rs)
+      : "memory");
+}
+
 // Fused BatchNorm-apply + ReLU of a staged 16-B chunk (8 bf16 channels c0..c0+7):
 // v = max(v * sc[c] + sh[c], 0).  Used by the halo kernels to read a conv's RAW output and
 // consume BN(y) directly, so the normalised activation is never written to memory.

@@ -53,7 +53,12 @@ def _env(threads):
     # test accuracy is capped near 91 %), so the comparisons do not all saturate at 100 %
     e.setdefault("DMLAB_SYNTH_NOISE", "0.7")
     e.setdefault("DMLAB_SYNTH_LABEL_NOISE", "0.1")
+    if _SHARED_GPU:
+        e.setdefault("DMLAB_BACKEND", "gloo")  # RCCL rejects two ranks on one GPU
     return e
+
+
+_SHARED_GPU = False  # set in main(): --device cuda with fewer GPUs than ranks
 
 
 def run_task(mod, args, nproc=1, threads=1, timeout=1200):
@@ -201,26 +206,32 @@ def exp_straggler(a, out):
     collective)."""
     res = []
     delays = (0, 20, 50)
-    for d in delays:
-        with tempfile.TemporaryDirectory() as td:
-            js = Path(td) / "s.json"
-            args = ["--device", a.device, "--synthetic", "--max-steps", str(a.steps3),
-                    "--no-test", "--epochs", "1", "--json", str(js)]
-            if d:
-                args += ["--straggler-rank", "1", "--straggler-delay-ms", str(d),
-                         "--straggler-mode", "host"]
-            o, dt = run_task("task2", args, nproc=2)
-            s = json.loads(js.read_text())
-        res.append({"delay_ms": d, "mode": "host", "steps": s["steps"],
-                    "step_ms": 1e3 * s["train_time"] / max(s["steps"], 1),
-                    "comm_ms_per_step": 1e3 * s["comm_time"] / max(s["steps"], 1),
-                    "samples_per_s": s["samples_per_s"]})
+    # host: time.sleep on the straggler (the reference's hook); device: a spin kernel on its
+    # stream, so the delay sits in the GPU queue in front of the collective (GPU only)
+    modes = ("host", "device") if a.device == "cuda" else ("host",)
+    for mode in modes:
+        for d in delays:
+            with tempfile.TemporaryDirectory() as td:
+                js = Path(td) / "s.json"
+                args = ["--device", a.device, "--synthetic", "--max-steps", str(a.steps3),
+                        "--no-test", "--epochs", "1", "--json", str(js)]
+                if d:
+                    args += ["--straggler-rank", "1", "--straggler-delay-ms", str(d),
+                             "--straggler-mode", mode]
+                o, dt = run_task("task2", args, nproc=2)
+                s = json.loads(js.read_text())
+            res.append({"delay_ms": d, "mode": mode, "steps": s["steps"],
+                        "step_ms": 1e3 * s["train_time"] / max(s["steps"], 1),
+                        "comm_ms_per_step": 1e3 * s["comm_time"] / max(s["steps"], 1),
+                        "samples_per_s": s["samples_per_s"]})
     (out / "c_straggler.json").write_text(json.dumps(res, indent=1))
-    _plot(out / "c_straggler.png",
-          {"step time (rank 0)": (delays, [r["step_ms"] for r in res]),
-           "comm time (rank 0)": (delays, [r["comm_ms_per_step"] for r in res])},
-          "straggler delay on rank 1 (ms per step)", "ms per step",
-          "Lab 2: bottleneck node (2 ranks, all-reduce)")
+    series = {}
+    for mode in modes:
+        rs = [r for r in res if r["mode"] == mode]
+        series[f"step time, {mode} delay"] = (delays, [r["step_ms"] for r in rs])
+        series[f"comm time, {mode} delay"] = (delays, [r["comm_ms_per_step"] for r in rs])
+    _plot(out / "c_straggler.png", series, "straggler delay on rank 1 (ms per step)",
+          "rank-0 ms per step", f"Lab 2: bottleneck node (2 ranks, all-reduce, {a.device})")
     return res
 
 
@@ -300,11 +311,11 @@ def write_report(out, R, a):
         L.append("")
     if "c" in R:
         L += ["## (c) Bottleneck node (checking.tex:22)", "", "![](c_straggler.png)", "",
-              "| delay on rank 1 (ms) | rank-0 step ms | rank-0 comm ms/step | samples/s |",
-              "|---|---|---|---|"]
+              "| delay mode | delay on rank 1 (ms) | rank-0 step ms | rank-0 comm ms/step | samples/s |",
+              "|---|---|---|---|---|"]
         for r in R["c"]:
-            L.append(f"| {r['delay_ms']} | {r['step_ms']:.2f} | {r['comm_ms_per_step']:.2f} | "
-                     f"{r['samples_per_s']:.0f} |")
+            L.append(f"| {r.get('mode', 'host')} | {r['delay_ms']} | {r['step_ms']:.2f} | "
+                     f"{r['comm_ms_per_step']:.2f} | {r['samples_per_s']:.0f} |")
         L.append("")
     if "d" in R:
         L += ["## (d) Data partitioning: random sampling vs random partition (checking.tex:15)", "",
@@ -344,6 +355,11 @@ def main(argv=None):
     ap.add_argument("--steps5", type=int, default=300)
     a = ap.parse_args(argv)
     a.world_sizes = [int(w) for w in a.world_sizes.split(",")]
+    global _SHARED_GPU
+    if a.device == "cuda":
+        import torch
+
+        _SHARED_GPU = torch.cuda.device_count() < max(a.world_sizes + [3])
     out = Path(a.out)
     out.mkdir(parents=True, exist_ok=True)
     exps = {"a": exp_optimizers, "b": exp_comm, "c": exp_straggler, "d": exp_sampling,
