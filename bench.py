@@ -128,7 +128,9 @@ def main():
               small_cap_mb=a.xgmi_cap_mb)
     net.fold_average_into(opt)
     if a.fused < 0:
-        a.fused = 0  # flipped on once the fused step beats the layer-wise one
+        # the 2-dispatch fused step: 587k vs 205k img/s layer-wise at batch 32
+        # (profiles/bench_lenet_fused_v2_r3b.jsonl)
+        a.fused = 1 if (a.model == "lenet" and a.backend == "native") else 0
     fused = None
     if a.fused and a.model == "lenet":
         from dmlab.models.lenet_fused import FusedLeNetStep

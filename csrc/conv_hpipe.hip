@@ -40,12 +40,12 @@ template <int BN, int HR, bool PRE>
 __global__ void __launch_bounds__(256, 2) conv_hpipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes, int mtiles, int ntN,
-    int nitems, const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
+    int nitems, int ipb, const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
   constexpr int NW = 4, WN = 2;
   constexpr int TN = BN / WN;             // wave tile 64 x TN
   constexpr int RM = 2, RN = TN / 32;     // 32x32 blocks per wave
   constexpr int NP = HR / 8;              // halo pieces (8 rows x 128 B) per chunk
-  constexpr int PPW = (NP + NW - 1) / NW; // pieces per wave, one per tap
+  constexpr int PPW = (NP + NW - 1) / NW; // pieces per wave, two per tap over taps 0-3
   constexpr int BI = BN / 32;             // weight pieces per wave per K step
   constexpr unsigned HB = HR * 128u, BB = BN * 128u;
   constexpr int ZROW = HR - 1;            // never DMA'd as a real row: stays zero
@@ -65,8 +65,12 @@ __global__ void __launch_bounds__(256, 2) conv_hpipe_kernel(
   const int hp = QBM + 2 * W + 2;  // halo rows an item reads (< HR: row HR-1 stays zero)
   const int nchunk = C / 64;
   const int SI = 9 * nchunk;       // K steps per item
+  // items of this workgroup: ipb > 0: the contiguous run [b*ipb, b*ipb + ipb) (the hardware
+  // balances the blocks over the CUs; a block prefetches across its own items only);
+  // ipb == 0: persistent, items b, b+G, b+2G, ...
   const int G = gridDim.x;
-  const int nmine = (nitems - (int)blockIdx.x + G - 1) / G;
+  const int nmine = ipb > 0 ? min(ipb, nitems - (int)blockIdx.x * ipb)
+                            : (nitems - (int)blockIdx.x + G - 1) / G;
   const int S = nmine * SI;
 
   // DMA lane geometry: lane l of piece p fills row 8p + l/8, physical 16-B slot l%8, which holds
@@ -76,7 +80,12 @@ __global__ void __launch_bounds__(256, 2) conv_hpipe_kernel(
   const unsigned choff = (unsigned)dch * 16u;
 
   auto item_mn = [&](int k, int& mt, int& nt) __attribute__((always_inline)) {
-    const int j = (int)blockIdx.x + k * G;
+    const int j = ipb > 0 ? (int)blockIdx.x * ipb + k : (int)blockIdx.x + k * G;
+    if (ntN == 1 || ipb > 0) {  // contiguous runs: a block takes all N tiles of its M tiles
+      mt = j / ntN;
+      nt = j - mt * ntN;
+      return;
+    }
     if (ntN == 1) {
       mt = j;
       nt = 0;
@@ -151,7 +160,7 @@ __global__ void __launch_bounds__(256, 2) conv_hpipe_kernel(
   auto xform = [&](int j, int hb) __attribute__((always_inline)) {
     if constexpr (PRE) {
       const int row = 8 * (wid + 4 * j) + (lane >> 3);
-      if (wid + 4 * j >= NP || row >= hp) return;
+      if (j >= PPW || wid + 4 * j >= NP || row >= hp) return;
       uint4* q = reinterpret_cast<uint4*>(smem + hb * HB + (wid + 4 * j) * 1024 + lane * 16);
       const uint4 v = *q;
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -351,8 +360,8 @@ __global__ void __launch_bounds__(256, 2) conv_hpipe_kernel(
 
   using T_ = std::true_type;
   using F_ = std::false_type;
-  int xpend = -1;  // PRE: halo piece issued at the previous DMA slot (transformed at the barrier)
-  int xhb = 0;
+  int xpend = -1;  // PRE: halo pieces 2j, 2j+1 issued at the previous DMA slot (transformed
+  int xhb = 0;     // after this step's barrier: nobody reads them before the next chunk)
   for (int s = 0; s < S; ++s) {
     const unsigned sto = (unsigned)(s & 1) * BB;
     const unsigned hbo = (unsigned)hbc * HB;
@@ -363,13 +372,18 @@ __global__ void __launch_bounds__(256, 2) conv_hpipe_kernel(
     for (int q = 0; q < BI; ++q) bdo[q] = kb < nmine ? b_off(q, n0b, ccb, tb) : QOOB;
     sub(f0, f1, hbo, ha, sto, 3, F_{}, 0u);
     // ---- the step's barrier: everything issued at the previous DMA slot has landed ----
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (xpend >= 0) xform(xpend, xhb);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // halo piece j = tc of the next chunk (this wave's share, one per tap)
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (xpend >= 0) {
+      xform(2 * xpend, xhb);
+      xform(2 * xpend + 1, xhb);
+    }
+    // halo pieces 2tc, 2tc + 1 of the next chunk (this wave's share, taps 0-3): landed by the
+    // next barrier, transformed after it, read from the next chunk on (>= 4 barriers later)
     xpend = -1;
-    if (hasn && tc < PPW && wid + 4 * tc < NP) {
-      pdma16(rsx, halo_lds(tc, hbc ^ 1), halo_off(tc, m0n, ccn));
+    if (hasn && 2 * tc < PPW) {
+      if (wid + 8 * tc < NP) pdma16(rsx, halo_lds(2 * tc, hbc ^ 1), halo_off(2 * tc, m0n, ccn));
+      if (2 * tc + 1 < PPW && wid + 4 * (2 * tc + 1) < NP)
+        pdma16(rsx, halo_lds(2 * tc + 1, hbc ^ 1), halo_off(2 * tc + 1, m0n, ccn));
       xpend = tc;
       xhb = hbc ^ 1;
     }
@@ -442,20 +456,33 @@ int num_cus_cached() {
   return cus[dev];
 }
 
+// items per workgroup (DMLAB_HPIPE_IPB; 0 = persistent, two workgroups per CU)
+int hpipe_ipb() {
+  static const int v = getenv("DMLAB_HPIPE_IPB") ? atoi(getenv("DMLAB_HPIPE_IPB")) : 4;
+  return v < 0 ? 0 : v;
+}
+
 template <int BN, int HR>
 void launch_hpipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                   const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh) {
   const int mtiles = (int)((g.M + QBM - 1) / QBM);
   const int ntN = g.Ncols / BN;
-  const int nitems = ntN == 1 ? mtiles : (mtiles + 7) / 8 * 8 * ntN;
-  int grid = 2 * num_cus_cached();
-  if (grid > nitems) grid = nitems;
+  const int ipb = hpipe_ipb();
+  const int nitems = (ntN == 1 || ipb > 0) ? mtiles * ntN : (mtiles + 7) / 8 * 8 * ntN;
+  int grid;
+  if (ipb > 0) {
+    grid = (nitems + ipb - 1) / ipb;
+  } else {
+    grid = 2 * num_cus_cached();
+    if (grid > nitems) grid = nitems;
+  }
   const size_t sm = (size_t)2 * HR * 128 + (size_t)2 * BN * 128;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
   auto k = pre_sc ? conv_hpipe_kernel<BN, HR, true> : conv_hpipe_kernel<BN, HR, false>;
   set_smem_attr(k, sm);
-  k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, mtiles, ntN, nitems, pre_sc, pre_sh);
+  k<<<grid, 256, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, mtiles, ntN, nitems, ipb, pre_sc,
+                           pre_sh);
   DM_CHECK(hipGetLastError());
 }
 }  // namespace
