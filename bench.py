@@ -221,6 +221,7 @@ def main():
                 "ddp": f"bucketed all-reduce overlapped with backward, bucket {a.bucket_mb} MB, comm {a.comm_dtype}",
                 "backend": a.backend,
                 "fused_step": bool(fused is not None),
+                "ddp_side_stream_hooks": getattr(net, "side_stream_hooks", None),
                 "hip_graph": bool(a.graph and a.backend == "native"),
             },
             "final_loss": round(final_loss, 4),

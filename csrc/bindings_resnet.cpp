@@ -92,12 +92,6 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
       return;
     }
     if (cfg >= 90 && cfg <= 93) cfg = 41;  // same 256-row tile (stats slab rows match)
-    if (cfg == 94 || cfg == 95) {
-      TORCH_CHECK(dm::conv_hpipe_supported(g, (int)cfg), "cfg 94/95: not a halo-pipe geometry");
-      dm::conv_hpipe(bp(x), bp(wpack), bp(y), ap, sp, g, (int)cfg, cur_stream(), fp(*pre_scale),
-                     fp(*pre_shift));
-      return;
-    }
     TORCH_CHECK(dm::halo_cfg((int)cfg, bn, waves) && dm::conv_halo_supported(g),
                 "fused pre-BN needs a halo-kernel cfg and a unit-stride 3x3 geometry");
     dm::conv_halo(bp(x), bp(wpack), bp(y), ap, sp, g, bn, waves, cur_stream(), fp(*pre_scale),

@@ -748,7 +748,6 @@ bool halo_cfg(int cfg, int& bn, int& waves) {
 //   20 / 21 / 42 / 39 / 41  halo-staged unit-stride tiles (conv_halo.hip, see halo_cfg)
 //   60           space-to-depth stem kernel (conv_stem.hip)
 //   90 - 93      pipelined LDS-DMA tiles (conv_pipe.hip)
-//   94 / 95      persistent halo-pipelined 3x3/s1 kernel (conv_hpipe.hip), 64-row statistics
 // Shapes a specialised kernel does not cover fall back to a v3 tile with the same row tile,
 // so the statistics slab rows (igemm_fwd_rowtile) still match.
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
@@ -757,10 +756,6 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     if (!bnb && conv_pipe_supported(g, cfg)) return conv_pipe(X, Wp, Y, ADD, stats, g, cfg, st);
     if (g.Ncols % 128 == 0) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
     return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-  }
-  if (cfg == 94 || cfg == 95) {
-    if (!bnb && conv_hpipe_supported(g, cfg)) return conv_hpipe(X, Wp, Y, ADD, stats, g, cfg, st);
-    return launch_fwd3<64, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);  // 64-row tile
   }
   if (cfg == 60) {
     if (!bnb && !ADD && stem_conv_supported(g)) return stem_conv(X, Wp, Y, stats, g, st);
@@ -790,7 +785,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
 
 int igemm_fwd_rowtile(int cfg) {
   if ((cfg >= 90 && cfg <= 93) || cfg == 60 || cfg == 39 || cfg == 41) return 256;
-  return (cfg == 11 || cfg == 14 || cfg == 17 || cfg == 94 || cfg == 95) ? 64 : 128;
+  return (cfg == 11 || cfg == 14 || cfg == 17) ? 64 : 128;
 }
 
 void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,

@@ -95,11 +95,6 @@ int stem_wgrad_dy_blocks(int N, int H);
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st);
-// conv_hpipe.hip: persistent halo-pipelined 3x3/s1 conv (cfg 94: 128 x 64, 95: 128 x 128 items)
-bool conv_hpipe_supported(const ConvGeom& g, int cfg);
-void conv_hpipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
-                const float* pre_sh = nullptr);
 // conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90-93: 256-pixel tiles)
 bool conv_pipe_supported(const ConvGeom& g, int cfg);
 bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,

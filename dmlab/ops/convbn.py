@@ -41,30 +41,12 @@ TILE_CFG = (15, 13, 11)
 _STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
 # DMLAB_NO_PIPE=1: the round-2 tile map without the pipelined tiles (A/B runs)
 _NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
-# DMLAB_NO_HPIPE=1: the 64/128-channel 3x3 layers on the per-tile halo kernels (A/B runs)
-_NO_HPIPE = os.environ.get("DMLAB_NO_HPIPE", "0") == "1"
-
-
-def _hpipe_cfg(ncols, k, stride, cin, W):
-    """94 / 95: the persistent halo-pipelined kernel (csrc/conv_hpipe.hip) for unit-stride
-    3x3 convs whose 128-pixel halo (130 + 2W rows) fits its LDS budget: 64 output channels
-    with W <= 58, multiples of 128 with W <= 30 (ResNet-18 layer1 / layer2 at 224x224)."""
-    if _NO_HPIPE or k != 3 or stride != 1 or cin % 64 or cin <= 0 or W <= 0:
-        return None
-    hp = 130 + 2 * W
-    if ncols % 128 == 0 and hp < 192:
-        return 95
-    if ncols % 64 == 0 and hp < 248:
-        return 94
-    return None
-
-
 def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
     """Kernel config of a data-gradient GEMM (dX has M pixels of ``cin`` channels)."""
-    return pick_cfg(M, cin, k, stride, cout, W)
+    return pick_cfg(M, cin, k, stride, cout)
 
 
-def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
+def pick_cfg(M, ncols, k=0, stride=0, cin=0):
     """Kernel config for a forward-style conv GEMM with M output pixels and ncols
     output channels.  ``k``/``stride``/``cin`` (kernel size, tap stride, input
     channels) enable the unit-stride halo kernel when they describe a k x k conv with
@@ -77,9 +59,6 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
     #   layer4 1x1/s2 442/367 (15: 351/299); the 64/128-channel layers keep the halo tiles
     if ncols % 256 == 0 and cin % 64 == 0 and cin > 0 and not _NO_PIPE:
         return 90
-    hc = _hpipe_cfg(ncols, k, stride, cin, W)
-    if hc is not None:
-        return hc
     if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
         # 64 output channels: the 256-pixel halo tile (2 x 2 waves of 128 x 32) amortises
         # the single-chunk halo prologue over twice the rows
@@ -267,10 +246,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     # s2d stem: the resident-weight stem kernel (60, csrc/conv_stem.hip) stages the weights
     # and the input halo once per 256 pixels (the v3 128x64 tile, 16, re-stages one 4-tap
     # K-slice per step: 382 TFLOP/s at batch 512, profiles/conv_stem_s2d_r1s4.jsonl)
-    cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C, OW if p == 1 else 0)
+    cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 39, 41, 42, 90, 91, 92, 93, 94, 95):
+        if cfg in (20, 21, 39, 41, 42, 90, 91, 92, 93):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)

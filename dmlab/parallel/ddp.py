@@ -25,10 +25,11 @@ task3/dist_utils.py:40-46).  Here:
 * Optional bf16 gradient communication (``comm_dtype=torch.bfloat16``) halves
   the bytes on the links.  The cast targets a persistent flat communication buffer
   (allocated once), so the hooks allocate nothing and stay on the side stream.
-* Bucket hooks on the weight-gradient side stream (``side_stream_hooks``, default on;
-  ``DMLAB_DDP_SIDE_HOOKS=0`` or ``side_stream_hooks=False`` keeps the one-layer-lag scheme
+* Bucket hooks on the weight-gradient side stream (``side_stream_hooks``; default on with
+  RCCL buckets, off with ``small_allreduce="xgmi"`` whose spinning kernel would block the
+  side stream; ``DMLAB_DDP_SIDE_HOOKS=0/1`` forces either).  Off = the one-layer-lag scheme
   in which the main stream waits for each layer's weight gradients before its bucket
-  launches).
+  launches.
 * ``broadcast_buffers`` (default on, as torch DDP): rank 0's module buffers (BatchNorm
   running statistics, ``num_batches_tracked``) are broadcast — coalesced, one collective
   per dtype — at every training forward (or every ``buffer_sync_every`` forwards), so the
@@ -91,7 +92,12 @@ class DistributedDataParallel(nn.Module):
         if side_stream_hooks is None:
             import os
 
-            side_stream_hooks = os.environ.get("DMLAB_DDP_SIDE_HOOKS", "1") != "0"
+            # default: on with RCCL buckets (the collective is enqueued on RCCL's own stream);
+            # off with the spinning xGMI kernel, which would sit on the weight-gradient stream
+            # in front of every later weight gradient until the peers arrive (unmeasured at
+            # 2-8 GPUs: ADVICE r2).  DMLAB_DDP_SIDE_HOOKS=0/1 forces either scheme.
+            e = os.environ.get("DMLAB_DDP_SIDE_HOOKS")
+            side_stream_hooks = (e != "0") if e is not None else small_allreduce != "xgmi"
         self.side_stream_hooks = bool(side_stream_hooks)
         self.broadcast_buffers = bool(broadcast_buffers)
         self.buffer_sync_every = max(1, int(buffer_sync_every))

@@ -601,67 +601,3 @@ def test_conv_dgrad_pipe(dev, geom, accumulate, cfg):
     if accumulate:
         ref = ref + _nchw(base).float()
     assert _rel(_nchw(dx), ref) < 6e-3
-
-
-# persistent halo-pipelined kernel (conv_hpipe.hip, cfg 94 = 128 x 64 items, 95 = 128 x 128):
-# layer-1 / layer-2 shapes, images and items crossing each other, a partial last item, one
-# item only, several 64-channel chunks (halo prefetch within an item), several N tiles
-# (XCD-grouped items incl. padding items), and shapes 95 cannot take (64-row v3 fallback)
-HPIPE_GEOMS = [
-    (3, 56, 64, 64, 3, 1, 1),
-    (2, 28, 128, 128, 3, 1, 1),
-    (5, 7, 128, 64, 3, 1, 1),
-    (2, 40, 64, 128, 3, 1, 1),
-    (1, 9, 256, 64, 3, 1, 1),
-    (4, 14, 64, 256, 3, 1, 1),
-    (11, 14, 128, 128, 3, 1, 1),
-]
-
-
-@pytest.mark.parametrize("geom", HPIPE_GEOMS)
-@pytest.mark.parametrize("cfg", [94, 95])
-def test_conv_fwd_hpipe(dev, geom, cfg):
-    _check_fwd(dev, geom, cfg)
-
-
-@pytest.mark.parametrize("geom", HPIPE_GEOMS)
-@pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [94, 95])
-def test_conv_dgrad_hpipe(dev, geom, accumulate, cfg):
-    N, H, Cin, Cout, k, s, p = geom
-    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
-    dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
-    ref = torch.nn.grad.conv2d_input((N, Cin, H, H), w.bfloat16().float(), dy.float(), s, p)
-    dx = torch.randn(N, H, H, Cin, device=dev).bfloat16()
-    base = dx.clone()
-    lib().conv_dgrad(_nhwc(dy), wd, dx, k, k, s, p, dx if accumulate else None, cfg)
-    if accumulate:
-        ref = ref + _nchw(base).float()
-    assert _rel(_nchw(dx), ref) < 6e-3
-
-
-@pytest.mark.parametrize("geom", HPIPE_GEOMS)
-@pytest.mark.parametrize("cfg", [94, 95])
-def test_conv_fwd_prebn_hpipe(dev, geom, cfg):
-    """cfg 94/95 with the previous layer's BN + ReLU applied once per staged halo."""
-    N, H, Cin, Cout, k, s, p = geom
-    if cfg == 95 and 130 + 2 * H >= 192 or Cout % (128 if cfg == 95 else 64):
-        pytest.skip("not a cfg-95 geometry (the pre-BN path has no fallback)")
-    g = torch.Generator(device=dev).manual_seed(2)
-    y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
-    sc = torch.rand(Cin, device=dev, generator=g) + 0.5
-    sh = torch.randn(Cin, device=dev, generator=g) * 0.5
-    w = torch.randn(Cout, Cin, k, k, device=dev, generator=g) / math.sqrt(Cin * k * k)
-    wf = torch.empty(Cout, k, k, Cin, device=dev, dtype=torch.bfloat16)
-    lib().pack_weights(w.contiguous(), wf, None, Cin)
-    a = (y.float() * sc + sh).relu().bfloat16().float()
-    ref = F.conv2d(_nchw(a), w.bfloat16().float(), None, s, p)
-    out = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
-    M = N * H * H
-    T = lib().conv_stats_rows(M, cfg, Cout)
-    stats = torch.empty(T * 2 * Cout, device=dev)
-    lib().conv_fwd(y, wf, out, stats, None, k, k, s, p, cfg, pre_scale=sc, pre_shift=sh)
-    assert _rel(_nchw(out), ref) < 6e-3
-    st = stats.view(T, 2, Cout).sum(0)
-    torch.testing.assert_close(st[0], ref.sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
-    torch.testing.assert_close(st[1], (ref * ref).sum((0, 2, 3)), rtol=1e-3, atol=1e-2 * math.sqrt(M))
