@@ -39,6 +39,7 @@ __device__ __forceinline__ pi32x4 prsrc(const void* base, unsigned bytes) {
 // Issued from inline asm so the compiler's alias-blind LDS-DMA tracking does not put a
 // vmcnt(0) before every ds_read; the caller retires it with its own s_waitcnt vmcnt.
 __device__ __forceinline__ void pdma16(const pi32x4& rs, unsigned lds, unsigned off) {
+  lds = __builtin_amdgcn_readfirstlane(lds);  // keep M0's source an SGPR under register pressure
   asm volatile(
       "s_mov_b32 m0, %1\n\t"
       "s_nop 0\n\t"

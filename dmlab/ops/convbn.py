@@ -108,7 +108,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
     else:
         cfg = 2 if cout % 128 == 0 else 3
     if cfg in (4, 5):
-        tiles = max(1, math.ceil(cout / 64) * (cin // 64) * (1 if cfg == 4 else 3))
+        tiles = max(1, math.ceil(cout / 64) * (cin // 64) * (3 if cfg == 5 else 1))
         max_split = max(1, M // 512)
     else:
         bm = 128 if cfg == 2 else 64

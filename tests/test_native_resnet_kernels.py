@@ -157,11 +157,12 @@ def test_conv_wgrad(dev, geom):
     assert M > 0
 
 
-@pytest.mark.parametrize("geom", [g for g in HALO_GEOMS if g[4] == 3])
+@pytest.mark.parametrize("geom", [g for g in HALO_GEOMS if g[4] == 3] + [(2, 20, 64, 128, 3, 1, 1)])
 @pytest.mark.parametrize("cfg", [4, 5])
-@pytest.mark.parametrize("S", [1, 3])
+@pytest.mark.parametrize("S", [1, 3, 7])
 def test_conv_wgrad_halo(dev, geom, cfg, S):
-    """Halo-staged 3x3 weight gradient (9 / 3 taps per block), split-m slabs."""
+    """Halo-staged 3x3 weight gradients: cfg 4 / 5 (9 / 3 taps per block); split-m slabs
+    with slices ending mid-step, images crossing slices, several co tiles and ci chunks."""
     N, H, Cin, Cout, k, s, p = geom
     x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
     dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
