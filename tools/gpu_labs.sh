@@ -3,6 +3,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r3c -o prof -- \
+    python bench.py --steps 10 --warmup 5 > gpurun_out/prof_r3c.log 2>&1 || exit 1
+tail -1 gpurun_out/prof_r3c.log
 timeout -k 10 1000 python -u -m pytest tests/test_multiproc_gpu.py -x -v --timeout 280 --timeout-method thread \
     -k "xgmi_many or bf16 or ddp_xgmi_graph or lenet_fused or pipeline_xgmi or bench_lenet" > gpurun_out/pytest_mp2.log 2>&1
 rc=$?; tail -16 gpurun_out/pytest_mp2.log; [ $rc -ne 0 ] && exit $rc
