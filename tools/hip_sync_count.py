@@ -39,8 +39,11 @@ def main():
                         launches += 1
             out = {"file": str(f), "launch_calls": launches, "host_sync_calls": dict(cnt)}
             if a.steps:
+                # hipStreamWaitEvent orders streams on the device; hipEventQuery / hipStreamQuery
+                # are non-blocking polls (the caching allocator's cross-stream frees)
                 blocking = sum(v for k, v in cnt.items()
-                               if k not in ("hipStreamWaitEvent", "hipMemset"))
+                               if k not in ("hipStreamWaitEvent", "hipMemset", "hipEventQuery",
+                                            "hipStreamQuery"))
                 out["blocking_per_step"] = round(blocking / a.steps, 3)
             print(json.dumps(out))
 

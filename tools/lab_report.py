@@ -286,8 +286,11 @@ def write_report(out, R, a):
     L = [f"# Lab deliverables (generated by `tools/lab_report.py`, device {a.device})", "",
          "Data: the learnable synthetic MNIST of `dmlab/data/datasets.py` with pixel noise 0.7 and "
          "10 % random labels (test accuracy capped near 91 %); every run is a lab entry point "
-         "(`dmlab.tasks.task1`..`task4`) launched with `torch.distributed.run`, gloo on the CPU "
-         "unless the device says otherwise.", ""]
+         "(`dmlab.tasks.task1`..`task4`) launched with `torch.distributed.run`, " +
+         ("gloo on the CPU." if a.device == "cpu" else
+          "all ranks on the box's one MI355X (native HIP kernels; gloo process groups, since RCCL "
+          "rejects two ranks on one GPU, so device tensors are staged through the host for the "
+          "collectives: the communication times are those of that path, not of xGMI)."), ""]
     if "a" in R:
         L += ["## (a) Optimisers: loss curves (checking.tex:8)", "",
               "![](a_optimizers.png)", "", "| optimiser | first loss | last loss | test accuracy |",
@@ -335,8 +338,8 @@ def write_report(out, R, a):
               "0.9, batch 32). The two pipeline runs match each other (micro-batch gradients "
               "accumulate to the full-batch gradient); the RPC placement (reference programming "
               "model: driver + 2 stage owners over TensorPipe, `codes/task4/model.py`) and the "
-              "tensor-parallel head reach the same loss and accuracy. On the CPU the step times "
-              "measure process hand-offs, not the GPU transports; the GPU numbers for the "
+              "tensor-parallel head reach the same loss and accuracy. The step times here include "
+              "the process-group path of this device; the transport-level numbers for the "
               "pipeline (RCCL and xGMI transports, GPipe/1F1B, bubble fraction) are in "
               "`profiles/bench_pipeline_r3.jsonl` (`tools/bench_pipeline.py`).", ""]
     (out / "REPORT.md").write_text("\n".join(L))
