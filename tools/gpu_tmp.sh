@@ -2,16 +2,15 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-out=gpurun_out/bench_ab_knobs_r3.jsonl; : > $out
-for v in "X=0" "DMLAB_WGRAD_BLOCKS=384" "DMLAB_WGRAD_BLOCKS=768" "DMLAB_WGRAD_STREAM_MIN_COUT=128" \
-         "DMLAB_WGRAD_PRIO=-1" "X=0" "DMLAB_WGRAD_BLOCKS=384" "DMLAB_WGRAD_BLOCKS=768" \
-         "DMLAB_WGRAD_STREAM_MIN_COUT=128" "DMLAB_WGRAD_PRIO=-1"; do
+out=gpurun_out/bench_ab_defer_r3.jsonl; : > $out
+for v in "X=0" "DMLAB_DEFER_WGRAD=1" "DMLAB_DEFER_WGRAD=2" "DMLAB_DEFER_WGRAD=4" \
+         "X=0" "DMLAB_DEFER_WGRAD=1" "DMLAB_DEFER_WGRAD=2" "DMLAB_DEFER_WGRAD=4"; do
   echo "$v" >> $out
   env $v timeout -k 10 300 python bench.py --steps 30 --warmup 10 >> $out 2>> gpurun_out/bench_ab.err || exit 1
 done
 python - <<'PY'
 import json
-for l in open('gpurun_out/bench_ab_knobs_r3.jsonl'):
+for l in open('gpurun_out/bench_ab_defer_r3.jsonl'):
     l = l.strip()
     if l.startswith('{'):
         r = json.loads(l); print(r['value'], r['ms_per_step'])
