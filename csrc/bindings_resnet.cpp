@@ -107,27 +107,10 @@ int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
   return (M + bm - 1) / bm;
 }
 
-// dx = conv_transpose(dy, w) for stride 1 or 2; accumulate => dx += ...
-// Slab rows the BN-backward epilogue of conv_dgrad writes (0: the shape/cfg cannot fuse it).
-int64_t dgrad_bnb_rows(int64_t N, int64_t H, int64_t W, int64_t stride, int64_t cfg) {
-  if (cfg < 9) return 0;
-  if (stride == 1) return conv_stats_rows(N * H * W, cfg, -1);
-  if (!(cfg == 12 || cfg == 13 || cfg == 15 || cfg == 16)) return 0;
-  const long long mmax = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);  // class (0, 0) is largest
-  return ((mmax + 127) / 128) * 4;
-}
-
-// dx = conv_transpose(dy, w) for stride 1 or 2; accumulate => dx += ...
-// bnb_*: optional BN-backward sums of the BN whose input gradient dx is (see BnBwdEpi):
-// written to bnb_slab [dgrad_bnb_rows][2][Cin]; returns the row count (0 = not computed).
-int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
-                   int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg,
-                   c10::optional<at::Tensor> bnb_y, c10::optional<at::Tensor> bnb_out,
-                   c10::optional<at::Tensor> bnb_mean, c10::optional<at::Tensor> bnb_invstd,
-                   c10::optional<at::Tensor> bnb_scale, c10::optional<at::Tensor> bnb_shift,
-                   int64_t bnb_mode, c10::optional<at::Tensor> bnb_slab,
-                   c10::optional<at::Tensor> bnb_mask) {
-  // add: tensor added to the result (may alias dx for in-place accumulation)
+// dx = conv_transpose(dy, w) for stride 1 or 2; add: tensor added to the result (may alias dx
+// for in-place accumulation)
+void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
+                int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg) {
   need_bf16_nhwc(dy, "dy");
   need_bf16_nhwc(dx, "dx");
   const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), Cout = dy.size(3);
@@ -145,51 +128,6 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
               "stride-2 dgrad accumulates only in place (add must alias dx)");
   const DeviceGuard guard(dy.device());
   auto st = cur_stream();
-  dm::BnBwdEpi bnb{};
-  int64_t bnb_rows = 0;
-  float* slabp = nullptr;
-  // the fused sums need every output pixel written by this launch: a stride-2 dgrad with
-  // a tap-less parity class (1x1/s2) only qualifies when it overwrites (those pixels are 0)
-  bool empty_class = false;
-  if (stride == 2)
-    for (int a = 0; a < 2; ++a)
-      for (int b = 0; b < 2; ++b)
-        if ((KH - ((a + pad) & 1) + 1) / 2 <= 0 || (KW - ((b + pad) & 1) + 1) / 2 <= 0)
-          empty_class = true;
-  if (bnb_y.has_value() && !(empty_class && addp)) bnb_rows = dgrad_bnb_rows(N, H, W, stride, cfg);
-  if (bnb_rows > 0) {
-    need_bf16_nhwc(*bnb_y, "bnb_y");
-    TORCH_CHECK(bnb_y->sizes() == dx.sizes(), "bnb_y: the BN input, shaped like dx");
-    TORCH_CHECK(bnb_mode >= 0 && bnb_mode <= 4 && bnb_mode != 3, "bnb_mode: 0, 1, 2 or 4");
-    TORCH_CHECK(bnb_slab.has_value(), "bnb_slab required");
-    need_f32(*bnb_slab, "bnb_slab", bnb_rows * 2 * Cin);
-    need_f32(*bnb_mean, "bnb_mean", Cin);
-    need_f32(*bnb_invstd, "bnb_invstd", Cin);
-    bnb.y = bp(*bnb_y);
-    bnb.mean = fp(*bnb_mean);
-    bnb.invstd = fp(*bnb_invstd);
-    bnb.mode = (int)bnb_mode;
-    if (bnb_mode == 1) {
-      TORCH_CHECK(bnb_out.has_value(), "bnb_out required for mode 1");
-      need_bf16_nhwc(*bnb_out, "bnb_out");
-      TORCH_CHECK(bnb_out->sizes() == dx.sizes());
-      bnb.out = bp(*bnb_out);
-    }
-    if (bnb_mode == 4) {
-      TORCH_CHECK(bnb_mask.has_value() && bnb_mask->is_cuda() && bnb_mask->scalar_type() == at::kByte &&
-                  bnb_mask->is_contiguous() && bnb_mask->numel() == dx.numel() / 8,
-                  "bnb_mode 4 needs the uint8 1-bit mask of the BN output");
-      bnb.mask = (const unsigned char*)bnb_mask->data_ptr();
-    }
-    if (bnb_mode == 2) {
-      need_f32(*bnb_scale, "bnb_scale", Cin);
-      need_f32(*bnb_shift, "bnb_shift", Cin);
-      bnb.sc = fp(*bnb_scale);
-      bnb.sh = fp(*bnb_shift);
-    }
-    slabp = fp(*bnb_slab);
-  }
-  const dm::BnBwdEpi* bnbp = bnb.y ? &bnb : nullptr;
   dm::ConvGeom base{};
   base.N = N; base.H = OH; base.W = OW; base.C = Cout; base.lgC8 = ilog2(Cout / 8);
   base.OH = H; base.OW = W; base.OC = Cin;
@@ -201,8 +139,8 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
-    dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, slabp, g, cfg, st, bnbp);
-    return bnb_rows;
+    dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
+    return;
   }
   // parity classes write disjoint output pixels; a class with no taps (e.g. the odd
   // pixels of a 1x1/s2 conv) is exactly zero, so zero-fill once up front when needed
@@ -233,25 +171,15 @@ int64_t conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int6
       set.g[ng++] = g;
     }
   // pipelined tiles: all parity classes in one launch (blockIdx.y = class)
-  if (cfg >= 90 && cfg <= 93 && !bnbp && ng > 0 &&
+  if (cfg >= 90 && cfg <= 93 && ng > 0 &&
       dm::conv_pipe_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, ng, (int)cfg, st))
-    return 0;
+    return;
   // all parity classes in one launch (blockIdx.z = class) when the tile supports it
-  if (bnbp) {
-    // slab rows of absent classes, or of row tiles past a smaller class's M (odd sizes),
-    // are never written: zero the slab first
-    bool uneven = ng != 4;
-    for (int i = 0; i < ng; ++i) uneven |= set.g[i].M != set.g[0].M;
-    if (uneven) TORCH_CHECK(hipMemsetAsync(slabp, 0, (size_t)bnb_rows * 2 * Cin * 4, st) == hipSuccess);
-    set.bnb = bnb;
-  }
-  if (ng > 0 && dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, slabp,
+  if (ng > 0 && dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr,
                                     set, ng, (int)cfg, st))
-    return bnb_rows;
-  TORCH_CHECK(!bnbp, "conv_dgrad: BN-backward epilogue unsupported for this cfg");
+    return;
   for (int i = 0; i < ng; ++i)
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, nullptr, set.g[i], cfg, st);
-  return 0;
 }
 
 // dw (fp32 OIHW [Cout][Cin][KH][KW]) = beta*dw + Σ_m dy ⊗ im2col(x)
@@ -455,60 +383,6 @@ void stem_bwd_fused(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor
   dm::wgrad_reduce_s2d(fp(slab), S, C, (int)Cin, xs.size(3), fp(dw), (float)wbeta, st);
 }
 
-// Split stem backward (the pipelined alternative to stem_bwd_fused): coefficients once,
-// then per batch slice the quad apply (dy) and the s2d weight gradient into its own slabs,
-// then one fixed-order reduce of all slabs.
-void stem_bwd_coef(at::Tensor y, at::Tensor mean, at::Tensor invstd, at::Tensor gamma,
-                   at::Tensor dgamma, at::Tensor dbeta, double gbeta, at::Tensor scale,
-                   at::Tensor shift, at::Tensor pdy, at::Tensor pidx, at::Tensor pre_slab,
-                   int64_t pre_rows, at::Tensor work) {
-  need_bf16_nhwc(y, "y");
-  need_bf16_nhwc(pdy, "pdy");
-  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
-  const long long M = (long long)N * H * W;
-  need_f32(work, "work", bn_bwd_work(M, C));
-  need_f32(pre_slab, "pre_slab", pre_rows * 2 * C);
-  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && pdy.size(1) == H / 2 && pdy.size(2) == W / 2);
-  const DeviceGuard guard(y.device());
-  dm::bn_backward(nullptr, nullptr, bp(y), fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
-                  (float)gbeta, M, C, 3, fp(scale), fp(shift), bp(pdy),
-                  (const uint8_t*)pidx.data_ptr(), H, W, H / 2, W / 2, 3, 2, 1, nullptr, nullptr,
-                  fp(work), cur_stream(), fp(pre_slab), (int)pre_rows, nullptr);
-}
-
-void bn_bwd_apply_quad(at::Tensor y, at::Tensor pdy, at::Tensor pidx, at::Tensor coef,
-                       at::Tensor scale, at::Tensor shift, at::Tensor dy) {
-  need_bf16_nhwc(y, "y");
-  need_bf16_nhwc(pdy, "pdy");
-  need_bf16_nhwc(dy, "dy");
-  const int N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
-  TORCH_CHECK(dy.sizes() == y.sizes() && H % 2 == 0 && W % 2 == 0);
-  TORCH_CHECK(pdy.size(0) == N && pdy.size(1) == H / 2 && pdy.size(2) == W / 2 && pdy.size(3) == C);
-  TORCH_CHECK(pidx.is_cuda() && pidx.scalar_type() == at::kByte && pidx.is_contiguous() &&
-              pidx.numel() == pdy.numel());
-  TORCH_CHECK(C % 8 == 0 && 256 % (C / 8) == 0);
-  need_f32(coef, "coef", 3 * C);
-  need_f32(scale, "scale", C);
-  need_f32(shift, "shift", C);
-  const DeviceGuard guard(y.device());
-  dm::bn_bwd_apply_quad(bp(y), bp(pdy), (const uint8_t*)pidx.data_ptr(), fp(coef), fp(scale),
-                        fp(shift), bp(dy), N, H, W, C, cur_stream());
-}
-
-int64_t stem_wgrad_blocks(int64_t N, int64_t H) { return dm::stem_wgrad_dy_blocks((int)N, (int)H); }
-
-// s2d stem weight-gradient slabs [S][64][256] of one batch slice (no reduce)
-void stem_wgrad_dy(at::Tensor xs, at::Tensor dy, at::Tensor slab, int64_t S) {
-  need_bf16_nhwc(xs, "xs");
-  need_bf16_nhwc(dy, "dy");
-  TORCH_CHECK(dm::stem_wgrad_fused_supported(dy.size(0), dy.size(1), dy.size(2), dy.size(3), xs.size(3)) &&
-              xs.size(0) == dy.size(0) && xs.size(1) == dy.size(1) && xs.size(2) == dy.size(2),
-              "stem_wgrad_dy: unsupported shape");
-  need_f32(slab, "slab", S * 64 * 256);
-  const DeviceGuard guard(xs.device());
-  dm::stem_wgrad_dy(bp(xs), bp(dy), fp(slab), dy.size(0), dy.size(1), dy.size(2), (int)S,
-                    cur_stream());
-}
 
 void wgrad_reduce_s2d(at::Tensor slab, int64_t S, int64_t Cout, int64_t Cin, int64_t Cp,
                       at::Tensor dw, double beta) {
@@ -697,13 +571,8 @@ void register_resnet(pybind11::module_& m) {
         py::arg("cfg"), py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
   m.def("conv_stats_rows", &conv_stats_rows, py::arg("M"), py::arg("cfg"), py::arg("ncols") = -1);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("dx"), py::arg("KH"),
-        py::arg("KW"), py::arg("stride"), py::arg("pad"), py::arg("add"), py::arg("cfg"),
-        py::arg("bnb_y") = py::none(), py::arg("bnb_out") = py::none(),
-        py::arg("bnb_mean") = py::none(), py::arg("bnb_invstd") = py::none(),
-        py::arg("bnb_scale") = py::none(), py::arg("bnb_shift") = py::none(),
-        py::arg("bnb_mode") = 0, py::arg("bnb_slab") = py::none(),
-        py::arg("bnb_mask") = py::none());
-  m.def("dgrad_bnb_rows", &dgrad_bnb_rows);
+        py::arg("KW"), py::arg("stride"), py::arg("pad"),
+        py::arg("add") = py::none(), py::arg("cfg") = 12);
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),
@@ -726,10 +595,6 @@ void register_resnet(pybind11::module_& m) {
         py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("pre_slab"), py::arg("pre_rows"),
         py::arg("xs"), py::arg("Cin"), py::arg("dw"), py::arg("wbeta"), py::arg("work"),
         py::arg("slab"));
-  m.def("stem_bwd_coef", &stem_bwd_coef);
-  m.def("bn_bwd_apply_quad", &bn_bwd_apply_quad);
-  m.def("stem_wgrad_blocks", &stem_wgrad_blocks);
-  m.def("stem_wgrad_dy", &stem_wgrad_dy);
   m.def("wgrad_reduce_s2d", &wgrad_reduce_s2d);
   m.def("bn_backward", &bn_backward, py::arg("dout"), py::arg("out"), py::arg("y"), py::arg("mean"), py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"), py::arg("mode"), py::arg("scale"), py::arg("shift"), py::arg("pdy"), py::arg("pidx"), py::arg("K"), py::arg("S"), py::arg("P"), py::arg("dy"), py::arg("dres"), py::arg("work"),
         py::arg("pre_slab") = py::none(), py::arg("pre_rows") = 0, py::arg("mask") = py::none());

@@ -1097,7 +1097,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                  int OH, int OW, int K, int S, int P, bf16_t* dy, bf16_t* dres, float* work,
                  hipStream_t st, const float* pre_part, int pre_rows, const uint8_t* mask) {
   // pre_part (optional): [pre_rows][2C] partial Σdz, Σdz·x̂ already reduced by the producing
-  // dgrad's epilogue (BnBwdEpi) — the reduction pass over dout and y is skipped
+  // kernel (the stem's pooled-domain sums) — the reduction pass over dout and y is skipped
   // work: [G][2C] partials + [3C] coefficients + [<=256][2C] second-level partials
   BnBwdArgs a{dout, out, y, mean, invstd, scale, shift, pdy, pidx, H, W, OH, OW, K, S, P, M, C,
               mask};
@@ -1153,24 +1153,12 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
 #undef DM_BNB
 }
 
-// The stem's quad apply (dy = a·dz + b·y + c, dz gathered from the 3x3/s2/p1 max-pool
-// gradient) on its own, for coefficients computed earlier (bn_backward with dy == nullptr):
-// lets the caller run it over batch slices and pipeline the weight gradient behind it.
-void bn_bwd_apply_quad(const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx, const float* coef,
-                       const float* scale, const float* shift, bf16_t* dy, int N, int H, int W,
-                       int C, hipStream_t st) {
-  BnBwdArgs a{nullptr, nullptr, y, nullptr, nullptr, scale, shift, pdy, pidx, H, W, H / 2, W / 2,
-              3, 2, 1, (long long)N * H * W, C, nullptr};
-  const long long n8 = a.M * C / 8;
-  bn_bwd_apply_quad_kernel<<<grid_for(n8 / 4, 256, 4096), 256, sizeof(float) * 5 * C, st>>>(a, coef, dy);
-}
 
 void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf16_t* out,
                      uint8_t* idx, int N, int H, int W, int C, int OH, int OW, int K, int S,
                      int P, hipStream_t st, bf16_t* yarg) {
   const long long total = (long long)N * OH * OW * (C / 8);
-  static const bool generic = getenv("DMLAB_POOL_GENERIC") && atoi(getenv("DMLAB_POOL_GENERIC"));
-  if (!generic && K == 3 && S == 2 && P == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 &&
+  if (K == 3 && S == 2 && P == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 &&
       (long long)N * H * W * C < (1LL << 31)) {
     const long long pairs = (long long)N * OH * ((OW + 1) / 2) * (C / 8);
     bn_relu_maxpool3s2_kernel<<<grid_for(pairs, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(

@@ -24,33 +24,12 @@ struct ConvGeom {
   unsigned wg_mul, wg_shr, hg_mul, hg_shr;
 };
 
-// BatchNorm-backward sums fused into a dgrad epilogue.  The dgrad output is the upstream
-// gradient `dout` of the BN that produced this conv's input; with y (that BN's input, same
-// NHWC layout as the dgrad output) the epilogue reduces per channel
-//     Σ dz,  Σ dz·(y - mean)·invstd       dz = dout masked by the BN's ReLU
-// into the stats slab rows (the layout of the forward statistics), so the BN backward
-// needs no separate reduction pass over dout and y.  mode: 0 no ReLU, 1 mask out > 0
-// (block output with residual), 2 mask y*sc + sh > 0, 4 the forward's 1-bit (out > 0) mask
-// (bit j of byte i: channel j of 8-channel chunk i).  y == nullptr: disabled.
-struct BnBwdEpi {
-  const unsigned short* y;
-  const unsigned short* out;
-  const float* mean;
-  const float* invstd;
-  const float* sc;
-  const float* sh;
-  int mode;
-  const unsigned char* mask;
-};
-
 // several geometries for one launch (selected by blockIdx.z)
 struct ConvGeomSet {
   ConvGeom g[4];
-  BnBwdEpi bnb;
-  static ConvGeomSet one(const ConvGeom& g0, const BnBwdEpi* b = nullptr) {
+  static ConvGeomSet one(const ConvGeom& g0) {
     ConvGeomSet s{};
     s.g[0] = g0;
-    if (b) s.bnb = *b;
     return s;
   }
 };

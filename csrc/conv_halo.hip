@@ -51,7 +51,7 @@ template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_HALO39_MINB : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, BnBwdEpi bnb,
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh,
     int xcd, int mtiles) {
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
   // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
@@ -295,8 +295,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       if (s + 1 < S) step(s + 1, rb, rb2);
     }
   }
-  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, bx, stats, g, Y, ADD,
-                                                       bnb);
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, bx, stats, g, Y, ADD);
 }
 
 int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
@@ -306,8 +305,7 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
 
 template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
-                 const BnBwdEpi& bnb) {
+                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
@@ -324,10 +322,10 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   if (nt > 1) {
     const unsigned mt8 = (mt + 7) / 8 * 8;
     k<<<dim3(mt8 * nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
-                                                bnb, (int)nt, (int)mt);
+                                                (int)nt, (int)mt);
     return;
   }
-  k<<<dim3(mt, nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh, bnb,
+  k<<<dim3(mt, nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
                                             0, (int)mt);
 }
 }  // namespace
@@ -349,31 +347,30 @@ bool conv_halo_supported(const ConvGeom& g) {
 // 64 x 32 (cfg 39); 32 = 256 px as 4 x 1 waves of 64 x 64 (cfg 41)
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
-               const float* pre_sh, const BnBwdEpi* bnbp) {
-  const BnBwdEpi bnb = bnbp ? *bnbp : BnBwdEpi{};
+               const float* pre_sh) {
   const int hp = halo_rows_needed(g), hp2 = halo_rows_needed(g, 256);
   if (waves == (4 | 0x100) && bn == 128) {
     const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-    if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    else launch_halo<128, 12, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
   } else if (waves == 16 && bn == 64) {
     const int hr = (hp2 + 63) / 64;
-    if (hr <= 5) launch_halo<64, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    else if (hr <= 6) launch_halo<64, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    else launch_halo<64, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    if (hr <= 5) launch_halo<64, 5, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    else if (hr <= 6) launch_halo<64, 6, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    else launch_halo<64, 7, 4, 2, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
   } else if (waves == 32 && bn == 64) {
     const int hr = (hp2 + 31) / 32;
-    if (hr <= 10) launch_halo<64, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    else if (hr <= 12) launch_halo<64, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
-    else launch_halo<64, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+    if (hr <= 10) launch_halo<64, 10, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    else if (hr <= 12) launch_halo<64, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
+    else launch_halo<64, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
   } else {
     DM_CHECK(waves == 4 ? hipSuccess : hipErrorInvalidValue);
     const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
 #define DM_HALO4(BN_)                                                                       \
-  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);      \
-  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb); \
-  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st, bnb);
+  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);      \
+  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st); \
+  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     if (bn == 128) { DM_HALO4(128) } else { DM_HALO4(64) }
 #undef DM_HALO4
   }

@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
   }
 
   mfma_tile_epilogue<BM, BN, WM, WN, MF32>(acc, smem, m0, n0, blockIdx.z * gridDim.x + blockIdx.x,
-                                           stats, g, Y, ADD, gs.bnb);
+                                           stats, g, Y, ADD);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -706,15 +706,13 @@ static void launch_fwd3_set(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const 
 
 template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
 static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                        float* stats, const ConvGeom& g, hipStream_t st,
-                        const BnBwdEpi* bnb = nullptr) {
-  launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g, bnb), 1,
+                        float* stats, const ConvGeom& g, hipStream_t st) {
+  launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1,
                                                st);
 }
 
 // up to four geometries sharing X / W / Y (the parity classes of a stride-2 dgrad) in one
 // launch on the v3 128x128 mf32 tile (no statistics: the classes' row tiles would collide)
-// stats (optional, with gs.bnb set): BN-backward sums, slab rows class * grid.x + row tile
 bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st) {
   switch (cfg) {  // the v3 mf32 tiles of igemm_fwd (12/13: one tile of prefetch, 15/16: two)
@@ -751,34 +749,34 @@ bool halo_cfg(int cfg, int& bn, int& waves) {
 // Shapes a specialised kernel does not cover fall back to a v3 tile with the same row tile,
 // so the statistics slab rows (igemm_fwd_rowtile) still match.
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb) {
+               const ConvGeom& g, int cfg, hipStream_t st) {
   if (cfg >= 90 && cfg <= 93) {
-    if (!bnb && conv_pipe_supported(g, cfg)) return conv_pipe(X, Wp, Y, ADD, stats, g, cfg, st);
-    if (g.Ncols % 128 == 0) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-    return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    if (conv_pipe_supported(g, cfg)) return conv_pipe(X, Wp, Y, ADD, stats, g, cfg, st);
+    if (g.Ncols % 128 == 0) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+    return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
   }
   if (cfg == 60) {
-    if (!bnb && !ADD && stem_conv_supported(g)) return stem_conv(X, Wp, Y, stats, g, st);
-    return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+    if (!ADD && stem_conv_supported(g)) return stem_conv(X, Wp, Y, stats, g, st);
+    return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
   }
   int bn, waves;
   if (halo_cfg(cfg, bn, waves)) {
-    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st, nullptr, nullptr, bnb);
+    if (conv_halo_supported(g)) return conv_halo(X, Wp, Y, ADD, stats, g, bn, waves, st);
     if (igemm_fwd_rowtile(cfg) == 256) {
-      if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-      return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
+      if (bn == 128) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+      return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
     }
     cfg = bn == 128 ? 12 : 13;
   }
   switch (cfg) {
-    case 9: return launch_fwd3<128, 128, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 10: return launch_fwd3<128, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 11: case 14: return launch_fwd3<64, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 12: return launch_fwd3<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 13: return launch_fwd3<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 15: return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 16: return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
-    case 17: return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st, bnb);
+    case 9: return launch_fwd3<128, 128, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st);
+    case 10: return launch_fwd3<128, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st);
+    case 11: case 14: return launch_fwd3<64, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, g, st);
+    case 12: return launch_fwd3<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+    case 13: return launch_fwd3<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
+    case 15: return launch_fwd3<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
+    case 16: return launch_fwd3<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, g, st);
+    case 17: return launch_fwd3<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, g, st);
     default: throw std::runtime_error("igemm_fwd: unknown cfg " + std::to_string(cfg));
   }
 }

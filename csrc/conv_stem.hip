@@ -37,126 +37,7 @@ constexpr unsigned SOOB = 0x80000000u;
 __device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ (row & 15); }
 __device__ __forceinline__ int hswz(int pix, int half) { return half ^ ((pix >> 3) & 1); }
 
-__global__ void __launch_bounds__(256, 2) stem_conv_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y,
-    float* __restrict__ stats, ConvGeom g, unsigned xbytes) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* Ws = reinterpret_cast<bf16_t*>(smem);  // [64][256]
-  bf16_t* Hs = Ws + SCO * SK;                     // [SHP + 1][16], last pixel = zeros
-  int4* taps = reinterpret_cast<int4*>(Hs + (SHP + 1) * SC);
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const long long m0 = (long long)blockIdx.x * SBM;
-  const int ntaps = g.nth * g.ntw;
-  const int NHW = g.N * g.H * g.W;
-  if (tid < ntaps) {
-    const int th = tid / g.ntw, tw = tid % g.ntw;
-    const int dy = g.dy0 + th * g.dys, dx = g.dx0 + tw * g.dxs;
-    taps[tid] = make_int4(dy, dx, ((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * SC,
-                          dy * g.W + dx);
-  }
-  if (tid < 2) *reinterpret_cast<uint4*>(Hs + SHP * SC + tid * 8) = make_uint4(0, 0, 0, 0);
-
-  // halo: flattened rows r0 + dymin .. r1 + dymax (the tap grid's row span)
-  const int dymin = g.dys > 0 ? g.dy0 : g.dy0 + (g.nth - 1) * g.dys;
-  const int dymax = g.dys > 0 ? g.dy0 + (g.nth - 1) * g.dys : g.dy0;
-  const int r0 = (int)fdiv((unsigned)m0, g.wg_mul, g.wg_shr);
-  const long long mlast = (m0 + SBM - 1 < g.M) ? m0 + SBM - 1 : g.M - 1;
-  const int r1 = (int)fdiv((unsigned)mlast, g.wg_mul, g.wg_shr);
-  const int hbase = (r0 + dymin) * g.W;
-  const int hp = (r1 - r0 + 1 + dymax - dymin) * g.W;
-
-  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
-  // stage the weights (64 x 32 chunks = 8 per thread) and the halo (2 chunks per pixel)
-  {
-    uint4 wv[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = tid + 256 * i, row = e >> 5, ch = e & 31;
-      wv[i] = *reinterpret_cast<const uint4*>(Wp + row * SK + ch * 8);
-    }
-    constexpr int HI = (2 * SHP + 255) / 256;
-    uint4 hv[HI];
-#pragma unroll
-    for (int i = 0; i < HI; ++i) {
-      const int e = tid + 256 * i, pix = e >> 1, half = e & 1;
-      const int gp = hbase + pix;
-      const bool ok = pix < hp && (unsigned)gp < (unsigned)NHW;
-      const unsigned off = ok ? ((unsigned)gp * SC + half * 8) * 2u : SOOB;
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
-      hv[i] = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = tid + 256 * i, row = e >> 5, ch = e & 31;
-      *reinterpret_cast<uint4*>(Ws + row * SK + wswz(row, ch) * 8) = wv[i];
-    }
-#pragma unroll
-    for (int i = 0; i < HI; ++i) {
-      const int e = tid + 256 * i, pix = e >> 1, half = e & 1;
-      if (pix < SHP) *reinterpret_cast<uint4*>(Hs + pix * SC + hswz(pix, half) * 8) = hv[i];
-    }
-  }
-  // per-lane A rows: halo pixel of the zero-offset tap and the pixel coordinates
-  int a_h[2], a_x[2], a_y[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long long m = m0 + wid * 64 + i * 32 + (lane & 31);
-    const unsigned r = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
-    a_x[i] = (int)((unsigned)m - r * (unsigned)g.W);
-    const unsigned n = fdiv(r, g.hg_mul, g.hg_shr);
-    a_y[i] = (m < g.M) ? (int)(r - n * (unsigned)g.H) : -(1 << 28);
-    a_h[i] = (int)(m - hbase);
-  }
-  __syncthreads();
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int h = lane >> 5;  // k half: channels 8h..8h+7 of the tap
-  auto frags = [&](int t, bf16x8 (&af)[2], bf16x8 (&bf)[2]) {
-    const int4 tp = taps[t];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bool ok = (unsigned)(a_x[i] + tp.y) < (unsigned)g.W &&
-                      (unsigned)(a_y[i] + tp.x) < (unsigned)g.H;
-      const int pix = ok ? a_h[i] + tp.w : SHP;
-      af[i] = *reinterpret_cast<const bf16x8*>(Hs + pix * SC + hswz(pix, h) * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = j * 32 + (lane & 31);
-      bf[j] = *reinterpret_cast<const bf16x8*>(Ws + row * SK + wswz(row, (tp.z >> 3) + h) * 8);
-    }
-  };
-  // 16 taps, fragments of tap t+1 read while tap t's MFMAs issue (static register sets)
-  bf16x8 a0[2], b0[2], a1[2], b1[2];
-  auto mma = [&](const bf16x8 (&af)[2], const bf16x8 (&bf)[2]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-  };
-  frags(0, a0, b0);
-#pragma unroll
-  for (int t = 0; t < 16; t += 2) {
-    frags(t + 1, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(a0, b0);
-    if (t + 2 < 16) frags(t + 2, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(a1, b1);
-  }
-  __syncthreads();  // the epilogue reuses the staging LDS
-  mfma_tile_epilogue<SBM, SCO, 4, 1, true, 1>(acc, smem, m0, 0, blockIdx.x, stats, g, Y, nullptr);
-}
-
-// Persistent variant: two workgroups per CU loop over the 256-pixel tiles.  The 32 KB weight
+// Persistent: two workgroups per CU loop over the 256-pixel tiles.  The 32 KB weight
 // matrix is staged ONCE per workgroup (the per-tile kernel re-reads it from L2 for every one
 // of the 25088 tiles at batch 512: as many bytes as the conv writes), and the input halo of
 // tile i+1 is loaded into registers while tile i runs its MFMAs and epilogue.  The epilogue
@@ -352,210 +233,10 @@ constexpr int FWP = FW + 3;    // padded halo row: 2 zero pixels left, 1 right (
 // zero padding comes from the pads and from the zero rows outside the image), every LDS
 // address of the k-loop is a per-lane base + a compile-time offset, and the global offsets
 // are 32-bit (all tensors < 2^31 elements, checked by stem_wgrad_fused_supported).
-__global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* Ds = reinterpret_cast<bf16_t*>(smem);  // [FR][FDP] dy tile
-  bf16_t* Xs = Ds + FR * FDP;                     // [5][FWP][16] padded input halo
-  float* cf = reinterpret_cast<float*>(Xs + 5 * FWP * SC);  // [5][64] a, b, cc, sc, sh
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int W = a.W, H = a.H, W2 = W >> 1, H2 = H >> 1;
-  const int R = 2 * W, nks = (R + 31) >> 5;
-  const int WP = W + 3;
-  const long long total = (long long)a.N * H2;
-  const long long s0 = (long long)blockIdx.x * a.spb;
-  const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
-
-  for (int i = tid; i < FR * FDP / 8; i += 512)
-    reinterpret_cast<uint4*>(Ds)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
-  for (int i = tid; i < 5 * FWP * SC / 8; i += 512)
-    reinterpret_cast<uint4*>(Xs)[i] = make_uint4(0, 0, 0, 0);  // pad columns stay zero
-  for (int c = tid; c < 64; c += 512) {
-    cf[c] = a.coef[c];
-    cf[64 + c] = a.coef[64 + c];
-    cf[128 + c] = a.coef[128 + c];
-    cf[192 + c] = a.sc[c];
-    cf[256 + c] = a.sh[c];
-  }
-
-  // staging roles: quad item tid (< W2 * 8): quad qb = tid >> 3, channel chunk tid & 7
-  const int chunk = tid & 7, c0 = chunk * 8;
-  const int nitems = W2 * 8;
-  const bool qitem = tid < nitems;
-  const int qb = tid >> 3;
-  constexpr int XI = (2 * FXH + 511) / 512;
-  // halo roles: 16-B piece e = tid + 512 i of the 5 x W x 32-B halo -> halo row hr, column x
-  int xh_row[XI], xh_lds[XI];
-#pragma unroll
-  for (int i = 0; i < XI; ++i) {
-    const int e = tid + 512 * i, pix = e >> 1;
-    const int hr = pix / W, x = pix - hr * W;
-    xh_row[i] = pix < 5 * W ? hr : 1 << 20;  // invalid pieces: never in range
-    xh_lds[i] = ((hr * WP + x + 2) * SC + (e & 1) * 8) * 2;
-  }
-  uint4 qy[4], qg[4];
-  uint2 qi[4];
-  uint4 xv[XI];
-  unsigned qok = 0;
-  const unsigned npix = (unsigned)a.N * H * W, npool = (unsigned)a.N * H2 * W2;
-  const auto ry = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, (int)(npix * 128u), 0x00020000);
-  const auto rg = __builtin_amdgcn_make_buffer_rsrc((void*)a.pdy, (short)0, (int)(npool * 128u), 0x00020000);
-  const auto ri = __builtin_amdgcn_make_buffer_rsrc((void*)a.pidx, (short)0, (int)(npool * 64u), 0x00020000);
-  const auto rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.xs, (short)0, (int)(npix * 32u), 0x00020000);
-  auto ld16 = [](decltype(ry) r, unsigned off) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    return make_uint4(v[0], v[1], v[2], v[3]);
-  };
-  auto load = [&](long long s) {
-    const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
-    if (qitem) {
-      const unsigned pix0 = ((unsigned)n * H + 2 * qa) * W + 2 * qb;
-#pragma unroll
-      for (int p = 0; p < 4; ++p)
-        qy[p] = ld16(ry, (pix0 + (p >> 1) * W + (p & 1)) * 128u + chunk * 16u);
-      qok = 0;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) {
-        const int oh = qa + (w >> 1), ow = qb + (w & 1);
-        const bool ok = oh < H2 && ow < W2;
-        qok |= ok ? 1u << w : 0u;
-        const unsigned o = ((unsigned)n * H2 + (ok ? oh : qa)) * W2 + (ok ? ow : qb);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b64(ri, o * 64u + chunk * 8u, 0, 0);
-        qi[w] = make_uint2(v[0], v[1]);
-        qg[w] = ld16(rg, o * 128u + chunk * 16u);
-      }
-    }
-    const int ylo = 2 - 2 * qa, yhi = H + 2 - 2 * qa;  // halo rows inside the image
-    // byte offset of halo row 0 (may be "negative" for the first pair of an image: those
-    // rows are never read)
-    const unsigned xb = ((unsigned)n * H + 2 * qa - 2) * (unsigned)W * 32u;
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      xv[i] = make_uint4(0, 0, 0, 0);
-      if (xh_row[i] >= ylo && xh_row[i] < yhi) xv[i] = ld16(rx, xb + (tid + 512 * i) * 16u);
-    }
-  };
-  // gather dz per quad (bn_bwd_apply_quad's terms, same order), dy to LDS; halo to LDS
-  auto store = [&]() {
-    if (qitem) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int ddy = p >> 1, ddx = p & 1;
-        float d[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = 0.f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int wa = w >> 1, wb = w & 1;
-          if (wa == 1 && ddy == 0) continue;
-          if (wb == 1 && ddx == 0) continue;
-          if (!(qok & (1u << w))) continue;
-          float gg[8];
-          s_unpack8(qg[w], gg);
-          const uint32_t aw[2] = {qi[w].x, qi[w].y};
-          const unsigned code = (unsigned)((ddy ? (wa ? 0 : 2) : 1) * 3 + (ddx ? (wb ? 0 : 2) : 1));
-#pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code) d[j] += gg[j];
-        }
-        float yv[8];
-        s_unpack8(qy[p], yv);
-        uint32_t o[4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const float4 ca = *reinterpret_cast<const float4*>(cf + c0 + 4 * h);
-          const float4 cb = *reinterpret_cast<const float4*>(cf + 64 + c0 + 4 * h);
-          const float4 cc = *reinterpret_cast<const float4*>(cf + 128 + c0 + 4 * h);
-          const float av[4] = {ca.x, ca.y, ca.z, ca.w}, bv[4] = {cb.x, cb.y, cb.z, cb.w};
-          const float cv[4] = {cc.x, cc.y, cc.z, cc.w};
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            float r2[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int jj = 2 * k + e, j = 4 * h + jj;
-              // no ReLU mask: a masked window's code is 15 (bn_relu_maxpool_kernel), so its
-              // gradient was never gathered into d
-              r2[e] = av[jj] * d[j] + bv[jj] * yv[j] + cv[jj];
-            }
-            o[2 * h + k] = pack_bf2(r2[0], r2[1]);
-          }
-        }
-        const int lp = ddy * W + 2 * qb + ddx;
-        *reinterpret_cast<uint4*>(Ds + lp * FDP + c0) = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < XI; ++i)
-      if (xh_row[i] < 5)
-        *reinterpret_cast<uint4*>(reinterpret_cast<unsigned char*>(Xs) + xh_lds[i]) = xv[i];
-  };
-
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // transposed-read roles: rows grp*4 + q (+16) of a 32-row k-step, column quad p
-  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int rbase = grp * 4 + q;
-  const int th = wid & 3;          // kernel row of this wave: dy = th - 2
-  const int cob = (wid >> 2) * 32;  // first output channel of this wave
-  // per-lane LDS bases: dy rows of k-step ks start at dsb + ks * 32 * FDP; the halo pixel of
-  // row r (pair-local, r < R) and tap column 0 is halo row (r >= W) + th, column r mod W - 2
-  const bf16_t* dsb = Ds + rbase * FDP + cob + 4 * pp;
-  auto xrow = [&](int r) -> const bf16_t* {
-    if (r >= R) r = 0;  // dy rows past the pair are zero: any in-bounds halo pixel will do
-    const int rr = r >= W ? 1 : 0;
-    return Xs + ((rr + th) * WP + (r - rr * W)) * SC + 4 * pp;
-  };
-
-  if (s0 < s1) load(s0);
-  __syncthreads();  // zeroed tiles, coefficients
-  for (long long s = s0; s < s1; ++s) {
-    store();
-    __syncthreads();
-    if (s + 1 < s1) load(s + 1);
-    for (int ks = 0; ks < nks; ++ks) {
-      const bf16_t* dk = dsb + ks * 32 * FDP;
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const s4v lo = tr_read4(dk + i * 16);
-        const s4v hi = tr_read4(dk + 16 * FDP + i * 16);
-        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-      const bf16_t* x0 = xrow(ks * 32 + rbase);
-      const bf16_t* x1 = xrow(ks * 32 + rbase + 16);
-#pragma unroll
-      for (int tw = 0; tw < 4; ++tw) {
-        const s4v lo = tr_read4(x0 + tw * SC);
-        const s4v hi = tr_read4(x1 + tw * SC);
-        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i][tw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][tw], 0, 0, 0);
-      }
-    }
-    __syncthreads();  // every wave done with the tiles before the next store
-  }
-  // slab[b][co][tap*16 + c]; 16x16 C map: col = lane & 15 (channel), row = (lane>>4)*4 + r (co)
-  float* out = a.slab + (long long)blockIdx.x * 64 * SK;
-  const int c = lane & 15;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int tw = 0; tw < 4; ++tw)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = cob + i * 16 + (lane >> 4) * 4 + r;
-        out[(long long)co * SK + (th * 4 + tw) * SC + c] = acc[i][tw][r];
-      }
-}
-
-// ------------------------------------------------------------------ warp-specialised variant
-// Same result as stem_wgrad_fused_kernel, but the VALU-heavy dy construction (quad gather +
-// BN apply, ~70 % of that kernel's cycles) and the MFMA reduction no longer alternate in
-// every wave.  Waves 0-7 (producers) build the dy tile of pair s+1 while waves 8-11
+// ------------------------------------------------------------------ warp-specialised kernel
+// The VALU-heavy dy construction (quad gather + BN apply, ~70 % of a single-role kernel's
+// cycles, where every wave alternated building dy and reducing it) and the MFMA reduction run
+// in different waves.  Waves 0-7 (producers) build the dy tile of pair s+1 while waves 8-11
 // (consumers) reduce pair s; the tiles (dy and the input halo) are double-buffered in LDS
 // and one barrier per pair hands them over.  Waves w, w+4 and w+8 share a SIMD (a
 // workgroup's waves go to the SIMDs cyclically), so every SIMD runs two producers (one
@@ -566,9 +247,6 @@ __global__ void __launch_bounds__(512) stem_wgrad_fused_kernel(StemBwdArgs a) {
 //   consumers: wave 8 + t owns kernel row t, all 64 output channels x 4 taps x 16 channels
 //              (16 accumulators); they also stage the next pair's halo and the pooled
 //              gradient rows into LDS
-// DIAG (timing diagnostics only, results wrong): 1 = consumers skip the MFMA k-loop,
-// 2 = producers skip the dy construction (loads still issued), 3 = both
-template <int DIAG>
 __global__ void __launch_bounds__(768) stem_wgrad_ws_kernel(StemBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* Ds0 = reinterpret_cast<bf16_t*>(smem);  // [2][FR][FDP] dy tiles
@@ -624,13 +302,6 @@ __global__ void __launch_bounds__(768) stem_wgrad_ws_kernel(StemBwdArgs a) {
     // dz gathered from the pooled gradient (masked windows carry code 15), dy = a dz + b y + cc
     auto store = [&](const Item& I, int it, long long s, bf16_t* Ds) {
       if (it >= nitems) return;
-      if (DIAG & 2) {
-        // keep the loads live without the gather / apply
-        const int lp = 2 * (it >> 3);
-        *reinterpret_cast<uint4*>(Ds + lp * FDP + (it & 7) * 8) =
-            make_uint4(I.qy[0].x ^ I.qy[1].x ^ I.qy[2].x ^ I.qy[3].x, 0, 0, 0);
-        return;
-      }
       const int chunk = it & 7, qb = it >> 3, c0 = chunk * 8;
       const int qa = (int)(s % H2);
       // the quad's 4 windows: pooled rows s (+1), columns qb (+1); masked off the image
@@ -845,7 +516,7 @@ __global__ void __launch_bounds__(768) stem_wgrad_ws_kernel(StemBwdArgs a) {
     const bf16_t* Xs = Xs0 + (i & 1) * XSZ;
     // one fragment set (the registers go to the producers' share); the two producer waves
     // on this SIMD cover the LDS latency
-    for (int ks = 0; ks < ((DIAG & 1) ? 0 : nks); ++ks) {
+    for (int ks = 0; ks < nks; ++ks) {
       frag(F0, Ds, Xs, ks);
       mma(F0);
     }
@@ -865,140 +536,6 @@ __global__ void __launch_bounds__(768) stem_wgrad_ws_kernel(StemBwdArgs a) {
       }
 }
 
-// ------------------------------------------------------------------ stem weight gradient
-// dW[co][tap*16 + c] = Σ_m dy[m][co] · xs[m + off(tap)][c] with dy read from memory (the
-// quad BN-backward apply wrote it).  Same row-pair steps, LDS images and MFMA loop as the
-// fused kernel above; the staging is plain 16-B loads, so a thread's share of a row pair
-// is small (4 dy chunks + 3 halo chunks) and NSET row pairs stay in flight in registers
-// (the fused kernel's quad gathers hold ~50 registers per pair and so stay one pair ahead,
-// which left it bound by memory latency).
-template <int NSET>
-__global__ void __launch_bounds__(512) stem_wgrad_dy_kernel(StemBwdArgs a, const bf16_t* __restrict__ dyp) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* Ds = reinterpret_cast<bf16_t*>(smem);  // [FR][FDP] dy tile
-  bf16_t* Xs = Ds + FR * FDP;                     // [FXH + 1][16] input halo, last = zeros
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int W = a.W, H = a.H, H2 = H >> 1;
-  const int R = 2 * W, nks = (R + 31) >> 5;
-  const long long total = (long long)a.N * H2;
-  const long long s0 = (long long)blockIdx.x * a.spb;
-  const long long s1 = s0 + a.spb < total ? s0 + a.spb : total;
-  for (int i = tid; i < FR * FDP / 8; i += 512)
-    reinterpret_cast<uint4*>(Ds)[i] = make_uint4(0, 0, 0, 0);  // rows >= R stay zero
-  if (tid < 2) *reinterpret_cast<uint4*>(Xs + FXH * SC + tid * 8) = make_uint4(0, 0, 0, 0);
-
-  constexpr int DI = (FR * 8 + 511) / 512;   // dy chunks per thread
-  constexpr int XI = (2 * FXH + 511) / 512;  // halo chunks per thread
-  uint4 dv[NSET][DI], xv[NSET][XI];
-  auto load = [&](long long s, uint4 (&d)[DI], uint4 (&x)[XI]) {
-    const int n = (int)(s / H2), qa = (int)(s - (long long)n * H2);
-    const long long base = ((long long)n * H + 2 * qa) * W;  // first pixel of the pair
-#pragma unroll
-    for (int i = 0; i < DI; ++i) {
-      const int e = tid + 512 * i;
-      d[i] = make_uint4(0, 0, 0, 0);
-      if (e < R * 8) d[i] = reinterpret_cast<const uint4*>(dyp)[base * 8 + e];
-    }
-    const int y0 = 2 * qa;
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
-      const int hr = pix / W, xx = pix - hr * W;
-      const int yy = y0 - 2 + hr;
-      x[i] = make_uint4(0, 0, 0, 0);
-      if (pix < 5 * W && yy >= 0 && yy < H)
-        x[i] = *reinterpret_cast<const uint4*>(a.xs + (((long long)n * H + yy) * W + xx) * SC + half * 8);
-    }
-  };
-  auto store = [&](const uint4 (&d)[DI], const uint4 (&x)[XI]) {
-#pragma unroll
-    for (int i = 0; i < DI; ++i) {
-      const int e = tid + 512 * i;
-      if (e < R * 8) *reinterpret_cast<uint4*>(Ds + (e >> 3) * FDP + (e & 7) * 8) = d[i];
-    }
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int e = tid + 512 * i, pix = e >> 1, half = e & 1;
-      if (pix < 5 * W) *reinterpret_cast<uint4*>(Xs + pix * SC + half * 8) = x[i];
-    }
-  };
-
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int rbase = grp * 4 + q;
-  const int th = wid & 3;
-  const int cob = (wid >> 2) * 32;
-  auto compute = [&](long long s) {
-    const int qa = (int)(s % H2);
-    const int y0 = 2 * qa;
-    for (int ks = 0; ks < nks; ++ks) {
-      int rlo[2], okrow[2], xr[2], rr[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = ks * 32 + rbase + 16 * u;
-        rlo[u] = r;
-        rr[u] = r >= W ? 1 : 0;
-        xr[u] = r - rr[u] * W;
-        okrow[u] = r < R && (unsigned)(y0 + rr[u] + th - 2) < (unsigned)H;
-      }
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const s4v lo = tr_read4(Ds + rlo[0] * FDP + cob + i * 16 + 4 * pp);
-        const s4v hi = tr_read4(Ds + rlo[1] * FDP + cob + i * 16 + 4 * pp);
-        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      }
-#pragma unroll
-      for (int tw = 0; tw < 4; ++tw) {
-        const bf16_t* src[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int xx = xr[u] + tw - 2;
-          const bool ok = okrow[u] && (unsigned)xx < (unsigned)W;
-          src[u] = ok ? Xs + ((rr[u] + th) * W + xx) * SC + 4 * pp : Xs + FXH * SC + 4 * pp;
-        }
-        const s4v lo = tr_read4(src[0]);
-        const s4v hi = tr_read4(src[1]);
-        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i][tw] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][tw], 0, 0, 0);
-      }
-    }
-  };
-  // NSET row pairs in flight: set k holds pair s with s % NSET == k (static register sets)
-#pragma unroll
-  for (int k = 0; k < NSET; ++k)
-    if (s0 + k < s1) load(s0 + k, dv[k], xv[k]);
-  __syncthreads();  // zeroed tiles
-  for (long long sb = s0; sb < s1; sb += NSET) {
-#pragma unroll
-    for (int k = 0; k < NSET; ++k) {
-      const long long s = sb + k;
-      if (s >= s1) break;
-      store(dv[k], xv[k]);
-      __syncthreads();
-      if (s + NSET < s1) load(s + NSET, dv[k], xv[k]);
-      compute(s);
-      __syncthreads();
-    }
-  }
-  float* out = a.slab + (long long)blockIdx.x * 64 * SK;
-  const int c = lane & 15;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int tw = 0; tw < 4; ++tw)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = cob + i * 16 + (lane >> 4) * 4 + r;
-        out[(long long)co * SK + (th * 4 + tw) * SC + c] = acc[i][tw][r];
-      }
-}
 }  // namespace
 
 bool stem_conv_supported(const ConvGeom& g) {
@@ -1016,89 +553,41 @@ bool stem_wgrad_fused_supported(int N, int H, int W, int C, int Cpad) {
          (long long)N * H * W * 64 < (1LL << 31);
 }
 
-static int stem_blocks_capped(int N, int H, long long cap) {
+// one 768-thread workgroup per CU (256 row-pair slices); each slice's slab is 64 KB
+int stem_wgrad_fused_blocks(int N, int H) {
   const long long pairs = (long long)N * (H / 2);
-  long long b = pairs < cap ? pairs : cap;
+  const long long b = pairs < 256 ? pairs : 256;
   const long long spb = (pairs + b - 1) / b;
   return (int)((pairs + spb - 1) / spb);
 }
-
-// fused kernel: one 512-thread block per CU; each block's slab is 64 KB.
-// DMLAB_STEM_BLOCKS overrides the cap (A/B runs)
-int stem_wgrad_fused_blocks(int N, int H) {
-  long long cap = 256;
-  if (const char* e = getenv("DMLAB_STEM_BLOCKS"))
-    if (atoi(e) > 0) cap = atoi(e);
-  return stem_blocks_capped(N, H, cap);
-}
-
-// stem_wgrad_dy_kernel (174 VGPRs): one block per CU
-int stem_wgrad_dy_blocks(int N, int H) { return stem_blocks_capped(N, H, 256); }
 
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st) {
   const long long pairs = (long long)N * (H / 2);
   StemBwdArgs a{xs, y, pdy, pidx, coef, sc, sh, slab, N, H, W, (int)((pairs + S - 1) / S)};
-  // DMLAB_STEM_WS=0: the single-role kernel (every wave builds dy, then reduces)
-  const char* ws = getenv("DMLAB_STEM_WS");
-  if (!ws || atoi(ws) != 0) {
-    const size_t sm = (size_t)2 * FR * FDP * 2 + (size_t)2 * 5 * FWP * SC * 2 +
-                      (size_t)4 * (FW / 2) * 64 * 3 + 3 * 64 * 4;
-    const char* dg = getenv("DMLAB_STEM_DIAG");
-    const int diag = dg ? atoi(dg) : 0;
-    auto k = diag == 1 ? stem_wgrad_ws_kernel<1> : diag == 2 ? stem_wgrad_ws_kernel<2>
-           : diag == 3 ? stem_wgrad_ws_kernel<3> : stem_wgrad_ws_kernel<0>;
-    set_smem_attr(k, sm);
-    k<<<S, 768, sm, st>>>(a);
-    DM_CHECK(hipGetLastError());
-    return;
-  }
-  const size_t sm = (size_t)FR * FDP * 2 + (size_t)5 * FWP * SC * 2 + 5 * 64 * 4;
-  set_smem_attr(stem_wgrad_fused_kernel, sm);
-  stem_wgrad_fused_kernel<<<S, 512, sm, st>>>(a);
-  DM_CHECK(hipGetLastError());
-}
-
-void stem_wgrad_dy(const bf16_t* xs, const bf16_t* dy, float* slab, int N, int H, int W, int S,
-                   hipStream_t st) {
-  const long long pairs = (long long)N * (H / 2);
-  StemBwdArgs a{xs, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, slab, N, H, W,
-                (int)((pairs + S - 1) / S)};
-  const size_t sm = (size_t)FR * FDP * 2 + (size_t)(FXH + 1) * SC * 2;
-  set_smem_attr(stem_wgrad_dy_kernel<3>, sm);
-  stem_wgrad_dy_kernel<3><<<S, 512, sm, st>>>(a, dy);
+  const size_t sm = (size_t)2 * FR * FDP * 2 + (size_t)2 * 5 * FWP * SC * 2 +
+                    (size_t)4 * (FW / 2) * 64 * 3 + 3 * 64 * 4;
+  set_smem_attr(stem_wgrad_ws_kernel, sm);
+  stem_wgrad_ws_kernel<<<S, 768, sm, st>>>(a);
   DM_CHECK(hipGetLastError());
 }
 
 void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const ConvGeom& g,
                hipStream_t st) {
-  const size_t main = (size_t)SCO * SK * 2 + (size_t)(SHP + 1) * SC * 2 + MAXTAPS * 16;
-  const size_t epi = (size_t)SBM * (SCO + 4) * 4;
-  const size_t sm = main > epi ? main : epi;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const int ntiles = (int)((g.M + SBM - 1) / SBM);
-  // DMLAB_STEM_PERSIST=0: one workgroup per tile (A/B runs)
-  static const bool pers = !getenv("DMLAB_STEM_PERSIST") || atoi(getenv("DMLAB_STEM_PERSIST"));
-  if (pers) {
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      DM_CHECK(hipGetDevice(&dev));
-      DM_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const size_t hal = (size_t)(SHP + 1) * SC * 2, band = (size_t)128 * (SCO + 4) * 4;
-    const size_t smp = (size_t)SCO * SK * 2 + (hal > band ? hal : band) + MAXTAPS * 16;
-    set_smem_attr(stem_conv_pers_kernel, smp);
-    const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
-    stem_conv_pers_kernel<<<grid, 256, smp, st>>>(X, Wp, Y, stats, g, xb, ntiles);
-    DM_CHECK(hipGetLastError());
-    return;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    DM_CHECK(hipGetDevice(&dev));
+    DM_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  set_smem_attr(stem_conv_kernel, sm);
-  // each wave's column of the MFMA epilogue needs rows >= M zeroed for the stats: the A rows
-  // of pixels past M are never valid (a_y poisoned), so their accumulators stay 0
-  stem_conv_kernel<<<(unsigned)ntiles, 256, sm, st>>>(X, Wp, Y, stats, g, xb);
+  const size_t hal = (size_t)(SHP + 1) * SC * 2, band = (size_t)128 * (SCO + 4) * 4;
+  const size_t smp = (size_t)SCO * SK * 2 + (hal > band ? hal : band) + MAXTAPS * 16;
+  set_smem_attr(stem_conv_pers_kernel, smp);
+  const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
+  stem_conv_pers_kernel<<<grid, 256, smp, st>>>(X, Wp, Y, stats, g, xb, ntiles);
   DM_CHECK(hipGetLastError());
 }
 

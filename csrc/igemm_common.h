@@ -88,16 +88,12 @@ using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 //    output pixel (y*osy+oy0, x*osx+ox0), optionally adding ADD (which may alias Y).
 // Rows >= g.M must hold zeros when stats are requested.  Requires (BM/PASSES)*(BN+4)*4 B of
 // LDS: with PASSES > 1 the tile is staged one band of BM/PASSES rows (whole wave rows) at a time.
-//  * optional BN-backward sums (bnb.y set; stats then receives Σdz, Σdz·x̂ — see BnBwdEpi)
-// LDS for the BN-backward combine: NT*16 + 2*BN*SPL floats (within the staging tile size)
 template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1>
 __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / WM / (MF32 ? 32 : 16)][BN / WN / (MF32 ? 32 : 16)],
                                                    unsigned char* smem, long long m0, int n0,
                                                    int stat_row, float* stats, const ConvGeom& g,
-                                                   bf16_t* Y, const bf16_t* ADD,
-                                                   const BnBwdEpi& bnb = BnBwdEpi{}) {
-  const bool bwd = stats && bnb.y;
-  float* fstats = bwd ? nullptr : stats;  // forward Σy, Σy² of the fp32 tile
+                                                   bf16_t* Y, const bf16_t* ADD) {
+  float* fstats = stats;  // Σy, Σy² of the fp32 tile
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = MF32 ? 32 : 16;
   constexpr int RM = TM / FM, RN = TN / FM;
@@ -153,21 +149,6 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
   float* cs = reinterpret_cast<float*>(smem);
   constexpr int CPR = BN / 8;
   static_assert(NT % CPR == 0, "a thread keeps one 8-column group across rows");
-  // BN-backward sums: this thread's 8 columns are fixed (e ≡ tid mod CPR)
-  float bs_[8], bq_[8], bmu[8], bis[8], bsc[8], bsh[8];
-  const int bcol = n0 + (tid % CPR) * 8;
-  if (bwd) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bs_[j] = 0.f;
-      bq_[j] = 0.f;
-      const bool okc = bcol + j < g.Ncols;
-      bmu[j] = okc ? bnb.mean[bcol + j] : 0.f;
-      bis[j] = okc ? bnb.invstd[bcol + j] : 0.f;
-      bsc[j] = okc && bnb.mode == 2 ? bnb.sc[bcol + j] : 0.f;
-      bsh[j] = okc && bnb.mode == 2 ? bnb.sh[bcol + j] : 0.f;
-    }
-  }
   constexpr int ITERS = RPB * CPR / NT;
   static_assert(ITERS * NT == RPB * CPR, "rows per band divisible by the block");
   const int cc = tid % CPR;
@@ -210,8 +191,8 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       }
     }
   };
-  if (!bwd) {
-    // plain store phase: the ADD loads of ALL bands are issued before the first accumulator
+  {
+    // store phase: the ADD loads of ALL bands are issued before the first accumulator
     // goes to LDS, so their latency overlaps the staging instead of being exposed per row
     // group (the main loop's staging registers are dead here: no rise in the kernel's peak)
     constexpr int NLD = PASSES * ITERS;
@@ -236,92 +217,6 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
         *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
                                                          pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
       }
-    }
-  } else {
-    // BN-backward sums: rows in groups of UNR, every load of a group (ADD, y, and the ReLU
-    // mask source) issued before its first store
-    constexpr int UNR = ITERS < 4 ? ITERS : 4;
-    static_assert(ITERS % UNR == 0, "row groups");
-#pragma unroll
-    for (int pb = 0; pb < PASSES; ++pb) {
-      stage_band(pb);
-#pragma unroll
-      for (int i0 = 0; i0 < ITERS; i0 += UNR) {
-        long long o[UNR];
-        bool ok[UNR];
-        uint4 av[UNR], yv[UNR], ov[UNR];
-        uint32_t mk[UNR];
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          row_off(pb, (tid + (i0 + u) * NT) / CPR, o[u], ok[u]);
-          av[u] = yv[u] = ov[u] = make_uint4(0, 0, 0, 0);
-          mk[u] = 0;
-          if (ok[u]) {
-            if (ADD) av[u] = *reinterpret_cast<const uint4*>(ADD + o[u]);
-            yv[u] = *reinterpret_cast<const uint4*>(bnb.y + o[u]);
-            if (bnb.mode == 1) ov[u] = *reinterpret_cast<const uint4*>(bnb.out + o[u]);
-            if (bnb.mode == 4) mk[u] = bnb.mask[o[u] >> 3];
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < UNR; ++u) {
-          if (!ok[u]) continue;
-          float v[8];
-          tile_vals((tid + (i0 + u) * NT) / CPR, av[u], v);
-          const uint4 packed = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                          pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
-          *reinterpret_cast<uint4*>(Y + o[u]) = packed;
-          // sums over the values as stored (bf16), exactly what a separate pass would read
-          const uint32_t pw[4] = {packed.x, packed.y, packed.z, packed.w};
-          const uint32_t yw[4] = {yv[u].x, yv[u].y, yv[u].z, yv[u].w};
-          const uint32_t ow[4] = {ov[u].x, ov[u].y, ov[u].z, ov[u].w};
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int sh16 = (j & 1) * 16;
-            float d = bf2f((bf16_t)(pw[j >> 1] >> sh16));
-            const float yf = bf2f((bf16_t)(yw[j >> 1] >> sh16));
-            if (bnb.mode == 1) d = bf2f((bf16_t)(ow[j >> 1] >> sh16)) > 0.f ? d : 0.f;
-            else if (bnb.mode == 2) d = yf * bsc[j] + bsh[j] > 0.f ? d : 0.f;
-            else if (bnb.mode == 4) d = (mk[u] >> j) & 1u ? d : 0.f;
-            bs_[j] += d;
-            bq_[j] += d * (yf - bmu[j]) * bis[j];
-          }
-        }
-      }
-    }
-  }
-  if (bwd) {
-    // fixed-order combine of the NT / CPR threads that share each 8-column group
-    __syncthreads();  // the staging tile is dead
-    float* rb = reinterpret_cast<float*>(smem);  // [NT][16]
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      rb[tid * 16 + j] = bs_[j];
-      rb[tid * 16 + 8 + j] = bq_[j];
-    }
-    __syncthreads();
-    // two levels, both in a fixed order: SPL threads per column each sum RL/SPL rows, then
-    // one thread per column sums the SPL partials (a serial RL-long LDS chain per column was
-    // the epilogue's tail)
-    constexpr int RL = NT / CPR;
-    constexpr int SPL = (NT / (2 * BN)) < 1 ? 1 : ((NT / (2 * BN)) > RL ? RL : (NT / (2 * BN)));
-    static_assert(RL % SPL == 0, "combine split");
-    float* rp = rb + NT * 16;  // [2 * BN][SPL] partials
-    for (int e = tid; e < 2 * BN * SPL; e += NT) {
-      const int cq = e / SPL, part = e % SPL;
-      const int c = cq >> 1, which = cq & 1;
-      const int grp = c >> 3, j = c & 7;
-      float a = 0.f;
-      for (int r = part * (RL / SPL); r < (part + 1) * (RL / SPL); ++r)
-        a += rb[(r * CPR + grp) * 16 + which * 8 + j];
-      rp[e] = a;
-    }
-    __syncthreads();
-    for (int cq = tid; cq < 2 * BN; cq += NT) {
-      const int c = cq >> 1, which = cq & 1;
-      float a = 0.f;
-      for (int part = 0; part < SPL; ++part) a += rp[cq * SPL + part];
-      if (n0 + c < g.Ncols) stats[((long long)stat_row * 2 + which) * g.Ncols + n0 + c] = a;
     }
   }
 }

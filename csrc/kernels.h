@@ -73,25 +73,17 @@ void p2p_xgmi_recv(void* dst, long long bytes, const void* ring, const void* ful
 // conv_igemm.hip
 struct ConvGeom;
 struct ConvGeomSet;
-struct BnBwdEpi;
 bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st, const BnBwdEpi* bnb = nullptr);
+               const ConvGeom& g, int cfg, hipStream_t st);
 // conv_stem.hip: s2d stem (16 channels, 16 taps, 64 outputs) with resident weights (cfg 60)
 bool stem_conv_supported(const ConvGeom& g);
 void stem_conv(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, float* stats, const ConvGeom& g,
                hipStream_t st);
 // fused stem BN backward (quad max-pool gather) + s2d weight gradient -> slabs [S][64][256]
 bool stem_wgrad_fused_supported(int N, int H, int W, int C, int Cpad);
-void bn_bwd_apply_quad(const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx, const float* coef,
-                       const float* scale, const float* shift, bf16_t* dy, int N, int H, int W,
-                       int C, hipStream_t st);
-// same s2d weight gradient from a materialised dy [N][H][W][64] (several row pairs in flight)
-void stem_wgrad_dy(const bf16_t* xs, const bf16_t* dy, float* slab, int N, int H, int W, int S,
-                   hipStream_t st);
 int stem_wgrad_fused_blocks(int N, int H);
-int stem_wgrad_dy_blocks(int N, int H);
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st);
@@ -106,8 +98,7 @@ bool conv_halo_supported(const ConvGeom& g);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,
-               const float* pre_sc = nullptr, const float* pre_sh = nullptr,
-               const BnBwdEpi* bnb = nullptr);
+               const float* pre_sc = nullptr, const float* pre_sh = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,

@@ -208,12 +208,11 @@ void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const Con
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
   auto k = pre_sc ? wgrad_halo_kernel<HRN, NTY, true> : wgrad_halo_kernel<HRN, NTY, false>;
   set_smem_attr(k, sm);
-  // XCD-grouped order for the 9-tap tiles (DMLAB_WGRAD_XCD=0: plain 3-D grid).  Measured
-  // (tools/bench_conv.py, one call): 9-tap layer2 +2-4 %, layer3/4 within 1 %, step 11.55 vs
-  // 11.57 ms; the 3-tap tiles lose (layer1 526 -> 475 TF/s) and keep the 3-D grid
-  static const int xcd_on = getenv("DMLAB_WGRAD_XCD") ? atoi(getenv("DMLAB_WGRAD_XCD")) : 1;
+  // XCD-grouped order for the 9-tap tiles.  Measured (tools/bench_conv.py, one call): 9-tap
+  // layer2 +2-4 %, layer3/4 within 1 %, step 11.55 vs 11.57 ms; the 3-tap tiles lose (layer1
+  // 526 -> 475 TF/s) and keep the 3-D grid
   const int xy = (int)(grid.x * grid.y);
-  if (xcd_on && NTY == 3 && xy > 1 && S > 1) {
+  if (NTY == 3 && xy > 1 && S > 1) {
     const unsigned z8 = (unsigned)((S + 7) / 8 * 8);
     k<<<dim3(z8 * xy), 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, xy,
                                        (int)grid.x, S);

@@ -160,11 +160,10 @@ class ConvBN(Layer):
 
         return CB.convbn_fwd(self, x, ctx, train, residual, raw=raw, pre=pre)
 
-    def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None, consumer=None):
+    def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None):
         from dmlab.ops import convbn as CB
 
-        return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into,
-                             consumer=consumer)
+        return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into)
 
 
 class ConvBNPool(ConvBN):
@@ -229,35 +228,16 @@ class BasicBlock(Layer):
 
     def _down_stream(self):
         prog = getattr(self, "_prog", None)
-        if prog is None or os.environ.get("DMLAB_DOWN_STREAM", "1") == "0":
+        if prog is None:
             return None
         return prog._side_stream() if prog._native_active else None
 
-    def bn_consumer(self, ctx):
-        """The ConvBN whose BN backward consumes this block's output gradient first."""
-        return self.c2, ctx["c2"]
-
     def native_bwd(self, dy, ctx, need_dx):
-        # The dgrad producing a BN's input gradient also reduces that BN's backward sums in
-        # its epilogue: c2's dgrad for c1's BN, c1's dgrad for the previous block's c2
-        # (``_prev``, set by the Program), so no BN backward re-reads dout and y to reduce.
-        prev = ctx.get("_prev")
-        outer = prev[0].bn_consumer(prev[1]) if prev is not None and hasattr(prev[0], "bn_consumer") else None
         # c2's backward returns (d_input_of_c2, d_residual); d_residual = ReLU-masked dy
-        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True, consumer=(self.c1, ctx["c1"]))
+        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True)
         if self.down is None:
             # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass)
-            return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None,
-                                      consumer=outer)
-        from dmlab.ops import convbn as CB
-
-        if outer is not None and CB._FUSE_BN_BWD:
-            # projection skip: its dgrad writes dx first, then c1's dgrad accumulates into it
-            # in place (the last writer of dx computes the fused sums over the final values)
-            dx = self.down.native_bwd(dres, ctx["cd"], need_dx)
-            self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_into=dx,
-                               consumer=outer if dx is not None else None)
-            return dx
+            return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None)
         dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
         # projection skip: its dgrad (one parity class of the 1x1/s2 conv) accumulates in place
         self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx)

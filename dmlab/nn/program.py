@@ -162,12 +162,6 @@ class _ProgramFn(torch.autograd.Function):
             side.wait_stream(main)  # fork (under hipGraph capture: joins the capture)
         prog._wgrad_stream = side
         pending = []  # (layer index, event after its wgrads) whose hooks have not run
-        # DMLAB_DEFER_WGRAD = d: the weight gradients of layers 1..d (the d layers after
-        # layer 0) are queued on the side stream only when layer 0's backward starts, so they
-        # overlap that backward (the ResNet stem: latency-bound, ~0.8 ms, alone on the GPU)
-        # instead of the compute-bound dgrads of their own layers
-        defer = prog._defer_wgrad_layers() if side is not None else 0
-        held, held_fns = [], []  # layers whose wgrads are held back, and their launches
 
         # Hooks registered stream_ok (DDP without a communication-dtype copy) are issued on
         # the side stream once it has caught up with the main stream: the collective they
@@ -185,61 +179,31 @@ class _ProgramFn(torch.autograd.Function):
                     for hook in prog._grad_hooks:
                         hook(prog, j)
 
-        def flush():
-            for fn in held_fns:
-                fn()
-            held_fns.clear()
-            if held and prog._grad_hooks:
-                if side_hooks:
-                    run_side_hooks(list(held))
-                else:
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    pending.extend((j, ev) for j in held)
-            held.clear()
-
         try:
             for i in range(n - 1, -1, -1):
                 layer = prog.layers[i]
                 need_dx = i > 0 or ctx.need_dx
-                if i == 0 and (held or held_fns):
-                    flush()
-                if i > 0 and ctx.ctxs[i] is not None:
-                    # the layer whose backward consumes this one's dx (lets a producer fuse
-                    # work of the consumer into its own kernels, e.g. BN-backward sums)
-                    ctx.ctxs[i]["_prev"] = (prog.layers[i - 1], ctx.ctxs[i - 1])
-                prog._deferred_wgrads = held_fns if 0 < i <= defer else None
                 with _range(f"bwd:{i}:{type(layer).__name__}"):
                     dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
-                prog._deferred_wgrads = None
                 ctx.ctxs[i] = None  # free saved activations as soon as possible
                 if side is None:
                     for hook in prog._grad_hooks:
                         hook(prog, i)
                     continue
                 if side_hooks:
-                    if 0 < i <= defer:
-                        held.append(i)
-                    else:
-                        run_side_hooks([i])
+                    run_side_hooks([i])
                     continue
                 for j, ev in pending:
                     main.wait_event(ev)
                     for hook in prog._grad_hooks:
                         hook(prog, j)
                 pending = []
-                if 0 < i <= defer:
-                    held.append(i)
-                    continue
                 if prog._grad_hooks:
                     ev = torch.cuda.Event()
                     ev.record(side)
                     pending.append((i, ev))
         finally:
             prog._wgrad_stream = None
-            prog._deferred_wgrads = None
-        if held or held_fns:
-            flush()
         if side is not None:
             main.wait_stream(side)
             for j, _ in pending:
@@ -278,7 +242,6 @@ class Program(nn.Module):
         self._uses_side_stream = False  # set by subclasses whose layers queue wgrads aside
         self._side_streams = {}
         self._wgrad_stream = None
-        self._deferred_wgrads = None  # set during backward: wgrad launches held back
 
     # ---------------------------------------------------------------- construction
     def build(self, layers):
@@ -379,12 +342,6 @@ class Program(nn.Module):
             h = layer.fwd(h, Ctx(), False)
         return h
 
-    def _defer_wgrad_layers(self):
-        """Number of layers after layer 0 whose weight gradients Program.backward holds
-        back until layer 0's backward (DMLAB_DEFER_WGRAD, default 0 = none)."""
-        d = int(os.environ.get("DMLAB_DEFER_WGRAD", "0"))
-        return max(0, min(d, len(self.layers) - 1))
-
     def _side_stream(self):
         """Second HIP stream for off-critical-path backward work (weight gradients), or
         None when disabled (``DMLAB_WGRAD_STREAM=0``) or no layer uses it."""
@@ -393,10 +350,9 @@ class Program(nn.Module):
         dev = torch.cuda.current_device()
         st = self._side_streams.get(dev)
         if st is None:
-            # DMLAB_WGRAD_PRIO: stream priority of the side stream (lower = higher priority);
-            # the weight gradients have slack until the end of backward, the main chain does not
-            prio = int(os.environ.get("DMLAB_WGRAD_PRIO", "0"))
-            st = self._side_streams[dev] = torch.cuda.Stream(device=dev, priority=prio)
+            # default priority (a higher-priority side stream measured -1.2 %:
+            # profiles/bench_ab_side_stream_knobs_r3.jsonl)
+            st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
         return st
 
     def prepare_native(self, x):

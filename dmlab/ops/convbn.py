@@ -308,54 +308,11 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-# Fused BN-backward sums in the dgrad epilogue: opt-in.  Measured on MI355X (ResNet-18,
-# batch 256): the separate reductions it removes cost ~460 us/step, but the heavier dgrad
-# epilogues (reading y, and `out` for residual BNs, behind the output store) cost ~600 us,
-# e.g. layer1 dgrad 84 -> 139 us.  Kept for A/B runs: DMLAB_FUSE_BN_BWD=1.
-_FUSE_BN_BWD = os.environ.get("DMLAB_FUSE_BN_BWD", "0") == "1"
-
-# Stem backward (DMLAB_STEM_BWD): "split" = coefficients once, then per batch slice the quad
-# BN-backward apply and, on the side stream, the s2d weight gradient of that slice
-# (DMLAB_STEM_SPLIT slices); "fused" = the apply computed inside the weight-gradient kernel
-# (dy never written, but its gathers keep only one row pair in flight); "legacy" = one
-# apply pass + the generic igemm weight gradient.  Kept for A/B runs.
-_STEM_BWD = os.environ.get("DMLAB_STEM_BWD", "fused")
-_STEM_SPLIT = int(os.environ.get("DMLAB_STEM_SPLIT", "4"))
-# weight gradient of the split path: "dy" (stem_wgrad_dy_kernel) or "igemm" (v2 s2d tiles)
-_STEM_WGRAD = os.environ.get("DMLAB_STEM_WGRAD", "dy")
-
-# Weight gradients of convs with at least this many output channels go to the Program's
-# side stream (DMLAB_WGRAD_STREAM_MIN_COUT; 0 = all).
-_SIDE_MIN_COUT = int(os.environ.get("DMLAB_WGRAD_STREAM_MIN_COUT", "0"))
-
-
-def bnb_spec(layer, ctx):
-    """conv_dgrad keyword arguments that make a dgrad epilogue reduce the BN-backward sums
-    (Σdz, Σdz·x̂) of ``layer`` — the ConvBN whose BN-output gradient the dgrad produces —
-    or None when that BN's backward cannot use them (stem pool gather, eval mode)."""
-    if getattr(layer, "pool_k", 0) or ctx.get("mean") is None or "y" not in ctx:
-        return None
-    if ctx["has_res"]:
-        # ReLU mask of a residual BN: the forward's 1-bit mask (4) or the saved output (1)
-        mode = 4 if ctx.get("mask") is not None else 1
-    else:
-        mode = 2 if layer.relu else 0
-    return dict(bnb_y=ctx["y"], bnb_out=ctx.get("out") if mode == 1 else None,
-                bnb_mean=ctx["mean"], bnb_invstd=ctx["invstd"],
-                bnb_scale=ctx["scale"] if mode == 2 else None,
-                bnb_shift=ctx["shift"] if mode == 2 else None, bnb_mode=mode,
-                bnb_mask=ctx.get("mask") if mode == 4 else None)
-
-
-def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=None):
+def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     """Returns dx (or (dx, dres) when the forward had a residual input).
 
     ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient)
-    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)
-    ``consumer``: (ConvBN, ctx) whose BN backward consumes dx; the dgrad epilogue then
-                  also reduces that BN's backward sums (stored in its ctx as
-                  ``dz_stats``), so its reduction pass over dx and y is skipped.  dx must
-                  be final after this call (the last writer of dx computes the sums)."""
+    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)"""
     L = lib()
     x, y = ctx["x"], ctx["y"]
     N, OH, OW, cout = y.shape
@@ -366,11 +323,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     dout = dout.contiguous()
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
     pre_sums = {}
-    zs = ctx.pop("dz_stats", None)
-    if zs is not None and zs[2].data_ptr() == dout.data_ptr() and zs[2].shape == dout.shape:
-        pre_sums = dict(pre_slab=zs[0], pre_rows=zs[1])  # sums from the producer's epilogue
     pool = getattr(layer, "pool_k", 0)
-    if pool and ctx.get("yarg") is not None and not pre_sums:
+    if pool and ctx.get("yarg") is not None:
         # stem: Σdz, Σdz·x̂ over the pooled grid (pooled grad masked at the argmax, x̂ from
         # y at the argmax) -- reads 2 pooled-size tensors instead of y + grad + codes
         Mp = ctx["yarg"].numel() // cout
@@ -381,54 +335,9 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
         pre_sums = dict(pre_slab=part, pre_rows=rows)
     stem_ok = (pool and s2d and pre_sums and ctx["first"] and not ctx["has_res"]
                and L.stem_bwd_fused_supported(y, x))
-    if stem_ok and _STEM_BWD == "split":
-        # coefficients once; then per batch slice the quad BN-backward apply (main stream)
-        # and the s2d weight gradient of that slice (side stream), so the weight gradient
-        # of slice i overlaps the apply of slice i+1; one fixed-order reduce of all slabs
-        L.stem_bwd_coef(y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
-                        layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
-                        ctx["scale"], ctx["shift"], dout, ctx["idx"], pre_sums["pre_slab"],
-                        pre_sums["pre_rows"], work)
-        coef = work[: 3 * cout]
-        dy = empty_nhwc(N, OH, OW, cout, y)
-        P = max(1, min(_STEM_SPLIT, N))
-        bounds = [N * i // P for i in range(P + 1)]
-        nblk = [L.stem_wgrad_blocks(bounds[i + 1] - bounds[i], OH) for i in range(P)]
-        side = getattr(layer._prog, "_wgrad_stream", None)
-        main = torch.cuda.current_stream()
-        with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            slab = torch.empty(sum(nblk) * 64 * 256, device=y.device, dtype=torch.float32)
-        off = 0
-        for i in range(P):
-            a, b = bounds[i], bounds[i + 1]
-            L.bn_bwd_apply_quad(y[a:b], dout[a:b], ctx["idx"][a:b], coef, ctx["scale"],
-                                ctx["shift"], dy[a:b])
-            if side is not None:
-                side.wait_stream(main)
-            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                if _STEM_WGRAD == "igemm":
-                    # the generic s2d igemm weight gradient of this slice, accumulated
-                    Mi = (b - a) * OH * OW
-                    wc, Si = _wgrad_plan(Mi, cout, 16 * x.shape[3])
-                    sl = torch.empty(Si * cout * 16 * x.shape[3], device=y.device,
-                                     dtype=torch.float32)
-                    L.conv_wgrad(x[a:b], dy[a:b], layer.grad_slot("weight"), sl, layer.cin, 4, 4,
-                                 1, 2, acc if i == 0 else 1.0, Si, wc, True)
-                else:
-                    L.stem_wgrad_dy(x[a:b], dy[a:b], slab[off * 16384:(off + nblk[i]) * 16384],
-                                    nblk[i])
-            off += nblk[i]
-        if side is not None:
-            dy.record_stream(side)
-            x.record_stream(side)
-        if _STEM_WGRAD != "igemm":
-            with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-                L.wgrad_reduce_s2d(slab, off, cout, layer.cin, x.shape[3],
-                                   layer.grad_slot("weight"), acc)
-        return None
-    if stem_ok and _STEM_BWD == "fused":
+    if stem_ok:
         # stem: BN-backward apply fused into the s2d weight gradient -- the full-resolution
-        # dy is never written (csrc/conv_stem.hip stem_wgrad_fused_kernel)
+        # dy is never written (csrc/conv_stem.hip stem_wgrad_ws_kernel)
         slab = torch.empty(L.stem_bwd_slab_floats(N, OH), device=y.device, dtype=torch.float32)
         L.stem_bwd_fused(y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
                          layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
@@ -462,8 +371,6 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
     # not hand their memory out again before the wgrad has read them.
     pre = ctx.get("pre")
     side = getattr(layer._prog, "_wgrad_stream", None)
-    if side is not None and layer.cout < _SIDE_MIN_COUT:
-        side = None
 
     def launch_wgrad():
         if side is not None:
@@ -482,33 +389,18 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, consumer=No
             L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S,
                          wcfg, s2d, **pre_kw)
 
-    deferred = getattr(layer._prog, "_deferred_wgrads", None) if side is not None else None
-    if deferred is not None:
-        # the Program launches it later (Program.backward: DMLAB_DEFER_WGRAD), e.g. next to
-        # the latency-bound stem backward instead of under this block's dgrads
-        deferred.append(launch_wgrad)
-    else:
-        launch_wgrad()
+    launch_wgrad()
     dx = None
     if need_dx and not ctx["first"]:
         _, wd = packed_weights(layer, need_wd=True)
         N_, H, W, Cin = x.shape
         cfg = dgrad_cfg(N_ * H * W, Cin, k, s, cout, H, W)
-        bkw = {}
-        spec = bnb_spec(*consumer) if (consumer is not None and _FUSE_BN_BWD) else None
-        if spec is not None:
-            rows = L.dgrad_bnb_rows(N_, H, W, s, cfg)
-            if rows:
-                bkw = dict(spec, bnb_slab=torch.empty(rows * 2 * Cin, device=y.device,
-                                                      dtype=torch.float32))
         if dx_into is not None:
             dx = dx_into
-            r = L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg, **bkw)
+            L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **bkw)
-        if bkw and r:
-            consumer[1]["dz_stats"] = (bkw["bnb_slab"], r, dx)
+            L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)
     if ctx["has_res"]:
         return dx, dres
     return dx

@@ -499,72 +499,6 @@ def test_pack_weights_tiled_matches_per_layer(dev):
         assert torch.equal(wd, rd)
 
 
-@pytest.mark.parametrize("geom", [(3, 14, 128, 128, 3, 1, 1), (2, 14, 64, 128, 3, 2, 1),
-                                  (2, 15, 64, 128, 3, 2, 1), (2, 9, 64, 64, 1, 2, 0),
-                                  (2, 7, 128, 256, 3, 1, 1)])
-@pytest.mark.parametrize("mode", [0, 1, 2, 4])
-@pytest.mark.parametrize("accumulate", [False, True])
-@pytest.mark.parametrize("cfg", [15, 16, 20, 39, 41, 42])
-def test_conv_dgrad_fused_bn_backward_sums(dev, geom, mode, accumulate, cfg):
-    """The dgrad epilogue's BN-backward sums (Σdz, Σdz·x̂ of the BN whose input gradient dx
-    is) equal the sums over the stored dx; the BN backward run from them equals the
-    unfused one bit for bit in the coefficients' inputs' tolerance."""
-    N, H, Cin, Cout, k, s, p = geom
-    if s == 2 and cfg not in (15, 16):
-        pytest.skip("stride-2 dgrad runs on the v3 tiles")
-    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
-    OH = (H + 2 * p - k) // s + 1
-    g = torch.Generator(device=dev).manual_seed(9)
-    dy = torch.randn(N, OH, OH, Cout, device=dev, generator=g).bfloat16()
-    y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()     # consumer BN input
-    out = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()   # its block output
-    f = dict(device=dev, dtype=torch.float32)
-    mean = torch.randn(Cin, **f) * 0.1
-    invstd = torch.rand(Cin, **f) + 0.5
-    sc, sh = torch.randn(Cin, **f), torch.randn(Cin, **f)
-    dx = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
-    # the forward's 1-bit ReLU mask of `out` (bit j of byte i: channel j of chunk i)
-    bits = (out.reshape(-1, 8) > 0).to(torch.int32) << torch.arange(8, device=dev, dtype=torch.int32)
-    mask = bits.sum(1).to(torch.uint8)
-    L = lib()
-    rows = L.dgrad_bnb_rows(N, H, H, s, cfg)
-    slab = torch.full((max(rows, 1) * 2 * Cin,), float("nan"), **f)
-    r = L.conv_dgrad(dy, wd, dx, k, k, s, p, dx if accumulate else None, cfg,
-                     bnb_y=y, bnb_out=out, bnb_mean=mean, bnb_invstd=invstd, bnb_scale=sc,
-                     bnb_shift=sh, bnb_mode=mode, bnb_slab=slab,
-                     bnb_mask=mask if mode == 4 else None)
-    if k == 1 and s == 2 and accumulate:
-        assert r == 0  # tap-less parity classes keep old values: not fusable
-        return
-    assert r == rows > 0
-    d = dx.float().reshape(-1, Cin)
-    yf = y.float().reshape(-1, Cin)
-    if mode in (1, 4):
-        d = torch.where(out.float().reshape(-1, Cin) > 0, d, torch.zeros_like(d))
-    elif mode == 2:
-        d = torch.where(yf * sc + sh > 0, d, torch.zeros_like(d))
-    ref_s = d.double().sum(0)
-    ref_q = (d.double() * ((yf.double() - mean.double()) * invstd.double())).sum(0)
-    part = slab[: r * 2 * Cin].view(r, 2, Cin).double().sum(0)
-    torch.testing.assert_close(part[0], ref_s, rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(part[1], ref_q, rtol=1e-4, atol=1e-3)
-    # the BN backward fed with these sums == the BN backward that reduces them itself
-    gamma = torch.rand(Cin, **f) + 0.5
-    res = []
-    for pre in (False, True):
-        dyy = torch.empty_like(y)
-        dg, db = torch.zeros(Cin, **f), torch.zeros(Cin, **f)
-        work = torch.empty(L.bn_bwd_work(N * H * H, Cin), **f)
-        kw = dict(pre_slab=slab, pre_rows=r) if pre else {}
-        L.bn_backward(dx, out if mode == 1 else None, y, mean, invstd, gamma, dg, db, 0.0, mode,
-                      sc if mode == 2 else None, sh if mode == 2 else None, None, None, 3, 2, 1,
-                      dyy, None, work, mask=mask if mode == 4 else None, **kw)
-        res.append((dyy.float(), dg, db))
-    torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-4, atol=1e-3)
-    torch.testing.assert_close(res[0][2], res[1][2], rtol=1e-4, atol=1e-3)
-    assert _rel(res[0][0], res[1][0]) < 1e-3
-
-
 # pipelined LDS-DMA tiles (conv_pipe.hip, cfg 90/91/92): 3x3 and 1x1 taps, stride 1 and 2,
 # odd and even K-step counts (1 step, 9 steps, 32 steps), several N tiles (XCD-grouped 1-D
 # grid), partial last M tile, and channel counts the tile cannot take (falls back)

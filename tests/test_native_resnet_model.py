@@ -72,12 +72,11 @@ def test_resnet18_eval_mode(dev):
 
 
 @pytest.mark.parametrize("res", [64, 224])
-@pytest.mark.parametrize("variant", ["fused", "split"])
-def test_fused_stem_backward_matches_unfused(dev, res, variant):
-    """The stem backward variants (conv_stem.hip: the BN-backward apply fused into the s2d
-    weight gradient, or per batch slice apply + pipelined s2d weight gradient) give the same
-    stem gradients as the separate quad-apply pass + igemm wgrad (same bf16 dy, fp32 sums in
-    another order), and every other gradient bit-for-bit."""
+def test_fused_stem_backward_matches_unfused(dev, res, monkeypatch):
+    """The fused stem backward (conv_stem.hip: the BN-backward apply and max-pool gather
+    computed inside the s2d weight gradient, dy never written) gives the same stem gradients
+    as the generic path (quad-apply pass writing dy + igemm s2d weight gradient; same bf16 dy,
+    fp32 sums in another order), and every other gradient bit for bit."""
     import dmlab.ops.convbn as cb
 
     torch.manual_seed(3)
@@ -85,16 +84,14 @@ def test_fused_stem_backward_matches_unfused(dev, res, variant):
     x = torch.rand(4, 3, res, res, device=dev)
     y = torch.randint(0, 10, (4,), device=dev)
     grads = []
-    old = cb._STEM_BWD
-    try:
-        for mode in ("legacy", variant):
-            cb._STEM_BWD = mode
+    for fused in (False, True):
+        with monkeypatch.context() as mp:
+            if not fused:
+                mp.setattr(cb.lib(), "stem_bwd_fused_supported", lambda *args: False)
             a.flat.grad.zero_()
             cross_entropy(a(x), y).backward()
             torch.cuda.synchronize()
-            grads.append({n: p.grad.detach().clone() for n, p in a.named_parameters()})
-    finally:
-        cb._STEM_BWD = old
+        grads.append({n: p.grad.detach().clone() for n, p in a.named_parameters()})
     for n in grads[0]:
         if n.startswith("stem."):
             assert _rel(grads[1][n], grads[0][n]) < 2e-3, n
@@ -102,40 +99,28 @@ def test_fused_stem_backward_matches_unfused(dev, res, variant):
             torch.testing.assert_close(grads[1][n], grads[0][n], rtol=0, atol=0, msg=n)
 
 
-@pytest.mark.parametrize("defer", [1, 2])
-def test_deferred_wgrads_match(dev, monkeypatch, defer):
-    """DMLAB_DEFER_WGRAD holds the weight gradients of layers 1..d back until the stem's
-    backward: every gradient is bit-identical, and each layer's grad hook (DDP's bucket
-    launch point) still sees its finished weight gradients on the main stream."""
+def test_grad_hooks_see_final_wgrads(dev):
+    """Each layer's grad hook (DDP's bucket launch point) runs after that layer's side-stream
+    weight gradients: the snapshot it takes is the final gradient, bit for bit."""
     torch.manual_seed(5)
     a = ResNet18(num_classes=10).to(dev)
     x = torch.rand(8, 3, 64, 64, device=dev)
     y = torch.randint(0, 10, (8,), device=dev)
-    runs = []
-    for d in (0, defer):
-        monkeypatch.setenv("DMLAB_DEFER_WGRAD", str(d))
-        snaps = {}
+    snaps = {}
 
-        def hook(prog, i):
-            # runs on the main stream after the wait for layer i's side-stream wgrads
-            snaps[i] = [p.grad.detach().clone() for p in prog.layers[i].parameters()]
+    def hook(prog, i):
+        snaps[i] = [p.grad.detach().clone() for p in prog.layers[i].parameters()]
 
-        a.register_grad_hook(hook)
-        try:
-            a.flat.grad.zero_()
-            cross_entropy(a(x), y).backward()
-            torch.cuda.synchronize()
-        finally:
-            a.remove_grad_hook(hook)
-        assert sorted(snaps) == list(range(len(a.layers)))
-        runs.append(({n: p.grad.detach().clone() for n, p in a.named_parameters()}, snaps))
-    (g0, s0), (g1, s1) = runs
-    for n in g0:
-        torch.testing.assert_close(g1[n], g0[n], rtol=0, atol=0, msg=n)
-    for i in s0:
-        for u, v in zip(s1[i], s0[i]):
-            torch.testing.assert_close(u, v, rtol=0, atol=0, msg=f"hook {i}")
-        # the hook snapshot is the final gradient
-        for u, p in zip(s1[i], a.layers[i].parameters()):
-            torch.testing.assert_close(u, g1[[n for n, q in a.named_parameters() if q is p][0]],
+    a.register_grad_hook(hook)
+    try:
+        a.flat.grad.zero_()
+        cross_entropy(a(x), y).backward()
+        torch.cuda.synchronize()
+    finally:
+        a.remove_grad_hook(hook)
+    assert sorted(snaps) == list(range(len(a.layers)))
+    g = {n: p.grad.detach().clone() for n, p in a.named_parameters()}
+    for i in snaps:
+        for u, p in zip(snaps[i], a.layers[i].parameters()):
+            torch.testing.assert_close(u, g[[n for n, q in a.named_parameters() if q is p][0]],
                                        rtol=0, atol=0)

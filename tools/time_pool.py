@@ -1,6 +1,6 @@
 """Time the fused stem BN+ReLU+max-pool kernel at the ResNet-18 batch-512 shape.
 
-    DMLAB_POOL_GENERIC=0|1 python tools/time_pool.py
+    python tools/time_pool.py
 """
 import sys
 from pathlib import Path
