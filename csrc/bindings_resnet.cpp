@@ -86,6 +86,10 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
     TORCH_CHECK(pre_shift.has_value(), "pre_scale needs pre_shift");
     need_f32(*pre_scale, "pre_scale", x.size(3));
     need_f32(*pre_shift, "pre_shift", x.size(3));
+    if (cfg == 80) {
+      dm::conv_res64(bp(x), bp(wpack), bp(y), ap, sp, g, cur_stream(), fp(*pre_scale), fp(*pre_shift));
+      return;
+    }
     if (cfg >= 90 && cfg <= 93 && dm::conv_pipe_supported(g, (int)cfg)) {
       dm::conv_pipe(bp(x), bp(wpack), bp(y), ap, sp, g, (int)cfg, cur_stream(), fp(*pre_scale),
                     fp(*pre_shift));
@@ -101,8 +105,10 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
   dm::igemm_fwd(bp(x), bp(wpack), bp(y), ap, sp, g, cfg, cur_stream());
 }
 
-// statistics rows a forward conv of this cfg writes (one per row tile); ncols is unused
+// statistics rows a forward conv of this cfg writes (one per row tile, or per workgroup of the
+// persistent cfg 80); ncols is unused
 int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
+  if (cfg == 80) return dm::res64_grid(M);
   const int bm = dm::igemm_fwd_rowtile(cfg);
   return (M + bm - 1) / bm;
 }

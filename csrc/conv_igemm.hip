@@ -745,6 +745,7 @@ bool halo_cfg(int cfg, int& bn, int& waves) {
 //   15 / 16 / 17 12 / 13 / 11 with two tiles of register prefetch
 //   20 / 21 / 42 / 39 / 41  halo-staged unit-stride tiles (conv_halo.hip, see halo_cfg)
 //   60           space-to-depth stem kernel (conv_stem.hip)
+//   80           persistent resident-weight 64 -> 64 channel 3x3 conv (conv_res64.hip)
 //   90 - 93      pipelined LDS-DMA tiles (conv_pipe.hip)
 // Shapes a specialised kernel does not cover fall back to a v3 tile with the same row tile,
 // so the statistics slab rows (igemm_fwd_rowtile) still match.
@@ -755,6 +756,7 @@ void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     if (g.Ncols % 128 == 0) return launch_fwd3<256, 128, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
     return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);
   }
+  if (cfg == 80) return conv_res64(X, Wp, Y, ADD, stats, g, st);  // throws if unsupported
   if (cfg == 60) {
     if (!ADD && stem_conv_supported(g)) return stem_conv(X, Wp, Y, stats, g, st);
     return launch_fwd3<256, 64, 4, 2, true, 1>(X, Wp, Y, ADD, stats, g, st);

@@ -94,6 +94,13 @@ bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
 void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
                const float* pre_sh = nullptr);
+// conv_res64.hip: persistent register-resident-weight 3x3 conv, 64 -> 64 channels (cfg 80);
+// statistics rows = res64_grid(M) (one per workgroup)
+bool conv_res64_supported(const ConvGeom& g);
+int res64_grid(long long M);
+void conv_res64(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+                const ConvGeom& g, hipStream_t st, const float* pre_sc = nullptr,
+                const float* pre_sh = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,

@@ -41,16 +41,26 @@ TILE_CFG = (15, 13, 11)
 _STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
 # DMLAB_NO_PIPE=1: the round-2 tile map without the pipelined tiles (A/B runs)
 _NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
+# DMLAB_NO_RES64=1: layer1 (64 -> 64 channel 3x3) convs on the round-2 halo tile (A/B runs)
+_NO_RES64 = os.environ.get("DMLAB_NO_RES64", "0") == "1"
+
+
 def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
     """Kernel config of a data-gradient GEMM (dX has M pixels of ``cin`` channels)."""
-    return pick_cfg(M, cin, k, stride, cout)
+    return pick_cfg(M, cin, k, stride, cout, W=W)
 
 
-def pick_cfg(M, ncols, k=0, stride=0, cin=0):
+def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
     """Kernel config for a forward-style conv GEMM with M output pixels and ncols
     output channels.  ``k``/``stride``/``cin`` (kernel size, tap stride, input
     channels) enable the unit-stride halo kernel when they describe a k x k conv with
-    unit tap stride over 64-channel-aligned input."""
+    unit tap stride over 64-channel-aligned input; ``W`` (image width, 0 = unknown)
+    enables the resident-weight 64-channel kernel."""
+    # 80: persistent resident-weight 64 -> 64 channel 3x3 conv (csrc/conv_res64.hip; its
+    # 128-pixel tile's halo, 128 + 2W + 2 rows, must fit the 256-row LDS image)
+    if (k == 3 and stride == 1 and cin == 64 and ncols == 64 and 0 < W <= 63
+            and not _NO_RES64):
+        return 80
     # 90: the pipelined LDS-DMA 256 x 256 tile (csrc/conv_pipe.hip), for >= 256 output
     # channels and 64-channel-aligned input, any tap geometry.  tools/bench_conv.py at batch
     # 1024 (profiles/conv_pipe_vs_halo_b1024_r3a.jsonl, TFLOP/s fwd/dgrad, best previous tile):
@@ -246,10 +256,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     # s2d stem: the resident-weight stem kernel (60, csrc/conv_stem.hip) stages the weights
     # and the input halo once per 256 pixels (the v3 128x64 tile, 16, re-stages one 4-tap
     # K-slice per step: 382 TFLOP/s at batch 512, profiles/conv_stem_s2d_r1s4.jsonl)
-    cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C)
+    cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C, W=OW if (OH, OW) == (H, W) else 0)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 39, 41, 42, 90, 91, 92, 93):
+        if cfg in (20, 21, 39, 41, 42, 80, 90, 91, 92, 93):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)

@@ -323,3 +323,15 @@ def test_ddp_make_buckets_invariants(numels, cap, first, last):
     last_alone = sizes[tail.params[-1]][2] - sizes[tail.params[-1]][0]
     if len(tail.params) > 1 and last_alone <= last:
         assert tail.hi - tail.lo <= last
+
+
+def test_res64_picked_for_layer1():
+    """cfg 80 (csrc/conv_res64.hip) only for 64 -> 64 channel 3x3/s1 convs of known width whose
+    128-pixel halo fits the kernel's 256-row LDS image."""
+    from dmlab.ops.convbn import pick_cfg, dgrad_cfg
+    assert pick_cfg(1024 * 56 * 56, 64, 3, 1, 64, W=56) == 80
+    assert dgrad_cfg(1024 * 56 * 56, 64, 3, 1, 64, 56, 56) == 80
+    assert pick_cfg(1024 * 56 * 56, 64, 3, 1, 64) != 80        # width unknown
+    assert pick_cfg(4 * 112 * 112, 64, 3, 1, 64, W=112) != 80  # halo too wide
+    assert pick_cfg(1024 * 28 * 28, 128, 3, 1, 128, W=28) != 80
+    assert dgrad_cfg(1024 * 56 * 56, 64, 3, 2, 128, 56, 56) != 80  # layer2 c1 data gradient

@@ -536,3 +536,51 @@ def test_conv_dgrad_pipe(dev, geom, accumulate, cfg):
     if accumulate:
         ref = ref + _nchw(base).float()
     assert _rel(_nchw(dx), ref) < 6e-3
+
+
+# persistent resident-weight 64 -> 64 channel 3x3 conv (conv_res64.hip, cfg 80): the layer1
+# shape, blocks crossing images (W = 7), a partial last tile (81 pixels), the widest supported
+# row (W = 63: halo 256 rows), more tiles than workgroups (N = 16 at 56 x 56)
+RES64_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 8, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
+               (1, 9, 64, 64, 3, 1, 1), (2, 63, 64, 64, 3, 1, 1), (16, 56, 64, 64, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geom", RES64_GEOMS)
+def test_conv_fwd_res64(dev, geom):
+    _check_fwd(dev, geom, 80)
+
+
+@pytest.mark.parametrize("geom", RES64_GEOMS[:4])
+def test_conv_fwd_res64_add(dev, geom):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p, seed=5)
+    ref = F.conv2d(x.float(), w.bfloat16().float(), None, s, p)
+    add = torch.randn(N, H, H, Cout, device=dev).bfloat16()
+    y = torch.empty_like(add)
+    lib().conv_fwd(xn, wf, y, None, add, k, k, s, p, 80)
+    assert _rel(_nchw(y), ref + _nchw(add).float()) < 6e-3
+
+
+@pytest.mark.parametrize("geom", RES64_GEOMS)
+def test_conv_fwd_prebn_res64(dev, geom):
+    test_conv_fwd_prebn(dev, geom, 80)
+
+
+@pytest.mark.parametrize("geom", RES64_GEOMS)
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_conv_dgrad_res64(dev, geom, accumulate):
+    test_conv_dgrad_halo(dev, geom, accumulate, 80)
+
+
+def test_conv_res64_matches_halo_bitwise(dev):
+    """Same fp32 accumulation order per output (taps outer, 16-deep k inner) as the halo tile:
+    the persistent kernel's outputs equal cfg 39's bit for bit; the stats rows differ (one per
+    workgroup) but sum to the same totals."""
+    N, H, Cin, Cout, k, s, p = RES64_GEOMS[0]
+    x, w, xn, wf, _ = _setup(dev, N, H, Cin, Cout, k, s, p, seed=7)
+    outs = []
+    for cfg in (39, 80):
+        y = torch.empty(N, H, H, Cout, device=dev, dtype=torch.bfloat16)
+        lib().conv_fwd(xn, wf, y, None, None, k, k, s, p, cfg)
+        outs.append(y)
+    assert torch.equal(outs[0], outs[1])

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--cfgs", default="15,13,39,41,42,90,91")
     ap.add_argument("--wcfgs", default="v2,h9,h3")
     ap.add_argument("--passes", default="fwd,dgrad,wgrad")
+    ap.add_argument("--pre", action="store_true", help="also time the fused pre-BN forward")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default: ResNet-18)")
     ap.add_argument("--smul", default="1", help="comma list of multipliers of the planned "
                     "wgrad m-split S (halo variants h9/h3)")
@@ -87,11 +88,20 @@ def main():
                     continue
                 if cfg == 60 and name != "stem_s2d":
                     continue
+                if cfg == 80 and (C, Co, k, s) != (64, 64, 3, 1):
+                    continue
                 M = N * OH * OH
                 T = L.conv_stats_rows(M, cfg, Co)
                 st = torch.empty(T * 2 * Co, device=dev)
                 t = timeit(lambda: L.conv_fwd(x, wf, y, st, None, k, k, s, p, cfg), a.iters)
                 row[f"fwd_c{cfg}_TF"] = round(flops / t / 1e12, 1)
+                if a.pre and cfg in (20, 21, 39, 41, 42, 80, 90, 91, 92, 93):
+                    sc = torch.rand(C, device=dev) + 0.5
+                    sh = torch.randn(C, device=dev) * 0.1
+                    t = timeit(lambda: L.conv_fwd(x, wf, y, st, None, k, k, s, p, cfg,
+                                                  pre_scale=sc, pre_shift=sh), a.iters)
+                    row[f"fwdpre_c{cfg}_TF"] = round(flops / t / 1e12, 1)
+                    L.conv_fwd(x, wf, y, st, None, k, k, s, p, cfg)
                 if ref is None:
                     ref = y.clone()
                 else:
@@ -100,6 +110,8 @@ def main():
             ref = None
             for cfg in cfgs:
                 if cfg in (9, 12, 15, 20, 42) and C % 128:
+                    continue
+                if cfg in (60, 80) and (C, Co, k, s) != (64, 64, 3, 1):
                     continue
                 t = timeit(lambda: L.conv_dgrad(dy, wd, dx, k, k, s, p, None, cfg), a.iters)
                 row[f"dgrad_c{cfg}_TF"] = round(flops / t / 1e12, 1)
