@@ -47,6 +47,7 @@ constexpr int RDMA = 9;                 // LDS-DMA instructions per wave per til
 constexpr int RSLOTS = RDMA * RNT;      // 16-B slots of the halo image (9 per row)
 constexpr int RHMAX = RSLOTS / 9;       // halo rows the image holds (256: W <= 63)
 constexpr unsigned ROOB = 0x80000000u;
+constexpr unsigned R_PADOFF = 0x40000000u;  // DMA pad pieces: past every supported tensor
 constexpr int R_ZROW = RSLOTS * 16;     // zero row
 constexpr int R_TAB = R_ZROW + RPITCH;  // PRE scale / shift (2 x 64 floats)
 constexpr int R_EPI = R_TAB + 2 * RC * 4;
@@ -111,34 +112,32 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
   const auto rsa =
       __builtin_amdgcn_make_buffer_rsrc((void*)(ADD ? ADD : Y), (short)0, (int)ybytes, 0x00020000);
   const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)smem;
-  const int NHW = g.N * g.H * g.W;
-  const int hr = RT + 2 * g.W + 2;
 
-  // halo of tile tt -> LDS image (slot s = 16-B piece s % 9 of halo row s / 9)
-  auto dma = [&](int tt) __attribute__((always_inline)) {
-    const int hstart = tt * RT - g.W - 1;
-    const int ln = (int)opq((unsigned)lane);
+  // halo of tile tt -> LDS image: piece s (16 B) of the image is piece s % 9 of halo row s / 9.
+  // pb[j]: byte offset of this thread's piece j relative to the halo's first pixel (pad pieces
+  // pushed past any tensor), so a tile's source offset is ONE add: the buffer range check turns
+  // rows before the tensor (negative, wrapped) or past it into zeros
+  unsigned pb[RDMA];
 #pragma unroll
-    for (int j = 0; j < RDMA; ++j) {
-      const int s = (j * 4 + wid) * 64 + ln;
-      const int row = div9(s);
-      const int c = s - row * 9;
-      const int gp = hstart + row;
-      const bool ok = c < 8 && row < hr && (unsigned)gp < (unsigned)NHW;
-      pdma16(rsx, lds0 + (unsigned)(j * 4 + wid) * 1024u, ok ? (unsigned)gp * 128u + (unsigned)c * 16u : ROOB);
-    }
+  for (int j = 0; j < RDMA; ++j) {
+    const int s = (j * 4 + wid) * 64 + lane;
+    const int row = div9(s), c = s - row * 9;
+    pb[j] = c < 8 ? (unsigned)(row * 128 + c * 16) : R_PADOFF;
+  }
+  auto dma = [&](int tt) __attribute__((always_inline)) {
+    const unsigned hs = (unsigned)((tt * RT - g.W - 1) * 128);
+#pragma unroll
+    for (int j = 0; j < RDMA; ++j) pdma16(rsx, lds0 + (unsigned)(j * 4 + wid) * 1024u, hs + pb[j]);
   };
-  // PRE: BN + ReLU of the chunks this thread's DMA landed (pad slots stay zero; rows outside
+  // PRE: BN + ReLU of the chunks this thread's DMA landed (pad pieces stay zero; rows outside
   // the image are never read: their taps go to the zero row)
   auto transform = [&]() __attribute__((always_inline)) {
     if constexpr (PRE) {
-      const int ln = (int)opq((unsigned)lane);
 #pragma unroll
       for (int j = 0; j < RDMA; ++j) {
-        const int s = (j * 4 + wid) * 64 + ln;
-        const int c = s - div9(s) * 9;
-        if (c < 8) {
-          uint4* q = reinterpret_cast<uint4*>(smem + s * 16);
+        if (pb[j] < R_PADOFF) {
+          const int c = (int)((pb[j] >> 4) & 7u);
+          uint4* q = reinterpret_cast<uint4*>(smem + ((j * 4 + wid) * 64 + lane) * 16);
           const float4 s0 = *reinterpret_cast<const float4*>(tab + c * 8);
           const float4 s1 = *reinterpret_cast<const float4*>(tab + c * 8 + 4);
           const float4 h0 = *reinterpret_cast<const float4*>(tab + RC + c * 8);
@@ -310,7 +309,9 @@ bool conv_res64_supported(const ConvGeom& g) {
   auto in1 = [](int v) { return v >= -1 && v <= 1; };
   if (!in1(g.dy0) || !in1(g.dy0 + 2 * g.dys) || !in1(g.dx0) || !in1(g.dx0 + 2 * g.dxs)) return false;
   if (RT + 2 * g.W + 2 > RHMAX) return false;
-  if ((long long)g.N * g.H * g.W * RC * 2 >= (1LL << 31) || g.M != (long long)g.N * g.H * g.W)
+  // pad pieces sit at R_PADOFF + (halo start) bytes: the tensor must end below 2^30 - 2^14
+  if ((long long)g.N * g.H * g.W * RC * 2 >= (1LL << 30) - (1LL << 14) ||
+      g.M != (long long)g.N * g.H * g.W)
     return false;
   return true;
 }
@@ -318,9 +319,9 @@ bool conv_res64_supported(const ConvGeom& g) {
 void conv_res64(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                 const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh) {
   if (!conv_res64_supported(g)) throw std::runtime_error("conv_res64: unsupported geometry");
-  const int ntiles = (int)((g.M + RT - 1) / RT);
   const int grid = res64_grid(g.M);
   const unsigned bytes = (unsigned)(g.M * RC * 2);
+  const int ntiles = (int)((g.M + RT - 1) / RT);
   auto k = pre_sc ? conv_res64_kernel<true> : conv_res64_kernel<false>;
   set_smem_attr(k, R_SMEM);
   k<<<grid, RNT, R_SMEM, st>>>(X, Wp, Y, ADD, stats, g, bytes, bytes, pre_sc, pre_sh, ntiles);

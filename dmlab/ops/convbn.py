@@ -57,9 +57,10 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
     unit tap stride over 64-channel-aligned input; ``W`` (image width, 0 = unknown)
     enables the resident-weight 64-channel kernel."""
     # 80: persistent resident-weight 64 -> 64 channel 3x3 conv (csrc/conv_res64.hip; its
-    # 128-pixel tile's halo, 128 + 2W + 2 rows, must fit the 256-row LDS image)
+    # 128-pixel tile's halo, 128 + 2W + 2 rows, must fit the 256-row LDS image; the input
+    # below 1 GiB: its DMA pad pieces are addressed past 2^30)
     if (k == 3 and stride == 1 and cin == 64 and ncols == 64 and 0 < W <= 63
-            and not _NO_RES64):
+            and M * 128 < 2**30 - 2**14 and not _NO_RES64):
         return 80
     # 90: the pipelined LDS-DMA 256 x 256 tile (csrc/conv_pipe.hip), for >= 256 output
     # channels and 64-channel-aligned input, any tap geometry.  tools/bench_conv.py at batch
