@@ -212,9 +212,13 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
     need_f32(*pre_scale, "pre_scale", x.size(3));
     need_f32(*pre_shift, "pre_shift", x.size(3));
     const float *psc = fp(*pre_scale), *psh = fp(*pre_shift);
-    TORCH_CHECK((cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
-                "fused pre-BN needs the halo wgrad (cfg 4/5) and a 3x3/s1/p1 geometry");
-    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh);
+    if (cfg == 8) {
+      dm::wgrad_res64(bp(x), bp(dy), fp(slab), g, (int)S, st, psc, psh);
+    } else {
+      TORCH_CHECK((cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
+                  "fused pre-BN needs the halo wgrad (cfg 4/5/8) and a 3x3/s1/p1 geometry");
+      dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh);
+    }
   } else {
     dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
   }

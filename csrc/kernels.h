@@ -107,6 +107,10 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const ConvGeom& g, int bn, int waves, hipStream_t st,
                const float* pre_sc = nullptr, const float* pre_sh = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
+// wgrad_res64.hip: row-streaming 64 -> 64 channel 3x3 weight gradient (wgrad cfg 8); S slabs
+bool wgrad_res64_supported(const ConvGeom& g);
+void wgrad_res64(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                 hipStream_t st, const float* pre_sc = nullptr, const float* pre_sh = nullptr);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
                 const float* pre_sh = nullptr);

@@ -101,14 +101,34 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 _WGRAD_BLOCKS = int(os.environ.get("DMLAB_WGRAD_BLOCKS", "512"))
 
 
-def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None):
+# DMLAB_NO_WRES64=1: layer1 weight gradients on the halo wgrad (cfg 5) instead of cfg 8 (A/B)
+_NO_WRES64 = os.environ.get("DMLAB_NO_WRES64", "0") == "1"
+_CUS = {}
+
+
+def _cu_count():
+    if not torch.cuda.is_available():
+        return 256
+    d = torch.cuda.current_device()
+    if d not in _CUS:
+        _CUS[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return _CUS[d]
+
+
+def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
-    cfg 4/5: halo-staged 3x3 unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per
-    block; cfg 2/3/6: v2 igemm tiles 128x128 / 64x128 / 64x256.
+    cfg 8: row-streaming 64 -> 64 channel 3x3 kernel (csrc/wgrad_res64.hip; ``W`` = image
+    width <= 60, ``rows`` = N*H image rows, S = one slab per CU); cfg 4/5: halo-staged 3x3
+    unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per block; cfg 2/3/6: v2 igemm
+    tiles 128x128 / 64x128 / 64x256.
     S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
     ~2 blocks per CU, each split >= 8 row steps, slab bytes S*cout*K*4."""
     halo = k == 3 and stride == 1 and cin % 64 == 0 and cout % 8 == 0
+    res64 = (k == 3 and stride == 1 and cin == 64 and cout == 64 and 0 < W <= 60 and rows > 0
+             and not _NO_WRES64)
+    if force == 8 or (force is None and res64):
+        return 8, max(1, min(rows, _cu_count()))
     if force is not None:
         cfg = force
     elif halo:
@@ -367,7 +387,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
         mode = 2       # mask recomputed from y (no `out` read)
     C = x.shape[3]
     K = k * k * C
-    wcfg, S = _wgrad_plan(M, cout, K, k, s, C)
+    same = not s2d and (OH, OW) == tuple(x.shape[1:3])
+    wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0)
     dy = empty_nhwc(N, OH, OW, cout, y)
     dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
     L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
@@ -393,7 +414,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
             pre_kw = {}
             xw = x
             if pre is not None:
-                if wcfg in (4, 5):
+                if wcfg in (4, 5, 8):
                     pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
                 else:
                     xw = _materialise(x, pre)

@@ -335,3 +335,15 @@ def test_res64_picked_for_layer1():
     assert pick_cfg(4 * 112 * 112, 64, 3, 1, 64, W=112) != 80  # halo too wide
     assert pick_cfg(1024 * 28 * 28, 128, 3, 1, 128, W=28) != 80
     assert dgrad_cfg(1024 * 56 * 56, 64, 3, 2, 128, 56, 56) != 80  # layer2 c1 data gradient
+
+
+def test_wgrad_res64_plan():
+    """wgrad cfg 8 (csrc/wgrad_res64.hip) for 64 -> 64 channel 3x3/s1 layers of width <= 60,
+    one slab per CU (at most one per image row)."""
+    from dmlab.ops.convbn import _wgrad_plan
+    cfg, S = _wgrad_plan(1024 * 56 * 56, 64, 576, 3, 1, 64, W=56, rows=1024 * 56)
+    assert cfg == 8 and 1 <= S <= 1024 * 56
+    assert _wgrad_plan(2 * 5 * 5, 64, 576, 3, 1, 64, W=5, rows=10)[1] <= 10
+    assert _wgrad_plan(1024 * 56 * 56, 64, 576, 3, 1, 64)[0] != 8           # width unknown
+    assert _wgrad_plan(4 * 112 * 112, 64, 576, 3, 1, 64, W=112, rows=448)[0] != 8
+    assert _wgrad_plan(1024 * 28 * 28, 128, 1152, 3, 1, 128, W=28, rows=1024 * 28)[0] != 8

@@ -584,3 +584,45 @@ def test_conv_res64_matches_halo_bitwise(dev):
         lib().conv_fwd(xn, wf, y, None, None, k, k, s, p, cfg)
         outs.append(y)
     assert torch.equal(outs[0], outs[1])
+
+
+# row-streaming 64 -> 64 channel weight gradient (wgrad_res64.hip, wgrad cfg 8): one slab per
+# workgroup, row ranges starting mid-image, several images per workgroup, W = 60 (widest)
+WRES64_GEOMS = [(3, 56, 64, 64, 3, 1, 1), (2, 8, 64, 64, 3, 1, 1), (5, 7, 64, 64, 3, 1, 1),
+                (1, 9, 64, 64, 3, 1, 1), (2, 60, 64, 64, 3, 1, 1)]
+
+
+@pytest.mark.parametrize("geom", WRES64_GEOMS)
+@pytest.mark.parametrize("S", [1, 5, "rows"])
+@pytest.mark.parametrize("pre", [False, True])
+def test_conv_wgrad_res64(dev, geom, S, pre):
+    N, H, Cin, Cout, k, s, p = geom
+    S = N * H if S == "rows" else min(S, N * H)
+    g = torch.Generator(device=dev).manual_seed(11)
+    y = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    dy = torch.randn(N, Cout, H, H, device=dev, generator=g).bfloat16()
+    kw = {}
+    a = y.float()
+    if pre:
+        sc = torch.rand(Cin, device=dev, generator=g) + 0.5
+        sh = torch.randn(Cin, device=dev, generator=g) * 0.5
+        a = (y.float() * sc + sh).relu().bfloat16().float()
+        kw = dict(pre_scale=sc, pre_shift=sh)
+    ref = torch.nn.grad.conv2d_weight(_nchw(a), (Cout, Cin, k, k), dy.float(), s, p)
+    slab = torch.full((S * Cout * k * k * Cin,), float("nan"), device=dev)
+    d = torch.empty(Cout, Cin, k, k, device=dev)
+    lib().conv_wgrad(y, _nhwc(dy), d, slab, Cin, k, k, s, p, 0.0, S, 8, False, **kw)
+    assert _rel(d, ref) < 2e-3
+
+
+def test_conv_wgrad_res64_accumulates(dev):
+    """beta = 1 adds onto the existing gradient (the step's accumulate path)."""
+    N, H, Cin, Cout, k, s, p = WRES64_GEOMS[1]
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p, seed=4)
+    dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, p)
+    base = torch.randn_like(w)
+    d = base.clone()
+    slab = torch.empty(4 * Cout * k * k * Cin, device=dev)
+    lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, 1.0, 4, 8, False)
+    assert _rel(d, ref + base) < 2e-3

@@ -129,9 +129,13 @@ def main():
             variants = [(v, m) for v in a.wcfgs.split(",") for m in
                         ([float(x) for x in a.smul.split(",")] if v in ("h9", "h3", "w6") else [1.0])]
             for v, mul in variants:
-                force = {"v2": None, "h9": 4, "h3": 5, "w6": 6}[v]
+                force = {"v2": None, "h9": 4, "h3": 5, "w6": 6, "q8": 8}[v]
                 if force is None:
                     c, S = _wgrad_plan(M, Co, K)
+                elif force == 8:
+                    if (C, Co, k, s) != (64, 64, 3, 1):
+                        continue
+                    c, S = _wgrad_plan(M, Co, K, k, s, C, force=8, W=OH, rows=N * OH)
                 else:
                     c, S = _wgrad_plan(M, Co, K, k, s, C, force=force)
                     S = max(1, int(S * mul))
