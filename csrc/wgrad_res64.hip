@@ -20,9 +20,11 @@
 //    channels 16 (w & 3) .. +15 x output channels 32 (w >> 2) .. +31 x 9 taps); per row and
 //    32-pixel k-step it reads 2 dY^T fragments and 9 shifted input fragments
 //    (ds_read_b64_tr_b16, 160-B slot pitch: conflict-free) for 18 v_mfma_f32_16x16x32_bf16;
-//  * rows stream in by LDS-DMA three rows ahead (3 instructions per wave per row; 60 lanes
-//    = 6 slots x 10 pieces, the last two pieces of a slot and pixels x >= W read zero through
-//    the buffer range check), one barrier per row; the fused pre-BN transform (PRE: the input
+//  * rows stream in by LDS-DMA, two rows per iteration and two iterations ahead (5
+//    instructions per wave per iteration; 60 lanes = 6 slots x 10 pieces, the last two pieces
+//    of a slot and pixels x >= W read zero through the buffer range check), one barrier per
+//    two rows, the fragments of k-step s+1 read while step s issues its MFMAs; the fused
+//    pre-BN transform (PRE: the input
 //    is the previous conv's raw output, the operand relu(x*sc + sh)) rewrites each thread's
 //    landed input pieces before the barrier that publishes them;
 //  * each workgroup writes one fp32 slab [64][576], reduced in fixed order by wgrad_reduce.
@@ -40,16 +42,15 @@ constexpr int QC = 64;                    // channels (in and out)
 constexpr int QP = 160;                   // LDS bytes per pixel slot (80 bf16: tr-read pitch)
 constexpr int QXS = 66;                   // input slots per row (x = -1 .. 64)
 constexpr int QDS = 64;                   // dY slots per row
-constexpr int QRX = 6;                    // input-row ring
-constexpr int QRD = 4;                    // dY-row ring
-constexpr int QPD = 3;                    // rows of DMA prefetch
+constexpr int QRX = 8;                    // input-row ring
+constexpr int QRD = 6;                    // dY-row ring
 constexpr int Q_XROW = QXS * QP;          // 10,560 B
 constexpr int Q_DROW = QDS * QP;          // 10,240 B
 constexpr int Q_X = 0;                    // QRX input rows
 constexpr int Q_Z = Q_X + QRX * Q_XROW;   // the all-zero input row
 constexpr int Q_D = Q_Z + Q_XROW;         // QRD dY rows
-constexpr int Q_SCR = Q_D + QRD * Q_DROW; // 1 KB: target of the padding DMA instructions
-constexpr int Q_TAB = Q_SCR + 1024;       // PRE scale / shift
+constexpr int Q_SCR = Q_D + QRD * Q_DROW; // end of the zero-initialised region
+constexpr int Q_TAB = Q_SCR;              // PRE scale / shift
 constexpr int Q_SMEM = Q_TAB + 2 * QC * 4;
 constexpr unsigned QOOB = 0x80000000u;
 
@@ -101,59 +102,70 @@ __global__ void __launch_bounds__(512, 2) wgrad_res64_kernel(
     const unsigned off = ok ? (unsigned)((row * W + x) * 128 + dpiece * 16) : QOOB;
     if (dlane) pdma16(rs, lds_row + (unsigned)(jj * 6 * QP), off);
   };
-  const int NR = g.N * H;  // input rows of the tensor
+  const int NR = g.N * H;  // image rows of the tensor
   auto xslot = [&](int row) { return (unsigned)(Q_X + ((row % QRX + QRX) % QRX) * Q_XROW); };
   auto dslotb = [&](int row) { return (unsigned)(Q_D + (row % QRD) * Q_DROW); };
-  // one row batch: input row rx (into its ring slot, from slot x = 0 = byte QP) and dY row rd;
-  // wave w issues instructions w, w + 8, w + 16 of 24 (10 input, 10 dY, 4 padding)
-  auto batch = [&](int rx, int rd) __attribute__((always_inline)) {
+  // the batch of iteration k (output rows r0 + 2k, +1): input rows r0 + 2k + 1, +2 and dY rows
+  // r0 + 2k, +1 = 40 instructions, wave w issues w, w + 8, ..., w + 32 (input row pieces
+  // j < 20 into slot x = 0 = byte QP of their ring slot, then dY rows)
+  auto batch = [&](int k) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int j = wid + 8 * k;
-      if (j < 10) {
-        dma_row(rsx, rx, j, lds0 + xslot(rx) + QP, NR);
-      } else if (j < 20) {
-        dma_row(rsd, rd, j - 10, lds0 + dslotb(rd), NR);
-      } else if (dlane) {
-        pdma16(rsd, lds0 + Q_SCR, QOOB);
+    for (int u = 0; u < 5; ++u) {
+      const int j = wid + 8 * u;
+      if (j < 20) {
+        const int rx = r0 + 2 * k + 1 + j / 10;
+        dma_row(rsx, rx, j % 10, lds0 + xslot(rx) + QP, NR);
+      } else {
+        const int rd = r0 + 2 * k + (j - 20) / 10;
+        dma_row(rsd, rd, (j - 20) % 10, lds0 + dslotb(rd), NR);
       }
     }
   };
-  // input-row-only batch (prologue): instructions w, w + 8 of 10
+  // input-row-only loads (prologue): instructions w, w + 8 of 10
   auto xonly = [&](int rx) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int j = wid + 8 * k;
+    for (int u = 0; u < 2; ++u) {
+      const int j = wid + 8 * u;
       if (j < 10) dma_row(rsx, rx, j, lds0 + xslot(rx) + QP, NR);
     }
   };
-  // PRE: BN + ReLU of this thread's landed pieces of input row rx (instructions w, w + 8)
-  auto transform = [&](int rx) __attribute__((always_inline)) {
+  // PRE: BN + ReLU of this thread's landed pieces of input row rx (piece instruction j)
+  auto tpiece = [&](int rx, int j) __attribute__((always_inline)) {
     if constexpr (PRE) {
+      const int x = 6 * j + dslot;
+      if (dlane && dpiece < 8 && x < W) {
+        uint4* p = reinterpret_cast<uint4*>(smem + xslot(rx) + QP + j * 6 * QP + lane * 16);
+        const float4 s0 = *reinterpret_cast<const float4*>(tab + dpiece * 8);
+        const float4 s1 = *reinterpret_cast<const float4*>(tab + dpiece * 8 + 4);
+        const float4 h0 = *reinterpret_cast<const float4*>(tab + QC + dpiece * 8);
+        const float4 h1 = *reinterpret_cast<const float4*>(tab + QC + dpiece * 8 + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+        const uint4 v = *p;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t o[4];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int j = wid + 8 * k;
-        const int x = 6 * j + dslot;
-        if (j < 10 && dlane && dpiece < 8 && x < W) {
-          uint4* p = reinterpret_cast<uint4*>(smem + xslot(rx) + QP + j * 6 * QP + lane * 16);
-          const float4 s0 = *reinterpret_cast<const float4*>(tab + dpiece * 8);
-          const float4 s1 = *reinterpret_cast<const float4*>(tab + dpiece * 8 + 4);
-          const float4 h0 = *reinterpret_cast<const float4*>(tab + QC + dpiece * 8);
-          const float4 h1 = *reinterpret_cast<const float4*>(tab + QC + dpiece * 8 + 4);
-          const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-          const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-          const uint4 v = *p;
-          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-          uint32_t o[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float lo = fmaxf(__uint_as_float(w[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
-            const float hi = fmaxf(__uint_as_float(w[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
-            o[q] = pack_bf2(lo, hi);
-          }
-          *p = make_uint4(o[0], o[1], o[2], o[3]);
+        for (int q = 0; q < 4; ++q) {
+          const float lo = fmaxf(__uint_as_float(w[q] << 16) * sc[2 * q] + sh[2 * q], 0.f);
+          const float hi = fmaxf(__uint_as_float(w[q] & 0xffff0000u) * sc[2 * q + 1] + sh[2 * q + 1], 0.f);
+          o[q] = pack_bf2(lo, hi);
         }
+        *p = make_uint4(o[0], o[1], o[2], o[3]);
       }
+    }
+  };
+  auto xform_batch = [&](int k) __attribute__((always_inline)) {  // input rows of batch k
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int j = wid + 8 * u;
+      if (j < 20) tpiece(r0 + 2 * k + 1 + j / 10, j % 10);
+    }
+  };
+  auto xform_row = [&](int rx) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int j = wid + 8 * u;
+      if (j < 10) tpiece(rx, j);
     }
   };
 
@@ -170,53 +182,81 @@ __global__ void __launch_bounds__(512, 2) wgrad_res64_kernel(
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  if (r0 < r1) {
+  const int niter = (r1 - r0 + 1) / 2;
+  if (niter > 0) {
     __syncthreads();  // zeroed LDS before any DMA lands
     xonly(r0 - 1);
     xonly(r0);
-    batch(r0 + 1, r0);  // the batch of iteration r0 - QPD
+    batch(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    transform(r0 - 1);
-    transform(r0);
+    xform_row(r0 - 1);
+    xform_row(r0);
     __syncthreads();
-#pragma unroll
-    for (int k = 1; k < QPD; ++k) batch(r0 + 1 + k, r0 + k);
+    batch(1);
   }
-  for (int r = r0; r < r1; ++r) {
-    // this wave's DMAs of input row r+1 / dY row r landed (the QPD-1 later batches may not)
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    transform(r + 1);
+  for (int it = 0; it < niter; ++it) {
+    // this wave's batch it landed (batch it+1, 5 instructions, may not have)
+    asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    xform_batch(it);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // the ring slots of input row r-2 and dY row r-1 are free: prefetch QPD rows ahead
-    batch(r + 1 + QPD, r + QPD);
+    // the ring slots of iteration it-1's rows are free: prefetch two iterations ahead
+    batch(it + 2);
 
-    const int y = r % H;
-    unsigned xb[3];
-    xb[0] = y > 0 ? xslot(r - 1) : (unsigned)Q_Z;
-    xb[1] = xslot(r);
-    xb[2] = y + 1 < H ? xslot(r + 1) : (unsigned)Q_Z;
-    const unsigned ab = lds0 + dslotb(r) + a_lane;
+    const int R = r0 + 2 * it;
+    const bool two = R + 1 < r1;  // the second row belongs to this workgroup
+    // input row bases per (output row ro, kernel row dyi): zero row outside the image
+    unsigned xb[2][3], ab[2];
 #pragma unroll
-    for (int t3 = 0; t3 < 3; ++t3) xb[t3] = lds0 + xb[t3] + b_lane;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      bf16x8 af[2];
+    for (int ro = 0; ro < 2; ++ro) {
+      const int y = (R + ro) % H;
+      xb[ro][0] = lds0 + (y > 0 ? xslot(R + ro - 1) : (unsigned)Q_Z) + b_lane;
+      xb[ro][1] = lds0 + xslot(R + ro) + b_lane;
+      xb[ro][2] = lds0 + (y + 1 < H ? xslot(R + ro + 1) : (unsigned)Q_Z) + b_lane;
+      ab[ro] = lds0 + dslotb(R + ro) + a_lane;
+    }
+    // four 32-pixel k-steps (row ro = ks >> 1, half kb = ks & 1), fragments of step ks+1 read
+    // while step ks issues its 18 MFMAs
+    bf16x8 fa[2][2], fb[2][9];
+    auto rdk = [&](int set, int ks) __attribute__((always_inline)) {
+      const int ro = ks >> 1, kb = ks & 1;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const s4 lo = qtr(ab + (kb * 32) * QP + i * 32);
-        const s4 hi = qtr(ab + (kb * 32 + 16) * QP + i * 32);
-        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const s4 lo = qtr(ab[ro] + (kb * 32) * QP + i * 32);
+        const s4 hi = qtr(ab[ro] + (kb * 32 + 16) * QP + i * 32);
+        fa[set][i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int dyi = t / 3, dxo = t % 3;  // input slot = x + dxo, row y + dyi - 1
-        const s4 lo = qtr(xb[dyi] + (kb * 32 + dxo) * QP);
-        const s4 hi = qtr(xb[dyi] + (kb * 32 + 16 + dxo) * QP);
-        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        const s4 lo = qtr(xb[ro][dyi] + (kb * 32 + dxo) * QP);
+        const s4 hi = qtr(xb[ro][dyi] + (kb * 32 + 16 + dxo) * QP);
+        fb[set][t] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    };
+    auto mm = [&](int set) __attribute__((always_inline)) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][t], 0, 0, 0);
-      }
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[set][i], fb[set][t], acc[i][t], 0, 0, 0);
+    };
+    rdk(0, 0);
+    rdk(1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (two) {
+      rdk(0, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(1);
+      __builtin_amdgcn_sched_barrier(0);
+      rdk(1, 3);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(1);
+    } else {
+      mm(1);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetches past the range

@@ -8,6 +8,5 @@ timeout -k 10 300 python -u -m pytest tests/test_native_resnet_kernels.py -m gpu
 timeout -k 10 200 python tools/bench_conv.py --batch 1024 --shapes l1_3x3 --passes wgrad --wcfgs h3,q8 \
     > gpurun_out/bench_conv_$tag.jsonl 2> gpurun_out/bench_conv_$tag.err || exit 1
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err || exit 1
-DMLAB_NO_WRES64=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_nowr_$tag.json 2> gpurun_out/bench_nowr_$tag.err || exit 1
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_$tag.json 2>> gpurun_out/bench_$tag.err || exit 1
-tail -3 gpurun_out/pytest_$tag.log; cat gpurun_out/bench_conv_$tag.jsonl; cut -c1-200 gpurun_out/bench_$tag.json gpurun_out/bench_nowr_$tag.json
+tail -3 gpurun_out/pytest_$tag.log; cat gpurun_out/bench_conv_$tag.jsonl; cut -c1-200 gpurun_out/bench_$tag.json
