@@ -127,9 +127,9 @@ def main():
             dw = torch.empty(Co, C, k, k, device=dev)
             ref = None
             variants = [(v, m) for v in a.wcfgs.split(",") for m in
-                        ([float(x) for x in a.smul.split(",")] if v in ("h9", "h3", "w6") else [1.0])]
+                        ([float(x) for x in a.smul.split(",")] if v in ("h9", "h3", "w6", "g2", "g3") else [1.0])]
             for v, mul in variants:
-                force = {"v2": None, "h9": 4, "h3": 5, "w6": 6, "q8": 8}[v]
+                force = {"v2": None, "h9": 4, "h3": 5, "w6": 6, "q8": 8, "g2": 2, "g3": 3}[v]
                 if force is None:
                     c, S = _wgrad_plan(M, Co, K)
                 elif force == 8:
