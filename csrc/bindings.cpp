@@ -272,6 +272,17 @@ void colsum(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor out, doubl
              (float)beta, cur_stream());
 }
 
+void bias_act(at::Tensor y, c10::optional<at::Tensor> bias, at::Tensor out, bool relu) {
+  CHECK_F32(y);
+  TORCH_CHECK(y.is_cuda() && y.dim() == 2 && y.is_contiguous());
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.sizes() == y.sizes() &&
+              (out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16));
+  if (bias.has_value()) { CHECK_F32(*bias); TORCH_CHECK(bias->numel() == y.size(1)); }
+  const DeviceGuard guard(y.device());
+  dm::bias_act(y.data_ptr<float>(), bias.has_value() ? bias->data_ptr<float>() : nullptr,
+               out.data_ptr(), is_bf16(out), y.size(0), y.size(1), relu ? 1 : 0, cur_stream());
+}
+
 // ------------------------------------------------------------------ loss / eval / spin
 void cross_entropy(at::Tensor logits, at::Tensor labels, at::Tensor rowloss, at::Tensor loss,
                    c10::optional<at::Tensor> dlogits, double scale) {
@@ -381,6 +392,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sbk"), py::arg("sbn"), py::arg("scm"), py::arg("alpha"), py::arg("beta"),
         py::arg("relu"), py::arg("lowp") = false);
   m.def("colsum", &colsum);
+  m.def("bias_act", &bias_act, py::arg("y"), py::arg("bias"), py::arg("out"), py::arg("relu"));
   m.def("xgmi_alloc", &xgmi_alloc);
   m.def("xgmi_free", &xgmi_free);
   m.def("xgmi_get_handle", &xgmi_get_handle);

@@ -367,4 +367,25 @@ void colsum(const void* A, const void* Amask, int bf16, float* out, int M, int N
                                                beta);
 }
 
+// out = act(y + bias) (fp32 -> fp32 or bf16): the tensor-parallel row-split head's epilogue,
+// after the all-reduce of the partial products (parallel/tensor_parallel.py RowParallelLinear)
+__global__ void __launch_bounds__(256) bias_act_kernel(const float* __restrict__ y,
+                                                       const float* __restrict__ bias, void* out,
+                                                       long long n, int N, int relu, int obf) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float v = y[i] + (bias ? bias[i % N] : 0.f);
+    if (relu) v = fmaxf(v, 0.f);
+    if (obf) reinterpret_cast<bf16_t*>(out)[i] = f2bf(v);
+    else reinterpret_cast<float*>(out)[i] = v;
+  }
+}
+
+void bias_act(const float* y, const float* bias, void* out, int out_bf16, int M, int N, int relu,
+              hipStream_t st) {
+  const long long n = (long long)M * N;
+  if (n == 0) return;
+  bias_act_kernel<<<grid_for(n, 256), 256, 0, st>>>(y, bias, out, n, N, relu, out_bf16);
+  DM_CHECK(hipGetLastError());
+}
+
 }  // namespace dm

@@ -36,6 +36,8 @@ void gemm_strided(const void* A, const void* Amask, int a_bf16, const void* B, i
                   long long sam, long long sak, long long sbk, long long sbn, long long scm,
                   float alpha, float beta, int relu, int lowp, float* part, int S,
                   hipStream_t st);
+void bias_act(const float* y, const float* bias, void* out, int out_bf16, int M, int N, int relu,
+              hipStream_t st);
 void colsum(const void* A, const void* Amask, int bf16, float* out, int M, int N, float beta,
             hipStream_t st);
 // loss.hip

@@ -20,6 +20,7 @@ import torch.nn as nn
 
 from dmlab.nn.layers import Conv2d, Flatten, Linear
 from dmlab.nn.program import Program
+from dmlab.ops._native import lib
 
 from . import env
 
@@ -83,6 +84,8 @@ class RowParallelLinear(Linear):
                 self.rbias.copy_(b)
 
     def fwd(self, x, ctx, train):
+        if self._prog._use_native(x):
+            return self._native_fwd(x, ctx, train)
         y = super().fwd(x, ctx, train)
         y = _all_reduce(y.float().contiguous(), self.group)
         if self.rbias is not None:
@@ -94,12 +97,53 @@ class RowParallelLinear(Linear):
         return y.to(x.dtype) if x.dtype != torch.float32 else y
 
     def bwd(self, dy, ctx, need_dx):
+        if self._prog._use_native(dy):
+            return self._native_bwd(dy, ctx, need_dx)
         if self.post_relu:
             dy = dy * (ctx["tp_y"] > 0)
         if self.rbias is not None:
             self._prog._write_grad_by_param(self.rbias, dy.float().sum(0))
         dy = dy.to(ctx["y"].dtype if "y" in ctx else dy.dtype)
         return super().bwd(dy, ctx, need_dx)
+
+    # native path (csrc/gemm.hip): the local partial product straight into an fp32 buffer
+    # (bf16 MFMA for bf16 activations), the all-reduce, then ONE kernel for bias + ReLU +
+    # the cast back; the backward takes the ReLU mask from the saved output inside the GEMM
+    # operand loads and the bias gradient from the masked column sum (no ATen elementwise)
+    def _native_fwd(self, x, ctx, train):
+        L = lib()
+        B = x.shape[0]
+        x2 = x.reshape(B, -1).contiguous()
+        assert x2.shape[1] == self.fin, (x2.shape, self.fin)
+        y32 = torch.empty((B, self.fout), device=x.device, dtype=torch.float32)
+        L.gemm(x2, None, self.weight.detach(), None, y32, None, B, self.fout, self.fin, self.fin,
+               1, 1, self.fin, self.fout, 1.0, 0.0, False, lowp=x2.dtype == torch.bfloat16)
+        y32 = _all_reduce(y32, self.group)
+        out = torch.empty((B, self.fout), device=x.device, dtype=x.dtype)
+        L.bias_act(y32, self.rbias.detach() if self.rbias is not None else None, out,
+                   self.post_relu)
+        if train:
+            ctx["x"], ctx["tp_y"], ctx["xshape"] = x2, out, x.shape
+        return out
+
+    def _native_bwd(self, dy, ctx, need_dx):
+        L = lib()
+        x, yo = ctx["x"], ctx["tp_y"]
+        dy = dy.to(yo.dtype).contiguous()
+        B, fin, fout = x.shape[0], self.fin, self.fout
+        mask = yo if self.post_relu else None
+        beta = 1.0 if self.accumulate else 0.0
+        lowp = x.dtype == torch.bfloat16
+        L.gemm(dy, mask, x, None, self.grad_slot("weight"), None, fout, fin, B, 1, fout, fin, 1,
+               fin, 1.0, beta, False, lowp=lowp)
+        if self.rbias is not None:
+            L.colsum(dy, mask, self.grad_slot("rbias"), beta)
+        if not need_dx:
+            return None
+        dx = torch.empty((B, fin), device=x.device, dtype=x.dtype)
+        L.gemm(dy, mask, self.weight.detach(), dx, None, None, B, fin, fout, fout, 1, fin, 1, fin,
+               1.0, 0.0, False, lowp=lowp)
+        return dx.reshape(ctx["xshape"])
 
     def t_bwd(self, dy, ctx, need_dx):  # reference path: local linear without the bias
         return Linear.t_bwd(self, dy, ctx, need_dx)
