@@ -62,6 +62,8 @@ __device__ inline void xg_signal(const XgmiPtrs& p, int phase, int b, int rank, 
   }
 }
 
+constexpr unsigned long long XG_TIMEOUT_TICKS = 400000000ull;  // 4 s at 100 MHz
+
 // wait until every rank's slot (phase, b, q) carries >= epoch; bounded spin -> false when a
 // peer never arrives (the caller reports through *err and exits instead of hanging the GPU)
 __device__ inline bool xg_wait(const XgmiPtrs& p, int phase, int b, int rank, int W,
@@ -71,10 +73,13 @@ __device__ inline bool xg_wait(const XgmiPtrs& p, int phase, int b, int rank, in
   __syncthreads();
   if (threadIdx.x < W) {
     const unsigned* f = p.flags[rank] + (phase * XG_FLAG_BLOCKS + b) * XG_MAX_RANKS + threadIdx.x;
-    long long spins = 0;
+    // bounded by wall time (s_memrealtime: 100 MHz), not by a spin count: a peer may lag by
+    // host work (logging, a checkpoint) or, with several ranks on one GPU, by the hardware
+    // scheduler time-slicing their queues; 4 s still frees the GPU when one never comes
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - epoch) < 0) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1LL << 22)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > XG_TIMEOUT_TICKS) {
         timed_out = 1;
         break;
       }

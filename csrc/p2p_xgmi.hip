@@ -26,11 +26,15 @@ namespace dm {
 namespace {
 constexpr int P2P_BLOCKS = 32;
 
+// bounded by wall time (s_memrealtime, 100 MHz): the peer stage may be busy with its own
+// compute for a while; 8 s still frees the GPU when it never sends
+constexpr unsigned long long P2P_TIMEOUT_TICKS = 800000000ull;
+
 __device__ inline bool p2p_wait_ge(const unsigned* f, unsigned v, unsigned* state) {
-  long long spins = 0;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - v) < 0) {
     __builtin_amdgcn_s_sleep(2);
-    if (++spins > (1LL << 24)) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > P2P_TIMEOUT_TICKS) {
       atomicExch(state + 2, 1u);
       return false;
     }
