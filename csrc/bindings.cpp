@@ -214,7 +214,7 @@ int64_t xgmi_open_handle(py::bytes handle) {
 void xgmi_close_handle(int64_t ptr) { dm::xgmi_close_handle((void*)(uintptr_t)ptr); }
 void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int64_t> data,
                     std::vector<int64_t> flags, int64_t rank, double scale, at::Tensor state,
-                    int64_t algo) {
+                    int64_t algo, int64_t share) {
   CHECK_F32(in);
   CHECK_F32(out);
   TORCH_CHECK(in.is_contiguous() && out.is_contiguous() && in.numel() == out.numel());
@@ -232,7 +232,8 @@ void xgmi_allreduce(at::Tensor in, at::Tensor out, int64_t cap, std::vector<int6
   const DeviceGuard guard(in.device());
   dm::xgmi_allreduce(in.data_ptr<float>(), out.data_ptr<float>(), in.numel(), cap, d.data(),
                      f.data(), (int)rank, W, (float)scale,
-                     reinterpret_cast<unsigned*>(state.data_ptr<int>()), (int)algo, cur_stream());
+                     reinterpret_cast<unsigned*>(state.data_ptr<int>()), (int)algo, cur_stream(),
+                     (int)share);
 }
 
 // P2P channel (csrc/p2p_xgmi.hip): src/dst tensors contiguous, 16-B aligned, bytes % 16 == 0;
@@ -398,7 +399,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xgmi_get_handle", &xgmi_get_handle);
   m.def("xgmi_open_handle", &xgmi_open_handle);
   m.def("xgmi_close_handle", &xgmi_close_handle);
-  m.def("xgmi_allreduce", &xgmi_allreduce);
+  m.def("xgmi_allreduce", &xgmi_allreduce, py::arg("in"), py::arg("out"), py::arg("cap"),
+        py::arg("data"), py::arg("flags"), py::arg("rank"), py::arg("scale"), py::arg("state"),
+        py::arg("algo"), py::arg("share") = 1);
   m.def("p2p_xgmi_send", &p2p_xgmi_send);
   m.def("p2p_xgmi_recv", &p2p_xgmi_recv);
   m.def("cross_entropy", &cross_entropy);

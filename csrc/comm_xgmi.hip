@@ -240,16 +240,22 @@ void* xgmi_open_handle(const void* handle64) {
 
 void xgmi_close_handle(void* ptr) { DM_CHECK(hipIpcCloseMemHandle(ptr)); }
 
+// share: ranks whose kernels run on this same GPU (1 on a node with one rank per GPU).  Every
+// block of the spinning kernels must be resident together with its namesakes on the peers;
+// W ranks sharing one device divide its CUs, so the grids shrink by that factor
 void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
                     void* const* flags, int rank, int W, float scale, unsigned* state, int algo,
-                    hipStream_t st) {
+                    hipStream_t st, int share) {
+  if (share < 1) share = 1;
+  const int g1 = XG_BLOCKS / share > 8 ? XG_BLOCKS / share : 8;
+  const int g2 = XG2_BLOCKS / share > 16 ? XG2_BLOCKS / share : 16;
   XgmiPtrs p{};
   for (int q = 0; q < W; ++q) {
     p.data[q] = (float*)data[q];
     p.flags[q] = (unsigned*)flags[q];
   }
   if (algo == 0) {
-    xgmi_allreduce_kernel<<<XG_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, scale,
+    xgmi_allreduce_kernel<<<g1, 256, 0, st>>>(in, out, n, cap, p, rank, W, scale,
                                                      state);
     return;
   }
@@ -258,10 +264,10 @@ void xgmi_allreduce(const float* in, float* out, long long n, long long cap, voi
   const bool v4 = n % 4 == 0 && cap % 4 == 0 && ((uintptr_t)in % 16) == 0 &&
                   ((uintptr_t)out % 16) == 0;
   if (v4)
-    xgmi_allreduce2_kernel<4><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n / 4, cap / 4, p, rank, W,
+    xgmi_allreduce2_kernel<4><<<g2, 256, 0, st>>>(in, out, n / 4, cap / 4, p, rank, W,
                                                           scale, state);
   else
-    xgmi_allreduce2_kernel<1><<<XG2_BLOCKS, 256, 0, st>>>(in, out, n, cap, p, rank, W, scale,
+    xgmi_allreduce2_kernel<1><<<g2, 256, 0, st>>>(in, out, n, cap, p, rank, W, scale,
                                                           state);
 }
 

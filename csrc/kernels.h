@@ -66,7 +66,7 @@ void* xgmi_open_handle(const void* handle64);
 void xgmi_close_handle(void* ptr);
 void xgmi_allreduce(const float* in, float* out, long long n, long long cap, void* const* data,
                     void* const* flags, int rank, int W, float scale, unsigned* state, int algo,
-                    hipStream_t st);
+                    hipStream_t st, int share = 1);
 // p2p_xgmi.hip: one-direction stage-to-stage channel over IPC peer memory
 void p2p_xgmi_send(const void* src, long long bytes, void* ring, void* full, const void* free_,
                    long long slot_bytes, int nslot, unsigned* state, hipStream_t st);

@@ -34,6 +34,21 @@ _TWO_SHOT_MIN = 1 << 18
 _ALGOS = {"one_shot": 0, "two_shot": 1}
 
 
+def _device_key(device) -> str:
+    """Identity of the physical GPU behind ``device`` (UUID or PCI location when the runtime
+    reports them; host + index otherwise)."""
+    import socket
+
+    p = torch.cuda.get_device_properties(device)
+    uuid = getattr(p, "uuid", None)
+    if uuid:
+        return str(uuid)
+    pci = tuple(getattr(p, a, None) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    if any(v is not None for v in pci):
+        return f"{socket.gethostname()}:{pci}"
+    return f"{socket.gethostname()}:{torch.device(device).index}"
+
+
 class XGMIAllReduce:
     def __init__(self, cap: int = 1 << 20, group=None, device=None, algo: str = "auto"):
         self.group = group
@@ -63,6 +78,12 @@ class XGMIAllReduce:
                 bases.append(p)
         self._data = bases
         self._flags = [b + 8 * self.cap for b in bases]
+        # ranks whose kernels share this physical GPU (1 on a node with one rank per GPU; the
+        # single-GPU rehearsals run W ranks on one device): the spinning grids shrink by it so
+        # every rank's blocks are resident together
+        keys = [None] * self.world
+        dist.all_gather_object(keys, _device_key(self.device), group=group)
+        self._share = max(1, keys.count(keys[self.rank]))
         # [timeout flag, last published epoch, done-block counter, pad] (device side)
         self._state = torch.zeros(4, dtype=torch.int32, device=self.device)
         self._calls = 0
@@ -87,7 +108,7 @@ class XGMIAllReduce:
         out = t if out is None else out
         self._calls += 1
         lib().xgmi_allreduce(t, out, self.cap, self._data, self._flags, self.rank, float(scale),
-                             self._state, self._algo(t.numel(), algo))
+                             self._state, self._algo(t.numel(), algo), self._share)
         return out
 
     @property

@@ -322,7 +322,9 @@ def test_xgmi_many_ranks_one_gpu(ws):
     """Four and eight ranks (the 8-GPU node's world size, all on this box's one GPU): 'auto'
     picks the two-shot kernel (W >= 3, >= 1 MB) -- W rank slices, reduce-scatter then
     all-gather through W IPC-mapped buffers; every wait in the kernels is bounded, so a
-    rank that never arrives sets the timeout flag instead of hanging the GPU."""
+    rank that never arrives sets the timeout flag instead of hanging the GPU.  The ranks find
+    that they share one device and shrink their spinning grids by W (8 x 256 two-shot blocks
+    do not all fit beside each other: resident blocks would wait on peers that cannot start)."""
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
