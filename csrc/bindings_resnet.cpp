@@ -116,7 +116,10 @@ int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
 // dx = conv_transpose(dy, w) for stride 1 or 2; add: tensor added to the result (may alias dx
 // for in-place accumulation)
 void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
-                int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg) {
+                int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg,
+                c10::optional<at::Tensor> add_mask) {
+  // add_mask (optional, stride 1): 1-bit mask of `add` (bit j of byte i = element 8i + j), so
+  // the identity-skip gradient dres = add * mask is added without being materialised
   need_bf16_nhwc(dy, "dy");
   need_bf16_nhwc(dx, "dx");
   const int N = dy.size(0), OH = dy.size(1), OW = dy.size(2), Cout = dy.size(3);
@@ -138,8 +141,18 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
   base.N = N; base.H = OH; base.W = OW; base.C = Cout; base.lgC8 = ilog2(Cout / 8);
   base.OH = H; base.OW = W; base.OC = Cin;
   base.KW = KW; base.Ncols = Cin; base.wK = KH * KW * Cout;
+  const unsigned char* addm = nullptr;
+  if (add_mask.has_value()) {
+    TORCH_CHECK(addp && stride == 1 && addp != bp(dx),
+                "add_mask needs a separate add tensor and a stride-1 data gradient");
+    TORCH_CHECK(add_mask->is_cuda() && add_mask->scalar_type() == at::kByte &&
+                    add_mask->is_contiguous() && add_mask->numel() * 8 >= dx.numel(),
+                "add_mask: uint8 [numel/8] on the device");
+    addm = add_mask->data_ptr<uint8_t>();
+  }
   if (stride == 1) {
     auto g = base;
+    g.addm = addm;
     g.Hg = H; g.Wg = W; g.isy = 1; g.isx = 1; g.osy = 1; g.osx = 1; g.oy0 = 0; g.ox0 = 0;
     g.nth = KH; g.ntw = KW; g.dy0 = pad; g.dys = -1; g.dx0 = pad; g.dxs = -1;
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
@@ -582,7 +595,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("conv_stats_rows", &conv_stats_rows, py::arg("M"), py::arg("cfg"), py::arg("ncols") = -1);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("dx"), py::arg("KH"),
         py::arg("KW"), py::arg("stride"), py::arg("pad"),
-        py::arg("add") = py::none(), py::arg("cfg") = 12);
+        py::arg("add") = py::none(), py::arg("cfg") = 12, py::arg("add_mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),

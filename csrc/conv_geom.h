@@ -22,6 +22,10 @@ struct ConvGeom {
   int K;                     // ntaps*C
   // magic-number division by Wg and Hg (m < 2^31): q = (umulhi(n, mul) + n) >> shr
   unsigned wg_mul, wg_shr, hg_mul, hg_shr;
+  // optional 1-bit mask of the epilogue's ADD operand (bit j of byte i = element 8i + j of the
+  // NHWC output): the identity-skip gradient dres = dout * mask is added without ever being
+  // materialised (0 = plain ADD)
+  const unsigned char* addm;
 };
 
 // several geometries for one launch (selected by blockIdx.z)

@@ -384,11 +384,12 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       if (ADD) {
         const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
+        const unsigned mb = g.addm ? g.addm[o >> 3] : 0xffu;  // identity-skip ReLU mask
         const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
-          v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+          v[2 * q] += ((mb >> (2 * q)) & 1u) ? bf2f((bf16_t)(aw[q] & 0xffff)) : 0.f;
+          v[2 * q + 1] += ((mb >> (2 * q + 1)) & 1u) ? bf2f((bf16_t)(aw[q] >> 16)) : 0.f;
         }
       }
       *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),

@@ -248,10 +248,12 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
         if (ADD) {
           const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0);
+          // identity-skip ReLU mask: one byte per 16-B chunk (byte offset / 16)
+          const unsigned mb = (g.addm && off != ROOB) ? g.addm[off >> 4] : 0xffu;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            v[2 * q] += __uint_as_float((unsigned)a[q] << 16);
-            v[2 * q + 1] += __uint_as_float((unsigned)a[q] & 0xffff0000u);
+            v[2 * q] += ((mb >> (2 * q)) & 1u) ? __uint_as_float((unsigned)a[q] << 16) : 0.f;
+            v[2 * q + 1] += ((mb >> (2 * q + 1)) & 1u) ? __uint_as_float((unsigned)a[q] & 0xffff0000u) : 0.f;
           }
         }
         const v4u32_t o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]),

@@ -177,7 +177,7 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
     }
     __syncthreads();
   };
-  auto tile_vals = [&](int row, const uint4& a, float (&v)[8]) {
+  auto tile_vals = [&](int row, const uint4& a, unsigned mb, float (&v)[8]) {
     const float4 v0 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8);
     const float4 v1 = *reinterpret_cast<const float4*>(cs + row * LDC + cc * 8 + 4);
     v[0] = v0.x; v[1] = v0.y; v[2] = v0.z; v[3] = v0.w;
@@ -186,8 +186,8 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        v[2 * q] += bf2f((bf16_t)(aw[q] & 0xffff));
-        v[2 * q + 1] += bf2f((bf16_t)(aw[q] >> 16));
+        v[2 * q] += ((mb >> (2 * q)) & 1u) ? bf2f((bf16_t)(aw[q] & 0xffff)) : 0.f;
+        v[2 * q + 1] += ((mb >> (2 * q + 1)) & 1u) ? bf2f((bf16_t)(aw[q] >> 16)) : 0.f;
       }
     }
   };
@@ -199,11 +199,16 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
     long long o[NLD];
     bool ok[NLD];
     uint4 av[NLD];
+    unsigned mb[NLD];
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
       row_off(k / ITERS, (tid + (k % ITERS) * NT) / CPR, o[k], ok[k]);
       av[k] = make_uint4(0, 0, 0, 0);
-      if (ADD && ok[k]) av[k] = *reinterpret_cast<const uint4*>(ADD + o[k]);
+      mb[k] = 0xffu;
+      if (ADD && ok[k]) {
+        av[k] = *reinterpret_cast<const uint4*>(ADD + o[k]);
+        if (g.addm) mb[k] = g.addm[o[k] >> 3];
+      }
     }
 #pragma unroll
     for (int pb = 0; pb < PASSES; ++pb) {
@@ -213,7 +218,7 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
         const int k = pb * ITERS + i;
         if (!ok[k]) continue;
         float v[8];
-        tile_vals((tid + i * NT) / CPR, av[k], v);
+        tile_vals((tid + i * NT) / CPR, av[k], mb[k], v);
         *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
                                                          pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
       }

@@ -43,6 +43,8 @@ _STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
 _NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
 # DMLAB_NO_RES64=1: layer1 (64 -> 64 channel 3x3) convs on the round-2 halo tile (A/B runs)
 _NO_RES64 = os.environ.get("DMLAB_NO_RES64", "0") == "1"
+# DMLAB_NO_FUSED_SKIP=1: materialise the identity-skip gradient dres (A/B runs)
+_NO_FUSED_SKIP = os.environ.get("DMLAB_NO_FUSED_SKIP", "0") == "1"
 
 
 def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
@@ -339,11 +341,16 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
+def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False):
     """Returns dx (or (dx, dres) when the forward had a residual input).
 
-    ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient)
-    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)"""
+    ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient), or
+                  ("masked", dout, mask): dout * mask added there (the fused skip below)
+    ``dx_into`` : accumulate dx in place into this tensor (downsample branch)
+    ``fused_skip``: with a residual input and the forward's 1-bit ReLU mask, the residual
+                  gradient dres = dout * mask is NOT materialised; the returned dres is
+                  ("masked", dout, mask) for the consumer's dgrad epilogue (saves writing
+                  and re-reading one activation-sized tensor per identity block)"""
     L = lib()
     x, y = ctx["x"], ctx["y"]
     N, OH, OW, cout = y.shape
@@ -390,7 +397,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
     same = not s2d and (OH, OW) == tuple(x.shape[1:3])
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0)
     dy = empty_nhwc(N, OH, OW, cout, y)
-    dres = empty_nhwc(N, OH, OW, cout, y) if ctx["has_res"] else None
+    masked_res = (fused_skip and ctx["has_res"] and mode == 4 and not _NO_FUSED_SKIP)
+    dres = empty_nhwc(N, OH, OW, cout, y) if (ctx["has_res"] and not masked_res) else None
     L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
                   layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
@@ -432,7 +440,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None):
             L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)
+            if isinstance(dx_add, tuple):
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2])
+            else:
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)
     if ctx["has_res"]:
-        return dx, dres
+        return dx, (("masked", dout, ctx["mask"]) if masked_res else dres)
     return dx

@@ -626,3 +626,28 @@ def test_conv_wgrad_res64_accumulates(dev):
     slab = torch.empty(4 * Cout * k * k * Cin, device=dev)
     lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, 1.0, 4, 8, False)
     assert _rel(d, ref + base) < 2e-3
+
+
+@pytest.mark.parametrize("geom,cfg", [(RES64_GEOMS[0], 80), (RES64_GEOMS[2], 80),
+                                      (HALO_GEOMS[1], 42), (HALO_GEOMS[2], 39),
+                                      ((2, 14, 256, 256, 3, 1, 1), 90),
+                                      ((3, 7, 512, 512, 3, 1, 1), 90),
+                                      ((2, 8, 64, 64, 3, 1, 1), 13)])
+def test_conv_dgrad_masked_add(dev, geom, cfg):
+    """Fused identity skip: dx = dgrad(dy) + add * mask with the 1-bit mask (bit j of byte i =
+    element 8i + j) applied in the epilogue equals the dgrad plus the materialised product,
+    bit for bit."""
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p, seed=13)
+    g = torch.Generator(device=dev).manual_seed(14)
+    dy = torch.randn(N, Cout, H, H, device=dev, generator=g).bfloat16()
+    add = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+    keep = torch.rand(N, H, H, Cin, device=dev, generator=g) > 0.4
+    bits = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, device=dev, dtype=torch.uint8)
+    mask = bits.sum(1, dtype=torch.uint8)
+    dres = (add.float() * keep).bfloat16()
+    ref = torch.empty(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
+    lib().conv_dgrad(_nhwc(dy), wd, ref, k, k, s, p, dres, cfg)
+    out = torch.empty_like(ref)
+    lib().conv_dgrad(_nhwc(dy), wd, out, k, k, s, p, add, cfg, add_mask=mask)
+    assert torch.equal(out, ref)
