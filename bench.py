@@ -225,6 +225,7 @@ def main():
                 "hip_graph": bool(a.graph and a.backend == "native"),
             },
             "final_loss": round(final_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),
         }
         if phases is not None:
             res["phases_ms"] = phases

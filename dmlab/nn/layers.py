@@ -234,11 +234,11 @@ class BasicBlock(Layer):
         return prog._side_stream() if prog._native_active else None
 
     def native_bwd(self, dy, ctx, need_dx):
-        # c2's backward returns (d_input_of_c2, d_residual); d_residual = ReLU-masked dy.  With
-        # an identity skip it stays unmaterialised ("masked", dy, mask): c1's dgrad epilogue
-        # adds dy where the forward's 1-bit mask is set
-        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True,
-                                       fused_skip=self.down is None and need_dx)
+        # c2's backward returns (d_input_of_c2, d_residual); d_residual = ReLU-masked dy stays
+        # unmaterialised ("masked", dy, mask): an identity skip adds dy where the forward's
+        # 1-bit mask is set in c1's dgrad epilogue, a projection shortcut's BN backward reads
+        # dy with that mask (its mode 4)
+        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True, fused_skip=need_dx)
         if self.down is None:
             # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass)
             return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None)

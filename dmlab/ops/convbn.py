@@ -358,6 +358,13 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     s2d = ctx.get("s2d", False)
     k, s, p = (4, 1, 2) if s2d else (layer.k, layer.stride, layer.padding)
     acc = 1.0 if layer.accumulate else 0.0
+    # ("masked", dout, mask): the upstream gradient is dout * mask (a projection shortcut fed
+    # the block's unmaterialised residual gradient); the BN backward's mode 4 applies exactly
+    # that mask, so no ReLU of its own is involved
+    in_mask = None
+    if isinstance(dout, tuple):
+        _, dout, in_mask = dout
+        assert not layer.relu and not ctx["has_res"], "masked upstream gradient: linear BN only"
     dout = dout.contiguous()
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
     pre_sums = {}
@@ -385,6 +392,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
         return None
     if pool:
         mode = 3       # dz gathered from the max-pool gradient, ReLU mask from y
+    elif in_mask is not None:
+        mode = 4       # dz = dout * the residual block's 1-bit mask
     elif not layer.relu:
         mode = 0
     elif ctx["has_res"]:
@@ -404,7 +413,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
                   layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
                   dout if pool else None, ctx.get("idx"),
                   getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
-                  getattr(layer, "pool_p", 1), dy, dres, work, mask=ctx.get("mask"), **pre_sums)
+                  getattr(layer, "pool_p", 1), dy, dres, work, mask=in_mask if in_mask is not None else ctx.get("mask"), **pre_sums)
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does
