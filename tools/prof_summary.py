@@ -21,7 +21,7 @@ def family(n):
 
 def rows_csv(path):
     for r in csv.DictReader(open(path)):
-        yield r["Name"], float(r["TotalDurationNs"])
+        yield r["Name"], float(r["TotalDurationNs"]), int(r.get("Calls") or 1)
 
 
 def rows_trace(path, keep_frac=None):
@@ -30,7 +30,7 @@ def rows_trace(path, keep_frac=None):
     if keep_frac:
         rs = rs[int(len(rs) * (1 - keep_frac)):]
     for n, s, e in rs:
-        yield n, float(e - s)
+        yield n, float(e - s), 1
 
 
 def step_rows(path):
@@ -49,7 +49,7 @@ def rows_db(path, keep_frac=None):
     if keep_frac:
         rs = rs[int(len(rs) * (1 - keep_frac)):]
     for n, s, e in rs:
-        yield n, float(e - s)
+        yield n, float(e - s), 1
 
 
 def main():
@@ -82,11 +82,11 @@ def main():
     fam = defaultdict(float)
     cnt = defaultdict(int)
     tot = 0.0
-    for n, ns in rows:
+    for n, ns, calls in rows:
         t = ns / 1e6 / steps
         k = family(n)
         fam[k] += t
-        cnt[k] += 1
+        cnt[k] += calls
         tot += t
     for k, v in sorted(fam.items(), key=lambda kv: -kv[1]):
         if v > 0.01:
