@@ -117,7 +117,13 @@ int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
 // for in-place accumulation)
 void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t KW,
                 int64_t stride, int64_t pad, c10::optional<at::Tensor> add, int64_t cfg,
-                c10::optional<at::Tensor> add_mask) {
+                c10::optional<at::Tensor> add_mask, c10::optional<at::Tensor> red_y,
+                c10::optional<at::Tensor> red_scale, c10::optional<at::Tensor> red_shift,
+                c10::optional<at::Tensor> red_mean, c10::optional<at::Tensor> red_invstd,
+                c10::optional<at::Tensor> red_part) {
+  // red_* (optional, cfg 80 only): the backward reduction of the BatchNorm + ReLU whose
+  // output gradient dx is (its input red_y, forward scale/shift, mean/invstd) runs in this
+  // dgrad's epilogue -> red_part [res64_grid(M)][2][Cin] (bn_backward's pre_slab)
   // add_mask (optional, stride 1): 1-bit mask of `add` (bit j of byte i = element 8i + j), so
   // the identity-skip gradient dres = add * mask is added without being materialised
   need_bf16_nhwc(dy, "dy");
@@ -158,9 +164,26 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
+    if (red_y.has_value()) {
+      TORCH_CHECK(cfg == 80 && !addp, "red_*: cfg 80 data gradient without add");
+      need_bf16_nhwc(*red_y, "red_y");
+      TORCH_CHECK(red_y->sizes() == dx.sizes(), "red_y: dx's shape");
+      TORCH_CHECK(red_scale && red_shift && red_mean && red_invstd && red_part,
+                  "red_*: scale, shift, mean, invstd and part are all required");
+      need_f32(*red_scale, "red_scale", Cin);
+      need_f32(*red_shift, "red_shift", Cin);
+      need_f32(*red_mean, "red_mean", Cin);
+      need_f32(*red_invstd, "red_invstd", Cin);
+      need_f32(*red_part, "red_part", (int64_t)dm::res64_grid(g.M) * 2 * Cin);
+      const dm::BnBwdRed red{bp(*red_y), nullptr, fp(*red_scale), fp(*red_shift), fp(*red_mean),
+                             fp(*red_invstd), fp(*red_part)};
+      dm::conv_res64(bp(dy), bp(wd), bp(dx), nullptr, nullptr, g, st, nullptr, nullptr, &red);
+      return;
+    }
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
     return;
   }
+  TORCH_CHECK(!red_y.has_value(), "red_*: stride-1 data gradients only");
   // parity classes write disjoint output pixels; a class with no taps (e.g. the odd
   // pixels of a 1x1/s2 conv) is exactly zero, so zero-fill once up front when needed
   bool any_empty = false;
@@ -595,7 +618,10 @@ void register_resnet(pybind11::module_& m) {
   m.def("conv_stats_rows", &conv_stats_rows, py::arg("M"), py::arg("cfg"), py::arg("ncols") = -1);
   m.def("conv_dgrad", &conv_dgrad, py::arg("dy"), py::arg("wd"), py::arg("dx"), py::arg("KH"),
         py::arg("KW"), py::arg("stride"), py::arg("pad"),
-        py::arg("add") = py::none(), py::arg("cfg") = 12, py::arg("add_mask") = py::none());
+        py::arg("add") = py::none(), py::arg("cfg") = 12, py::arg("add_mask") = py::none(),
+        py::arg("red_y") = py::none(), py::arg("red_scale") = py::none(),
+        py::arg("red_shift") = py::none(), py::arg("red_mean") = py::none(),
+        py::arg("red_invstd") = py::none(), py::arg("red_part") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),

@@ -53,6 +53,14 @@ constexpr int R_TAB = R_ZROW + RPITCH;  // PRE scale / shift (2 x 64 floats)
 constexpr int R_EPI = R_TAB + 2 * RC * 4;
 constexpr int R_LDC = 36;               // epilogue band pitch (floats): 32 rows x 32 columns
 constexpr int R_SMEM = R_EPI + 4 * 32 * R_LDC * 4;
+// RED (BN-backward reduction of the next layer, dgrad only): the reduced BN's sc / sh / mu,
+// per-lane running sums [4 waves][64 lanes][2], and the tile's y (that BN's input) landed by
+// LDS-DMA as [channel half][128 pixels][32 channels].  Nothing of it lives in registers
+// across tiles: the kernel already holds 240 of its 256 VGPRs.
+constexpr int R_RTAB = R_SMEM;
+constexpr int R_RACC = R_RTAB + 3 * RC * 4;
+constexpr int R_Y = R_RACC + RNT * 2 * 4;
+constexpr int R_SMEM_RED = R_Y + RT * RC * 2;
 typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int div9(int s) { return (s * 7282) >> 16; }  // exact for s < 3584
@@ -63,11 +71,13 @@ __device__ __forceinline__ unsigned opq(unsigned v) {
   return v;
 }
 
-template <bool PRE>
+template <bool PRE, bool RED>
 __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned ybytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int ntiles) {
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int ntiles,
+    BnBwdRed red) {
+  static_assert(!(PRE && RED), "RED is a data-gradient epilogue (no PRE input)");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -106,6 +116,15 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
     tab[tid] = pre_sc[tid];
     tab[RC + tid] = pre_sh[tid];
   }
+  if (RED) {
+    float* rtab = reinterpret_cast<float*>(smem + R_RTAB);
+    if (tid < RC) {
+      rtab[tid] = red.sc[tid];
+      rtab[RC + tid] = red.sh[tid];
+      rtab[2 * RC + tid] = red.mu[tid];
+    }
+    reinterpret_cast<float2*>(smem + R_RACC)[tid] = make_float2(0.f, 0.f);
+  }
 
   const pi32x4 rsx = prsrc(X, xbytes);
   const auto rsy = __builtin_amdgcn_make_buffer_rsrc((void*)Y, (short)0, (int)ybytes, 0x00020000);
@@ -124,6 +143,18 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
     const int row = div9(s), c = s - row * 9;
     pb[j] = c < 8 ? (unsigned)(row * 128 + c * 16) : R_PADOFF;
   }
+  // RED: y of tile tt -> R_Y; LDS piece s = (j*4 + wid)*64 + lane is channel half s >> 9,
+  // pixel (s >> 2) & 127, 16-B chunk s & 3 (rows past M read zero)
+  const pi32x4 rsr = prsrc(RED ? (const void*)red.y : (const void*)X, ybytes);
+  auto ydma = [&](int tt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned s = (unsigned)(j * 4 + wid) * 64u + opq((unsigned)lane);
+      const unsigned off = (unsigned)tt * (RT * 128u) + ((s >> 2) & 127u) * 128u + (s >> 9) * 64u +
+                           (s & 3u) * 16u;
+      pdma16(rsr, lds0 + (unsigned)(R_Y + (j * 4 + wid) * 1024), off);
+    }
+  };
   auto dma = [&](int tt) __attribute__((always_inline)) {
     const unsigned hs = (unsigned)((tt * RT - g.W - 1) * 128);
 #pragma unroll
@@ -177,6 +208,8 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
   }
   for (int tt = t_begin; tt < t_end; ++tt) {
     const int m0 = tt * RT;
+    // every wave is past the previous tile's epilogue (loop-end barrier): y(tt) may land
+    if (RED) ydma(tt);
     // taps inside the image, per fragment row (bit th*3 + tw)
     unsigned mk[2];
 #pragma unroll
@@ -223,11 +256,24 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
       __builtin_amdgcn_sched_barrier(0);
     }
     // every wave is done reading the halo image: the next tile's DMA may overwrite it
+    // (RED: and every wave's share of y(tt), issued a whole tile ago, has landed)
+    if (RED) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const bool more = tt + 1 < t_end;
     if (more) dma(tt + 1);
 
     // epilogue: statistics, then 32-row bands through this wave's LDS region to 16-B stores
+    // RED: this lane's channel (its MFMA output column) is fixed; its BN constants are
+    // re-read per tile through a laundered address (kept out of the register budget)
+    float rsc = 0.f, rsh = 0.f, rmu = 0.f, rs = 0.f, rq = 0.f;
+    const unsigned char* ybase = smem;
+    if constexpr (RED) {
+      ybase = smem + opq((unsigned)(R_Y + wn * 8192 + (wm * 64 + 4 * hsel) * 64 + l32 * 2));
+      const float* rt = reinterpret_cast<const float*>(smem + opq((unsigned)(R_RTAB + (wn * 32 + l32) * 4)));
+      rsc = rt[0];
+      rsh = rt[RC];
+      rmu = rt[2 * RC];
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
@@ -235,6 +281,18 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         const float v = acc[i][r];
         ssum += v;
         ssq += v * v;
+        if constexpr (RED) {
+          // dz = the stored (bf16) gradient where the reduced BN's ReLU passed
+          const int pr = i * 32 + (r & 3) + 8 * (r >> 2);  // + wm*64 + 4*hsel in ybase
+          const float yj = __uint_as_float(
+              (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
+          const float gj = __uint_as_float(pack_bf2(v, 0.f) << 16);
+          const float dz = yj * rsc + rsh > 0.f ? gj : 0.f;
+          rs += dz;
+          rq += dz * (yj - rmu);
+          // bound the y reads in flight (the scheduler would hoist all 32 into registers)
+          if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
         cs[((r & 3) + 8 * (r >> 2) + 4 * hsel) * R_LDC + l32] = v;
       }
 #pragma unroll
@@ -246,7 +304,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         const float4 v0 = *reinterpret_cast<const float4*>(cs + rr * R_LDC + cq * 8);
         const float4 v1 = *reinterpret_cast<const float4*>(cs + rr * R_LDC + cq * 8 + 4);
         float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        if (ADD) {
+        if (!RED && ADD) {  // (RED variant: no residual input, which frees its registers)
           const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0);
           // identity-skip ReLU mask: one byte per 16-B chunk (byte offset / 16)
           const unsigned mb = (g.addm && off != ROOB) ? g.addm[off >> 4] : 0xffu;
@@ -261,6 +319,11 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         __builtin_amdgcn_raw_buffer_store_b128(o, rsy, off, 0, 0);
       }
     }
+    if constexpr (RED) {
+      float2* ra = reinterpret_cast<float2*>(smem + R_RACC) + tid;
+      const float2 o = *ra;
+      *ra = make_float2(o.x + rs, o.y + rq);
+    }
     if (more) {
       // the DMA is older than the 4 stores above: vmcnt(4) retires it, not them
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -269,6 +332,27 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
     }
   }
 
+  if constexpr (RED) {
+    // workgroup row: both row halves (hsel) and the two pixel-half waves (wm) add up;
+    // Σdz(y - mu) scales by invstd
+    // lane slot tid = (wm*2 + wn)*64 + hsel*32 + l32 holds channel wn*32 + l32
+    __syncthreads();
+    const float2* ra = reinterpret_cast<const float2*>(smem + R_RACC);
+    if (tid < RC) {
+      const int h = tid >> 5, c = tid & 31;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < 2; ++w)
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+          const float2 v = ra[(w * 2 + h) * 64 + hs * 32 + c];
+          s += v.x;
+          q += v.y;
+        }
+      red.part[(long long)b * 2 * RC + tid] = s;
+      red.part[(long long)b * 2 * RC + RC + tid] = q * red.is[tid];
+    }
+  }
   if (stats) {
     ssum += __shfl_xor(ssum, 32, 64);
     ssq += __shfl_xor(ssq, 32, 64);
@@ -319,14 +403,26 @@ bool conv_res64_supported(const ConvGeom& g) {
 }
 
 void conv_res64(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh) {
+                const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh,
+                const BnBwdRed* red) {
   if (!conv_res64_supported(g)) throw std::runtime_error("conv_res64: unsupported geometry");
   const int grid = res64_grid(g.M);
   const unsigned bytes = (unsigned)(g.M * RC * 2);
   const int ntiles = (int)((g.M + RT - 1) / RT);
-  auto k = pre_sc ? conv_res64_kernel<true> : conv_res64_kernel<false>;
-  set_smem_attr(k, R_SMEM);
-  k<<<grid, RNT, R_SMEM, st>>>(X, Wp, Y, ADD, stats, g, bytes, bytes, pre_sc, pre_sh, ntiles);
+  if (red) {
+    if (pre_sc || ADD || red->mask || !red->y || !red->sc || !red->sh || !red->mu || !red->is ||
+        !red->part)
+      throw std::runtime_error("conv_res64: BN-backward reduction needs y, sc, sh, mu, is, part "
+                               "(ReLU mask from y; no PRE or ADD input)");
+    set_smem_attr(conv_res64_kernel<false, true>, R_SMEM_RED);
+    conv_res64_kernel<false, true><<<grid, RNT, R_SMEM_RED, st>>>(
+        X, Wp, Y, ADD, stats, g, bytes, bytes, pre_sc, pre_sh, ntiles, *red);
+  } else {
+    auto k = pre_sc ? conv_res64_kernel<true, false> : conv_res64_kernel<false, false>;
+    set_smem_attr(k, R_SMEM);
+    k<<<grid, RNT, R_SMEM, st>>>(X, Wp, Y, ADD, stats, g, bytes, bytes, pre_sc, pre_sh, ntiles,
+                                 BnBwdRed{});
+  }
   DM_CHECK(hipGetLastError());
 }
 

@@ -100,9 +100,22 @@ void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
 // statistics rows = res64_grid(M) (one per workgroup)
 bool conv_res64_supported(const ConvGeom& g);
 int res64_grid(long long M);
+// The BatchNorm backward reduction of the layer whose output gradient a data gradient
+// produces, done in that dgrad's epilogue: with dz = Y * relu-mask (mask from y*sc + sh > 0,
+// or the 1-bit `mask` when set), part[wg][0][c] = Σ dz and part[wg][1][c] = Σ dz (y - mu) is
+// (one row per workgroup, the layout bn_backward's pre_part consumes)
+struct BnBwdRed {
+  const bf16_t* y;
+  const uint8_t* mask;
+  const float* sc;
+  const float* sh;
+  const float* mu;
+  const float* is;
+  float* part;
+};
 void conv_res64(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                 const ConvGeom& g, hipStream_t st, const float* pre_sc = nullptr,
-                const float* pre_sh = nullptr);
+                const float* pre_sh = nullptr, const BnBwdRed* red = nullptr);
 bool conv_halo_supported(const ConvGeom& g);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,

@@ -160,11 +160,12 @@ class ConvBN(Layer):
 
         return CB.convbn_fwd(self, x, ctx, train, residual, raw=raw, pre=pre)
 
-    def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False):
+    def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
+                   red_for=None):
         from dmlab.ops import convbn as CB
 
         return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into,
-                             fused_skip=fused_skip)
+                             fused_skip=fused_skip, red_for=red_for)
 
 
 class ConvBNPool(ConvBN):
@@ -238,7 +239,10 @@ class BasicBlock(Layer):
         # unmaterialised ("masked", dy, mask): an identity skip adds dy where the forward's
         # 1-bit mask is set in c1's dgrad epilogue, a projection shortcut's BN backward reads
         # dy with that mask (its mode 4)
-        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True, fused_skip=need_dx)
+        # c1's BN backward sums (Σdz, Σdz·x̂ over c2's data gradient) reduce in that dgrad's
+        # epilogue where the kernel supports it (layer1: csrc/conv_res64.hip RED)
+        dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True, fused_skip=need_dx,
+                                       red_for=(self.c1, ctx["c1"]))
         if self.down is None:
             # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass)
             return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None)

@@ -45,6 +45,8 @@ _NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
 _NO_RES64 = os.environ.get("DMLAB_NO_RES64", "0") == "1"
 # DMLAB_NO_FUSED_SKIP=1: materialise the identity-skip gradient dres (A/B runs)
 _NO_FUSED_SKIP = os.environ.get("DMLAB_NO_FUSED_SKIP", "0") == "1"
+# DMLAB_NO_DGRAD_RED=1: run the next BN's backward reduction as its own pass (A/B runs)
+_NO_DGRAD_RED = os.environ.get("DMLAB_NO_DGRAD_RED", "0") == "1"
 
 
 def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
@@ -341,7 +343,24 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False):
+def _dgrad_red(L, red_for, cfg, dx_add, dx):
+    """conv_dgrad kwargs that reduce the consumer BN's backward sums in the dgrad epilogue
+    (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify."""
+    rl, rctx = red_for
+    if (_NO_DGRAD_RED or cfg != 80 or dx_add is not None or not rl.relu or rctx.get("has_res")
+            or getattr(rl, "pool_k", 0) or rctx.get("mean") is None
+            or rctx.get("pre_sums") is not None or tuple(rctx["y"].shape) != tuple(dx.shape)):
+        return {}
+    N, H, W, C = dx.shape
+    rows = L.conv_stats_rows(N * H * W, cfg, C)
+    part = torch.empty(rows * 2 * C, device=dx.device, dtype=torch.float32)
+    rctx["pre_sums"] = dict(pre_slab=part, pre_rows=rows)
+    return dict(red_y=rctx["y"], red_scale=rctx["scale"], red_shift=rctx["shift"],
+                red_mean=rctx["mean"], red_invstd=rctx["invstd"], red_part=part)
+
+
+def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
+               red_for=None):
     """Returns dx (or (dx, dres) when the forward had a residual input).
 
     ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient), or
@@ -350,7 +369,11 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     ``fused_skip``: with a residual input and the forward's 1-bit ReLU mask, the residual
                   gradient dres = dout * mask is NOT materialised; the returned dres is
                   ("masked", dout, mask) for the consumer's dgrad epilogue (saves writing
-                  and re-reading one activation-sized tensor per identity block)"""
+                  and re-reading one activation-sized tensor per identity block)
+    ``red_for``  : (layer, ctx) of the ConvBN + ReLU whose output gradient dx is.  When the
+                  dgrad kernel supports it (cfg 80), that BN's backward reduction (Σdz, Σdz·x̂)
+                  runs in this dgrad's epilogue and is left in its ctx["pre_sums"], so its
+                  own backward skips the pass that re-reads dx and y"""
     L = lib()
     x, y = ctx["x"], ctx["y"]
     N, OH, OW, cout = y.shape
@@ -367,7 +390,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
         assert not layer.relu and not ctx["has_res"], "masked upstream gradient: linear BN only"
     dout = dout.contiguous()
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
-    pre_sums = {}
+    pre_sums = ctx.pop("pre_sums", None) or {}
     pool = getattr(layer, "pool_k", 0)
     if pool and ctx.get("yarg") is not None:
         # stem: Σdz, Σdz·x̂ over the pooled grid (pooled grad masked at the argmax, x̂ from
@@ -449,7 +472,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            if isinstance(dx_add, tuple):
+            red_kw = _dgrad_red(L, red_for, cfg, dx_add, dx) if red_for is not None else {}
+            if red_kw:
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, None, cfg, **red_kw)
+            elif isinstance(dx_add, tuple):
                 L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2])
             else:
                 L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)

@@ -651,3 +651,33 @@ def test_conv_dgrad_masked_add(dev, geom, cfg):
     out = torch.empty_like(ref)
     lib().conv_dgrad(_nhwc(dy), wd, out, k, k, s, p, add, cfg, add_mask=mask)
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("geom", RES64_GEOMS)
+def test_conv_dgrad_bn_reduce(dev, geom):
+    """cfg 80 data gradient with the consumer BN's backward reduction in its epilogue: dx is
+    bit-identical to the plain dgrad, and the per-workgroup rows add up to that BN's Σdz and
+    Σdz·x̂ (dz = the stored bf16 dx where y*scale + shift > 0), against a float64 torch sum."""
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p, seed=21)
+    g = torch.Generator(device=dev).manual_seed(22)
+    dy = torch.randn(N, Cout, H, H, device=dev, generator=g).bfloat16()
+    ref = torch.empty(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
+    lib().conv_dgrad(_nhwc(dy), wd, ref, k, k, s, p, None, 80)
+    yb = (torch.randn(N, H, H, Cin, device=dev, generator=g) * 2 + 0.3).bfloat16()
+    sc = torch.rand(Cin, device=dev, generator=g) + 0.5
+    sh = torch.randn(Cin, device=dev, generator=g) * 0.5
+    mu = torch.randn(Cin, device=dev, generator=g) * 0.2
+    inv = torch.rand(Cin, device=dev, generator=g) + 0.5
+    rows = lib().conv_stats_rows(N * H * H, 80, Cin)
+    part = torch.full((rows * 2 * Cin,), float("nan"), device=dev)
+    out = torch.empty_like(ref)
+    lib().conv_dgrad(_nhwc(dy), wd, out, k, k, s, p, None, 80, red_y=yb, red_scale=sc,
+                     red_shift=sh, red_mean=mu, red_invstd=inv, red_part=part)
+    assert torch.equal(out, ref)
+    yf = yb.double()
+    dz = torch.where(yb.float() * sc + sh > 0, ref.double(), torch.zeros((), device=dev,
+                                                                           dtype=torch.float64))
+    want = torch.stack([dz.sum((0, 1, 2)), (dz * (yf - mu.double())).sum((0, 1, 2)) * inv.double()])
+    got = part.view(rows, 2, Cin).double().sum(0)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4 * float(want.abs().max()))

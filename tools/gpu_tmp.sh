@@ -1,15 +1,26 @@
-# Ad-hoc GPU step (overwritten per experiment): repeatability of the fused-skip step.
+# Ad-hoc GPU step (overwritten per experiment): BN-backward reduction in the res64 dgrad
+# epilogue -- kernel tests, resnet model tests, interleaved A/B bench, step trace.
 set -o pipefail
 tag=${1:-tmp}
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for i in 1 2 3 4; do
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_native_resnet_kernels.py -k "res64 or bn_reduce or masked_add" \
+    > gpurun_out/pytest_$tag.log 2>&1 || { tail -30 gpurun_out/pytest_$tag.log; exit 1; }
+tail -2 gpurun_out/pytest_$tag.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+    tests/test_native_resnet_model.py > gpurun_out/pytest_model_$tag.log 2>&1 || { tail -30 gpurun_out/pytest_model_$tag.log; exit 1; }
+tail -2 gpurun_out/pytest_model_$tag.log
+for i in 1 2 3; do
 timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_$tag.json 2>> gpurun_out/bench_$tag.err || exit 1
+DMLAB_NO_DGRAD_RED=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_nored_$tag.json 2>> gpurun_out/bench_nored_$tag.err || exit 1
 done
-DMLAB_NO_FUSED_SKIP=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_nofs_$tag.json 2>> gpurun_out/bench_nofs_$tag.err || exit 1
-python - <<'PY'
-import json,sys
-for f in ("gpurun_out/bench_fs3.json","gpurun_out/bench_nofs_fs3.json"):
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_$tag -o tr -- \
+    python bench.py --steps 4 --warmup 2 > gpurun_out/trace_$tag.log 2>&1 || exit 1
+python - "$tag" <<'PY'
+import json, sys
+t = sys.argv[1]
+for f in (f"gpurun_out/bench_{t}.json", f"gpurun_out/bench_nored_{t}.json"):
     for l in open(f):
-        d=json.loads(l); print(f, d["value"], d["ms_per_step"], d.get("peak_mem_gb"))
+        d = json.loads(l); print(f, d["value"], d["ms_per_step"], d.get("final_loss"))
 PY
