@@ -226,6 +226,10 @@ def main():
             },
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),
+            "peak_alloc_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+            # allocator retries (a failed hipMalloc frees the cache and synchronises): >0
+            # means the step ran short of device memory
+            "alloc_retries": int(torch.cuda.memory_stats().get("num_alloc_retries", 0)),
         }
         if phases is not None:
             res["phases_ms"] = phases

@@ -132,7 +132,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0):
     res64 = (k == 3 and stride == 1 and cin == 64 and cout == 64 and 0 < W <= 60 and rows > 0
              and not _NO_WRES64)
     if force == 8 or (force is None and res64):
-        return 8, max(1, min(rows, _cu_count()))
+        return 8, max(1, min(rows, int(os.environ.get("DMLAB_WRES64_S", 0)) or _cu_count()))
     if force is not None:
         cfg = force
     elif halo:

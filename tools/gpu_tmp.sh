@@ -1,26 +1,19 @@
-# Ad-hoc GPU step (overwritten per experiment): BN-backward reduction in the res64 dgrad
-# epilogue -- kernel tests, resnet model tests, interleaved A/B bench, step trace.
+# Ad-hoc GPU step (overwritten per experiment): host run-ahead bound (Program.max_inflight)
+# vs throughput and reserved device memory.
 set -o pipefail
 tag=${1:-tmp}
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-    tests/test_native_resnet_kernels.py -k "res64 or bn_reduce or masked_add" \
-    > gpurun_out/pytest_$tag.log 2>&1 || { tail -30 gpurun_out/pytest_$tag.log; exit 1; }
-tail -2 gpurun_out/pytest_$tag.log
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-    tests/test_native_resnet_model.py > gpurun_out/pytest_model_$tag.log 2>&1 || { tail -30 gpurun_out/pytest_model_$tag.log; exit 1; }
-tail -2 gpurun_out/pytest_model_$tag.log
-for i in 1 2 3; do
-timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_$tag.json 2>> gpurun_out/bench_$tag.err || exit 1
-DMLAB_NO_DGRAD_RED=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_nored_$tag.json 2>> gpurun_out/bench_nored_$tag.err || exit 1
+for i in 1 2; do
+for K in 2 1 4 0; do
+DMLAB_MAX_INFLIGHT=$K timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_k${K}_$tag.json 2>> gpurun_out/bench_$tag.err || exit 1
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_$tag -o tr -- \
-    python bench.py --steps 4 --warmup 2 > gpurun_out/trace_$tag.log 2>&1 || exit 1
+done
 python - "$tag" <<'PY'
 import json, sys
 t = sys.argv[1]
-for f in (f"gpurun_out/bench_{t}.json", f"gpurun_out/bench_nored_{t}.json"):
-    for l in open(f):
-        d = json.loads(l); print(f, d["value"], d["ms_per_step"], d.get("final_loss"))
+for K in (2, 1, 4, 0):
+    for l in open(f"gpurun_out/bench_k{K}_{t}.json"):
+        d = json.loads(l)
+        print(K, d["value"], d["peak_mem_gb"], d["peak_alloc_gb"], d["alloc_retries"])
 PY
