@@ -123,7 +123,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
     cfg 8: row-streaming 64 -> 64 channel 3x3 kernel (csrc/wgrad_res64.hip; ``W`` = image
-    width <= 60, ``rows`` = N*H image rows, S = one slab per CU); cfg 4/5: halo-staged 3x3
+    width <= 60, ``rows`` = N*H image rows, S = 5/8 of the CUs); cfg 4/5: halo-staged 3x3
     unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per block; cfg 2/3/6: v2 igemm
     tiles 128x128 / 64x128 / 64x256.
     S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
@@ -132,7 +132,11 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0):
     res64 = (k == 3 and stride == 1 and cin == 64 and cout == 64 and 0 < W <= 60 and rows > 0
              and not _NO_WRES64)
     if force == 8 or (force is None and res64):
-        return 8, max(1, min(rows, int(os.environ.get("DMLAB_WRES64_S", 0)) or _cu_count()))
+        # 5/8 of the CUs: the kernel runs on the side stream next to the dgrad + BN-backward
+        # chain, and leaving that chain CUs of its own is 0.8% faster per step than one
+        # workgroup on every CU (128-192 of 256 tie; profiles/wgrad_res64_slabs_ab_r3s3.txt)
+        S = int(os.environ.get("DMLAB_WRES64_S", 0)) or max(1, _cu_count() * 5 // 8)
+        return 8, max(1, min(rows, S))
     if force is not None:
         cfg = force
     elif halo:

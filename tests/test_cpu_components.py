@@ -339,7 +339,7 @@ def test_res64_picked_for_layer1():
 
 def test_wgrad_res64_plan():
     """wgrad cfg 8 (csrc/wgrad_res64.hip) for 64 -> 64 channel 3x3/s1 layers of width <= 60,
-    one slab per CU (at most one per image row)."""
+    one slab per workgroup on 5/8 of the CUs (at most one per image row)."""
     from dmlab.ops.convbn import _wgrad_plan
     cfg, S = _wgrad_plan(1024 * 56 * 56, 64, 576, 3, 1, 64, W=56, rows=1024 * 56)
     assert cfg == 8 and 1 <= S <= 1024 * 56
