@@ -120,7 +120,7 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
                 c10::optional<at::Tensor> add_mask, c10::optional<at::Tensor> red_y,
                 c10::optional<at::Tensor> red_scale, c10::optional<at::Tensor> red_shift,
                 c10::optional<at::Tensor> red_mean, c10::optional<at::Tensor> red_invstd,
-                c10::optional<at::Tensor> red_part) {
+                c10::optional<at::Tensor> red_part, c10::optional<at::Tensor> red_mask) {
   // red_* (optional, cfg 80 only): the backward reduction of the BatchNorm + ReLU whose
   // output gradient dx is (its input red_y, forward scale/shift, mean/invstd) runs in this
   // dgrad's epilogue -> red_part [res64_grid(M)][2][Cin] (bn_backward's pre_slab)
@@ -165,7 +165,9 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
     if (red_y.has_value()) {
-      TORCH_CHECK(cfg == 80 && !addp, "red_*: cfg 80 data gradient without add");
+      const bool pipe = cfg >= 90 && cfg <= 93 && dm::conv_pipe_supported(g, (int)cfg);
+      TORCH_CHECK((cfg == 80 && !addp) || pipe,
+                  "red_*: a cfg 80 data gradient without add, or a pipelined (90-93) one");
       need_bf16_nhwc(*red_y, "red_y");
       TORCH_CHECK(red_y->sizes() == dx.sizes(), "red_y: dx's shape");
       TORCH_CHECK(red_scale && red_shift && red_mean && red_invstd && red_part,
@@ -174,10 +176,21 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       need_f32(*red_shift, "red_shift", Cin);
       need_f32(*red_mean, "red_mean", Cin);
       need_f32(*red_invstd, "red_invstd", Cin);
-      need_f32(*red_part, "red_part", (int64_t)dm::res64_grid(g.M) * 2 * Cin);
-      const dm::BnBwdRed red{bp(*red_y), nullptr, fp(*red_scale), fp(*red_shift), fp(*red_mean),
+      need_f32(*red_part, "red_part", conv_stats_rows(g.M, cfg, Cin) * 2 * Cin);
+      const unsigned char* rmask = nullptr;
+      if (red_mask.has_value()) {
+        TORCH_CHECK(pipe, "red_mask: pipelined (90-93) data gradients only");
+        TORCH_CHECK(red_mask->is_cuda() && red_mask->scalar_type() == at::kByte &&
+                        red_mask->is_contiguous() && red_mask->numel() * 8 >= dx.numel(),
+                    "red_mask: uint8 [numel/8] on the device");
+        rmask = red_mask->data_ptr<uint8_t>();
+      }
+      const dm::BnBwdRed red{bp(*red_y), rmask, fp(*red_scale), fp(*red_shift), fp(*red_mean),
                              fp(*red_invstd), fp(*red_part)};
-      dm::conv_res64(bp(dy), bp(wd), bp(dx), nullptr, nullptr, g, st, nullptr, nullptr, &red);
+      if (pipe)
+        dm::conv_pipe(bp(dy), bp(wd), bp(dx), addp, nullptr, g, (int)cfg, st, nullptr, nullptr, &red);
+      else
+        dm::conv_res64(bp(dy), bp(wd), bp(dx), nullptr, nullptr, g, st, nullptr, nullptr, &red);
       return;
     }
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
@@ -621,7 +634,8 @@ void register_resnet(pybind11::module_& m) {
         py::arg("add") = py::none(), py::arg("cfg") = 12, py::arg("add_mask") = py::none(),
         py::arg("red_y") = py::none(), py::arg("red_scale") = py::none(),
         py::arg("red_shift") = py::none(), py::arg("red_mean") = py::none(),
-        py::arg("red_invstd") = py::none(), py::arg("red_part") = py::none());
+        py::arg("red_invstd") = py::none(), py::arg("red_part") = py::none(),
+        py::arg("red_mask") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),

@@ -34,6 +34,7 @@
 #include "igemm_common.h"
 #include "kernels.h"
 
+#include <stdexcept>
 #include <type_traits>
 
 namespace dm {
@@ -49,11 +50,15 @@ constexpr unsigned POOB = 0x80000000u;
 // rewrites the 16-B chunks its own DMA landed, between its vmcnt wait and the barrier that
 // publishes the stage, skipping the zero rows of padding taps (the padding stays zero AFTER
 // the BatchNorm, as in the unfused conv)
-template <int BN, int WM, int WN, int MINW, bool PRE>
+// RED (data gradients): the backward reduction of the BatchNorm whose output gradient Y is
+// (kernels.h BnBwdRed) runs in the store loop -- each lane's 8 channels of the stored bf16
+// value against that BN's input y -- and leaves one [2][Ncols] row per M tile in red.part
+template <int BN, int WM, int WN, int MINW, bool PRE, bool RED = false>
 __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeomSet gs, unsigned xbytes, unsigned wbytes, int ntN,
-    int mtiles_max, int xcd, const float* __restrict__ pre_sc, const float* __restrict__ pre_sh) {
+    int mtiles_max, int xcd, const float* __restrict__ pre_sc, const float* __restrict__ pre_sh,
+    BnBwdRed red) {
   // blockIdx.y selects one of up to four geometries sharing X / W / Y (the parity classes of a
   // stride-2 data gradient, which write disjoint output pixels); one geometry otherwise
   const ConvGeom g = gs.g[blockIdx.y];
@@ -315,7 +320,7 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   // ---- epilogue ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave is done with the stage buffers (LDS reused below)
-  float* red = reinterpret_cast<float*>(smem);  // [WM][BN][2] statistics partials
+  float* sred = reinterpret_cast<float*>(smem);  // [WM][BN][2] statistics partials
   if (stats) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
@@ -332,8 +337,8 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
       q += __shfl_xor(q, 32, 64);
       if (lane < 32) {
         const int c = wn * TN + j * 32 + lane;
-        red[(wm * BN + c) * 2 + 0] = sm;
-        red[(wm * BN + c) * 2 + 1] = q;
+        sred[(wm * BN + c) * 2 + 0] = sm;
+        sred[(wm * BN + c) * 2 + 1] = q;
       }
     }
     __syncthreads();
@@ -342,8 +347,8 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
         float a = 0.f, b = 0.f;
 #pragma unroll
         for (int w = 0; w < WM; ++w) {
-          a += red[(w * BN + c) * 2 + 0];
-          b += red[(w * BN + c) * 2 + 1];
+          a += sred[(w * BN + c) * 2 + 0];
+          b += sred[(w * BN + c) * 2 + 1];
         }
         stats[((long long)bx * 2 + 0) * g.Ncols + n0 + c] = a;
         stats[((long long)bx * 2 + 1) * g.Ncols + n0 + c] = b;
@@ -359,8 +364,66 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   const int cq = lane % CPR, rsub = lane / CPR;
   const int col = n0 + wn * TN + cq * 8;
   const int fcol = lane & 31;
+  float rsc[8], rsh[8], rmu[8], rs[8], rq[8];
+  if constexpr (RED) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = col + j < g.Ncols ? col + j : 0;
+      rsc[j] = red.mask ? 0.f : red.sc[c];
+      rsh[j] = red.mask ? 0.f : red.sh[c];
+      rmu[j] = red.mu[c];
+      rs[j] = rq[j] = 0.f;
+    }
+  }
+  // RED: the y chunks (and 1-bit masks) of row block i + 1 are loaded while block i is
+  // staged and stored (a load per chunk in the store loop left its latency exposed: layer4's
+  // 1.5 workgroups per CU have nothing else to run)
+  // The residual ADD chunks (and identity-skip masks) of block i are loaded before block i
+  // is staged, for the same reason.
+  constexpr int NIT = 32 / RPI;
+  uint4 ypf[2][NIT], apf[NIT];
+  unsigned mpf[2][NIT], ampf[NIT];
+  auto aload = [&](int i) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + wm * TM + i * 32 + it * RPI + rsub;
+      apf[it] = make_uint4(0, 0, 0, 0);
+      ampf[it] = 0xffu;
+      if (m >= g.M || col >= g.Ncols) continue;
+      const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
+      const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+      const int y = (int)(t - n * (unsigned)g.Hg);
+      const long long o =
+          (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+      apf[it] = *reinterpret_cast<const uint4*>(ADD + o);
+      if (g.addm) ampf[it] = g.addm[o >> 3];
+    }
+  };
+  auto yload = [&](int i, int bsel) __attribute__((always_inline)) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = m0 + wm * TM + i * 32 + it * RPI + rsub;
+      ypf[bsel][it] = make_uint4(0, 0, 0, 0);
+      mpf[bsel][it] = 0u;
+      if (m >= g.M || col >= g.Ncols) continue;
+      const unsigned t = fdiv((unsigned)m, g.wg_mul, g.wg_shr);
+      const int x = (int)((unsigned)m - t * (unsigned)g.Wg);
+      const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+      const int y = (int)(t - n * (unsigned)g.Hg);
+      const long long o =
+          (((long long)n * g.OH + (y * g.osy + g.oy0)) * g.OW + (x * g.osx + g.ox0)) * g.OC + col;
+      ypf[bsel][it] = *reinterpret_cast<const uint4*>(red.y + o);
+      if (red.mask) mpf[bsel][it] = red.mask[o >> 3];
+    }
+  };
+  if constexpr (RED) yload(0, 0);
 #pragma unroll
   for (int i = 0; i < RM; ++i) {
+    if (ADD) aload(i);
+    if constexpr (RED) {
+      if (i + 1 < RM) yload(i + 1, (i + 1) & 1);
+    }
     // stage rows wm*128 + i*32 .. +31 of this wave's columns
 #pragma unroll
     for (int j = 0; j < RN; ++j)
@@ -383,8 +446,8 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
       const float4 v1 = *reinterpret_cast<const float4*>(cs + rr * LDC + cq * 8 + 4);
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
       if (ADD) {
-        const uint4 a = *reinterpret_cast<const uint4*>(ADD + o);
-        const unsigned mb = g.addm ? g.addm[o >> 3] : 0xffu;  // identity-skip ReLU mask
+        const uint4 a = apf[it];
+        const unsigned mb = ampf[it];  // identity-skip ReLU mask
         const uint32_t aw[4] = {a.x, a.y, a.z, a.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -392,8 +455,57 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
           v[2 * q + 1] += ((mb >> (2 * q + 1)) & 1u) ? bf2f((bf16_t)(aw[q] >> 16)) : 0.f;
         }
       }
-      *reinterpret_cast<uint4*>(Y + o) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                                    pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+      const uint4 ov = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
+                                  pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+      *reinterpret_cast<uint4*>(Y + o) = ov;
+      if constexpr (RED) {
+        // dz = the stored gradient where the reduced BN's ReLU passed (1-bit mask, or
+        // y*sc + sh > 0); Σdz and Σdz (y - mu) per channel
+        const uint4 yv = ypf[i & 1][it];
+        const unsigned mb = mpf[i & 1][it];
+        const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w}, ow[4] = {ov.x, ov.y, ov.z, ov.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float yj = __uint_as_float((j & 1) ? (yw[j >> 1] & 0xffff0000u) : (yw[j >> 1] << 16));
+          const float gj = __uint_as_float((j & 1) ? (ow[j >> 1] & 0xffff0000u) : (ow[j >> 1] << 16));
+          const bool pass = red.mask ? ((mb >> j) & 1u) != 0u : yj * rsc[j] + rsh[j] > 0.f;
+          const float dz = pass ? gj : 0.f;
+          rs[j] += dz;
+          rq[j] += dz * (yj - rmu[j]);
+        }
+      }
+    }
+  }
+  if constexpr (RED) {
+    // lanes of one channel chunk (same cq, rsub = lane / CPR) add up, then the WM waves of
+    // one channel range, in LDS past every wave's staging region
+#pragma unroll
+    for (int sft = CPR; sft < 64; sft <<= 1)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        rs[j] += __shfl_xor(rs[j], sft, 64);
+        rq[j] += __shfl_xor(rq[j], sft, 64);
+      }
+    float* rr2 = reinterpret_cast<float*>(smem) + NW * 32 * LDC;  // [WM][BN][2]
+    if (lane < CPR)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = wn * TN + cq * 8 + j;
+        rr2[(wm * BN + c) * 2 + 0] = rs[j];
+        rr2[(wm * BN + c) * 2 + 1] = rq[j];
+      }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      if (n0 + c < g.Ncols) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) {
+          a += rr2[(w * BN + c) * 2 + 0];
+          b += rr2[(w * BN + c) * 2 + 1];
+        }
+        red.part[((long long)bx * 2 + 0) * g.Ncols + n0 + c] = a;
+        red.part[((long long)bx * 2 + 1) * g.Ncols + n0 + c] = b * red.is[n0 + c];
+      }
     }
   }
 }
@@ -401,11 +513,11 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
 template <int BN, int WM, int WN, int MINW>
 void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeomSet& gs, int ng, hipStream_t st, const float* pre_sc,
-                 const float* pre_sh) {
+                 const float* pre_sh, const BnBwdRed* red = nullptr) {
   const ConvGeom& g = gs.g[0];
   constexpr size_t STG = (size_t)PBM * PBK * 2 + (size_t)BN * PBK * 2;
   const size_t sm_main = 2 * STG + (pre_sc ? (size_t)g.C * 8 : 0);
-  constexpr size_t sm_epi = (size_t)WM * WN * 32 * (BN / WN + 4) * 4;
+  const size_t sm_epi = (size_t)WM * WN * 32 * (BN / WN + 4) * 4 + (red ? (size_t)WM * BN * 8 : 0);
   const size_t sm = sm_main > sm_epi ? sm_main : sm_epi;
   long long mmax = 0;
   for (int i = 0; i < ng; ++i) mmax = gs.g[i].M > mmax ? gs.g[i].M : mmax;
@@ -413,24 +525,30 @@ void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   const int ntN = (g.Ncols + BN - 1) / BN;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = pre_sc ? conv_pipe_kernel<BN, WM, WN, MINW, true> : conv_pipe_kernel<BN, WM, WN, MINW, false>;
+  if (red && (pre_sc || ng != 1))
+    throw std::runtime_error("conv_pipe: BN-backward reduction is for one-geometry data gradients");
+  auto k = red ? conv_pipe_kernel<BN, WM, WN, MINW, false, true>
+               : pre_sc ? conv_pipe_kernel<BN, WM, WN, MINW, true> : conv_pipe_kernel<BN, WM, WN, MINW, false>;
+  const BnBwdRed rarg = red ? *red : BnBwdRed{};
   constexpr int NT = WM * WN * 64;
   set_smem_attr(k, sm);
   if (ntN > 1) {
     const unsigned mt8 = (unsigned)((mtiles + 7) / 8 * 8);
     k<<<dim3(mt8 * ntN, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, ntN, mtiles, 1, pre_sc,
-                                           pre_sh);
+                                           pre_sh, rarg);
   } else {
     k<<<dim3((unsigned)mtiles, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, 1, mtiles, 0,
-                                                  pre_sc, pre_sh);
+                                                  pre_sc, pre_sh, rarg);
   }
   DM_CHECK(hipGetLastError());
 }
 
 template <int BN, int WM, int WN, int MINW>
 void launch_pipe1(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                  const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh) {
-  launch_pipe<BN, WM, WN, MINW>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1, st, pre_sc, pre_sh);
+                  const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh,
+                  const BnBwdRed* red) {
+  launch_pipe<BN, WM, WN, MINW>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1, st, pre_sc, pre_sh,
+                                red);
 }
 }  // namespace
 
@@ -447,14 +565,14 @@ bool conv_pipe_supported(const ConvGeom& g, int cfg) {
 
 void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc,
-               const float* pre_sh) {
+               const float* pre_sh, const BnBwdRed* red) {
   // 90: 256 x 256, 8 waves (2 x 4) of 128 x 64; 91: 256 x 128, 8 waves (4 x 2) of 64 x 64;
   // 92: 256 x 128, 4 waves (2 x 2) of 128 x 64; 93: 256 x 64, 4 waves (4 x 1) of 64 x 64,
   // two workgroups per CU (80 KB of LDS each)
-  if (cfg == 90) launch_pipe1<256, 2, 4, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh);
-  else if (cfg == 91) launch_pipe1<128, 4, 2, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh);
-  else if (cfg == 92) launch_pipe1<128, 2, 2, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh);
-  else launch_pipe1<64, 4, 1, 2>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh);
+  if (cfg == 90) launch_pipe1<256, 2, 4, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
+  else if (cfg == 91) launch_pipe1<128, 4, 2, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
+  else if (cfg == 92) launch_pipe1<128, 2, 2, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
+  else launch_pipe1<64, 4, 1, 2>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
 }
 
 // the parity classes of a stride-2 data gradient (no statistics) in one launch

@@ -89,17 +89,6 @@ int stem_wgrad_fused_blocks(int N, int H);
 void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, const uint8_t* pidx,
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st);
-// conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90-93: 256-pixel tiles)
-bool conv_pipe_supported(const ConvGeom& g, int cfg);
-bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
-void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
-               const float* pre_sh = nullptr);
-// conv_res64.hip: persistent register-resident-weight 3x3 conv, 64 -> 64 channels (cfg 80);
-// statistics rows = res64_grid(M) (one per workgroup)
-bool conv_res64_supported(const ConvGeom& g);
-int res64_grid(long long M);
 // The BatchNorm backward reduction of the layer whose output gradient a data gradient
 // produces, done in that dgrad's epilogue: with dz = Y * relu-mask (mask from y*sc + sh > 0,
 // or the 1-bit `mask` when set), part[wg][0][c] = Σ dz and part[wg][1][c] = Σ dz (y - mu) is
@@ -113,6 +102,17 @@ struct BnBwdRed {
   const float* is;
   float* part;
 };
+// conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90-93: 256-pixel tiles)
+bool conv_pipe_supported(const ConvGeom& g, int cfg);
+bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
+void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
+               const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
+               const float* pre_sh = nullptr, const BnBwdRed* red = nullptr);
+// conv_res64.hip: persistent register-resident-weight 3x3 conv, 64 -> 64 channels (cfg 80);
+// statistics rows = res64_grid(M) (one per workgroup)
+bool conv_res64_supported(const ConvGeom& g);
+int res64_grid(long long M);
 void conv_res64(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                 const ConvGeom& g, hipStream_t st, const float* pre_sc = nullptr,
                 const float* pre_sh = nullptr, const BnBwdRed* red = nullptr);

@@ -244,8 +244,14 @@ class BasicBlock(Layer):
         dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True, fused_skip=need_dx,
                                        red_for=(self.c1, ctx["c1"]))
         if self.down is None:
-            # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass)
-            return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None)
+            # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass), and
+            # that dgrad's output is the previous block's output gradient: its c2 BN-backward
+            # sums reduce there too (Program sets _bwd_next to the preceding layer)
+            nxt = getattr(self, "_bwd_next", None)
+            red_for = ((nxt[0].c2, nxt[1]["c2"]) if nxt is not None and isinstance(nxt[0], BasicBlock)
+                       else None)
+            return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None,
+                                      red_for=red_for)
         dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
         # projection skip: its dgrad (one parity class of the 1x1/s2 conv) accumulates in place
         self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx)

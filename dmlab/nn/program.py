@@ -184,8 +184,14 @@ class _ProgramFn(torch.autograd.Function):
             for i in range(n - 1, -1, -1):
                 layer = prog.layers[i]
                 need_dx = i > 0 or ctx.need_dx
-                with _range(f"bwd:{i}:{type(layer).__name__}"):
-                    dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
+                # the layer whose output gradient this one produces (its backward runs next):
+                # layers may fold that layer's BN-backward reduction into their last kernel
+                layer._bwd_next = (prog.layers[i - 1], ctx.ctxs[i - 1]) if i > 0 else None
+                try:
+                    with _range(f"bwd:{i}:{type(layer).__name__}"):
+                        dy = layer.bwd(dy, ctx.ctxs[i], need_dx)
+                finally:
+                    layer._bwd_next = None
                 ctx.ctxs[i] = None  # free saved activations as soon as possible
                 if side is None:
                     for hook in prog._grad_hooks:

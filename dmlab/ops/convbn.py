@@ -347,20 +347,35 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def _dgrad_red(L, red_for, cfg, dx_add, dx):
+def _dgrad_red(L, red_for, cfg, stride, dx_add, dx):
     """conv_dgrad kwargs that reduce the consumer BN's backward sums in the dgrad epilogue
-    (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify."""
+    (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify.
+
+    cfg 80 (layer1) handles a plain ReLU consumer (mask from y*scale + shift > 0) and no
+    residual add; the pipelined tiles (90-93) also take the residual block's 1-bit mask and
+    the fused identity-skip add (the consumer's output gradient is dgrad + skip)."""
     rl, rctx = red_for
-    if (_NO_DGRAD_RED or cfg != 80 or dx_add is not None or not rl.relu or rctx.get("has_res")
+    pipe = 90 <= cfg <= 93
+    if (_NO_DGRAD_RED or stride != 1 or not (cfg == 80 or pipe) or not rl.relu
             or getattr(rl, "pool_k", 0) or rctx.get("mean") is None
             or rctx.get("pre_sums") is not None or tuple(rctx["y"].shape) != tuple(dx.shape)):
+        return {}
+    mask = None
+    if rctx.get("has_res"):
+        mask = rctx.get("mask")
+        if mask is None or not pipe:
+            return {}
+    elif cfg == 80 and dx_add is not None:
         return {}
     N, H, W, C = dx.shape
     rows = L.conv_stats_rows(N * H * W, cfg, C)
     part = torch.empty(rows * 2 * C, device=dx.device, dtype=torch.float32)
     rctx["pre_sums"] = dict(pre_slab=part, pre_rows=rows)
-    return dict(red_y=rctx["y"], red_scale=rctx["scale"], red_shift=rctx["shift"],
-                red_mean=rctx["mean"], red_invstd=rctx["invstd"], red_part=part)
+    kw = dict(red_y=rctx["y"], red_scale=rctx["scale"], red_shift=rctx["shift"],
+              red_mean=rctx["mean"], red_invstd=rctx["invstd"], red_part=part)
+    if mask is not None:
+        kw["red_mask"] = mask
+    return kw
 
 
 def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
@@ -476,13 +491,11 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            red_kw = _dgrad_red(L, red_for, cfg, dx_add, dx) if red_for is not None else {}
-            if red_kw:
-                L.conv_dgrad(dy, wd, dx, k, k, s, p, None, cfg, **red_kw)
-            elif isinstance(dx_add, tuple):
-                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2])
+            red_kw = _dgrad_red(L, red_for, cfg, s, dx_add, dx) if red_for is not None else {}
+            if isinstance(dx_add, tuple):
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2], **red_kw)
             else:
-                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg)
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **red_kw)
     if ctx["has_res"]:
         return dx, (("masked", dout, ctx["mask"]) if masked_res else dres)
     return dx

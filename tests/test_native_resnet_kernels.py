@@ -681,3 +681,53 @@ def test_conv_dgrad_bn_reduce(dev, geom):
     want = torch.stack([dz.sum((0, 1, 2)), (dz * (yf - mu.double())).sum((0, 1, 2)) * inv.double()])
     got = part.view(rows, 2, Cin).double().sum(0)
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4 * float(want.abs().max()))
+
+
+@pytest.mark.parametrize("geom,cfg", [((2, 14, 256, 256, 3, 1, 1), 90), ((3, 7, 512, 512, 3, 1, 1), 90),
+                                      ((2, 28, 128, 128, 3, 1, 1), 91), ((2, 28, 128, 128, 3, 1, 1), 92),
+                                      ((2, 14, 64, 64, 3, 1, 1), 93)])
+@pytest.mark.parametrize("masked", [False, True])
+def test_conv_dgrad_bn_reduce_pipe(dev, geom, cfg, masked):
+    """Pipelined data gradient (cfg 90-93) with the consumer BN's backward reduction in its
+    store loop: ReLU mask from y*scale + shift (a block's inner BN), or the residual block's
+    1-bit mask together with the fused identity-skip add (the previous block's output BN).
+    dx is bit-identical to the plain dgrad; the rows add up to Σdz, Σdz·x̂ (float64 torch)."""
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p, seed=31)
+    g = torch.Generator(device=dev).manual_seed(32)
+    dy = _nhwc(torch.randn(N, Cout, H, H, device=dev, generator=g).bfloat16())
+    kw, keep_add = {}, None
+    if masked:
+        add = torch.randn(N, H, H, Cin, device=dev, generator=g).bfloat16()
+        keep_add = torch.rand(N, H, H, Cin, device=dev, generator=g) > 0.4
+        kw = dict(add=add, add_mask=_bits(keep_add))
+    ref = torch.empty(N, H, H, Cin, device=dev, dtype=torch.bfloat16)
+    lib().conv_dgrad(dy, wd, ref, k, k, s, p, kw.get("add"), cfg, add_mask=kw.get("add_mask"))
+    yb = (torch.randn(N, H, H, Cin, device=dev, generator=g) * 2 + 0.3).bfloat16()
+    sc = torch.rand(Cin, device=dev, generator=g) + 0.5
+    sh = torch.randn(Cin, device=dev, generator=g) * 0.5
+    mu = torch.randn(Cin, device=dev, generator=g) * 0.2
+    inv = torch.rand(Cin, device=dev, generator=g) + 0.5
+    rows = lib().conv_stats_rows(N * H * H, cfg, Cin)
+    part = torch.full((rows * 2 * Cin,), float("nan"), device=dev)
+    out = torch.empty_like(ref)
+    if masked:
+        keep = torch.rand(N, H, H, Cin, device=dev, generator=g) > 0.5
+        kw["red_mask"] = _bits(keep)
+    else:
+        keep = yb.float() * sc + sh > 0
+    lib().conv_dgrad(dy, wd, out, k, k, s, p, kw.get("add"), cfg, add_mask=kw.get("add_mask"),
+                     red_y=yb, red_scale=sc, red_shift=sh, red_mean=mu, red_invstd=inv,
+                     red_part=part, red_mask=kw.get("red_mask"))
+    assert torch.equal(out, ref)
+    yf = yb.double()
+    dz = torch.where(keep, ref.double(), torch.zeros((), device=dev, dtype=torch.float64))
+    want = torch.stack([dz.sum((0, 1, 2)), (dz * (yf - mu.double())).sum((0, 1, 2)) * inv.double()])
+    got = part.view(rows, 2, Cin).double().sum(0)
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4 * float(want.abs().max()))
+
+
+def _bits(keep):
+    """1-bit mask layout of the kernels: bit j of byte i = element 8i + j (NHWC order)."""
+    b = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, device=keep.device, dtype=torch.uint8)
+    return b.sum(1, dtype=torch.uint8)

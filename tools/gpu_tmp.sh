@@ -1,19 +1,21 @@
-# Ad-hoc GPU step (overwritten per experiment): host run-ahead bound (Program.max_inflight)
-# vs throughput and reserved device memory.
+# Ad-hoc GPU step (overwritten per experiment): BN-backward reduction in the dgrad epilogues,
+# longer interleaved A/B and both step traces.
 set -o pipefail
 tag=${1:-tmp}
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-for i in 1 2; do
-for K in 2 1 4 0; do
-DMLAB_MAX_INFLIGHT=$K timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_k${K}_$tag.json 2>> gpurun_out/bench_$tag.err || exit 1
+for i in 1 2 3 4 5; do
+timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_$tag.json 2>> gpurun_out/bench_$tag.err || exit 1
+DMLAB_NO_DGRAD_RED=1 timeout -k 10 200 python bench.py --steps 20 --warmup 5 >> gpurun_out/bench_nored_$tag.json 2>> gpurun_out/bench_nored_$tag.err || exit 1
 done
-done
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_$tag -o tr -- \
+    python bench.py --steps 4 --warmup 2 > gpurun_out/trace_$tag.log 2>&1 || exit 1
+DMLAB_NO_DGRAD_RED=1 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/trace_nored_$tag -o tr -- \
+    python bench.py --steps 4 --warmup 2 > gpurun_out/trace_nored_$tag.log 2>&1 || exit 1
 python - "$tag" <<'PY'
 import json, sys
 t = sys.argv[1]
-for K in (2, 1, 4, 0):
-    for l in open(f"gpurun_out/bench_k{K}_{t}.json"):
-        d = json.loads(l)
-        print(K, d["value"], d["peak_mem_gb"], d["peak_alloc_gb"], d["alloc_retries"])
+for f in (f"gpurun_out/bench_{t}.json", f"gpurun_out/bench_nored_{t}.json"):
+    v = [json.loads(l)["value"] for l in open(f)]
+    print(f, [round(x) for x in v], round(sum(v) / len(v)))
 PY
