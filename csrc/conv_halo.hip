@@ -29,6 +29,8 @@
 #include "igemm_common.h"
 #include "kernels.h"
 
+#include <stdexcept>
+
 namespace dm {
 
 namespace {
@@ -47,12 +49,14 @@ constexpr unsigned OOB = 0x80000000u;
 #ifndef DM_HALO39_MINB
 #define DM_HALO39_MINB 4
 #endif
-template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF>
+// RED: the data gradient's epilogue also reduces the consumer BatchNorm's backward sums
+// (mfma_tile_epilogue RED)
+template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF, bool RED = false>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_HALO39_MINB : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh,
-    int xcd, int mtiles) {
+    int xcd, int mtiles, BnBwdRed red) {
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
   // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
   // image taps still read the zero row, i.e. the padding stays zero AFTER the BN.
@@ -295,7 +299,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       if (s + 1 < S) step(s + 1, rb, rb2);
     }
   }
-  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128>(acc, smem, m0, n0, bx, stats, g, Y, ADD);
+  mfma_tile_epilogue<BMH, BN, WM, WN, true, BMH / 128, RED>(acc, smem, m0, n0, bx, stats, g, Y, ADD,
+                                                           red);
 }
 
 int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
@@ -303,9 +308,10 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
   return ((g.W - 1 + bm - 1) / g.W + 3) * g.W;
 }
 
-template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1>
+template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1, bool RED = false>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st) {
+                 const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
+                 const BnBwdRed* red = nullptr) {
   constexpr int RPP = WM * WN * 8;
   const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
@@ -313,8 +319,10 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   const unsigned mt = (unsigned)((g.M + BMH - 1) / BMH), nt = (g.Ncols + BN - 1) / BN;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
+  auto k = RED ? conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF, RED>
+         : pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
                   : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
+  const BnBwdRed rarg = red ? *red : BnBwdRed{};
   set_smem_attr(k, sm);
   // XCD-aware 1-D grid over the M tiles (padded to a multiple of 8) x N tiles: the N tiles of
   // one M tile share an XCD's L2.  Measured (tools/bench_conv.py, batch 512): layer3 fwd
@@ -322,11 +330,11 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   if (nt > 1) {
     const unsigned mt8 = (mt + 7) / 8 * 8;
     k<<<dim3(mt8 * nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
-                                                (int)nt, (int)mt);
+                                                (int)nt, (int)mt, rarg);
     return;
   }
   k<<<dim3(mt, nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
-                                            0, (int)mt);
+                                            0, (int)mt, rarg);
 }
 }  // namespace
 
@@ -347,8 +355,19 @@ bool conv_halo_supported(const ConvGeom& g) {
 // 64 x 32 (cfg 39); 32 = 256 px as 4 x 1 waves of 64 x 64 (cfg 41)
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
-               const float* pre_sh) {
+               const float* pre_sh, const BnBwdRed* red) {
   const int hp = halo_rows_needed(g), hp2 = halo_rows_needed(g, 256);
+  if (red) {
+    // the BN-backward reduction epilogue is built for the cfg 42 tile (layer2's data gradient)
+    if (waves != (4 | 0x100) || bn != 128 || pre_sc)
+      throw std::runtime_error("conv_halo: BN-backward reduction needs cfg 42, no PRE input");
+    const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
+    if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2, true>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red);
+    else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2, true>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red);
+    else launch_halo<128, 12, 2, 2, HBM, 2, true>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red);
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   if (waves == (4 | 0x100) && bn == 128) {
     const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
     if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);

@@ -2,6 +2,7 @@
 #pragma once
 #include "common.h"
 #include "conv_geom.h"
+#include "kernels.h"
 
 #include <type_traits>
 
@@ -88,11 +89,15 @@ using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 //    output pixel (y*osy+oy0, x*osx+ox0), optionally adding ADD (which may alias Y).
 // Rows >= g.M must hold zeros when stats are requested.  Requires (BM/PASSES)*(BN+4)*4 B of
 // LDS: with PASSES > 1 the tile is staged one band of BM/PASSES rows (whole wave rows) at a time.
-template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1>
+// RED (data gradients, kernels.h BnBwdRed): the backward reduction of the BatchNorm whose
+// output gradient Y is, from the stored bf16 values and that BN's input y (prefetched with
+// the ADD chunks): one [2][Ncols] row per stat_row in red.part.
+template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1, bool RED = false>
 __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / WM / (MF32 ? 32 : 16)][BN / WN / (MF32 ? 32 : 16)],
                                                    unsigned char* smem, long long m0, int n0,
                                                    int stat_row, float* stats, const ConvGeom& g,
-                                                   bf16_t* Y, const bf16_t* ADD) {
+                                                   bf16_t* Y, const bf16_t* ADD,
+                                                   const BnBwdRed& red = BnBwdRed{}) {
   float* fstats = stats;  // Σy, Σy² of the fp32 tile
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = MF32 ? 32 : 16;
@@ -103,7 +108,7 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
   const int wm = wid / WN, wn = wid % WN;
   auto frow = [&](int r) { return MF32 ? (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5) : (lane >> 4) * 4 + r; };
   const int fcol = MF32 ? (lane & 31) : (lane & 15);
-  float* red = reinterpret_cast<float*>(smem);
+  float* sred = reinterpret_cast<float*>(smem);
   if (fstats) {
 #pragma unroll
     for (int j = 0; j < RN; ++j) {
@@ -124,8 +129,8 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       q += __shfl_xor(q, 32, 64);
       if (lane < FM) {
         const int c = wn * TN + j * FM + lane;
-        red[(wm * BN + c) * 2 + 0] = sm;
-        red[(wm * BN + c) * 2 + 1] = q;
+        sred[(wm * BN + c) * 2 + 0] = sm;
+        sred[(wm * BN + c) * 2 + 1] = q;
       }
     }
     __syncthreads();
@@ -133,8 +138,8 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       float sm = 0.f, q = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) {
-        sm += red[(w * BN + c) * 2 + 0];
-        q += red[(w * BN + c) * 2 + 1];
+        sm += sred[(w * BN + c) * 2 + 0];
+        q += sred[(w * BN + c) * 2 + 1];
       }
       if (n0 + c < g.Ncols) {
         fstats[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = sm;
@@ -200,6 +205,8 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
     bool ok[NLD];
     uint4 av[NLD];
     unsigned mb[NLD];
+    uint4 yv[RED ? NLD : 1];
+    unsigned ym[RED ? NLD : 1];
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {
       row_off(k / ITERS, (tid + (k % ITERS) * NT) / CPR, o[k], ok[k]);
@@ -208,6 +215,26 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       if (ADD && ok[k]) {
         av[k] = *reinterpret_cast<const uint4*>(ADD + o[k]);
         if (g.addm) mb[k] = g.addm[o[k] >> 3];
+      }
+      if constexpr (RED) {
+        yv[k] = make_uint4(0, 0, 0, 0);
+        ym[k] = 0u;
+        if (ok[k]) {
+          yv[k] = *reinterpret_cast<const uint4*>(red.y + o[k]);
+          if (red.mask) ym[k] = red.mask[o[k] >> 3];
+        }
+      }
+    }
+    // RED: this thread's 8 channels are fixed (col); Σdz, Σdz (y - mu) accumulate in registers
+    float rs[8], rq[8], rsc[8], rsh[8], rmu[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      rs[j] = rq[j] = 0.f;
+      if constexpr (RED) {
+        const int c = col + j < g.Ncols ? col + j : 0;
+        rsc[j] = red.mask ? 0.f : red.sc[c];
+        rsh[j] = red.mask ? 0.f : red.sh[c];
+        rmu[j] = red.mu[c];
       }
     }
 #pragma unroll
@@ -219,8 +246,52 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
         if (!ok[k]) continue;
         float v[8];
         tile_vals((tid + i * NT) / CPR, av[k], mb[k], v);
-        *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
-                                                         pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+        const uint32_t ow[4] = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]),
+                                pack_bf2(v[6], v[7])};
+        *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        if constexpr (RED) {
+          const uint32_t yw[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float yj = __uint_as_float((j & 1) ? (yw[j >> 1] & 0xffff0000u) : (yw[j >> 1] << 16));
+            const float gj = __uint_as_float((j & 1) ? (ow[j >> 1] & 0xffff0000u) : (ow[j >> 1] << 16));
+            const bool pass = red.mask ? ((ym[k] >> j) & 1u) != 0u : yj * rsc[j] + rsh[j] > 0.f;
+            const float dz = pass ? gj : 0.f;
+            rs[j] += dz;
+            rq[j] += dz * (yj - rmu[j]);
+          }
+        }
+      }
+    }
+    if constexpr (RED) {
+      // threads of one channel group (tid % CPR) add up: lanes by shuffle, waves in LDS
+#pragma unroll
+      for (int sft = CPR; sft < 64; sft <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          rs[j] += __shfl_xor(rs[j], sft, 64);
+          rq[j] += __shfl_xor(rq[j], sft, 64);
+        }
+      __syncthreads();  // staging reads done: the LDS is reused below
+      float* rr2 = reinterpret_cast<float*>(smem);  // [NT/64][BN][2]
+      if (lane < CPR)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          rr2[(wid * BN + cc * 8 + j) * 2 + 0] = rs[j];
+          rr2[(wid * BN + cc * 8 + j) * 2 + 1] = rq[j];
+        }
+      __syncthreads();
+      for (int c = tid; c < BN; c += NT) {
+        if (n0 + c < g.Ncols) {
+          float a = 0.f, b = 0.f;
+#pragma unroll
+          for (int w = 0; w < NT / 64; ++w) {
+            a += rr2[(w * BN + c) * 2 + 0];
+            b += rr2[(w * BN + c) * 2 + 1];
+          }
+          red.part[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = a;
+          red.part[((long long)stat_row * 2 + 1) * g.Ncols + n0 + c] = b * red.is[n0 + c];
+        }
       }
     }
   }

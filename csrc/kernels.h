@@ -120,7 +120,8 @@ bool conv_halo_supported(const ConvGeom& g);
 bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,
-               const float* pre_sc = nullptr, const float* pre_sh = nullptr);
+               const float* pre_sc = nullptr, const float* pre_sh = nullptr,
+               const BnBwdRed* red = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
 // wgrad_res64.hip: row-streaming 64 -> 64 channel 3x3 weight gradient (wgrad cfg 8); S slabs
 bool wgrad_res64_supported(const ConvGeom& g);

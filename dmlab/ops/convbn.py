@@ -352,18 +352,19 @@ def _dgrad_red(L, red_for, cfg, stride, dx_add, dx):
     (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify.
 
     cfg 80 (layer1) handles a plain ReLU consumer (mask from y*scale + shift > 0) and no
-    residual add; the pipelined tiles (90-93) also take the residual block's 1-bit mask and
-    the fused identity-skip add (the consumer's output gradient is dgrad + skip)."""
+    residual add; the pipelined tiles (90-93, layers 3-4) and the cfg 42 halo tile (layer2)
+    also take the residual block's 1-bit mask and the fused identity-skip add (the
+    consumer's output gradient is dgrad + skip)."""
     rl, rctx = red_for
-    pipe = 90 <= cfg <= 93
-    if (_NO_DGRAD_RED or stride != 1 or not (cfg == 80 or pipe) or not rl.relu
+    tile = 90 <= cfg <= 93 or cfg == 42  # mask + add capable
+    if (_NO_DGRAD_RED or stride != 1 or not (cfg == 80 or tile) or not rl.relu
             or getattr(rl, "pool_k", 0) or rctx.get("mean") is None
             or rctx.get("pre_sums") is not None or tuple(rctx["y"].shape) != tuple(dx.shape)):
         return {}
     mask = None
     if rctx.get("has_res"):
         mask = rctx.get("mask")
-        if mask is None or not pipe:
+        if mask is None or not tile:
             return {}
     elif cfg == 80 and dx_add is not None:
         return {}
