@@ -168,8 +168,8 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       const bool pipe = cfg >= 90 && cfg <= 93 && dm::conv_pipe_supported(g, (int)cfg);
       int hbn = 0, hwv = 0;
       const bool halo = cfg == 42 && dm::halo_cfg((int)cfg, hbn, hwv) && dm::conv_halo_supported(g);
-      TORCH_CHECK((cfg == 80 && !addp) || pipe || halo,
-                  "red_*: a cfg 80 data gradient without add, a pipelined (90-93) or a cfg 42 one");
+      TORCH_CHECK(cfg == 80 || pipe || halo,
+                  "red_*: a cfg 80, pipelined (90-93) or cfg 42 data gradient");
       need_bf16_nhwc(*red_y, "red_y");
       TORCH_CHECK(red_y->sizes() == dx.sizes(), "red_y: dx's shape");
       TORCH_CHECK(red_scale && red_shift && red_mean && red_invstd && red_part,
@@ -181,7 +181,6 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       need_f32(*red_part, "red_part", conv_stats_rows(g.M, cfg, Cin) * 2 * Cin);
       const unsigned char* rmask = nullptr;
       if (red_mask.has_value()) {
-        TORCH_CHECK(pipe || halo, "red_mask: pipelined (90-93) or cfg 42 data gradients only");
         TORCH_CHECK(red_mask->is_cuda() && red_mask->scalar_type() == at::kByte &&
                         red_mask->is_contiguous() && red_mask->numel() * 8 >= dx.numel(),
                     "red_mask: uint8 [numel/8] on the device");
@@ -194,7 +193,7 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       else if (halo)
         dm::conv_halo(bp(dy), bp(wd), bp(dx), addp, nullptr, g, hbn, hwv, st, nullptr, nullptr, &red);
       else
-        dm::conv_res64(bp(dy), bp(wd), bp(dx), nullptr, nullptr, g, st, nullptr, nullptr, &red);
+        dm::conv_res64(bp(dy), bp(wd), bp(dx), addp, nullptr, g, st, nullptr, nullptr, &red);
       return;
     }
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);

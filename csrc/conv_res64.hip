@@ -60,7 +60,8 @@ constexpr int R_SMEM = R_EPI + 4 * 32 * R_LDC * 4;
 constexpr int R_RTAB = R_SMEM;
 constexpr int R_RACC = R_RTAB + 3 * RC * 4;
 constexpr int R_Y = R_RACC + RNT * 2 * 4;
-constexpr int R_SMEM_RED = R_Y + RT * RC * 2;
+constexpr int R_MK = R_Y + RT * RC * 2;  // the tile's 1-bit ReLU mask (8 B per pixel)
+constexpr int R_SMEM_RED = R_MK + RT * 8;
 typedef unsigned v4u32_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int div9(int s) { return (s * 7282) >> 16; }  // exact for s < 3584
@@ -146,7 +147,10 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
   // RED: y of tile tt -> R_Y; LDS piece s = (j*4 + wid)*64 + lane is channel half s >> 9,
   // pixel (s >> 2) & 127, 16-B chunk s & 3 (rows past M read zero)
   const pi32x4 rsr = prsrc(RED ? (const void*)red.y : (const void*)X, ybytes);
+  const pi32x4 rsm = prsrc(RED && red.mask ? (const void*)red.mask : (const void*)X, ybytes >> 4);
   auto ydma = [&](int tt) __attribute__((always_inline)) {
+    // the 1-bit mask of the tile's 128 pixels is 1 KB: one instruction of wave 0
+    if (red.mask && wid == 0) pdma16(rsm, lds0 + (unsigned)R_MK, (unsigned)tt * (RT * 8u) + lane * 16u);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const unsigned s = (unsigned)(j * 4 + wid) * 64u + opq((unsigned)lane);
@@ -267,8 +271,10 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
     // re-read per tile through a laundered address (kept out of the register budget)
     float rsc = 0.f, rsh = 0.f, rmu = 0.f, rs = 0.f, rq = 0.f;
     const unsigned char* ybase = smem;
+    const unsigned char* mbase = smem;
     if constexpr (RED) {
       ybase = smem + opq((unsigned)(R_Y + wn * 8192 + (wm * 64 + 4 * hsel) * 64 + l32 * 2));
+      mbase = smem + opq((unsigned)(R_MK + (wm * 64 + 4 * hsel) * 8 + wn * 4 + (l32 >> 3)));
       const float* rt = reinterpret_cast<const float*>(smem + opq((unsigned)(R_RTAB + (wn * 32 + l32) * 4)));
       rsc = rt[0];
       rsh = rt[RC];
@@ -279,19 +285,9 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float v = acc[i][r];
-        ssum += v;
-        ssq += v * v;
-        if constexpr (RED) {
-          // dz = the stored (bf16) gradient where the reduced BN's ReLU passed
-          const int pr = i * 32 + (r & 3) + 8 * (r >> 2);  // + wm*64 + 4*hsel in ybase
-          const float yj = __uint_as_float(
-              (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
-          const float gj = __uint_as_float(pack_bf2(v, 0.f) << 16);
-          const float dz = yj * rsc + rsh > 0.f ? gj : 0.f;
-          rs += dz;
-          rq += dz * (yj - rmu);
-          // bound the y reads in flight (the scheduler would hoist all 32 into registers)
-          if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!RED) {  // (data gradients have no statistics)
+          ssum += v;
+          ssq += v * v;
         }
         cs[((r & 3) + 8 * (r >> 2) + 4 * hsel) * R_LDC + l32] = v;
       }
@@ -304,7 +300,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         const float4 v0 = *reinterpret_cast<const float4*>(cs + rr * R_LDC + cq * 8);
         const float4 v1 = *reinterpret_cast<const float4*>(cs + rr * R_LDC + cq * 8 + 4);
         float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-        if (!RED && ADD) {  // (RED variant: no residual input, which frees its registers)
+        if (ADD) {
           const auto a = __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0);
           // identity-skip ReLU mask: one byte per 16-B chunk (byte offset / 16)
           const unsigned mb = (g.addm && off != ROOB) ? g.addm[off >> 4] : 0xffu;
@@ -317,6 +313,33 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         const v4u32_t o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]),
                            pack_bf2(v[6], v[7])};
         __builtin_amdgcn_raw_buffer_store_b128(o, rsy, off, 0, 0);
+        if (RED && ADD) {  // the band keeps the stored values for the reduction below
+          *reinterpret_cast<float4*>(cs + rr * R_LDC + cq * 8) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(cs + rr * R_LDC + cq * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+      if constexpr (RED) {
+        // dz = the stored (bf16) gradient where the reduced BN's ReLU passed, read back from
+        // the band in the MFMA layout (this lane's channel is its column)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = (r & 3) + 8 * (r >> 2) + 4 * hsel;
+          const int pr = i * 32 + (r & 3) + 8 * (r >> 2);  // + wm*64 + 4*hsel in ybase
+          const float v = cs[row * R_LDC + l32];
+          const float yj = __uint_as_float(
+              (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
+          const float gj = __uint_as_float(pack_bf2(v, 0.f) << 16);
+          bool pass;
+          if (red.mask)
+            pass = (mbase[pr * 8] >> (l32 & 7)) & 1u;
+          else
+            pass = yj * rsc + rsh > 0.f;
+          const float dz = pass ? gj : 0.f;
+          rs += dz;
+          rq += dz * (yj - rmu);
+          // bound the LDS reads in flight (the scheduler would hoist all of them)
+          if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
     if constexpr (RED) {
@@ -353,7 +376,7 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
       red.part[(long long)b * 2 * RC + RC + tid] = q * red.is[tid];
     }
   }
-  if (stats) {
+  if (!RED && stats) {
     ssum += __shfl_xor(ssum, 32, 64);
     ssq += __shfl_xor(ssq, 32, 64);
     __syncthreads();  // staging bands free
@@ -410,10 +433,10 @@ void conv_res64(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
   const unsigned bytes = (unsigned)(g.M * RC * 2);
   const int ntiles = (int)((g.M + RT - 1) / RT);
   if (red) {
-    if (pre_sc || ADD || red->mask || !red->y || !red->sc || !red->sh || !red->mu || !red->is ||
+    if (pre_sc || !red->y || !red->sc || !red->sh || !red->mu || !red->is ||
         !red->part)
       throw std::runtime_error("conv_res64: BN-backward reduction needs y, sc, sh, mu, is, part "
-                               "(ReLU mask from y; no PRE or ADD input)");
+                               "(no PRE input)");
     set_smem_attr(conv_res64_kernel<false, true>, R_SMEM_RED);
     conv_res64_kernel<false, true><<<grid, RNT, R_SMEM_RED, st>>>(
         X, Wp, Y, ADD, stats, g, bytes, bytes, pre_sc, pre_sh, ntiles, *red);

@@ -248,8 +248,11 @@ class BasicBlock(Layer):
             # that dgrad's output is the previous block's output gradient: its c2 BN-backward
             # sums reduce there too (Program sets _bwd_next to the preceding layer)
             nxt = getattr(self, "_bwd_next", None)
-            red_for = ((nxt[0].c2, nxt[1]["c2"]) if nxt is not None and isinstance(nxt[0], BasicBlock)
-                       else None)
+            red_for = None
+            if nxt is not None and isinstance(nxt[0], BasicBlock):
+                red_for = (nxt[0].c2, nxt[1]["c2"])
+            elif nxt is not None and isinstance(nxt[0], ConvBN):  # the stem
+                red_for = nxt
             return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None,
                                       red_for=red_for)
         dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)

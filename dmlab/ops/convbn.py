@@ -347,32 +347,35 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def _dgrad_red(L, red_for, cfg, stride, dx_add, dx):
+def _dgrad_red(L, red_for, cfg, stride, dx):
     """conv_dgrad kwargs that reduce the consumer BN's backward sums in the dgrad epilogue
     (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify.
 
-    cfg 80 (layer1) handles a plain ReLU consumer (mask from y*scale + shift > 0) and no
-    residual add; the pipelined tiles (90-93, layers 3-4) and the cfg 42 halo tile (layer2)
-    also take the residual block's 1-bit mask and the fused identity-skip add (the
-    consumer's output gradient is dgrad + skip)."""
+    cfg 80 (layer1), the pipelined tiles (90-93, layers 3-4) and the cfg 42 halo tile
+    (layer2) take a plain ReLU consumer (mask from y*scale + shift > 0), the residual
+    block's 1-bit mask, and the fused identity-skip add (the consumer's output gradient is
+    dgrad + skip).  The stem (BN + ReLU + max-pool) reduces over the pooled grid: y is its
+    value at each window's argmax (ctx["yarg"]), as bn_bwd_reduce_masked does."""
     rl, rctx = red_for
-    tile = 90 <= cfg <= 93 or cfg == 42  # mask + add capable
-    if (_NO_DGRAD_RED or stride != 1 or not (cfg == 80 or tile) or not rl.relu
-            or getattr(rl, "pool_k", 0) or rctx.get("mean") is None
-            or rctx.get("pre_sums") is not None or tuple(rctx["y"].shape) != tuple(dx.shape)):
+    kernel_ok = cfg == 80 or 90 <= cfg <= 93 or cfg == 42
+    pool = getattr(rl, "pool_k", 0)
+    y = rctx.get("yarg") if pool else rctx.get("y")
+    if (_NO_DGRAD_RED or stride != 1 or not kernel_ok or not rl.relu or y is None
+            or rctx.get("mean") is None or rctx.get("pre_sums") is not None
+            or tuple(y.shape) != tuple(dx.shape)):
         return {}
     mask = None
     if rctx.get("has_res"):
         mask = rctx.get("mask")
-        if mask is None or not tile:
+        if mask is None:
             return {}
-    elif cfg == 80 and dx_add is not None:
+    if cfg == 80 and (mask is not None or pool) and os.environ.get("DMLAB_NO_RES64_ADD_RED") == "1":
         return {}
     N, H, W, C = dx.shape
     rows = L.conv_stats_rows(N * H * W, cfg, C)
     part = torch.empty(rows * 2 * C, device=dx.device, dtype=torch.float32)
     rctx["pre_sums"] = dict(pre_slab=part, pre_rows=rows)
-    kw = dict(red_y=rctx["y"], red_scale=rctx["scale"], red_shift=rctx["shift"],
+    kw = dict(red_y=y, red_scale=rctx["scale"], red_shift=rctx["shift"],
               red_mean=rctx["mean"], red_invstd=rctx["invstd"], red_part=part)
     if mask is not None:
         kw["red_mask"] = mask
@@ -412,7 +415,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
     pre_sums = ctx.pop("pre_sums", None) or {}
     pool = getattr(layer, "pool_k", 0)
-    if pool and ctx.get("yarg") is not None:
+    if pool and ctx.get("yarg") is not None and not pre_sums:
         # stem: Σdz, Σdz·x̂ over the pooled grid (pooled grad masked at the argmax, x̂ from
         # y at the argmax) -- reads 2 pooled-size tensors instead of y + grad + codes
         Mp = ctx["yarg"].numel() // cout
@@ -492,7 +495,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            red_kw = _dgrad_red(L, red_for, cfg, s, dx_add, dx) if red_for is not None else {}
+            red_kw = _dgrad_red(L, red_for, cfg, s, dx) if red_for is not None else {}
             if isinstance(dx_add, tuple):
                 L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2], **red_kw)
             else:

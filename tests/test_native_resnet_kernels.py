@@ -683,14 +683,15 @@ def test_conv_dgrad_bn_reduce(dev, geom):
     torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-4 * float(want.abs().max()))
 
 
-@pytest.mark.parametrize("geom,cfg", [((2, 14, 256, 256, 3, 1, 1), 90), ((3, 7, 512, 512, 3, 1, 1), 90),
+@pytest.mark.parametrize("geom,cfg", [(RES64_GEOMS[0], 80), (RES64_GEOMS[2], 80), (RES64_GEOMS[4], 80),
+                                      ((2, 14, 256, 256, 3, 1, 1), 90), ((3, 7, 512, 512, 3, 1, 1), 90),
                                       ((2, 28, 128, 128, 3, 1, 1), 91), ((2, 28, 128, 128, 3, 1, 1), 92),
                                       ((2, 14, 64, 64, 3, 1, 1), 93),
                                       ((2, 28, 128, 128, 3, 1, 1), 42), ((3, 14, 256, 256, 3, 1, 1), 42)])
 @pytest.mark.parametrize("masked", [False, True])
 def test_conv_dgrad_bn_reduce_pipe(dev, geom, cfg, masked):
-    """Pipelined (cfg 90-93) or cfg 42 halo data gradient with the consumer BN's backward
-    reduction in its store loop: ReLU mask from y*scale + shift (a block's inner BN), or the residual block's
+    """res64 (cfg 80), pipelined (cfg 90-93) or cfg 42 halo data gradient with the consumer
+    BN's backward reduction in its epilogue: ReLU mask from y*scale + shift (a block's inner BN), or the residual block's
     1-bit mask together with the fused identity-skip add (the previous block's output BN).
     dx is bit-identical to the plain dgrad; the rows add up to Σdz, Σdz·x̂ (float64 torch)."""
     N, H, Cin, Cout, k, s, p = geom
