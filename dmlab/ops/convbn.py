@@ -369,7 +369,11 @@ def _dgrad_red(L, red_for, cfg, stride, dx):
         mask = rctx.get("mask")
         if mask is None:
             return {}
-    if cfg == 80 and (mask is not None or pool) and os.environ.get("DMLAB_NO_RES64_ADD_RED") == "1":
+    # layer1's identity-block dgrads (res64 with the fused skip add, reducing the previous
+    # block's or the stem's BN): correct (tests) but 0.3% slower per step -- the add/mask
+    # epilogue costs the kernel ~100 us, more than the contended pass it saves
+    # (profiles/dgrad_bn_reduce_ab_r3s3.txt, red9); opt in with DMLAB_RES64_ADD_RED=1
+    if cfg == 80 and (mask is not None or pool) and os.environ.get("DMLAB_RES64_ADD_RED") != "1":
         return {}
     N, H, W, C = dx.shape
     rows = L.conv_stats_rows(N * H * W, cfg, C)
