@@ -119,7 +119,7 @@ def _cu_count():
     return _CUS[d]
 
 
-def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0):
+def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=False):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
     cfg 8: row-streaming 64 -> 64 channel 3x3 kernel (csrc/wgrad_res64.hip; ``W`` = image
@@ -135,7 +135,12 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0):
         # 5/8 of the CUs: the kernel runs on the side stream next to the dgrad + BN-backward
         # chain, and leaving that chain CUs of its own is 0.8% faster per step than one
         # workgroup on every CU (128-192 of 256 tie; profiles/wgrad_res64_slabs_ab_r3s3.txt)
-        S = int(os.environ.get("DMLAB_WRES64_S", 0)) or max(1, _cu_count() * 5 // 8)
+        # ``tail``: the last conv before the stem, whose weight gradient runs next to the stem's
+        # fused BN-backward + weight-gradient kernel at the end of the step, not next to a
+        # dgrad chain: there it takes every CU
+        S = int(os.environ.get("DMLAB_WRES64_S", 0)) or (
+            _cu_count() if tail and os.environ.get("DMLAB_TAIL_WGRAD_FULL", "1") == "1"
+            else max(1, _cu_count() * 5 // 8))
         return 8, max(1, min(rows, S))
     if force is not None:
         cfg = force
@@ -454,7 +459,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     C = x.shape[3]
     K = k * k * C
     same = not s2d and (OH, OW) == tuple(x.shape[1:3])
-    wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0)
+    # red_for is the stem (a pooled ConvBN) only for the first block's c1: the step's last conv
+    tail = red_for is not None and bool(getattr(red_for[0], "pool_k", 0))
+    wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
+                          tail=tail)
     dy = empty_nhwc(N, OH, OW, cout, y)
     masked_res = (fused_skip and ctx["has_res"] and mode == 4 and not _NO_FUSED_SKIP)
     dres = empty_nhwc(N, OH, OW, cout, y) if (ctx["has_res"] and not masked_res) else None
