@@ -10,6 +10,8 @@
 // branch gradient dz when the block has a skip connection.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace dm {
 
 __device__ __forceinline__ void unpack8(const uint4& v, float f[8]) {
@@ -1131,7 +1133,13 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                                                                     (double)M, fb);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
-  const int grid = grid_for(n8, 256, 4096);
+  // DMLAB_BN_BWD_GRID: workgroup cap of the apply pass (A/B runs; default 4096)
+  static const int cap = [] {
+    const char* e = std::getenv("DMLAB_BN_BWD_GRID");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? v : 4096;
+  }();
+  const int grid = grid_for(n8, 256, cap);
   const size_t sh = sizeof(float) * 5 * C;
 #define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
   if (quad) {
