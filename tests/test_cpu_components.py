@@ -347,3 +347,48 @@ def test_wgrad_res64_plan():
     assert _wgrad_plan(1024 * 56 * 56, 64, 576, 3, 1, 64)[0] != 8           # width unknown
     assert _wgrad_plan(4 * 112 * 112, 64, 576, 3, 1, 64, W=112, rows=448)[0] != 8
     assert _wgrad_plan(1024 * 28 * 28, 128, 1152, 3, 1, 128, W=28, rows=1024 * 28)[0] != 8
+
+
+def test_dgrad_red_selection():
+    """Which data gradients reduce the consumer BN's backward sums in their epilogue
+    (ops/convbn.py _dgrad_red): cfg 80 / 90-93 / 42, stride 1, a ReLU consumer of dx's shape;
+    the residual block's 1-bit mask rides along; layer1's masked case (cfg 80 + mask, or the
+    stem's pooled grid) is opt-in; the consumer's ctx receives the partial-sum slab."""
+    from types import SimpleNamespace as NS
+    import torch
+    from dmlab.ops import convbn as CB
+
+    L = NS(conv_stats_rows=lambda M, cfg, C: 7)
+    dx = torch.zeros(2, 4, 4, 64)
+
+    def ctx(has_res=False, mask=False, pool=False):
+        c = dict(y=torch.zeros(2, 4, 4, 64), mean=torch.zeros(64), invstd=torch.ones(64),
+                 scale=torch.ones(64), shift=torch.zeros(64), has_res=has_res)
+        if mask:
+            c["mask"] = torch.zeros(2 * 4 * 4 * 64 // 8, dtype=torch.uint8)
+        if pool:
+            c["yarg"] = torch.zeros(2, 4, 4, 64)
+            c["y"] = torch.zeros(2, 8, 8, 64)
+        return c
+
+    relu, stem = NS(relu=True), NS(relu=True, pool_k=3)
+    c = ctx()
+    kw = CB._dgrad_red(L, (relu, c), 80, 1, dx)
+    assert kw["red_y"] is c["y"] and "red_mask" not in kw and kw["red_part"].numel() == 7 * 2 * 64
+    assert c["pre_sums"]["pre_rows"] == 7 and c["pre_sums"]["pre_slab"] is kw["red_part"]
+    assert CB._dgrad_red(L, (relu, c), 80, 1, dx) == {}            # sums already planned
+    assert CB._dgrad_red(L, (relu, ctx()), 80, 2, dx) == {}        # stride-2 dgrad
+    assert CB._dgrad_red(L, (relu, ctx()), 39, 1, dx) == {}        # kernel without the epilogue
+    assert CB._dgrad_red(L, (NS(relu=False), ctx()), 90, 1, dx) == {}
+    assert CB._dgrad_red(L, (relu, ctx()), 90, 1, torch.zeros(2, 4, 4, 128)) == {}
+    assert CB._dgrad_red(L, (relu, ctx(has_res=True)), 90, 1, dx) == {}   # no 1-bit mask
+    c = ctx(has_res=True, mask=True)
+    assert CB._dgrad_red(L, (relu, c), 42, 1, dx)["red_mask"] is c["mask"]
+    assert CB._dgrad_red(L, (relu, ctx(has_res=True, mask=True)), 80, 1, dx) == {}
+    assert CB._dgrad_red(L, (stem, ctx(pool=True)), 80, 1, dx) == {}
+    os.environ["DMLAB_RES64_ADD_RED"] = "1"
+    try:
+        c = ctx(pool=True)
+        assert CB._dgrad_red(L, (stem, c), 80, 1, dx)["red_y"] is c["yarg"]
+    finally:
+        del os.environ["DMLAB_RES64_ADD_RED"]
