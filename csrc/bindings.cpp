@@ -317,14 +317,29 @@ void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w
                       at::Tensor cslab, at::Tensor rowloss, at::Tensor grad,
                       std::vector<int64_t> off, c10::optional<at::Tensor> p,
                       c10::optional<at::Tensor> mom, double lr, double momentum, double dampening,
-                      double wd, double gscale, bool nesterov, bool first, at::Tensor loss) {
+                      double wd, double gscale, bool nesterov, bool first, at::Tensor loss,
+                      c10::optional<at::Tensor> sidx, c10::optional<at::Tensor> cursor,
+                      int64_t batch, c10::optional<at::Tensor> loss_sum) {
   CHECK_CUDA(x); CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28,
               "x: [B, 1, 28, 28]");
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "x: fp32 or bf16");
-  const int B = (int)x.size(0);
+  // sidx given: x / labels are the whole device-resident dataset; this step's samples are rows
+  // sidx[cursor*batch : (cursor+1)*batch] (sampler order), the cursor advancing on the device
+  const bool indexed = sidx.has_value() && sidx->defined();
+  const int B = indexed ? (int)batch : (int)x.size(0);
+  int nbatch = 0;
+  if (indexed) {
+    CHECK_CUDA(*sidx); CHECK_CONTIG(*sidx);
+    TORCH_CHECK(sidx->scalar_type() == at::kLong && batch >= 1, "sidx: int64 row indices");
+    TORCH_CHECK(cursor.has_value() && cursor->is_cuda() && cursor->scalar_type() == at::kInt &&
+                    cursor->numel() == 1, "cursor: int32 [1] on the device");
+    nbatch = (int)(sidx->numel() / batch);
+    TORCH_CHECK(nbatch >= 1, "sidx holds fewer than one batch");
+    TORCH_CHECK(labels.numel() == x.size(0), "labels: one per dataset row");
+  }
   TORCH_CHECK(B >= 1 && labels.is_cuda() && labels.scalar_type() == at::kLong &&
-                  labels.is_contiguous() && labels.numel() == B, "labels: int64 [B]");
+                  labels.is_contiguous() && (indexed || labels.numel() == B), "labels: int64 [B]");
   TORCH_CHECK(w.size() == 8 && off.size() == 8, "8 parameter tensors / offsets");
   const int64_t want[8] = {150, 6, 2400, 16, 48000, 120, 1200, 10};
   const float* wp[8];
@@ -355,13 +370,22 @@ void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w
       mp = mom->data_ptr<float>();
     }
   }
+  float* lsum = nullptr;
+  if (loss_sum.has_value() && loss_sum->defined()) {
+    CHECK_CUDA(*loss_sum); CHECK_F32(*loss_sum);
+    TORCH_CHECK(loss_sum->numel() == 1, "loss_sum: fp32 [1] on the device");
+    lsum = loss_sum->data_ptr<float>();
+  }
   const DeviceGuard guard(x.device());
   dm::lenet_fused_step(x.data_ptr(), x.scalar_type() == at::kBFloat16,
                        reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()),
                        B, wp, rec.data_ptr<float>(), cslab.data_ptr<float>(),
                        rowloss.data_ptr<float>(), grad.data_ptr<float>(), o, pp, mp, (float)lr,
                        (float)momentum, (float)dampening, (float)wd, (float)gscale, nesterov,
-                       first, pp != nullptr, loss.data_ptr<float>(), cur_stream());
+                       first, pp != nullptr, loss.data_ptr<float>(),
+                       indexed ? reinterpret_cast<const long long*>(sidx->data_ptr<int64_t>()) : nullptr,
+                       indexed ? cursor->data_ptr<int>() : nullptr, x.size(0), nbatch, lsum,
+                       cur_stream());
 }
 
 int num_cus(int device) {
@@ -407,7 +431,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cross_entropy", &cross_entropy);
   m.def("argmax_count", &argmax_count);
   m.def("spin_us", &spin_us);
-  m.def("lenet_fused_step", &lenet_fused_step, "one fused LeNet training step (2 dispatches)");
+  m.def("lenet_fused_step", &lenet_fused_step, "one fused LeNet training step (2 dispatches)",
+        py::arg("x"), py::arg("labels"), py::arg("w"), py::arg("rec"), py::arg("cslab"),
+        py::arg("rowloss"), py::arg("grad"), py::arg("off"), py::arg("p"), py::arg("mom"),
+        py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"),
+        py::arg("gscale"), py::arg("nesterov"), py::arg("first"), py::arg("loss"),
+        py::arg("sidx") = py::none(), py::arg("cursor") = py::none(), py::arg("batch") = 0,
+        py::arg("loss_sum") = py::none());
   m.def("lenet_record_floats", &dm::lenet_record_floats);
   m.def("lenet_slab_floats", &dm::lenet_slab_floats);
   m.attr("arch") = "gfx950";

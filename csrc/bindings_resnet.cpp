@@ -291,17 +291,27 @@ void pack_weights_s2d(at::Tensor w, at::Tensor wf) {
   dm::pack_weights_s2d(fp(w), bp(wf), Cout, C, Cp, cur_stream());
 }
 
-void pack_input_s2d(at::Tensor x, at::Tensor y) {
+// idx (optional, int64 [y.size(0)] on the device): y's image n is x's row idx[n] -- the
+// device-resident loader's batch gather fused into the packing pass (x = the whole dataset)
+void pack_input_s2d(at::Tensor x, at::Tensor y, c10::optional<at::Tensor> idx) {
   TORCH_CHECK(x.is_cuda() && x.dim() == 4);
   TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16);
   need_bf16_nhwc(y, "y");
   TORCH_CHECK(x.size(2) % 2 == 0 && x.size(3) % 2 == 0, "s2d needs even H, W");
-  TORCH_CHECK(y.size(0) == x.size(0) && y.size(1) * 2 == x.size(2) && y.size(2) * 2 == x.size(3) &&
-              y.size(3) >= 4 * x.size(1));
+  const bool gather = idx.has_value() && idx->defined();
+  if (gather) {
+    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == at::kLong && idx->is_contiguous() &&
+                    idx->numel() == y.size(0), "idx: int64 [N] row indices on the device");
+  } else {
+    TORCH_CHECK(y.size(0) == x.size(0));
+  }
+  TORCH_CHECK(y.size(1) * 2 == x.size(2) && y.size(2) * 2 == x.size(3) && y.size(3) >= 4 * x.size(1));
   const DeviceGuard guard(x.device());
-  dm::pack_input_s2d(x.data_ptr(), x.scalar_type() == at::kBFloat16, bp(y), x.size(0), x.size(1),
+  dm::pack_input_s2d(x.data_ptr(), x.scalar_type() == at::kBFloat16, bp(y), y.size(0), x.size(1),
                      y.size(1), y.size(2), y.size(3), x.stride(0), x.stride(1), x.stride(2),
-                     x.stride(3), cur_stream());
+                     x.stride(3),
+                     gather ? reinterpret_cast<const long long*>(idx->data_ptr<int64_t>()) : nullptr,
+                     x.size(0), cur_stream());
 }
 
 void pack_weights(at::Tensor w, at::Tensor wf, c10::optional<at::Tensor> wd, int64_t Cpad) {
@@ -675,6 +685,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("pack_input", &pack_input);
-  m.def("pack_input_s2d", &pack_input_s2d);
+  m.def("pack_input_s2d", &pack_input_s2d, py::arg("x"), py::arg("y"),
+        py::arg("idx") = py::none());
   m.def("pack_weights_s2d", &pack_weights_s2d);
 }

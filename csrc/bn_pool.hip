@@ -955,12 +955,22 @@ __global__ void __launch_bounds__(256) pack_input_kernel(const T* __restrict__ x
 // channel (dy*2+dx)*C + c holding x[n, c, 2i+dy, 2j+dx]; the stem then runs as a
 // 4x4/s1 conv over 4C (<= Cp) channels: K = 16*16 = 256 instead of 49*8 = 392
 // (padded to 448), and every tap is one contiguous 32-B channel vector.
+// idx (optional): output image n is source row idx[n] of a device-resident dataset (the
+// data loader's gather fused into the packing pass; clamped to [0, nsrc)).
+__device__ __forceinline__ long long s2d_src_row(const long long* idx, long long n, long long nsrc) {
+  if (idx == nullptr) return n;
+  const long long r = idx[n];
+  return r < 0 ? 0 : (r >= nsrc ? nsrc - 1 : r);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) pack_input_s2d_kernel(const T* __restrict__ x,
                                                              bf16_t* __restrict__ y, int N, int C,
                                                              int H2, int W2, int Cp, long long sn,
                                                              long long sc, long long sh,
-                                                             long long sw) {
+                                                             long long sw,
+                                                             const long long* __restrict__ idx,
+                                                             long long nsrc) {
   const long long total = (long long)N * H2 * W2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
@@ -976,7 +986,7 @@ __global__ void __launch_bounds__(256) pack_input_s2d_kernel(const T* __restrict
         const int sub = ch / C, c = ch % C;
         if (sub < 4) {
           const int dy = sub >> 1, dx = sub & 1;
-          const T v = x[n * sn + c * sc + (2 * r + dy) * sh + (2 * j + dx) * sw];
+          const T v = x[s2d_src_row(idx, n, nsrc) * sn + c * sc + (2 * r + dy) * sh + (2 * j + dx) * sw];
           if constexpr (sizeof(T) == 4) f[q] = v;
           else f[q] = bf2f(v);
         } else {
@@ -995,7 +1005,9 @@ __global__ void __launch_bounds__(256) pack_input_s2d_kernel(const T* __restrict
 // of bf16 stores, instead of 24 scalar loads.
 __global__ void __launch_bounds__(256) pack_input_s2d_cl3_kernel(const float* __restrict__ x,
                                                                  bf16_t* __restrict__ y, int N,
-                                                                 int H2, int W2, long long sn) {
+                                                                 int H2, int W2, long long sn,
+                                                                 const long long* __restrict__ idx,
+                                                                 long long nsrc) {
   const int Q = W2 >> 1;
   const long long total = (long long)N * H2 * Q;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -1005,7 +1017,7 @@ __global__ void __launch_bounds__(256) pack_input_s2d_cl3_kernel(const float* __
     const long long t = i / Q;
     const int r = (int)(t % H2);
     const int n = (int)(t / H2);
-    const float* a = x + n * sn + (long long)(2 * r) * rowf + 12LL * q;
+    const float* a = x + s2d_src_row(idx, n, nsrc) * sn + (long long)(2 * r) * rowf + 12LL * q;
     float A[12], B[12];
 #pragma unroll
     for (int v = 0; v < 3; ++v) {
@@ -1030,20 +1042,21 @@ __global__ void __launch_bounds__(256) pack_input_s2d_cl3_kernel(const float* __
 
 // ------------------------------------------------------------------ launchers
 void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, int W2, int Cp,
-                    long long sn, long long sc, long long sh, long long sw, hipStream_t st) {
+                    long long sn, long long sc, long long sh, long long sw, const long long* idx,
+                    long long nsrc, hipStream_t st) {
   const long long total = (long long)N * H2 * W2;
   if (!bf16 && C == 3 && Cp == 16 && sc == 1 && sw == 3 && sh == 3LL * 2 * W2 && W2 % 2 == 0 &&
       ((uintptr_t)x & 15) == 0 && sn % 4 == 0) {
     pack_input_s2d_cl3_kernel<<<grid_for(total / 2, 256, 8192), 256, 0, st>>>(
-        (const float*)x, y, N, H2, W2, sn);
+        (const float*)x, y, N, H2, W2, sn, idx, nsrc);
     return;
   }
   if (bf16)
     pack_input_s2d_kernel<bf16_t><<<grid_for(total, 256, 8192), 256, 0, st>>>(
-        (const bf16_t*)x, y, N, C, H2, W2, Cp, sn, sc, sh, sw);
+        (const bf16_t*)x, y, N, C, H2, W2, Cp, sn, sc, sh, sw, idx, nsrc);
   else
     pack_input_s2d_kernel<float><<<grid_for(total, 256, 8192), 256, 0, st>>>(
-        (const float*)x, y, N, C, H2, W2, Cp, sn, sc, sh, sw);
+        (const float*)x, y, N, C, H2, W2, Cp, sn, sc, sh, sw, idx, nsrc);
 }
 
 void bn_stats_finalize(const float* stats, int T, int C, double count, const float* gamma,

@@ -54,7 +54,8 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
                       const float* const* w, float* rec, float* cslab, float* rowloss, float* grad,
                       const int* off, float* p, float* mom, float lr, float momentum,
                       float dampening, float wd, float gscale, bool nesterov, bool first,
-                      bool do_sgd, float* loss, hipStream_t st);
+                      bool do_sgd, float* loss, const long long* sidx, int* cursor,
+                      long long nrows, int nbatch, float* loss_sum, hipStream_t st);
 }  // namespace dm
 
 namespace dm {
@@ -174,7 +175,8 @@ void avgpool_bwd(const bf16_t* dy, bf16_t* dx, int N, int HW, int C, hipStream_t
 void pack_input(const void* x, bool bf16, bf16_t* y, int N, int C, int H, int W, int Cp,
                 long long sn, long long sc, long long sh, long long sw, hipStream_t st);
 void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, int W2, int Cp,
-                    long long sn, long long sc, long long sh, long long sw, hipStream_t st);
+                    long long sn, long long sc, long long sh, long long sw, const long long* idx,
+                    long long nsrc, hipStream_t st);
 void pack_weights_s2d(const float* w, bf16_t* wf, int Cout, int C, int Cp, hipStream_t st);
 void wgrad_reduce_s2d(const float* slab, int S, int Cout, int C, int Cp, float* dw, float beta,
                       hipStream_t st);

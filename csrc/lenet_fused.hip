@@ -47,8 +47,17 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     const float* __restrict__ c1w, const float* __restrict__ c1b, const float* __restrict__ c2w,
     const float* __restrict__ c2b, const float* __restrict__ f1w, const float* __restrict__ f1b,
     const float* __restrict__ f2w, const float* __restrict__ f2b, float* __restrict__ rec,
-    float* __restrict__ cslab, float* __restrict__ rowloss, float inv_b) {
+    float* __restrict__ cslab, float* __restrict__ rowloss, float inv_b,
+    const long long* __restrict__ sidx, const int* __restrict__ cursor, long long nrows) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // device-resident loader: sample b of this step is dataset row sidx[cursor * B + b] (the
+  // epoch's sampler order, uploaded once per epoch; the cursor advances on the device in the
+  // gradient kernel, so a captured graph walks the epoch); clamped, never out of bounds
+  long long row = b;
+  if (sidx != nullptr) {
+    const long long r = sidx[(long long)(*cursor) * gridDim.x + b];
+    row = r < 0 ? 0 : (r >= nrows ? nrows - 1 : r);
+  }
   __shared__ float xs[32 * 32];            // input with the conv1 zero padding (2)
   __shared__ float w1[152], bb1[8], w2[2400], bb2[16], fw2[1200], fb2[16];
   __shared__ float p1[6 * 196];            // relu(conv1) max-pooled
@@ -63,7 +72,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   // ---- stage input and the small weights (fc1's 192 KB stream from L2 instead) ----
   for (int i = tid; i < 1024; i += LT) {
     const int y = (i >> 5) - 2, x = (i & 31) - 2;
-    xs[i] = ((unsigned)y < 28u && (unsigned)x < 28u) ? ldx<XT>(X + (long long)b * 784 + y * 28 + x)
+    xs[i] = ((unsigned)y < 28u && (unsigned)x < 28u) ? ldx<XT>(X + row * 784 + y * 28 + x)
                                                      : 0.f;
   }
   for (int i = tid; i < 2400; i += LT) w2[i] = c2w[i];
@@ -172,7 +181,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     const float mx = wave_max(z);
     const float e = lane < 10 ? __expf(z - mx) : 0.f;
     const float se = wave_sum(e);
-    const int lab = (int)labels[b];
+    const int lab = (int)labels[row];
     const float zl = __shfl(z, lab, 64);
     if (lane < 10) dl[lane] = (e / se - (lane == lab ? 1.f : 0.f)) * inv_b;
     if (lane == 0) rowloss[b] = mx + __logf(se) - zl;
@@ -319,13 +328,19 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
     const float* __restrict__ rec, const float* __restrict__ cslab, int B, float* __restrict__ grad,
     LenetFlat fl, float* __restrict__ p, float* __restrict__ mom, float lr, float momentum,
     float dampening, float wd, float gscale, int nesterov, int first, int do_sgd,
-    const float* __restrict__ rowloss, float* __restrict__ loss) {
+    const float* __restrict__ rowloss, float* __restrict__ loss, int* __restrict__ cursor,
+    int nbatch, float* __restrict__ loss_sum) {
   int i = blockIdx.x * 256 + threadIdx.x;
   if (blockIdx.x == 0 && threadIdx.x < 64) {  // mean loss, fixed order
     float a = 0.f;
     for (int j = threadIdx.x; j < B; j += 64) a += rowloss[j];
     a = wave_sum(a);
-    if (threadIdx.x == 0) *loss = a / (float)B;
+    if (threadIdx.x == 0) {
+      *loss = a / (float)B;
+      if (loss_sum != nullptr) *loss_sum += a / (float)B;  // device-side running sum (logging)
+      // next batch of the epoch (the sample kernel that read the cursor has finished)
+      if (cursor != nullptr) *cursor = (*cursor + 1 >= nbatch) ? 0 : *cursor + 1;
+    }
   }
   int seg = 0;
   while (seg < 8 && i >= seg_n(seg)) {
@@ -373,14 +388,17 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
                       const float* const* w, float* rec, float* cslab, float* rowloss, float* grad,
                       const int* off, float* p, float* mom, float lr, float momentum,
                       float dampening, float wd, float gscale, bool nesterov, bool first,
-                      bool do_sgd, float* loss, hipStream_t st) {
+                      bool do_sgd, float* loss, const long long* sidx, int* cursor,
+                      long long nrows, int nbatch, float* loss_sum, hipStream_t st) {
   const float inv_b = 1.f / (float)B;
   if (x_bf16)
     lenet_sample_kernel<bf16_t><<<B, LT, 0, st>>>((const bf16_t*)x, labels, w[0], w[1], w[2], w[3],
-                                                  w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b);
+                                                  w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b,
+                                                  sidx, cursor, nrows);
   else
     lenet_sample_kernel<float><<<B, LT, 0, st>>>((const float*)x, labels, w[0], w[1], w[2], w[3],
-                                                 w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b);
+                                                 w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b,
+                                                 sidx, cursor, nrows);
   DM_CHECK(hipGetLastError());
   LenetFlat fl;
   for (int j = 0; j < 8; ++j) fl.off[j] = off[j];
@@ -388,7 +406,9 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
   lenet_grad_kernel<<<(total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
                                                          momentum, dampening, wd, gscale,
                                                          nesterov ? 1 : 0, first ? 1 : 0,
-                                                         do_sgd ? 1 : 0, rowloss, loss);
+                                                         do_sgd ? 1 : 0, rowloss, loss,
+                                                         sidx != nullptr ? cursor : nullptr,
+                                                         nbatch, loss_sum);
   DM_CHECK(hipGetLastError());
 }
 

@@ -146,7 +146,8 @@ class Reducer {
     // collected at interpreter shutdown
     auto pg = pg_.lock();
     TORCH_CHECK(pg, "Reducer: the process group was destroyed");
-    if (pg->getSize() <= 1) return;
+    // a 1-rank group is launched too: DDP builds the reducer at world size 1 only when
+    // communication is forced (the RCCL path exercised on a single GPU)
     at::Tensor view = buf_.slice(0, buckets_[b].lo, buckets_[b].hi);
     if (!small_fn_.is_none() && !comm_dtype_ && view.numel() <= small_cap_) {
       small_fn_(view, avg_scale_);  // one stream-ordered kernel, scale in its epilogue

@@ -9,7 +9,58 @@ list, which is itself uploaded once per epoch.
 """
 from __future__ import annotations
 
+from typing import NamedTuple
+
 import torch
+
+
+class Gathered(NamedTuple):
+    """A batch named by row indices into a device-resident dataset, not yet gathered.
+
+    A consumer that can fuse the gather into its first pass takes it as is (the ResNet stem's
+    space-to-depth packing reads ``images[idx[n]]`` directly: the batch is never copied);
+    every other consumer calls :meth:`materialize` (one ``index_select``)."""
+
+    images: torch.Tensor
+    idx: torch.Tensor
+
+    @property
+    def shape(self):
+        return (self.idx.numel(),) + tuple(self.images.shape[1:])
+
+    @property
+    def device(self):
+        return self.images.device
+
+    @property
+    def is_cuda(self):
+        return self.images.is_cuda
+
+    def materialize(self) -> torch.Tensor:
+        return self.images.index_select(0, self.idx)
+
+
+class DeviceCursor:
+    """The epoch's sampler order resident on the device plus a device-side batch cursor.
+
+    For steps captured into a hipGraph: the graph reads batch ``cursor`` of ``order`` and
+    advances the cursor itself (no per-step host work, not even an index copy).  ``refill``
+    uploads the next epoch's order into the SAME buffer (captured pointers stay valid) and
+    rewinds the cursor."""
+
+    def __init__(self, loader: "DeviceLoader"):
+        self.loader = loader
+        bs = loader.batch_size
+        self.nbatch = len(loader.sampler if loader.sampler is not None else loader.dataset) // bs  # whole batches only (drop_last): a fixed batch shape
+        if self.nbatch < 1:
+            raise ValueError("the sampler's shard holds fewer than one batch")
+        self.order = loader._device_indices()[: self.nbatch * bs].contiguous()
+        self.cursor = torch.zeros(1, dtype=torch.int32, device=loader.device)
+
+    def refill(self, epoch: int):
+        self.loader.set_epoch(epoch)
+        self.order.copy_(self.loader._device_indices()[: self.order.numel()])
+        self.cursor.zero_()
 
 
 class DeviceLoader:
@@ -40,14 +91,40 @@ class DeviceLoader:
             return torch.randperm(n, generator=g)
         return torch.arange(n)
 
+    def _device_indices(self) -> torch.Tensor:
+        """The epoch's index list on the loader's device.  Uploaded from pinned memory without
+        blocking: a pageable copy would synchronise the stream once per epoch and drain the
+        host's run-ahead of the GPU."""
+        idx = self._indices()
+        if self.device.type == "cuda":
+            return idx.pin_memory().to(self.device, non_blocking=True)
+        return idx.to(self.device)
+
     def __len__(self):
         n = len(self.sampler) if self.sampler is not None else len(self.dataset)
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
-        idx = self._indices().to(self.device)
+        idx = self._device_indices()
         n = idx.numel()
         bs = self.batch_size
         stop = (n // bs) * bs if self.drop_last else n
         for s in range(0, stop, bs):
             yield self.dataset.batch(idx[s: s + bs])
+
+    def iter_gathered(self):
+        """Like iteration, but yields ``(Gathered(images, idx), labels)``: the image gather is
+        left to the consumer (fused into the ResNet stem's input packing); labels are
+        gathered (B int64)."""
+        idx = self._device_indices()
+        n = idx.numel()
+        bs = self.batch_size
+        stop = (n // bs) * bs if self.drop_last else n
+        im, lb = self.dataset.images, self.dataset.labels
+        for s in range(0, stop, bs):
+            sl = idx[s: s + bs]
+            yield Gathered(im, sl), lb.index_select(0, sl)
+
+    def cursor(self) -> DeviceCursor:
+        """Device-resident epoch order + cursor, for hipGraph-captured steps."""
+        return DeviceCursor(self)

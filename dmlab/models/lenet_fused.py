@@ -36,6 +36,9 @@ class FusedLeNetStep:
                         net.fc1.weight, net.fc1.bias, net.fc2.weight, net.fc2.bias]
         self._ws = {}
         self.loss = torch.zeros((), device=flat.device, dtype=torch.float32)
+        # running sum of the step losses, accumulated on the device by the gradient kernel
+        # (a training loop reads it every `log_every` steps without a per-step sync)
+        self.loss_sum = torch.zeros(1, device=flat.device, dtype=torch.float32)
 
     def _workspace(self, B):
         w = self._ws.get(B)
@@ -55,28 +58,37 @@ class FusedLeNetStep:
 
         opt = self.opt
         return (isinstance(opt, SGD) and opt.flat is self.net.flat and
-                (self.ddp is None or self.ddp.ws <= 1))
+                (self.ddp is None or not self.ddp.comm_active))
 
-    def __call__(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def __call__(self, x: torch.Tensor, y: torch.Tensor, cursor=None) -> torch.Tensor:
+        """One step on batch (x, y); or, with ``cursor`` (:class:`dmlab.data.DeviceCursor`),
+        on the cursor's next batch of the device-resident dataset ``(x, y)`` = (all images,
+        all labels): the sample kernel gathers its rows through the epoch order and the
+        gradient kernel advances the cursor, so a captured graph walks the epoch."""
         if not x.is_cuda or self.net.backend == "torch":
+            if cursor is not None:
+                raise ValueError("the device cursor needs the native GPU step")
             return self._autograd_step(x, y)
         from dmlab.ops._native import lib
 
         flat = self.net.flat
-        rec, slab, rowloss = self._workspace(x.shape[0])
+        B = cursor.loader.batch_size if cursor is not None else x.shape[0]
+        rec, slab, rowloss = self._workspace(B)
         x = x.contiguous()
+        ix = {} if cursor is None else dict(sidx=cursor.order, cursor=cursor.cursor, batch=B)
+        ix["loss_sum"] = self.loss_sum
         if self._fused_sgd():
             opt = self.opt
             opt.step_count += 1
             lib().lenet_fused_step(x, y, self.weights, rec, slab, rowloss, flat.grad, self.offsets,
                                    flat.data, opt.buf, opt.lr, opt.momentum, opt.dampening,
                                    opt.weight_decay, opt.grad_scale, opt.nesterov,
-                                   opt.step_count == 1, self.loss)
+                                   opt.step_count == 1, self.loss, **ix)
             flat.mark_updated()
             flat.mark_grads_consumed()
             return self.loss
         lib().lenet_fused_step(x, y, self.weights, rec, slab, rowloss, flat.grad, self.offsets,
-                               None, None, 0.0, 0.0, 0.0, 0.0, 1.0, False, False, self.loss)
+                               None, None, 0.0, 0.0, 0.0, 0.0, 1.0, False, False, self.loss, **ix)
         flat.grad_valid = True
         if self.ddp is not None:
             self.ddp.reduce_now()

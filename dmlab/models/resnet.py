@@ -20,6 +20,9 @@ from dmlab.nn.program import Program
 
 
 class ResNet18(Program):
+    # the s2d stem packing gathers a loader batch by index itself (no batch copy)
+    accepts_gathered = True
+
     def __init__(self, num_classes: int = 1000, in_channels: int = 3,
                  widths=(64, 128, 256, 512)):
         super().__init__()

@@ -143,7 +143,7 @@ class _ProgramFn(torch.autograd.Function):
             ctxs.append(c)
         ctx.prog = prog
         ctx.ctxs = ctxs
-        ctx.need_dx = x.requires_grad
+        ctx.need_dx = isinstance(x, torch.Tensor) and x.requires_grad
         return h
 
     @staticmethod
@@ -320,7 +320,7 @@ class Program(nn.Module):
     def _use_native(self, t: torch.Tensor) -> bool:
         if self.backend == "torch":
             return False
-        if t.is_cuda:
+        if t.is_cuda:  # a tensor, or a not-yet-gathered loader batch (dmlab.data.Gathered)
             return True
         if self.backend == "native":
             raise RuntimeError("native backend requested for a CPU tensor")
@@ -350,7 +350,14 @@ class Program(nn.Module):
         return [self._param_index[id(p)] for p in self.layers[i].parameters()]
 
     # ---------------------------------------------------------------- execution
+    # the first layer's native forward reads a dmlab.data.Gathered batch straight from the
+    # dataset (subclasses whose stem fuses the loader gather set this)
+    accepts_gathered = False
+
     def forward(self, x):
+        if not isinstance(x, torch.Tensor) and hasattr(x, "materialize"):
+            if not (self.accepts_gathered and self._use_native(x)):
+                x = x.materialize()
         self._native_active = self._use_native(x)
         if self._inflight and not torch.cuda.is_current_stream_capturing():
             while len(self._inflight) >= max(1, self.max_inflight):

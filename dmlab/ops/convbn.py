@@ -264,13 +264,21 @@ def _materialise(x, pre):
 
 def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     L = lib()
+    gidx = None
+    if not isinstance(x, torch.Tensor):  # dmlab.data.Gathered: a loader batch by row index
+        if use_s2d(layer, x.images) and x.images.dtype in (torch.float32, torch.bfloat16):
+            x, gidx = x.images, x.idx  # the s2d packing below gathers the rows itself
+        else:
+            x = x.materialize()
     first = not (x.dim() == 4 and getattr(x, "_dm_nhwc", False))
     s2d = first and use_s2d(layer, x)
     if s2d:
         # stem as a 4x4/s1 conv over the space-to-depth input (pad 2 top/left, 1 bottom/right)
         Nn, Cc, Hh, Ww = x.shape
+        if gidx is not None:
+            Nn = gidx.numel()
         xs = empty_nhwc(Nn, Hh // 2, Ww // 2, _cpad(4 * Cc), x)
-        L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs)
+        L.pack_input_s2d(x if x.dtype in (torch.float32, torch.bfloat16) else x.float(), xs, gidx)
         x = xs
         k, s, p = 4, 1, 2
         OH, OW = Hh // 2, Ww // 2

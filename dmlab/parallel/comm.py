@@ -113,10 +113,11 @@ def get_world_size():
 
 
 @torch.no_grad()
-def init_parameters(model, src: int = 0, buffers: bool = True):
+def init_parameters(model, src: int = 0, buffers: bool = True, force: bool = False):
     """Broadcast rank-``src`` parameters (and BN buffers) to every rank in ONE
-    collective over the flat buffer (reference: one broadcast per tensor)."""
-    if env.get_world_size() <= 1:
+    collective over the flat buffer (reference: one broadcast per tensor).  ``force``:
+    broadcast through an initialised 1-rank group too (exercises the collective path)."""
+    if env.get_world_size() <= 1 and not (force and env.is_initialized()):
         return
     flat = _flat_of_model(model)
     if flat is not None:
@@ -138,9 +139,10 @@ def init_parameters(model, src: int = 0, buffers: bool = True):
 
 
 @torch.no_grad()
-def allreduce_average_gradients(model, granularity: str = "flat", average: bool = True):
+def allreduce_average_gradients(model, granularity: str = "flat", average: bool = True,
+                                force: bool = False):
     ws = env.get_world_size()
-    if ws <= 1:
+    if ws <= 1 and not (force and env.is_initialized()):
         return
     flat = _flat_of_model(model)
     if granularity == "per_param":
@@ -171,10 +173,10 @@ average_gradients = allreduce_average_gradients
 
 
 @torch.no_grad()
-def allgather_average_gradients(model, granularity: str = "flat"):
+def allgather_average_gradients(model, granularity: str = "flat", force: bool = False):
     """Correct all-gather mean for any world size (fixes SURVEY B1)."""
     ws = env.get_world_size()
-    if ws <= 1:
+    if ws <= 1 and not (force and env.is_initialized()):
         return
     flat = _flat_of_model(model)
     if granularity == "per_param":
@@ -246,11 +248,14 @@ class GradAggregator:
     On the CPU (gloo) the collectives are synchronous and wall time is exact."""
 
     def __init__(self, model, method="allreduce", granularity="flat", timing=None,
-                 sync_timing=None):
+                 sync_timing=None, force=False):
         self.model, self.method, self.granularity = model, method, granularity
         if timing is None:
-            timing = "sync" if sync_timing else "events"
+            # the legacy flag keeps its meaning: True = synchronised wall clock, False = host
+            # wall time only; neither given = device-side event timing
+            timing = "events" if sync_timing is None else ("sync" if sync_timing else "host")
         self.timing = timing
+        self.force = force
         self._host_time = 0.0
         self._events = []
         self.calls = 0
@@ -260,9 +265,9 @@ class GradAggregator:
 
     def _aggregate(self):
         if self.method == "allreduce":
-            allreduce_average_gradients(self.model, self.granularity)
+            allreduce_average_gradients(self.model, self.granularity, force=self.force)
         elif self.method == "allgather":
-            allgather_average_gradients(self.model, self.granularity)
+            allgather_average_gradients(self.model, self.granularity, force=self.force)
         elif self.method == "allgather_ref":
             allgather_average_gradients_reference_compat(self.model)
         else:

@@ -30,11 +30,21 @@ task3/dist_utils.py:40-46).  Here:
   side stream; ``DMLAB_DDP_SIDE_HOOKS=0/1`` forces either).  Off = the one-layer-lag scheme
   in which the main stream waits for each layer's weight gradients before its bucket
   launches.
-* ``broadcast_buffers`` (default on, as torch DDP): rank 0's module buffers (BatchNorm
-  running statistics, ``num_batches_tracked``) are broadcast — coalesced, one collective
-  per dtype — at every training forward (or every ``buffer_sync_every`` forwards), so the
-  running statistics agree on every rank and a rank-0 checkpoint holds what every rank
-  evaluates with.
+* ``broadcast_buffers`` (default on, as torch DDP): rank 0's floating-point module buffers
+  (BatchNorm running statistics) are broadcast once per training step (or every
+  ``buffer_sync_every`` forwards), so the running statistics agree on every rank and a
+  rank-0 checkpoint holds what every rank evaluates with.  The buffers are re-pointed into
+  ONE flat tensor at construction (one in-place collective, no flatten/unflatten copies),
+  and the broadcast is issued asynchronously at the first gradient hook of backward — the
+  forward is done updating the statistics and backward never reads them — and waited for
+  at the end of backward, so it overlaps backward instead of heading the next forward.
+  ``num_batches_tracked`` advances identically on every rank and is not sent.  Nothing is broadcast when the wrapper switches to ``eval()`` (a rank-0-
+  only evaluation must not enter a collective): to evaluate every rank with rank 0's final
+  statistics, call :meth:`sync_buffers` on every rank first.
+* ``force_comm`` (or ``DMLAB_DDP_FORCE_COMM=1``): at world size 1 with an initialised
+  process group (a 1-rank RCCL communicator), run the full multi-rank path anyway — native
+  reducer, bucket hooks, one collective per bucket, buffer broadcasts — so the RCCL code is
+  exercised on a single GPU exactly as it runs on eight.
 * ``small_allreduce="xgmi"``: buckets of at most ``small_cap_mb`` go through the
   one-shot xGMI peer-memory all-reduce (:mod:`dmlab.parallel.xgmi`, one kernel, no ring
   steps) instead of RCCL — the latency-bound case of the labs' LeNet (207 KB of grads).
@@ -78,14 +88,25 @@ class DistributedDataParallel(nn.Module):
                  process_group=None, average: bool = True, small_allreduce: str | None = None,
                  small_cap_mb: float = 4.0, native: bool | None = None, xgmi_algo: str = "auto",
                  side_stream_hooks: bool | None = None, broadcast_buffers: bool = True,
-                 buffer_sync_every: int = 1):
+                 buffer_sync_every: int = 1, force_comm: bool | None = None):
         super().__init__()
         self.module = module
         self.ws = env.get_world_size()
+        if force_comm is None:
+            import os
+
+            force_comm = os.environ.get("DMLAB_DDP_FORCE_COMM", "0") == "1"
+        if force_comm and not env.is_initialized():
+            raise RuntimeError("DDP(force_comm=True) needs an initialised process group "
+                               "(e.g. a 1-rank 'nccl' group: env.init(backend='nccl'))")
+        # communication is live at ws > 1, or at ONE rank when forced: a 1-rank RCCL group
+        # then runs the whole multi-rank machinery (native reducer, bucket hooks on the side
+        # stream, every bucket's collective, buffer broadcasts) on the one-GPU box
+        self.comm_active = self.ws > 1 or bool(force_comm)
         self.pg = process_group
         self.comm_dtype = comm_dtype
         self.average = average
-        self._use_avg = avg_supported() if self.ws > 1 else False
+        self._use_avg = avg_supported() if self.comm_active else False
         self._fold = False  # 1/ws folded into the optimiser
         self.program = module if hasattr(module, "register_grad_hook") else None
         self._last_mb = last_bucket_mb
@@ -102,9 +123,14 @@ class DistributedDataParallel(nn.Module):
         self.broadcast_buffers = bool(broadcast_buffers)
         self.buffer_sync_every = max(1, int(buffer_sync_every))
         self._fwd_count = 0
-        self._buffers = [b for b in module.buffers()] if self.ws > 1 else []
-        if broadcast_init and self.ws > 1:
-            init_parameters(module)
+        self._bcast_bufs = [b for b in module.buffers()] if self.comm_active else []
+        self._buf_flat = None      # floating buffers re-pointed into one flat tensor
+        self._buf_state = None     # "due": broadcast at the next backward's first hook
+        self._buf_work = None      # the in-flight asynchronous broadcast
+        if self.comm_active and self.broadcast_buffers:
+            self._flatten_buffers()
+        if broadcast_init and self.comm_active:
+            init_parameters(module, force=True)
         if self.program is not None:
             self._setup_program(bucket_cap_mb, first_bucket_mb)
         else:
@@ -117,7 +143,7 @@ class DistributedDataParallel(nn.Module):
         self._xgmi = None
         if small_allreduce not in (None, "rccl", "xgmi"):
             raise ValueError("small_allreduce: None | 'rccl' | 'xgmi'")
-        if small_allreduce == "xgmi" and self.ws > 1:
+        if small_allreduce == "xgmi" and self.comm_active:
             cap = int(small_cap_mb * 2**20 / 4)
             small = [b.hi - b.lo for b in self.buckets if b.hi - b.lo <= cap]
             if self.grad_buf.dtype == torch.float32 and self.grad_buf.is_cuda and small:
@@ -126,14 +152,15 @@ class DistributedDataParallel(nn.Module):
                 self._xgmi = XGMIAllReduce(cap=max(small), group=self.pg, algo=xgmi_algo)
         self._native = None
         if native is None:
-            native = self.ws > 1 and _native_reducer_available()
+            native = self.comm_active and _native_reducer_available()
         # persistent communication buffer of the low-precision gradient copy (no per-step
         # allocation: graph-capturable, and safe to fill on the side stream)
         self._comm_flat = None
-        if self.comm_dtype is not None and self.comm_dtype != self.grad_buf.dtype and self.ws > 1:
+        if self.comm_dtype is not None and self.comm_dtype != self.grad_buf.dtype and \
+                self.comm_active:
             self._comm_flat = torch.empty(self.grad_buf.numel(), dtype=self.comm_dtype,
                                           device=self.grad_buf.device)
-        if native and self.ws > 1:
+        if native and self.comm_active:
             self._build_native(small_cap_mb)
 
     # ------------------------------------------------------------------ native reducer
@@ -229,7 +256,7 @@ class DistributedDataParallel(nn.Module):
         self._bucket_of_index = {i: self._bucket_of[i] for i in range(len(flat.params))
                                  if i in self._bucket_of}
         self._layer_params = [prog.layer_params(i) for i in range(len(prog.layers))]
-        if self.ws > 1:  # one rank: nothing to launch per layer (finalize still runs)
+        if self.comm_active:  # one rank: nothing to launch per layer (finalize still runs)
             # stream_ok: the bucket launches only enqueue collectives (or the xGMI kernel), and
             # the bf16 cast into the persistent communication buffer, on the current stream
             prog.register_grad_hook(self._on_layer_done, stream_ok=self.side_stream_hooks)
@@ -277,6 +304,8 @@ class DistributedDataParallel(nn.Module):
             if not self._final_queued:
                 self._final_queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
+            if self._buf_state == "due":
+                self._launch_buffer_sync()
             self._mark_ready(i)
         return hook
 
@@ -291,7 +320,7 @@ class DistributedDataParallel(nn.Module):
         return optimizer
 
     def _launch(self, b: _Bucket):
-        if b.work is not None or self.ws <= 1:
+        if b.work is not None or not self.comm_active:
             b.work = b.work or True
             return
         view = self.grad_buf[b.lo:b.hi]
@@ -329,6 +358,8 @@ class DistributedDataParallel(nn.Module):
             self._launch(b)
 
     def _on_layer_done(self, prog, layer_idx):
+        if self._buf_state == "due":
+            self._launch_buffer_sync()
         if self._native is not None:
             if self._sync_enabled:
                 self._native.mark_layer(layer_idx)
@@ -339,6 +370,8 @@ class DistributedDataParallel(nn.Module):
     def _finalize(self):
         if self.on_compute_done is not None:
             self.on_compute_done()
+        if self._buf_state is not None or self._buf_work is not None:
+            self._wait_buffer_sync()
         if not self._sync_enabled:
             if self.program is None:
                 self._final_queued = False
@@ -361,7 +394,7 @@ class DistributedDataParallel(nn.Module):
             if b.comm_buf is not None:
                 view.copy_(b.comm_buf)
                 b.comm_buf = None
-            if scale is not None and self.ws > 1 and not b.scaled:
+            if scale is not None and self.comm_active and not b.scaled:
                 view.mul_(scale)
             b.work, b.scaled = None, False
             b.pending = set(b.params)
@@ -372,36 +405,85 @@ class DistributedDataParallel(nn.Module):
         """Reduce the whole gradient buffer now (every bucket, then the end-of-backward
         wait / cast-back / average): for steps that produce all gradients outside the
         per-layer hooks, e.g. :class:`dmlab.models.lenet_fused.FusedLeNetStep`."""
-        if self.ws <= 1:
+        if not self.comm_active:
             return
         if self._native is not None and self._sync_enabled:
             for lp in range(len(getattr(self, "_layer_params", []))):
                 self._native.mark_layer(lp)
         self._finalize()
 
-    def sync_buffers(self):
-        """Broadcast rank 0's module buffers to every rank (coalesced per dtype)."""
-        if self.ws <= 1 or not self._buffers:
+    # ------------------------------------------------------------------ buffers
+    def _flatten_buffers(self):
+        """Re-point every floating-point module buffer (BN running mean / var) into ONE flat
+        tensor so a buffer sync is a single in-place collective: no per-step flatten /
+        unflatten copies (``_broadcast_coalesced`` costs ~60 copy launches per ResNet-18
+        forward).  Integer buffers (``num_batches_tracked``) advance identically on every
+        rank and are not broadcast on this path."""
+        slots = [(m, n, b) for m in self.module.modules() for n, b in m._buffers.items()
+                 if b is not None and b.is_floating_point()]
+        if not slots or len({(b.dtype, b.device) for _, _, b in slots}) != 1:
+            self._buf_flat = None
             return
+        flat = torch.cat([b.detach().reshape(-1) for _, _, b in slots])
+        o = 0
+        for m, n, b in slots:
+            m._buffers[n] = flat[o:o + b.numel()].view_as(b)
+            o += b.numel()
+        self._buf_flat = flat
+        self._buf_slots = slots
+        self._buf_ptrs = [m._buffers[n].data_ptr() for m, n, _ in slots]
+
+    def _buffers_still_flat(self) -> bool:
+        return self._buf_flat is not None and all(
+            m._buffers.get(n) is not None and m._buffers[n].data_ptr() == p
+            for (m, n, _), p in zip(self._buf_slots, self._buf_ptrs))
+
+    def _pg(self):
         from torch.distributed import distributed_c10d as c10d
 
-        pg = self.pg if self.pg is not None else c10d._get_default_group()
-        dist._broadcast_coalesced(pg, self._buffers, 256 * 2**20, 0)
+        return self.pg if self.pg is not None else c10d._get_default_group()
+
+    def _launch_buffer_sync(self):
+        """Start the flat buffer broadcast asynchronously: issued at the first hook of
+        backward (the forward has finished updating the running statistics and nothing in
+        backward reads them), waited for at the end of backward, so it overlaps the whole
+        backward instead of sitting at the head of the next forward."""
+        self._buf_state = None
+        if self._buffers_still_flat():
+            self._buf_work = dist.broadcast(self._buf_flat, 0, group=self.pg, async_op=True)
+        else:
+            self.sync_buffers()
+
+    def _wait_buffer_sync(self):
+        if self._buf_state == "due":  # a training forward without a backward through hooks
+            self._launch_buffer_sync()
+        if self._buf_work is not None:
+            self._buf_work.wait()
+            self._buf_work = None
+
+    def sync_buffers(self):
+        """Broadcast rank 0's module buffers to every rank now (one collective on the flat
+        buffer, or coalesced per dtype when the buffers were re-allocated)."""
+        if not self.comm_active or not self._bcast_bufs:
+            return
+        if self._buf_work is not None:
+            self._buf_work.wait()
+            self._buf_work = None
+        if self._buffers_still_flat():
+            dist.broadcast(self._buf_flat, 0, group=self.pg)
+            return
+        self._bcast_bufs = [b for b in self.module.buffers()]
+        dist._broadcast_coalesced(self._pg(), self._bcast_bufs, 256 * 2**20, 0)
 
     def forward(self, *a, **kw):
-        if self.broadcast_buffers and self._buffers and self.module.training and \
+        if self.broadcast_buffers and self._bcast_bufs and self.module.training and \
                 torch.is_grad_enabled():
+            if self._buf_state == "due" or self._buf_work is not None:
+                self._wait_buffer_sync()  # the previous forward never reached a backward
             if self._fwd_count % self.buffer_sync_every == 0:
-                self.sync_buffers()
+                self._buf_state = "due"
             self._fwd_count += 1
         return self.module(*a, **kw)
-
-    def train(self, mode: bool = True):
-        # entering evaluation: every rank evaluates with rank 0's running statistics (the
-        # last training forward updated each rank's copy from its own batch)
-        if not mode and self.module.training and self.broadcast_buffers:
-            self.sync_buffers()
-        return super().train(mode)
 
     def check(self):
         """Raise if the xGMI all-reduce reported a timed-out peer.  The per-step poll in

@@ -53,6 +53,13 @@ class _ShapeCache:
 
     def send(self, t, dst, key):
         if key in self.shapes:
+            if self.shapes[key] != (tuple(t.shape), t.dtype):
+                # the receiver sizes its buffer from the cached header: a silent mismatch
+                # would truncate (xGMI ring) or deadlock (RCCL size mismatch)
+                raise ValueError(
+                    f"p2p message {key!r}: shape/dtype {tuple(t.shape)}/{t.dtype} differs from "
+                    f"the negotiated {self.shapes[key][0]}/{self.shapes[key][1]}; use "
+                    "static_shapes=False (a header per message) or a fixed batch (drop_last)")
             return []
         hdr = torch.zeros(16, dtype=torch.long)
         hdr[0] = t.dim()
@@ -81,6 +88,11 @@ def _direction(key):
 class PGTransport:
     def __init__(self, ranks=None, static_shapes=True):
         ranks = list(ranks) if ranks is not None else list(range(dist.get_world_size()))
+        if dist.get_world_size() < 2:
+            # torch.distributed refuses point-to-point to the caller's own rank (and RCCL has
+            # no self-channel in ProcessGroupNCCL's isend/irecv): a pipeline needs >= 2 ranks
+            raise RuntimeError("PGTransport: stage-to-stage send/recv needs >= 2 ranks "
+                               "(point-to-point to self is unsupported)")
         # new_group is collective over the default group: every rank builds both
         self.groups = {"fwd": dist.new_group(ranks), "bwd": dist.new_group(ranks)}
         self.gloo = dist.get_backend(self.groups["fwd"]) == "gloo"

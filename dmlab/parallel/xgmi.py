@@ -78,12 +78,14 @@ class XGMIAllReduce:
                 bases.append(p)
         self._data = bases
         self._flags = [b + 8 * self.cap for b in bases]
-        # ranks whose kernels share this physical GPU (1 on a node with one rank per GPU; the
+        # ranks whose kernels share one physical GPU (1 on a node with one rank per GPU; the
         # single-GPU rehearsals run W ranks on one device): the spinning grids shrink by it so
-        # every rank's blocks are resident together
+        # every rank's blocks are resident together.  The kernels split the data by gridDim
+        # and match flags by block index, so EVERY rank must launch the same grid: the divisor
+        # is the most crowded device's count, identical on all ranks
         keys = [None] * self.world
         dist.all_gather_object(keys, _device_key(self.device), group=group)
-        self._share = max(1, keys.count(keys[self.rank]))
+        self._share = max(1, max(keys.count(k) for k in keys))
         # [timeout flag, last published epoch, done-block counter, pad] (device side)
         self._state = torch.zeros(4, dtype=torch.int32, device=self.device)
         self._calls = 0

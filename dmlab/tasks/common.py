@@ -92,6 +92,101 @@ def train(model, loader, loss_fn, optimizer, num_epochs=2, *, rank=None, aggrega
     return stats
 
 
+def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, log_every=20,
+                graph=True, max_steps=None, print_fn=print, writer=None):
+    """The lab-3 loop (codes/task3/model.py:39-64) on the GPU fast path: the reference LeNet
+    step as the 2-dispatch fused kernel pair (:class:`~dmlab.models.lenet_fused.
+    FusedLeNetStep`; with ``ddp`` the bucket all-reduce sits between them), its samples
+    gathered on the device through the sampler's epoch order (:class:`~dmlab.data.
+    DeviceCursor`), the whole step captured in ONE hipGraph (``graph``) and replayed per
+    iteration.  Same console output as :func:`train`; the running loss is summed on the
+    device and copied to pinned host memory every ``log_every`` steps, and each line prints
+    once its copy has landed (at the next log point or the end) -- no host synchronisation
+    inside the loop.  Returns the same stats dict as :func:`train`."""
+    from dmlab.models.lenet_fused import FusedLeNetStep
+
+    if rank is not None:
+        print_fn("Device {} starts training ...".format(rank))
+    net.train()
+    step_fn = FusedLeNetStep(net, optimizer, ddp=ddp)
+    cur = loader.cursor()
+    ds = loader.dataset
+    if graph:
+        from dmlab.utils.graph import CapturedStep
+
+        # the capture's eager warm-up steps must not count as training: snapshot the weights
+        # and the momentum buffer, restore them in place afterwards (the graph keeps the
+        # pointers).  The restored zero momentum with the captured not-first-step update is
+        # the first step's buf = grad (dampening 0, the labs' setting).
+        if getattr(optimizer, "dampening", 0.0):
+            raise ValueError("graph-captured fused step: SGD dampening != 0 is not supported")
+        flat = net.flat
+        saved = [flat.data.clone()]
+        runner = CapturedStep(lambda x, y: step_fn(x, y, cursor=cur), [ds.images, ds.labels],
+                              warmup=2, bind_inputs=True)
+        with torch.no_grad():
+            flat.data.copy_(saved[0])
+            flat.mark_updated()
+            if getattr(optimizer, "buf", None) is not None:
+                optimizer.buf.zero_()
+
+        def run():
+            runner(ds.images, ds.labels)
+    else:
+        def run():
+            step_fn(ds.images, ds.labels, cursor=cur)
+    stats = {"losses": [], "steps": 0, "samples": 0, "comm_time": 0.0}
+    pending = []  # (epoch, iters, pinned copy, event) awaiting print
+    host = [torch.zeros(1, pin_memory=True) for _ in range(4)]
+
+    def flush(block):
+        while pending and (block or pending[0][3].query()):
+            ep, it, buf, ev = pending.pop(0)
+            ev.synchronize()
+            avg = float(buf[0]) / log_every
+            stats["losses"].append(avg)
+            if writer is not None:
+                writer.add_scalar("Train Loss", avg, stats["steps"])
+            print_fn('Device: %d epoch: %d, iters: %5d, loss: %.3f' % (rank or 0, ep, it, avg))
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step = 0
+    nlog = 0
+    done = False
+    for epoch in range(num_epochs):
+        cur.refill(epoch)  # this epoch's shard order (set_epoch), cursor rewound
+        step_fn.loss_sum.zero_()
+        for i in range(cur.nbatch):
+            run()
+            step += 1
+            if i % log_every == log_every - 1:
+                flush(False)
+                buf = host[nlog % len(host)]
+                if len(pending) >= len(host) - 1:
+                    flush(True)
+                buf.copy_(step_fn.loss_sum, non_blocking=True)
+                step_fn.loss_sum.zero_()
+                ev = torch.cuda.Event()
+                ev.record()
+                pending.append((epoch + 1, i + 1, buf, ev))
+                nlog += 1
+            if max_steps is not None and step >= max_steps:
+                done = True
+                break
+        if done:
+            break
+    torch.cuda.synchronize()
+    stats["train_time"] = time.perf_counter() - t0
+    flush(True)
+    stats["steps"] = step
+    stats["samples"] = step * loader.batch_size
+    print_fn("Training Finished!")
+    if writer is not None:
+        writer.flush()
+    return stats
+
+
 @torch.no_grad()
 def test(model, test_loader, print_fn=print):
     model.eval()

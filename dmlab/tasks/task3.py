@@ -28,6 +28,12 @@ from dmlab.parallel import DDP, comm, env
 from dmlab.tasks.common import test, train
 
 
+def dist_backend():
+    import torch.distributed as dist
+
+    return dist.get_backend() if dist.is_initialized() else None
+
+
 def parse_args(argv=None):
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--n_devices", default=1, type=int)
@@ -63,6 +69,12 @@ def parse_args(argv=None):
                    help="ResNet-18 synthetic image side (224 = the BASELINE/ImageNet shape)")
     p.add_argument("--num-classes", type=int, default=10,
                    help="ResNet-18 classifier width (1000 = the BASELINE/ImageNet head)")
+    p.add_argument("--fused", default="auto", choices=["auto", "0", "1"],
+                   help="LeNet on the GPU: the fused 2-dispatch training step fed by the "
+                        "device-side sampler cursor (auto: on for LeNet + DDP + SGD on a GPU)")
+    p.add_argument("--graph", default="auto", choices=["auto", "0", "1"],
+                   help="capture the fused step (with its all-reduce) in a hipGraph (auto: "
+                        "on when --fused is, unless the group is gloo at ws > 1)")
     return p.parse_args(argv)
 
 
@@ -110,10 +122,27 @@ def main(argv=None):
     else:
         comm.init_parameters(model)
         net = model
-        agg = comm.GradAggregator(model, "allreduce", sync_timing=False)
-    stats = train(net, loader, CrossEntropyLoss(), opt, a.epochs, rank=rank, aggregate=agg,
-                  batch_size=a.batch_size, max_steps=a.max_steps)
+        agg = comm.GradAggregator(model, "allreduce", timing="events")
+    fused = a.fused == "1" or (a.fused == "auto" and a.model == "lenet" and dev.type == "cuda"
+                               and a.dp == "ddp")
+    if fused:
+        if a.model != "lenet" or dev.type != "cuda" or a.dp != "ddp":
+            raise SystemExit("--fused 1 needs --model lenet on a GPU with --dp ddp")
+        from dmlab.tasks.common import train_fused
+
+        capturable = ws == 1 or dist_backend() == "nccl" or a.allreduce == "xgmi"
+        graph = a.graph == "1" or (a.graph == "auto" and capturable)
+        loader.drop_last = True  # fixed batch shape (the last partial batch of a shard drops)
+        stats = train_fused(model, loader, opt, a.epochs, ddp=net, rank=rank, graph=graph,
+                            max_steps=a.max_steps)
+        stats.update(fused=True, hip_graph=graph)
+    else:
+        stats = train(net, loader, CrossEntropyLoss(), opt, a.epochs, rank=rank, aggregate=agg,
+                      batch_size=a.batch_size, max_steps=a.max_steps)
     print("Training time: {}".format(stats["train_time"]))
+    if rank == 0:
+        print("Throughput: {:.1f} samples/s (whole job, {} rank{})".format(
+            stats["samples"] * ws / stats["train_time"], ws, "s" if ws > 1 else ""))
     if a.save:
         from dmlab.utils import checkpoint
 

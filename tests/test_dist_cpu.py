@@ -287,7 +287,8 @@ def test_partition_sampler_disjoint_ws8():
 def _buffers_synced(rank, ws, path):
     """broadcast_buffers: BatchNorm running statistics agree on every rank after 3 DDP
     steps with a different batch per rank (rank 0's buffers are broadcast at each training
-    forward and when the model enters evaluation)."""
+    forward; ``sync_buffers()`` on every rank before evaluating brings the last forward's
+    update across too -- ``eval()`` itself enters no collective)."""
     from dmlab.parallel import DDP
 
     torch.manual_seed(0)
@@ -300,8 +301,16 @@ def _buffers_synced(rank, ws, path):
         for _ in range(3):
             x = torch.rand(4, 1, 28, 28, generator=g) * (1 + rank)
             F.cross_entropy(ddp(x), torch.zeros(4, dtype=torch.long)).backward()
-        ddp.eval()  # entering evaluation syncs the buffers (the last forward updated them locally)
+        ddp.eval()  # no collective here (a rank-0-only evaluation must not deadlock)
         bn = m[1]
+        if sync:
+            # the flat broadcast issued during each backward already left rank 0's statistics
+            # of the last forward on every rank; an explicit sync is idempotent
+            assert ddp._buf_flat is not None and ddp._buffers_still_flat()
+            rm0 = [torch.zeros_like(bn.running_mean) for _ in range(ws)]
+            dist.all_gather(rm0, bn.running_mean)
+            assert all(torch.equal(rm0[0], r) for r in rm0), rm0
+            ddp.sync_buffers()
         rm = [torch.zeros_like(bn.running_mean) for _ in range(ws)]
         dist.all_gather(rm, bn.running_mean)
         same = all(torch.equal(rm[0], r) for r in rm)

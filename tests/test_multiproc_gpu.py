@@ -315,6 +315,11 @@ def test_bench_two_ranks(tmp_path):
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["steps"] == 3 and res["value"] > 0
     assert res["config"]["parallelism"] == "dp2" and res["config"]["global_batch"] == 16
+    # the multi-rank self-check (both ranks on this box's one GPU, gloo group)
+    assert res["distinct_gpus"] == 1 and res["rccl_world"] is None
+    assert res["replicas_in_sync"] is True and res["buckets_launched"] > 0
+    assert set(res["phases_ms"]) == {"fwd", "bwd_compute", "comm_exposed", "opt"}
+    assert res["config"]["sampler"] == "MySampler(partition)"
 
 
 @pytest.mark.parametrize("ws", [4, 8])

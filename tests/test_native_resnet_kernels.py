@@ -309,6 +309,26 @@ def test_stem_s2d_packing_layouts(dev, layout, H):
     assert torch.equal(xs.float(), ref.bfloat16().float())
 
 
+@pytest.mark.parametrize("layout", ["channels_last", "nchw_bf16"])
+def test_stem_s2d_packing_gathers_rows(dev, layout):
+    """The loader's gather fused into the packing: xs[n] = pack(x[idx[n]]) for a batch of
+    row indices into a device-resident dataset (repeats allowed; out-of-range rows clamp)."""
+    Nsrc, C, H = 11, 3, 32
+    x = torch.randn(Nsrc, C, H, H, device=dev)
+    if layout == "channels_last":
+        x = x.contiguous(memory_format=torch.channels_last)
+    else:
+        x = x.bfloat16()
+    idx = torch.tensor([7, 0, 10, 7, 3, 42], device=dev)
+    xs = torch.empty(6, H // 2, H // 2, 16, device=dev, dtype=torch.bfloat16)
+    lib().pack_input_s2d(x, xs, idx)
+    ref = torch.empty_like(xs)
+    lib().pack_input_s2d(x.index_select(0, idx.clamp(max=Nsrc - 1)).contiguous(
+        memory_format=torch.channels_last if layout == "channels_last" else torch.contiguous_format),
+        ref)
+    assert torch.equal(xs, ref)
+
+
 @pytest.mark.parametrize("H,W,C", [(18, 18, 64), (17, 17, 64), (56, 56, 32), (9, 14, 64)])
 def test_bn_relu_maxpool_3x3s2_codes(dev, H, W, C):
     """The 3x3/s2 fused stem tail (two pooled outputs per thread) against torch: pooled
