@@ -1146,13 +1146,9 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                                                                     (double)M, fb);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
-  // DMLAB_BN_BWD_GRID: workgroup cap of the apply pass (A/B runs; default 4096)
-  static const int cap = [] {
-    const char* e = std::getenv("DMLAB_BN_BWD_GRID");
-    const int v = e ? std::atoi(e) : 0;
-    return v > 0 ? v : 4096;
-  }();
-  const int grid = grid_for(n8, 256, cap);
+  // workgroup cap of the apply pass: 4096 (1024-8192 within noise,
+  // profiles/bn_bwd_apply_grid_ab_r3s3.txt)
+  const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;
 #define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
   if (quad) {

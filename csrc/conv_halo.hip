@@ -350,9 +350,9 @@ bool conv_halo_supported(const ConvGeom& g) {
   return halo_rows_needed(g) <= 32 * 12 && halo_rows_needed(g, 256) <= 32 * 14;
 }
 
-// tiles (igemm_fwd's halo cfgs): waves 4 = 128 px as 2 x 2 waves of 64 x BN/2 (cfg 20 / 21;
-// | 0x100: two weight tiles of register prefetch, cfg 42); 16 = 256 px as 4 x 2 waves of
-// 64 x 32 (cfg 39); 32 = 256 px as 4 x 1 waves of 64 x 64 (cfg 41)
+// tiles (igemm_fwd's halo cfgs): waves 4 | 0x100 = 128 px as 2 x 2 waves of 64 x 64 with two
+// weight tiles of register prefetch (cfg 42); 16 = 256 px as 4 x 2 waves of 64 x 32 (cfg 39);
+// 32 = 256 px as 4 x 1 waves of 64 x 64 (cfg 41)
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
                const float* pre_sh, const BnBwdRed* red) {
@@ -384,14 +384,7 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
     else if (hr <= 12) launch_halo<64, 12, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
     else launch_halo<64, 14, 4, 1, 256>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
   } else {
-    DM_CHECK(waves == 4 ? hipSuccess : hipErrorInvalidValue);
-    const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-#define DM_HALO4(BN_)                                                                       \
-  if (hr == 6) launch_halo<BN_, 6, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);      \
-  else if (hr == 8) launch_halo<BN_, 8, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st); \
-  else launch_halo<BN_, 12, 2, 2>(X, Wp, Y, ADD, stats, g, pre_sc, pre_sh, st);
-    if (bn == 128) { DM_HALO4(128) } else { DM_HALO4(64) }
-#undef DM_HALO4
+    throw std::runtime_error("conv_halo: unknown tile (cfg 39 / 41 / 42)");
   }
   DM_CHECK(hipGetLastError());
 }

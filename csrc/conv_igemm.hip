@@ -724,14 +724,13 @@ bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
   }
 }
 
-// halo-kernel configs (conv_halo.hip): 20 / 21 = 128-pixel tile of 2 x 2 waves, BN 128 / 64;
-// 42 = 20 with two weight tiles of register prefetch (waves bit 8); 39 = 256-pixel tile of
-// 4 x 2 waves, BN 64; 41 = 256-pixel tile of 4 x 1 waves of 64 x 64
+// halo-kernel configs (conv_halo.hip): 42 = 128-pixel tile of 2 x 2 waves, BN 128, with
+// two weight tiles of register prefetch (waves bit 8); 39 = 256-pixel tile of 4 x 2 waves,
+// BN 64; 41 = 256-pixel tile of 4 x 1 waves of 64 x 64.  (The round-2 tiles 20 / 21, 42
+// without the prefetch and BN 64, lost on every layer and are removed.)
 int igemm_fwd_rowtile(int cfg);
 bool halo_cfg(int cfg, int& bn, int& waves) {
   switch (cfg) {
-    case 20: bn = 128; waves = 4; return true;
-    case 21: bn = 64; waves = 4; return true;
     case 42: bn = 128; waves = 4 | 0x100; return true;
     case 39: bn = 64; waves = 16; return true;
     case 41: bn = 64; waves = 32; return true;

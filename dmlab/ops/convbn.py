@@ -38,15 +38,10 @@ def _cpad(c):
 #     channels: v3 tiles 15 / 13 / 11 by the block-count rule below (256-row tiles lose
 #     there: one workgroup per CU exposes the staging latency).
 TILE_CFG = (15, 13, 11)
-_STEM_CFG = int(os.environ.get("DMLAB_STEM_CFG", "60"))
-# DMLAB_NO_PIPE=1: the round-2 tile map without the pipelined tiles (A/B runs)
-_NO_PIPE = os.environ.get("DMLAB_NO_PIPE", "0") == "1"
-# DMLAB_NO_RES64=1: layer1 (64 -> 64 channel 3x3) convs on the round-2 halo tile (A/B runs)
-_NO_RES64 = os.environ.get("DMLAB_NO_RES64", "0") == "1"
-# DMLAB_NO_FUSED_SKIP=1: materialise the identity-skip gradient dres (A/B runs)
-_NO_FUSED_SKIP = os.environ.get("DMLAB_NO_FUSED_SKIP", "0") == "1"
-# DMLAB_NO_DGRAD_RED=1: run the next BN's backward reduction as its own pass (A/B runs)
-_NO_DGRAD_RED = os.environ.get("DMLAB_NO_DGRAD_RED", "0") == "1"
+_STEM_CFG = 60
+# The round-3 A/B switches (DMLAB_NO_PIPE / NO_RES64 / NO_FUSED_SKIP / NO_DGRAD_RED /
+# NO_WRES64 / WRES64_S / TAIL_WGRAD_FULL / WGRAD_BLOCKS / RES64_ADD_RED / STEM_CFG) are
+# settled and removed; their measurements stay in docs/KERNELS.md and profiles/.
 
 
 def dgrad_cfg(M, cin, k, stride, cout, H=0, W=0):
@@ -64,7 +59,7 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
     # 128-pixel tile's halo, 128 + 2W + 2 rows, must fit the 256-row LDS image; the input
     # below 1 GiB: its DMA pad pieces are addressed past 2^30)
     if (k == 3 and stride == 1 and cin == 64 and ncols == 64 and 0 < W <= 63
-            and M * 128 < 2**30 - 2**14 and not _NO_RES64):
+            and M * 128 < 2**30 - 2**14):
         return 80
     # 90: the pipelined LDS-DMA 256 x 256 tile (csrc/conv_pipe.hip), for >= 256 output
     # channels and 64-channel-aligned input, any tap geometry.  tools/bench_conv.py at batch
@@ -72,7 +67,7 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
     #   layer3 3x3 975/1004 (41: 897/971), layer4 3x3 1151/1160 (41: 933/957),
     #   layer4 3x3/s2 1030/901 (15: 750/724), layer3 3x3/s2 fwd 778 (42: 690),
     #   layer4 1x1/s2 442/367 (15: 351/299); the 64/128-channel layers keep the halo tiles
-    if ncols % 256 == 0 and cin % 64 == 0 and cin > 0 and not _NO_PIPE:
+    if ncols % 256 == 0 and cin % 64 == 0 and cin > 0:
         return 90
     if k == 3 and stride == 1 and cin % 64 == 0 and ncols % 64 == 0:
         # 64 output channels: the 256-pixel halo tile (2 x 2 waves of 128 x 32) amortises
@@ -102,11 +97,7 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 # (profiles/wgrad_blocks_r2c.jsonl, one call): 512 -> 44.2/44.4k img/s, 384 44.2k,
 # 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k; at 1024 images per GPU 512 -> 46.6k,
 # 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl)
-_WGRAD_BLOCKS = int(os.environ.get("DMLAB_WGRAD_BLOCKS", "512"))
-
-
-# DMLAB_NO_WRES64=1: layer1 weight gradients on the halo wgrad (cfg 5) instead of cfg 8 (A/B)
-_NO_WRES64 = os.environ.get("DMLAB_NO_WRES64", "0") == "1"
+_WGRAD_BLOCKS = 512
 _CUS = {}
 
 
@@ -129,8 +120,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
     S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
     ~2 blocks per CU, each split >= 8 row steps, slab bytes S*cout*K*4."""
     halo = k == 3 and stride == 1 and cin % 64 == 0 and cout % 8 == 0
-    res64 = (k == 3 and stride == 1 and cin == 64 and cout == 64 and 0 < W <= 60 and rows > 0
-             and not _NO_WRES64)
+    res64 = k == 3 and stride == 1 and cin == 64 and cout == 64 and 0 < W <= 60 and rows > 0
     if force == 8 or (force is None and res64):
         # 5/8 of the CUs: the kernel runs on the side stream next to the dgrad + BN-backward
         # chain, and leaving that chain CUs of its own is 0.8% faster per step than one
@@ -138,9 +128,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # ``tail``: the last conv before the stem, whose weight gradient runs next to the stem's
         # fused BN-backward + weight-gradient kernel at the end of the step, not next to a
         # dgrad chain: there it takes every CU
-        S = int(os.environ.get("DMLAB_WRES64_S", 0)) or (
-            _cu_count() if tail and os.environ.get("DMLAB_TAIL_WGRAD_FULL", "1") == "1"
-            else max(1, _cu_count() * 5 // 8))
+        S = _cu_count() if tail else max(1, _cu_count() * 5 // 8)
         return 8, max(1, min(rows, S))
     if force is not None:
         cfg = force
@@ -301,7 +289,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C, W=OW if (OH, OW) == (H, W) else 0)
     pre_kw = {}
     if pre is not None:
-        if cfg in (20, 21, 39, 41, 42, 80, 90, 91, 92, 93):
+        if cfg in (39, 41, 42, 80, 90, 91, 92, 93):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)
@@ -360,7 +348,7 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def _dgrad_red(L, red_for, cfg, stride, dx):
+def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
     """conv_dgrad kwargs that reduce the consumer BN's backward sums in the dgrad epilogue
     (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify.
 
@@ -373,7 +361,7 @@ def _dgrad_red(L, red_for, cfg, stride, dx):
     kernel_ok = cfg == 80 or 90 <= cfg <= 93 or cfg == 42
     pool = getattr(rl, "pool_k", 0)
     y = rctx.get("yarg") if pool else rctx.get("y")
-    if (_NO_DGRAD_RED or stride != 1 or not kernel_ok or not rl.relu or y is None
+    if (stride != 1 or not kernel_ok or not rl.relu or y is None
             or rctx.get("mean") is None or rctx.get("pre_sums") is not None
             or tuple(y.shape) != tuple(dx.shape)):
         return {}
@@ -385,8 +373,8 @@ def _dgrad_red(L, red_for, cfg, stride, dx):
     # layer1's identity-block dgrads (res64 with the fused skip add, reducing the previous
     # block's or the stem's BN): correct (tests) but 0.3% slower per step -- the add/mask
     # epilogue costs the kernel ~100 us, more than the contended pass it saves
-    # (profiles/dgrad_bn_reduce_ab_r3s3.txt, red9); opt in with DMLAB_RES64_ADD_RED=1
-    if cfg == 80 and (mask is not None or pool) and os.environ.get("DMLAB_RES64_ADD_RED") != "1":
+    # (profiles/dgrad_bn_reduce_ab_r3s3.txt, red9); ``allow_res64_add`` (tests) opts in
+    if cfg == 80 and (mask is not None or pool) and not allow_res64_add:
         return {}
     N, H, W, C = dx.shape
     rows = L.conv_stats_rows(N * H * W, cfg, C)
@@ -472,7 +460,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
                           tail=tail)
     dy = empty_nhwc(N, OH, OW, cout, y)
-    masked_res = (fused_skip and ctx["has_res"] and mode == 4 and not _NO_FUSED_SKIP)
+    masked_res = fused_skip and ctx["has_res"] and mode == 4
     dres = empty_nhwc(N, OH, OW, cout, y) if (ctx["has_res"] and not masked_res) else None
     L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
                   layer.bn_weight.detach(), layer.grad_slot("bn_weight"),

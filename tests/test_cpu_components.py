@@ -386,9 +386,5 @@ def test_dgrad_red_selection():
     assert CB._dgrad_red(L, (relu, c), 42, 1, dx)["red_mask"] is c["mask"]
     assert CB._dgrad_red(L, (relu, ctx(has_res=True, mask=True)), 80, 1, dx) == {}
     assert CB._dgrad_red(L, (stem, ctx(pool=True)), 80, 1, dx) == {}
-    os.environ["DMLAB_RES64_ADD_RED"] = "1"
-    try:
-        c = ctx(pool=True)
-        assert CB._dgrad_red(L, (stem, c), 80, 1, dx)["red_y"] is c["yarg"]
-    finally:
-        del os.environ["DMLAB_RES64_ADD_RED"]
+    c = ctx(pool=True)
+    assert CB._dgrad_red(L, (stem, c), 80, 1, dx, allow_res64_add=True)["red_y"] is c["yarg"]

@@ -124,3 +124,21 @@ def test_grad_hooks_see_final_wgrads(dev):
         for u, p in zip(snaps[i], a.layers[i].parameters()):
             torch.testing.assert_close(u, g[[n for n, q in a.named_parameters() if q is p][0]],
                                        rtol=0, atol=0)
+
+
+def test_resnet18_training_trajectory_224(dev):
+    """Ten SGD-momentum steps at the headline image shape (224 x 224, 1000 classes; batch
+    32): the native kernels (res64 / pipe / halo / stem dispatch, fused dgrad-epilogue BN
+    reductions, side-stream weight gradients) track the fp32 PyTorch run as closely as stock
+    bf16 autocast does (tools/numerics_resnet.py; the long runs at batch 256 / 1024 are in
+    profiles/numerics_resnet18_224_*.jsonl)."""
+    from tools.numerics_resnet import run, summarize
+
+    models, hist = run(32, 10, 224, nbatches=2, log=lambda s: None)
+    s = summarize(models, hist)
+    assert all(h["native"] == h["native"] for h in hist)  # finite
+    assert s["max_loss_dist_native_fp32"] <= 2.0 * s["max_loss_dist_autocast_fp32"] + 0.05, s
+    med = s["gnorm_rel_err_median"]
+    assert med["native"] <= 2.0 * med["autocast"] + 0.1, s
+    bn = s["bn_running_rel_err_max"]
+    assert bn["native"] <= 2.0 * bn["autocast"] + 0.05, s
