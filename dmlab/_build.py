@@ -105,7 +105,10 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
                     raise RuntimeError(f"hipcc failed:\n{cmd}\n{out}")
     out = ext_path()
     if force or jobs_list or not out.exists():
-        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(out)] + [
+        # link to a temporary file and rename it into place: the in-tree .so is always a
+        # complete library (a snapshot of the tree taken mid-build never sees a partial one)
+        tmp = out.with_name(out.name + ".tmp")
+        link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp)] + [
             str(o) for o in objs] + [f"-L{p}" for p in lib] + [
             f"-Wl,-rpath,{p}" for p in lib] + [
             "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python"]
@@ -115,6 +118,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             print(txt)
         if rc != 0:
             raise RuntimeError(f"link failed:\n{cmd}\n{txt}")
+        os.replace(tmp, out)
     return out
 
 

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--micro", default="1,4,8")
     ap.add_argument("--schedules", default="gpipe,1f1b")
     ap.add_argument("--out", default=None, help="append the JSON lines to this file")
+    ap.add_argument("--epochs", type=int, default=0,
+                    help="epochs of the 60k-sample synthetic set (0: enough for --steps)")
     a = ap.parse_args()
     env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2")
     if a.device == "cuda":
@@ -55,7 +57,8 @@ def main():
                        "--nproc-per-node=2", "--master-addr=127.0.0.1", f"--master-port={_port()}",
                        "-m", "dmlab.tasks.task4", "--mode", "pipeline", "--device", a.device,
                        "--synthetic", "--schedule", sch, "--micro", str(m), "--batch-size",
-                       str(a.batch), "--max-steps", str(a.steps), "--epochs", "1",
+                       str(a.batch), "--max-steps", str(a.steps), "--epochs",
+                       str(a.epochs or max(1, -(-a.steps * a.batch // 60000) + 1)),
                        "--transport", a.transport if a.device == "cuda" else "pg",
                        "--bench-json", str(js), "--no-test"]
                 r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
