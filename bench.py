@@ -92,9 +92,6 @@ def parse():
     ap.add_argument("--dataset-batches", type=int, default=2,
                     help="ResNet-18: dataset size in per-rank batches (x world size images, "
                          "held on every GPU)")
-    ap.add_argument("--deterministic", type=int, default=0,
-                    help="torch.use_deterministic_algorithms: the weight gradients' m-splits "
-                         "reduce in fixed order through fp32 slabs instead of atomic adds")
     ap.add_argument("--pg-timeout", type=float, default=120.0,
                     help="process-group timeout (s): a hung collective fails the run fast")
     ap.add_argument("--fused", type=int, default=-1,
@@ -152,8 +149,6 @@ def main():
     if a.gpus != ws:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
     comm = ws > 1 or bool(a.force_comm)
-    if a.deterministic:
-        torch.use_deterministic_algorithms(True, warn_only=True)
 
     torch.manual_seed(0)
     if a.model == "resnet18":
@@ -352,7 +347,6 @@ def main():
                 "ddp_side_stream_hooks": (net.side_stream_hooks if comm else None),
                 "hip_graph": a.graph,
                 "sampler": ("MySampler(partition)" if loader is not None else None),
-                "wgrad_finish": "fixed-order slab reduce" if a.deterministic else "fp32 atomics",
             },
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),

@@ -253,30 +253,11 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   need_f32(dw, "dw", s2d ? (int64_t)Cout * Cin * 49 : (int64_t)Cout * Cin * KH * KW);
   auto g = fwd_geom(x, Cout, KH, KW, stride, pad, dy.size(1), dy.size(2));
   TORCH_CHECK(dy.size(0) == x.size(0));
-  // an EMPTY slab selects the atomic finish: every split adds its partial sums straight into
-  // dw (hardware fp32 atomics), no slab and no reduce launch (not with the s2d stem, whose
-  // slab reduce also permutes the 4x4 x 16 taps back to 7x7)
-  const bool atomic = slab.numel() == 0;
-  TORCH_CHECK(!(atomic && s2d), "the s2d stem weight gradient needs a slab");
-  if (!atomic) need_f32(slab, "slab", (int64_t)S * Cout * g.K);
+  need_f32(slab, "slab", (int64_t)S * Cout * g.K);
   const long long steps = (g.M + 63) / 64;
   const long long mchunk = ((steps + S - 1) / S) * 64;  // multiple of both kernels' row step
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
-  dm::WgradDst dst;
-  dst.C = g.C;
-  dst.Cin = (int)Cin;
-  dst.KHW = (int)(KH * KW);
-  if (atomic) {
-    dst.dw = fp(dw);
-    TORCH_CHECK(beta == 0.0 || beta == 1.0, "atomic weight gradient: beta must be 0 or 1");
-    if (beta == 0.0) {
-      TORCH_CHECK(hipMemsetAsync(dst.dw, 0, (size_t)dw.numel() * sizeof(float), st) == hipSuccess,
-                  "hipMemsetAsync failed");
-    }
-  } else {
-    dst.slab = fp(slab);
-  }
   if (pre_scale.has_value()) {
     // x = previous conv's raw output, operand relu(x*sc + sh)
     TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
@@ -284,16 +265,15 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
     need_f32(*pre_shift, "pre_shift", x.size(3));
     const float *psc = fp(*pre_scale), *psh = fp(*pre_shift);
     if (cfg == 8) {
-      dm::wgrad_res64(bp(x), bp(dy), dst, g, (int)S, st, psc, psh);
+      dm::wgrad_res64(bp(x), bp(dy), fp(slab), g, (int)S, st, psc, psh);
     } else {
       TORCH_CHECK((cfg == 4 || cfg == 5) && dm::wgrad_halo_supported(g),
                   "fused pre-BN needs the halo wgrad (cfg 4/5/8) and a 3x3/s1/p1 geometry");
-      dm::wgrad_halo(bp(x), bp(dy), dst, g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh);
+      dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg == 4 ? 3 : 1, st, psc, psh);
     }
   } else {
-    dm::igemm_wgrad(bp(x), bp(dy), dst, g, (int)S, mchunk, cfg, st);
+    dm::igemm_wgrad(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, cfg, st);
   }
-  if (atomic) return;
   if (s2d)
     dm::wgrad_reduce_s2d(fp(slab), (int)S, Cout, (int)Cin, g.C, fp(dw), (float)beta, st);
   else

@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
 // loads with range-check zero fill, magic-number row decomposition.
 template <int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(256, 2) igemm_wgrad2_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, WgradDst dst,
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes) {
   constexpr int BKM = 64;
   constexpr int PAD = 16;
@@ -392,19 +392,17 @@ __global__ void __launch_bounds__(256, 2) igemm_wgrad2_kernel(
     if (st + 1 < nsteps) store(buf ^ 1);
     __syncthreads();
   }
-  const long long zoff = (long long)blockIdx.z * g.Ncols * g.K;
+  float* out = slab + (long long)blockIdx.z * g.Ncols * g.K;
 #pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int k = k0 + wn * TN + j * 16 + (lane & 15);
-    const int tap = k / g.C, c = k - tap * g.C;  // K = tap-major, channel-minor
+  for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int i = 0; i < RM; ++i)
+    for (int j = 0; j < RN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + wm * TM + i * 16 + (lane >> 4) * 4 + r;
-        if (co < g.Ncols && k < g.K) wgrad_put(dst, zoff, co, g.K, tap, c, acc[i][j][r]);
+        const int k = k0 + wn * TN + j * 16 + (lane & 15);
+        if (co < g.Ncols && k < g.K) out[(long long)co * g.K + k] = acc[i][j][r];
       }
-  }
 }
 
 // dw[co][ci][kh][kw] = beta*dw + Σ_s slab[s][co][(kh*KW+kw)*C + ci]   (ci < Cin)
@@ -789,8 +787,8 @@ int igemm_fwd_rowtile(int cfg) {
   return (cfg == 11 || cfg == 14 || cfg == 17) ? 64 : 128;
 }
 
-void igemm_wgrad(const bf16_t* X, const bf16_t* DY, const WgradDst& slab, const ConvGeom& g,
-                 int S, long long mchunk, int cfg, hipStream_t st) {
+void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                 long long mchunk, int cfg, hipStream_t st) {
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
   // 8: row-streaming 64 -> 64 channel 3x3 kernel (wgrad_res64.hip), one slab per workgroup;

@@ -53,17 +53,6 @@ __device__ __forceinline__ void pdma16(const pi32x4& rs, unsigned lds, unsigned 
 // Fused BatchNorm-apply + ReLU of a staged 16-B chunk (8 bf16 channels c0..c0+7):
 // v = max(v * sc[c] + sh[c], 0).  Used by the halo kernels to read a conv's RAW output and
 // consume BN(y) directly, so the normalised activation is never written to memory.
-// one fp32 partial sum of a weight-gradient kernel: slab element [z][co][tap*C + c], or an
-// atomic add into the OIHW gradient (WgradDst, kernels.h).  zoff = z * Ncols * K.
-__device__ __forceinline__ void wgrad_put(const WgradDst& d, long long zoff, int co, long long K,
-                                          int tap, int c, float v) {
-  if (d.dw != nullptr) {
-    if (c < d.Cin) unsafeAtomicAdd(d.dw + ((long long)co * d.Cin + c) * d.KHW + tap, v);
-  } else {
-    d.slab[zoff + (long long)co * K + (long long)tap * d.C + c] = v;
-  }
-}
-
 struct PreBN {
   float sc[8], sh[8];
   __device__ __forceinline__ void load(const float* __restrict__ scale,

@@ -123,22 +123,12 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const ConvGeom& g, int bn, int waves, hipStream_t st,
                const float* pre_sc = nullptr, const float* pre_sh = nullptr,
                const BnBwdRed* red = nullptr);
-// Where a weight-gradient kernel puts its fp32 partial sums over its m-split: a slab
-// [S][Ncols][K] (K = taps x C, channel-minor) reduced afterwards in fixed order by
-// wgrad_reduce (deterministic), or -- dw set -- straight into the OIHW gradient
-// [Ncols][Cin][KHW] by hardware fp32 atomic adds (no slab traffic, no reduce launch; the
-// summation order, and so the last bits, vary run to run).
-struct WgradDst {
-  float* slab = nullptr;
-  float* dw = nullptr;
-  int C = 0, Cin = 0, KHW = 0;
-};
 bool wgrad_halo_supported(const ConvGeom& g);
-// wgrad_res64.hip: row-streaming 64 -> 64 channel 3x3 weight gradient (wgrad cfg 8); S splits
+// wgrad_res64.hip: row-streaming 64 -> 64 channel 3x3 weight gradient (wgrad cfg 8); S slabs
 bool wgrad_res64_supported(const ConvGeom& g);
-void wgrad_res64(const bf16_t* X, const bf16_t* DY, const WgradDst& dst, const ConvGeom& g, int S,
+void wgrad_res64(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                  hipStream_t st, const float* pre_sc = nullptr, const float* pre_sh = nullptr);
-void wgrad_halo(const bf16_t* X, const bf16_t* DY, const WgradDst& dst, const ConvGeom& g, int S,
+void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
                 const float* pre_sh = nullptr);
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
@@ -146,8 +136,8 @@ void pack_weights_multi(const long long* desc, const long long* prefix, int nl, 
 void pack_weights_tiled(const long long* desc, const int* tprefix, int nl, int ntiles,
                         hipStream_t st);
 int igemm_fwd_rowtile(int cfg);
-void igemm_wgrad(const bf16_t* X, const bf16_t* DY, const WgradDst& dst, const ConvGeom& g,
-                 int S, long long mchunk, int cfg, hipStream_t st);
+void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                 long long mchunk, int cfg, hipStream_t st);
 void wgrad_reduce(const float* slab, int S, int Cout, int C, int Cin, int KH, int KW, float* dw,
                   float beta, hipStream_t st);
 void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int Cpad, int KH,

@@ -47,7 +47,7 @@ __device__ __forceinline__ s4 tr_read(const bf16_t* p) {
 // row of 3 taps (smaller halo, 3x more output tiles -> 3x fewer m-splits and slab bytes)
 template <int HRN, int NTY, bool PRE>
 __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, WgradDst dst,
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int xy, int gx, int nz) {
   // pre_sc/pre_sh (optional): X is the previous conv's raw output; the operand is
@@ -183,9 +183,8 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     if (s + 1 < nsteps) store(buf ^ 1, m0 + WBK);
     __syncthreads();
   }
-  // slab[z][co][tap*C + c] or OIHW atomics; 16x16 C map: col = lane & 15 (channel),
-  // row = (lane>>4)*4 + r (co)
-  const long long zoff = (long long)bz * g.Ncols * g.K;
+  // slab[z][co][tap*C + c]; 16x16 C map: col = lane & 15 (channel), row = (lane>>4)*4 + r (co)
+  float* out = slab + (long long)bz * g.Ncols * g.K;
   const int c = cc0 + wid * 16 + (lane & 15);
   const int t0 = (dy_lo + 1) * 3;  // global tap index of the block's first tap
 #pragma unroll
@@ -195,12 +194,12 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + i * 16 + (lane >> 4) * 4 + r;
-        if (co < g.Ncols) wgrad_put(dst, zoff, co, g.K, t0 + t, c, acc[i][t][r]);
+        if (co < g.Ncols) out[(long long)co * g.K + (t0 + t) * g.C + c] = acc[i][t][r];
       }
 }
 
 template <int HRN, int NTY>
-void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, const WgradDst& slab, const ConvGeom& g, int S,
+void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                        long long mchunk, hipStream_t st, const float* pre_sc,
                        const float* pre_sh) {
   const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
@@ -234,7 +233,7 @@ bool wgrad_halo_supported(const ConvGeom& g) {
   return WBK + 2 * g.W + 2 <= 6 * 32;
 }
 
-void wgrad_halo(const bf16_t* X, const bf16_t* DY, const WgradDst& slab, const ConvGeom& g, int S,
+void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc,
                 const float* pre_sh) {
   if (nty == 1) {

@@ -63,7 +63,7 @@ __device__ __forceinline__ s4 qtr(unsigned lds_byte) {
 
 template <bool PRE>
 __global__ void __launch_bounds__(512, 2) wgrad_res64_kernel(
-    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, WgradDst dst,
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, unsigned xbytes, unsigned dybytes, const float* __restrict__ pre_sc,
     const float* __restrict__ pre_sh, int nrows) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -261,9 +261,8 @@ __global__ void __launch_bounds__(512, 2) wgrad_res64_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the prefetches past the range
 
-  // slab[b][co][tap*64 + c] or OIHW atomics; 16x16 C map: col = lane & 15 (c),
-  // row = (lane>>4)*4 + r (co)
-  const long long zoff = (long long)b * QC * 9 * QC;
+  // slab[b][co][tap*64 + c]; 16x16 C map: col = lane & 15 (c), row = (lane>>4)*4 + r (co)
+  float* out = slab + (long long)b * QC * 9 * QC;
   const int c = cb * 16 + (lane & 15);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -272,7 +271,7 @@ __global__ void __launch_bounds__(512, 2) wgrad_res64_kernel(
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int co = ch * 32 + i * 16 + (lane >> 4) * 4 + rr;
-        wgrad_put(dst, zoff, co, 9 * QC, t, c, acc[i][t][rr]);
+        out[co * 9 * QC + t * QC + c] = acc[i][t][rr];
       }
 }
 }  // namespace
@@ -286,7 +285,7 @@ bool wgrad_res64_supported(const ConvGeom& g) {
 }
 
 // S = slab count = workgroups (each owns a contiguous range of the N*H image rows)
-void wgrad_res64(const bf16_t* X, const bf16_t* DY, const WgradDst& slab, const ConvGeom& g, int S,
+void wgrad_res64(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                  hipStream_t st, const float* pre_sc, const float* pre_sh) {
   if (!wgrad_res64_supported(g)) throw std::runtime_error("wgrad_res64: unsupported geometry");
   const int nrows = g.N * g.H;

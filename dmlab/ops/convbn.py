@@ -481,10 +481,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             for t in (x, dy) + (tuple(pre) if pre is not None else ()):
                 t.record_stream(side)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
-            # the m-splits add into the gradient with fp32 atomics (no slab, no reduce pass);
-            # torch.use_deterministic_algorithms(True) keeps the fixed-order slab reduce
-            det = s2d or torch.are_deterministic_algorithms_enabled()
-            slab = torch.empty(S * cout * K if det else 0, device=y.device, dtype=torch.float32)
+            slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
             pre_kw = {}
             xw = x
             if pre is not None:

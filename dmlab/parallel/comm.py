@@ -232,7 +232,9 @@ def allgather_average_gradients_reference_compat(model):
 class GradAggregator:
     """Callable gradient aggregation with communication timing (lab 2).
 
-    ``method``: ``allreduce`` | ``allgather`` | ``allgather_ref`` (B1 compat);
+    ``method``: ``allreduce`` | ``allgather`` | ``allgather_ref`` (B1 compat) |
+    ``allreduce_xgmi`` (the one-shot peer-memory kernel of :mod:`dmlab.parallel.xgmi` over
+    the flat gradient buffer, averaging folded into its epilogue: GPU ranks of one node);
     ``granularity``: ``flat`` (one coalesced collective) | ``per_param``.
 
     ``timing``:
@@ -270,6 +272,18 @@ class GradAggregator:
             allgather_average_gradients(self.model, self.granularity, force=self.force)
         elif self.method == "allgather_ref":
             allgather_average_gradients_reference_compat(self.model)
+        elif self.method == "allreduce_xgmi":
+            ws = env.get_world_size()
+            if ws <= 1 and not (self.force and env.is_initialized()):
+                return
+            flat = _flat_of_model(self.model)
+            if flat is None or not flat.grad.is_cuda:
+                raise ValueError("allreduce_xgmi: a Program model on a GPU")
+            if getattr(self, "_xgmi", None) is None:
+                from .xgmi import XGMIAllReduce
+
+                self._xgmi = XGMIAllReduce(cap=flat.grad.numel())
+            self._xgmi(flat.grad, scale=1.0 / ws)
         else:
             raise ValueError(self.method)
 

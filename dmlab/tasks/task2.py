@@ -45,7 +45,13 @@ def parse_args(argv=None):
     p.add_argument("--epochs", type=int, default=2)
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--momentum", type=float, default=0.9)
-    p.add_argument("--aggregation", default="allreduce", choices=["allreduce", "allgather", "allgather_ref"])
+    p.add_argument("--aggregation", default="allreduce",
+                   choices=["allreduce", "allgather", "allgather_ref", "allreduce_xgmi"],
+                   help="allreduce_xgmi: the one-shot xGMI peer-memory kernel over the flat "
+                        "gradient buffer (GPU ranks of one node)")
+    p.add_argument("--force-comm", action="store_true",
+                   help="at one rank with a process group (--backend nccl): run the collectives "
+                        "anyway, to measure the device communication path on a single GPU")
     p.add_argument("--granularity", default="flat", choices=["flat", "per_param"])
     p.add_argument("--straggler-rank", type=int, default=None)
     p.add_argument("--straggler-delay-ms", type=float, default=100.0)
@@ -71,7 +77,7 @@ def run(a):
     loader = DeviceLoader(train_set.to(dev), a.batch_size, sampler=sampler)
     opt = SGD(model.parameters(), lr=a.lr, momentum=a.momentum)
     comm.init_parameters(model)                       # task2/model.py:46
-    agg = comm.GradAggregator(model, a.aggregation, a.granularity)
+    agg = comm.GradAggregator(model, a.aggregation, a.granularity, force=a.force_comm)
     strag = Straggler(a.straggler_rank, a.straggler_delay_ms, a.straggler_mode)
     stats = train(model, loader, CrossEntropyLoss(), opt, a.epochs, rank=rank, aggregate=agg,
                   straggler=strag, batch_size=a.batch_size, max_steps=a.max_steps)

@@ -46,9 +46,7 @@ def _grads_resnet(ddp_kw, force):
 
 def scenario_resnet_fp32():
     """(a) ResNet-18 DDP, side-stream bucket hooks, fp32 RCCL all-reduce of every bucket ==
-    the no-communication run, bit for bit (SUM over one rank is the identity; the weight
-    gradients use the deterministic slab reduce so two runs can be compared bitwise)."""
-    torch.use_deterministic_algorithms(True, warn_only=True)
+    the no-communication run, bit for bit (SUM over one rank is the identity)."""
     ddp, g1, p1 = _grads_resnet({}, True)
     assert ddp._native is not None and ddp.side_stream_hooks
     launched = ddp.buckets_launched
@@ -62,7 +60,6 @@ def scenario_resnet_fp32():
 def scenario_resnet_bf16():
     """(a) bf16 gradient communication through the persistent comm buffer: the reduced
     gradient is exactly the bf16 rounding of the local one (first step; same init)."""
-    torch.use_deterministic_algorithms(True, warn_only=True)
     ddp, g1, _ = _grads_resnet({"comm_dtype": torch.bfloat16}, True)
     assert ddp._comm_flat is not None and ddp.side_stream_hooks
     _, g0, _ = _grads_resnet({}, False)

@@ -174,36 +174,6 @@ def test_conv_wgrad_halo(dev, geom, cfg, S):
     assert _rel(d, ref) < 2e-3
 
 
-@pytest.mark.parametrize("geom", GEOMS + [g for g in HALO_GEOMS if g[4] == 3])
-@pytest.mark.parametrize("beta", [0.0, 1.0])
-def test_conv_wgrad_atomic_finish(dev, geom, beta):
-    """The atomic finish (an EMPTY slab: every m-split adds into the OIHW gradient with fp32
-    atomics, no reduce pass) == the fixed-order slab reduce, for the v2 igemm tiles (2/3/6),
-    the halo kernels (4/5) and the layer-1 row-streaming kernel (8), beta 0 and 1."""
-    from dmlab.ops.convbn import _wgrad_plan
-
-    N, H, Cin, Cout, k, s, p = geom
-    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
-    OH = (H + 2 * p - k) // s + 1
-    dy = _nhwc(torch.randn(N, Cout, OH, OH, device=dev).bfloat16())
-    K = k * k * _cpad(Cin)
-    cfgs = [2 if Cout % 128 == 0 else 3, 3, 6]
-    if k == 3 and s == 1 and Cin % 64 == 0:
-        cfgs += [4, 5]
-    if k == 3 and s == 1 and Cin == 64 and Cout == 64 and OH <= 60:
-        cfgs.append(8)
-    base = torch.randn_like(w)
-    for cfg in cfgs:
-        S = 5 if cfg != 8 else min(5, N * OH)
-        slab = torch.empty(S * Cout * K, device=dev)
-        d_slab, d_atom = base.clone(), base.clone()
-        lib().conv_wgrad(xn, dy, d_slab, slab, Cin, k, k, s, p, beta, S, cfg, False)
-        lib().conv_wgrad(xn, dy, d_atom, torch.empty(0, device=dev), Cin, k, k, s, p, beta, S,
-                         cfg, False)
-        assert _rel(d_atom, d_slab) < 1e-5, (cfg, _rel(d_atom, d_slab))
-    assert _wgrad_plan(N * OH * OH, Cout, K, k, s, Cin)[1] >= 1
-
-
 @pytest.mark.parametrize("C,M", [(64, 4096), (512, 98), (128, 1000)])
 @pytest.mark.parametrize("relu,res", [(True, False), (True, True), (False, False)])
 def test_bn_forward_backward(dev, C, M, relu, res):

@@ -90,3 +90,36 @@ def test_bench_force_comm_lenet_graph():
     res = _bench(["--model", "lenet", "--steps", "50", "--warmup", "5"])
     assert res["config"]["hip_graph"] is True and res["config"]["fused_step"] is True
     assert res["replicas_in_sync"] is True and res["value"] > 0
+
+
+def _task2(nproc, args, extra_env=None, timeout=300):
+    import re
+
+    env = dict(os.environ, PYTHONPATH=str(ROOT), OMP_NUM_THREADS="2", **(extra_env or {}))
+    cmd = ([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+            str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(free_port())]
+           if nproc > 1 else [sys.executable])
+    if nproc == 1:
+        args = args + ["--master_port", str(free_port())]
+    r = subprocess.run(cmd + ["-m", "dmlab.tasks.task2", "--device", "cuda", "--synthetic",
+                              "--epochs", "1", "--max-steps", "60", "--no-test"] + args,
+                       env=env, capture_output=True, text=True, timeout=timeout, cwd=str(ROOT))
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    losses = [float(v) for v in re.findall(r"Device: 0 epoch: \d+, iters:\s+\d+, loss: (\d+\.\d+)",
+                                           r.stdout)]
+    comm = float(re.search(r"Total communication time: ([\d.eE+-]+)", r.stdout).group(1))
+    return losses, comm
+
+
+def test_task2_rccl_one_rank_forced():
+    """Lab 2's aggregation through a 1-rank RCCL communicator (task2 --backend nccl
+    --force-comm): every collective issued and timed on the device path."""
+    for agg in ("allreduce", "allgather"):
+        losses, comm = _task2(1, ["--backend", "nccl", "--force-comm", "--aggregation", agg])
+        assert len(losses) == 3 and comm > 0
+
+
+def test_task2_xgmi_kernel_two_ranks():
+    """Lab 2's all-reduce on the one-shot xGMI peer-memory kernel, two ranks sharing the GPU."""
+    losses, comm = _task2(2, ["--aggregation", "allreduce_xgmi"], {"DMLAB_BACKEND": "gloo"})
+    assert len(losses) == 3 and losses[-1] < losses[0] + 0.5 and comm > 0

@@ -146,3 +146,21 @@ def test_aggregator_timing_flags():
     assert GradAggregator(m).timing == "events"
     assert GradAggregator(m, sync_timing=True).timing == "sync"
     assert GradAggregator(m, sync_timing=False).timing == "host"
+
+
+def test_import_raises_hip_hw_queues():
+    """`import dmlab` gives each process 8 HIP hardware queues (before the runtime starts) so
+    the main, weight-gradient, downsample and RCCL streams do not share a queue; an explicit
+    larger value is kept."""
+    import os
+    import subprocess
+    import sys
+
+    code = "import os, dmlab; print(os.environ['GPU_MAX_HW_QUEUES'])"
+    for given, want in ((None, "8"), ("4", "8"), ("16", "16")):
+        env = {k: v for k, v in os.environ.items() if k != "GPU_MAX_HW_QUEUES"}
+        if given:
+            env["GPU_MAX_HW_QUEUES"] = given
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True,
+                             text=True, cwd=str(__import__("pathlib").Path(__file__).parent.parent))
+        assert out.stdout.strip() == want, (given, out.stdout, out.stderr[-500:])

@@ -186,12 +186,36 @@ def exp_comm(a, out):
                             "comm_fraction": s["comm_time"] / max(s["train_time"], 1e-9),
                             "samples_per_s": s["samples_per_s"], "final_loss":
                                 (s["losses"] or [None])[-1]})
+    if a.device == "cuda":
+        # the DEVICE communication paths a one-GPU box can run: the one-shot xGMI peer-memory
+        # kernel between two ranks sharing the GPU (IPC-mapped buffers, no host staging), and
+        # RCCL itself through a 1-rank communicator (every collective issued, no link traffic)
+        for path, ws, agg, gran, extra in (
+                ("xgmi kernel", 2, "allreduce_xgmi", "flat", []),
+                ("rccl 1-rank", 1, "allreduce", "flat", ["--backend", "nccl", "--force-comm"]),
+                ("rccl 1-rank", 1, "allreduce", "per_param", ["--backend", "nccl", "--force-comm"]),
+                ("rccl 1-rank", 1, "allgather", "flat", ["--backend", "nccl", "--force-comm"]),
+                ("rccl 1-rank", 1, "allgather", "per_param", ["--backend", "nccl", "--force-comm"])):
+            with tempfile.TemporaryDirectory() as td:
+                js = Path(td) / "s.json"
+                args = ["--device", "cuda", "--synthetic", "--aggregation", agg, "--granularity",
+                        gran, "--max-steps", str(a.steps2), "--no-test", "--epochs", "1",
+                        "--json", str(js)] + extra
+                o, dt = run_task("task2", args, nproc=ws)
+                s = json.loads(js.read_text())
+            res.append({"world_size": ws, "aggregation": agg, "granularity": gran, "path": path,
+                        "steps": s["steps"], "comm_s": s["comm_time"], "train_s": s["train_time"],
+                        "comm_ms_per_step": 1e3 * s["comm_time"] / max(s["steps"], 1),
+                        "comm_fraction": s["comm_time"] / max(s["train_time"], 1e-9),
+                        "samples_per_s": s["samples_per_s"],
+                        "final_loss": (s["losses"] or [None])[-1]})
     (out / "b_comm.json").write_text(json.dumps(res, indent=1))
+    res_pg = [r for r in res if "path" not in r]
     labels = [f"ws={w}" for w in a.world_sizes]
     groups = {}
     for agg in ("allreduce", "allgather"):
         for gran in ("flat", "per_param"):
-            groups[f"{agg}/{gran}"] = [r["comm_ms_per_step"] for w in a.world_sizes for r in res
+            groups[f"{agg}/{gran}"] = [r["comm_ms_per_step"] for w in a.world_sizes for r in res_pg
                                        if r["world_size"] == w and r["aggregation"] == agg
                                        and r["granularity"] == gran]
     _bars(out / "b_comm.png", labels, groups, "communication ms / step",
@@ -306,11 +330,21 @@ def write_report(out, R, a):
     if "b" in R:
         L += ["## (b) Aggregation primitives: communication cost (checking.tex:20-21)", "",
               "![](b_comm.png)", "",
-              "| ranks | aggregation | granularity | comm ms/step | comm fraction | samples/s |",
-              "|---|---|---|---|---|---|"]
+              "| ranks | path | aggregation | granularity | comm ms/step | comm fraction | samples/s |",
+              "|---|---|---|---|---|---|---|"]
         for r in R["b"]:
-            L.append(f"| {r['world_size']} | {r['aggregation']} | {r['granularity']} | "
+            path = r.get("path", "process group (gloo, host-staged)" if a.device == "cuda"
+                         else "process group")
+            L.append(f"| {r['world_size']} | {path} | {r['aggregation']} | {r['granularity']} | "
                      f"{r['comm_ms_per_step']:.3f} | {r['comm_fraction']:.2f} | {r['samples_per_s']:.0f} |")
+        if a.device == "cuda":
+            L += ["", "Device paths on this one-GPU box: `xgmi kernel` = the one-shot peer-memory "
+                  "all-reduce (`csrc/comm_xgmi.hip`) between two ranks sharing the GPU through "
+                  "IPC-mapped buffers, one kernel per aggregation, timed with HIP events; `rccl "
+                  "1-rank` = the same aggregation calls issued to a 1-rank RCCL communicator "
+                  "(`task2 --backend nccl --force-comm`): RCCL's launch and synchronisation cost "
+                  "per collective without link traffic, i.e. the floor of what the flat and "
+                  "per-parameter call patterns pay on xGMI."]
         L.append("")
     if "c" in R:
         L += ["## (c) Bottleneck node (checking.tex:22)", "", "![](c_straggler.png)", "",
