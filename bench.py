@@ -25,6 +25,7 @@ communication left exposed after backward / optimizer, HIP events over a few ext
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -92,6 +93,11 @@ def parse():
     ap.add_argument("--dataset-batches", type=int, default=2,
                     help="ResNet-18: dataset size in per-rank batches (x world size images, "
                          "held on every GPU)")
+    ap.add_argument("--stream-priority", default="high", choices=["normal", "high"],
+                    help="high (default): run the step on a high-priority stream "
+                         "(dmlab.utils.streams): the critical path gets workgroups ahead of the "
+                         "weight-gradient stream; +1.3 %% on one MI355X, 51.1-51.5k vs 50.5-50.7k "
+                         "img/s interleaved (profiles/stream_priority_ab_r4d.txt)")
     ap.add_argument("--pg-timeout", type=float, default=120.0,
                     help="process-group timeout (s): a hung collective fails the run fast")
     ap.add_argument("--fused", type=int, default=-1,
@@ -277,17 +283,25 @@ def main():
                 epoch_state["it"] = None
                 epoch_state["epoch"] += 1
 
-    for i in range(a.warmup):
-        loss = step(i)
-    torch.cuda.synchronize()
-    env.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    env.barrier()
-    torch.cuda.synchronize()
+    run_ctx = contextlib.nullcontext()
+    if a.stream_priority == "high":
+        from dmlab.utils.streams import compute_stream
+
+        cs = compute_stream(dev)
+        cs.wait_stream(torch.cuda.current_stream())
+        run_ctx = torch.cuda.stream(cs)
+    with run_ctx:
+        for i in range(a.warmup):
+            loss = step(i)
+        torch.cuda.synchronize()
+        env.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            loss = step(i)
+        torch.cuda.synchronize()
+        env.barrier()
+        torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if ws > 1:
         t = torch.tensor([dt], device=dev)
@@ -346,6 +360,7 @@ def main():
                 "fused_step": bool(fused is not None),
                 "ddp_side_stream_hooks": (net.side_stream_hooks if comm else None),
                 "hip_graph": a.graph,
+                "stream_priority": a.stream_priority,
                 "sampler": ("MySampler(partition)" if loader is not None else None),
             },
             "final_loss": round(final_loss, 4),

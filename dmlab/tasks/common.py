@@ -15,11 +15,28 @@ and evaluation counts correct predictions on the device (K26).
 """
 from __future__ import annotations
 
+import contextlib
 import time
 
 import torch
 
 from dmlab.nn.loss import count_correct
+
+
+def _step_stream(model):
+    """Training runs on a high-priority stream on the GPU (dmlab.utils.streams): the
+    critical path's workgroups go ahead of the weight-gradient side stream's."""
+    try:
+        p = next(model.parameters())
+    except (StopIteration, AttributeError):
+        return contextlib.nullcontext()
+    if not p.is_cuda:
+        return contextlib.nullcontext()
+    from dmlab.utils.streams import compute_stream
+
+    st = compute_stream(p.device)
+    st.wait_stream(torch.cuda.current_stream(p.device))
+    return torch.cuda.stream(st)
 
 
 def train(model, loader, loss_fn, optimizer, num_epochs=2, *, rank=None, aggregate=None,
@@ -35,6 +52,19 @@ def train(model, loader, loss_fn, optimizer, num_epochs=2, *, rank=None, aggrega
         print_fn("Start training ...")
     model.train()
     stats = {"losses": [], "steps": 0, "samples": 0, "comm_time": 0.0}
+    with _step_stream(model):
+        _train_loop(model, loader, loss_fn, optimizer, num_epochs, stats, rank, aggregate,
+                    straggler, log_every, writer, batch_size, max_steps, print_fn, task1_format,
+                    after_step)
+    print_fn("Training Finished!")
+    if writer is not None:
+        writer.flush()
+    return stats
+
+
+def _train_loop(model, loader, loss_fn, optimizer, num_epochs, stats, rank, aggregate,
+                straggler, log_every, writer, batch_size, max_steps, print_fn, task1_format,
+                after_step):
     loss_acc = None
     train_cnt = 0
     t0 = time.perf_counter()
@@ -86,10 +116,6 @@ def train(model, loader, loss_fn, optimizer, num_epochs=2, *, rank=None, aggrega
     stats["steps"] = step
     if aggregate is not None and hasattr(aggregate, "comm_time"):
         stats["comm_time"] = aggregate.comm_time  # event-timed aggregators report here
-    print_fn("Training Finished!")
-    if writer is not None:
-        writer.flush()
-    return stats
 
 
 def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, log_every=20,

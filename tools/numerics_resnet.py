@@ -66,10 +66,11 @@ def run(batch, steps, res, nbatches=4, lr=0.1, seed=0, classes=1000, log=print):
                 rec[k + "_gnorm"] = {n: float(p.grad.float().norm())
                                      for n, p in m.named_parameters() if p.grad is not None}
             opts[k].step()
-            rec[k] = float(loss)
+            rec[k] = float(loss.detach())
         hist.append(rec)
         log(json.dumps({kk: (round(v, 5) if isinstance(v, float) else v)
                         for kk, v in rec.items() if not kk.endswith("gnorm")}))
+        sys.stdout.flush()
     return models, hist
 
 
