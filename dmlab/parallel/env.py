@@ -105,6 +105,14 @@ def init(world_size: int | None = None, rank: int | None = None, master_addr: st
                       timeout=datetime.timedelta(seconds=timeout_s))
             if backend == "nccl":
                 kw["device_id"] = _DEVICE
+                # RCCL on a high-priority stream: the training step's critical path already
+                # runs at high priority (dmlab.utils.streams), and the bucket all-reduces must
+                # keep progressing next to it rather than queue behind the weight gradients
+                opts = getattr(dist, "ProcessGroupNCCL", None)
+                if opts is not None and hasattr(opts, "Options"):
+                    o = opts.Options()
+                    o.is_high_priority_stream = True
+                    kw["pg_options"] = o
             dist.init_process_group(**kw)
         assert dist.is_initialized(), "Error! The distributed env is not initialized!"
     return _DEVICE

@@ -140,8 +140,10 @@ def run_pipeline(a):
     module = (SubNetConv(1) if rank == 0 else SubNetFC(10)).to(dev)
     opt = SGD(module.parameters(), lr=a.lr, momentum=a.momentum)
     # every batch one shape (drop_last): message shapes are negotiated once and cached
+    # ring slots sized for the largest message: a (batch, 400) fp32 activation / gradient
+    cap = max(1 << 20, a.batch_size * 400 * 4)
     stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
-                          transport=a.transport, timing=bool(a.bench_json))
+                          transport=a.transport, timing=bool(a.bench_json), cap_bytes=cap)
     train_loader, test_loader = _data(a, dev, drop_last=True, test_batch=16) if rank == 0 \
         else (None, None)
     nsteps = len(train_loader) if rank == 0 else 0

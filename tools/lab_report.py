@@ -314,7 +314,7 @@ def write_report(out, R, a):
          ("gloo on the CPU." if a.device == "cpu" else
           "all ranks on the box's one MI355X (native HIP kernels; gloo process groups, since RCCL "
           "rejects two ranks on one GPU, so device tensors are staged through the host for the "
-          "collectives: the communication times are those of that path, not of xGMI)."), ""]
+          "collectives: the communication times are those of that path, except the device-path rows of (b): the xGMI peer-memory kernel and a 1-rank RCCL communicator)."), ""]
     if "a" in R:
         L += ["## (a) Optimisers: loss curves (checking.tex:8)", "",
               "![](a_optimizers.png)", "", "| optimiser | first loss | last loss | test accuracy |",
