@@ -97,8 +97,7 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 # (profiles/wgrad_blocks_r2c.jsonl, one call): 512 -> 44.2/44.4k img/s, 384 44.2k,
 # 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k; at 1024 images per GPU 512 -> 46.6k,
 # 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl)
-_WGRAD_BLOCKS = int(os.environ.get("DMLAB_TUNE_WGRAD_BLOCKS", "512"))  # TEMP sweep (r4)
-_WRES64_EIGHTHS = int(os.environ.get("DMLAB_TUNE_WRES64_EIGHTHS", "5"))  # TEMP sweep (r4)
+_WGRAD_BLOCKS = 512
 _CUS = {}
 
 
@@ -129,7 +128,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # ``tail``: the last conv before the stem, whose weight gradient runs next to the stem's
         # fused BN-backward + weight-gradient kernel at the end of the step, not next to a
         # dgrad chain: there it takes every CU
-        S = _cu_count() if tail else max(1, _cu_count() * _WRES64_EIGHTHS // 8)
+        S = _cu_count() if tail else max(1, _cu_count() * 5 // 8)
         return 8, max(1, min(rows, S))
     if force is not None:
         cfg = force
@@ -372,11 +371,12 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
         if mask is None:
             return {}
     # layer1's identity-block dgrads (res64 with the fused skip add, reducing the previous
-    # block's or the stem's BN): correct (tests) but 0.3% slower per step -- the add/mask
-    # epilogue costs the kernel ~100 us, more than the contended pass it saves
-    # (profiles/dgrad_bn_reduce_ab_r3s3.txt, red9); ``allow_res64_add`` (tests) opts in
-    if cfg == 80 and (mask is not None or pool) and not allow_res64_add and not (
-            pool and os.environ.get("DMLAB_TUNE_RES64_POOLRED") == "1"):  # TEMP sweep (r4)
+    # block's BN): correct (tests) but 0.3% slower per step -- the add/mask epilogue costs
+    # the kernel ~100 us, more than the contended pass it saves (profiles/
+    # dgrad_bn_reduce_ab_r3s3.txt, red9); ``allow_res64_add`` (tests) opts in.  The STEM's
+    # pooled-grid sums in the last layer-1 dgrad do pay: +0.5 % (the separate pooled reduce ran
+    # next to the full-CU tail weight gradient at ~2 TB/s; profiles/side_stream_sweep_r4f.txt)
+    if cfg == 80 and mask is not None and not pool and not allow_res64_add:
         return {}
     N, H, W, C = dx.shape
     rows = L.conv_stats_rows(N * H * W, cfg, C)

@@ -385,6 +385,7 @@ def test_dgrad_red_selection():
     c = ctx(has_res=True, mask=True)
     assert CB._dgrad_red(L, (relu, c), 42, 1, dx)["red_mask"] is c["mask"]
     assert CB._dgrad_red(L, (relu, ctx(has_res=True, mask=True)), 80, 1, dx) == {}
-    assert CB._dgrad_red(L, (stem, ctx(pool=True)), 80, 1, dx) == {}
-    c = ctx(pool=True)
-    assert CB._dgrad_red(L, (stem, c), 80, 1, dx, allow_res64_add=True)["red_y"] is c["yarg"]
+    c = ctx(pool=True)  # the stem's pooled-grid sums: reduced in the last layer-1 dgrad
+    assert CB._dgrad_red(L, (stem, c), 80, 1, dx)["red_y"] is c["yarg"]
+    c = ctx(has_res=True, mask=True)
+    assert CB._dgrad_red(L, (relu, c), 80, 1, dx, allow_res64_add=True)["red_mask"] is c["mask"]

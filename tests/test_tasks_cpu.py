@@ -67,6 +67,16 @@ def test_task2_spawn_allgather_straggler(tmp_path):
     assert "Total communication time:" in out and "Training time:" in out
 
 
+def test_task2_force_comm_one_rank(tmp_path):
+    """task2 --force-comm at one rank: the aggregation collectives run through a 1-rank
+    process group (gloo here; RCCL on the GPU box) and are timed."""
+    out = _run(["-m", "dmlab.tasks.task2", "--device", "cpu", "--backend", "gloo", "--force-comm",
+                "--synthetic", "--train-samples", "1280", "--epochs", "1", "--master_port",
+                str(free_port()), "--no-test"], tmp_path)
+    t = float(re.search(r"Total communication time: ([\d.eE+-]+)", out).group(1))
+    assert t > 0 and "Device: 0 epoch: 1, iters:    20" in out
+
+
 def test_task3_torchrun_random_sampler(tmp_path):
     out = _run(["-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
                 "127.0.0.1", "--master-port", str(free_port()), "-m", "dmlab.tasks.task3",
