@@ -198,6 +198,28 @@ void gemm(at::Tensor A, c10::optional<at::Tensor> Amask, at::Tensor B, c10::opti
                    S > 1 ? part.data_ptr<float>() : nullptr, S, cur_stream());
 }
 
+// ------------------------------------------------------------ CU-masked streams
+// A stream whose kernels may only use the CUs set in `mask` (32 CUs per word).  Its own
+// hardware queue carries the mask, so two processes on one GPU can each own a disjoint CU
+// partition: the lab-4 pipeline uses it to give every stage a "device" of its own.
+int64_t cu_mask_stream(std::vector<int64_t> mask) {
+  TORCH_CHECK(!mask.empty(), "empty CU mask");
+  std::vector<uint32_t> m(mask.begin(), mask.end());
+  hipStream_t st = nullptr;
+  TORCH_CHECK(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()) == hipSuccess,
+              "hipExtStreamCreateWithCUMask failed");
+  return (int64_t)(uintptr_t)st;
+}
+std::vector<int64_t> cu_mask_of(int64_t stream, int64_t words) {
+  std::vector<uint32_t> m((size_t)words, 0u);
+  TORCH_CHECK(hipExtStreamGetCUMask((hipStream_t)(uintptr_t)stream, (uint32_t)words, m.data()) ==
+              hipSuccess, "hipExtStreamGetCUMask failed");
+  return std::vector<int64_t>(m.begin(), m.end());
+}
+void stream_destroy(int64_t stream) {
+  TORCH_CHECK(hipStreamDestroy((hipStream_t)(uintptr_t)stream) == hipSuccess);
+}
+
 // ------------------------------------------------------------ xGMI one-/two-shot all-reduce
 int64_t xgmi_alloc(int64_t bytes) { return (int64_t)(uintptr_t)dm::xgmi_alloc((size_t)bytes); }
 void xgmi_free(int64_t ptr) { dm::xgmi_free((void*)(uintptr_t)ptr); }
@@ -418,6 +440,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("relu"), py::arg("lowp") = false);
   m.def("colsum", &colsum);
   m.def("bias_act", &bias_act, py::arg("y"), py::arg("bias"), py::arg("out"), py::arg("relu"));
+  m.def("cu_mask_stream", &cu_mask_stream);
+  m.def("cu_mask_of", &cu_mask_of);
+  m.def("stream_destroy", &stream_destroy);
   m.def("xgmi_alloc", &xgmi_alloc);
   m.def("xgmi_free", &xgmi_free);
   m.def("xgmi_get_handle", &xgmi_get_handle);

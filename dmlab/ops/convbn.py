@@ -127,7 +127,8 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # workgroup on every CU (128-192 of 256 tie; profiles/wgrad_res64_slabs_ab_r3s3.txt)
         # ``tail``: the last conv before the stem, whose weight gradient runs next to the stem's
         # fused BN-backward + weight-gradient kernel at the end of the step, not next to a
-        # dgrad chain: there it takes every CU
+        # dgrad chain: there it takes every CU (5/8 there, or the main stream instead of the
+        # side stream, measure the same or slower: profiles/tail_wgrad_placement_ab_r4i.txt)
         S = _cu_count() if tail else max(1, _cu_count() * 5 // 8)
         return 8, max(1, min(rows, S))
     if force is not None:

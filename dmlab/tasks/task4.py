@@ -50,6 +50,9 @@ def parse_args(argv=None):
     p.add_argument("--bench-json", default=None,
                    help="pipeline: write per-rank step ms, compute ms and bubble fraction "
                         "(HIP events) to <path>.rank<r>")
+    p.add_argument("--cu-partition", action="store_true",
+                   help="pipeline on one shared GPU: every stage runs on its own equal CU "
+                        "partition (a CU-masked stream), emulating one device per stage")
     p.add_argument("--batch-size", type=int, default=32)
     p.add_argument("--epochs", type=int, default=2)
     p.add_argument("--lr", type=float, default=0.01)
@@ -130,12 +133,21 @@ def run_rpc(a):
 
 
 def run_pipeline(a):
-    from dmlab.models import SubNetConv, SubNetFC
-    from dmlab.parallel.pipeline import PipelineStage
-
     dev = env.init(a.n_devices, a.rank, a.master_addr, a.master_port, device_type=a.device)
     rank, ws = env.get_rank(), env.get_world_size()
     assert ws == 2, "the LeNet pipeline has 2 stages"
+    if a.cu_partition and dev.type == "cuda":
+        from dmlab.utils.streams import partition_stream
+
+        with torch.cuda.stream(partition_stream(rank, ws, dev)):
+            return _run_pipeline(a, dev, rank, ws)
+    return _run_pipeline(a, dev, rank, ws)
+
+
+def _run_pipeline(a, dev, rank, ws):
+    from dmlab.models import SubNetConv, SubNetFC
+    from dmlab.parallel.pipeline import PipelineStage
+
     torch.manual_seed(0)
     module = (SubNetConv(1) if rank == 0 else SubNetFC(10)).to(dev)
     opt = SGD(module.parameters(), lr=a.lr, momentum=a.momentum)
@@ -183,6 +195,7 @@ def run_pipeline(a):
         else:  # CPU: wall time only (no device events)
             warm, step_ms, comp_ms, bubble = 0, 1e3 * dt / max(step, 1), float("nan"), float("nan")
         res = {"rank": rank, "stage": "conv" if rank == 0 else "fc", "schedule": a.schedule,
+               "cu_partition": bool(a.cu_partition and dev.type == "cuda"),
                "n_micro": a.micro, "transport": a.transport, "batch": a.batch_size,
                "steps_timed": step - warm, "step_ms": round(step_ms, 4),
                "compute_ms": round(comp_ms, 4), "bubble": round(bubble, 4),

@@ -23,3 +23,25 @@ def compute_stream(device=None) -> torch.cuda.Stream:
         lo, hi = torch.cuda.Stream.priority_range()  # (least, greatest): greatest is smaller
         st = _STREAMS[dev] = torch.cuda.Stream(device=dev, priority=min(lo, hi))
     return st
+
+
+def partition_stream(part: int, nparts: int, device=None) -> torch.cuda.ExternalStream:
+    """A stream restricted to CU partition ``part`` of ``nparts`` equal contiguous CU ranges.
+
+    Processes sharing one GPU that each run on a different partition do not compete for CUs,
+    so each sees a (smaller) device of its own: the lab-4 pipeline uses this to emulate
+    one-GPU-per-stage on a one-GPU box (``task4 --cu-partition``).  The stream has its own
+    hardware queue carrying the mask (``hipExtStreamCreateWithCUMask``)."""
+    from dmlab.ops._native import lib
+
+    if not 0 <= part < nparts:
+        raise ValueError(f"partition {part} of {nparts}")
+    dev = torch.cuda.current_device() if device is None else torch.device(device).index
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    lo, hi = part * ncu // nparts, (part + 1) * ncu // nparts
+    words = [0] * ((ncu + 31) // 32)
+    for c in range(lo, hi):
+        words[c // 32] |= 1 << (c % 32)
+    with torch.cuda.device(dev):
+        ptr = lib().cu_mask_stream(words)
+    return torch.cuda.ExternalStream(ptr, device=torch.device("cuda", dev))

@@ -195,11 +195,18 @@ def _entry(rank, ws, port, kind, q):
                 runs.append([p.detach().clone() for p in model.parameters()])
             err = max((a - b).abs().max().item() for a, b in zip(*runs))
             assert err == 0.0, err
-        elif kind in ("pipeline_xgmi", "pipeline_xgmi_gpipe"):
+        elif kind in ("pipeline_xgmi", "pipeline_xgmi_gpipe", "pipeline_xgmi_cupart"):
             # the native xGMI stage transport (IPC ring, device flags; the two ranks share
-            # the GPU here), prefetched receives, 1F1B / GPipe
-            from dmlab.parallel.pipeline import PipelineStage
+            # the GPU here), prefetched receives, 1F1B / GPipe; ``cupart``: every stage on its
+            # own half of the CUs (a CU-masked stream), as task4 --cu-partition
+            import contextlib
 
+            from dmlab.parallel.pipeline import PipelineStage
+            from dmlab.utils.streams import partition_stream
+
+            scope = (torch.cuda.stream(partition_stream(rank, 2, dev)) if kind.endswith("cupart")
+                     else contextlib.nullcontext())
+            scope.__enter__()
             mod = (SubNetConv() if rank == 0 else SubNetFC()).to(dev)
             sd = {k: v for k, v in ref.state_dict().items()
                   if k.startswith("conv" if rank == 0 else "fc")}
@@ -218,6 +225,7 @@ def _entry(rank, ws, port, kind, q):
             err = max((p - ref.get_parameter(n)).abs().max().item()
                       for n, p in mod.named_parameters())
             st.p2p.close()
+            scope.__exit__(None, None, None)
         else:
             from dmlab.parallel.pipeline import PipelineStage
 
@@ -245,7 +253,8 @@ def _entry(rank, ws, port, kind, q):
 @pytest.mark.parametrize("kind", ["ddp", "ddp_xgmi", "ddp_resnet", "ddp_resnet_xgmi2",
                                   "ddp_resnet_bf16", "pipeline",
                                   "xgmi", "xgmi_graph", "lenet_fused_ddp", "lenet_fused_ddp_xgmi",
-                                  "ddp_xgmi_graph", "pipeline_xgmi", "pipeline_xgmi_gpipe"])
+                                  "ddp_xgmi_graph", "pipeline_xgmi", "pipeline_xgmi_gpipe",
+                                  "pipeline_xgmi_cupart"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 
@@ -265,6 +274,30 @@ def test_two_ranks_one_gpu(kind):
     for rank, err, tb in res:
         assert tb is None, tb
         assert err < 2e-4, (rank, err)
+
+
+def test_partition_stream_mask_and_compute():
+    """A CU-masked stream reports the mask it was built with and computes correctly; the two
+    halves are disjoint and cover every CU."""
+    import torch
+
+    from dmlab.ops._native import lib
+    from dmlab.utils.streams import partition_stream
+
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    words = (ncu + 31) // 32
+    masks = []
+    for part in range(2):
+        st = partition_stream(part, 2)
+        m = lib().cu_mask_of(st.cuda_stream, words)
+        masks.append(sum(int(w) << (32 * i) for i, w in enumerate(m)))
+        a = torch.randn(512, 512, device="cuda")
+        with torch.cuda.stream(st):
+            c = a @ a
+        st.synchronize()
+        assert torch.allclose(c, (a.double() @ a.double()).float(), rtol=1e-3, atol=1e-2)
+    assert masks[0] & masks[1] == 0
+    assert bin(masks[0] | masks[1]).count("1") == ncu
 
 
 def test_rpc_stages_on_gpu(tmp_path):

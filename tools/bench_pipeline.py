@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--micro", default="1,4,8")
     ap.add_argument("--schedules", default="gpipe,1f1b")
     ap.add_argument("--out", default=None, help="append the JSON lines to this file")
+    ap.add_argument("--cu-partition", action="store_true",
+                    help="each stage on its own half of the CUs (one device per stage, emulated)")
     ap.add_argument("--epochs", type=int, default=0,
                     help="epochs of the 60k-sample synthetic set (0: enough for --steps)")
     a = ap.parse_args()
@@ -61,6 +63,8 @@ def main():
                        str(a.epochs or max(1, -(-a.steps * a.batch // 60000) + 1)),
                        "--transport", a.transport if a.device == "cuda" else "pg",
                        "--bench-json", str(js), "--no-test"]
+                if a.cu_partition:
+                    cmd.append("--cu-partition")
                 r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
                                    timeout=600)
                 if r.returncode != 0:
@@ -69,6 +73,7 @@ def main():
                 ranks = [json.loads((Path(td) / f"b.json.rank{k}").read_text()) for k in range(2)]
             row = {"schedule": sch, "n_micro": m, "batch": a.batch, "device": a.device,
                    "transport": ranks[0]["transport"],
+                   "cu_partition": ranks[0].get("cu_partition", False),
                    "step_ms": max(x["step_ms"] for x in ranks),
                    "samples_per_s": round(a.batch / max(x["step_ms"] for x in ranks) * 1e3, 1),
                    "stage_compute_ms": [x["compute_ms"] for x in ranks],

@@ -116,6 +116,19 @@ def main():
     ap.add_argument("--nbatches", type=int, default=4)
     ap.add_argument("--lr", type=float, default=0.1)
     a = ap.parse_args()
+    # first steps of the PyTorch backends can sit in MIOpen's kernel search for minutes at
+    # b1024: keep a heartbeat on stderr so a supervising runner does not take it as hung
+    import threading
+    import time
+
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(20)
+            print(f"[numerics] alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     models, hist = run(a.batch, a.steps, a.res, a.nbatches, a.lr)
     s = summarize(models, hist)
     s.update(batch=a.batch, steps=a.steps, res=a.res, lr=a.lr, nbatches=a.nbatches)
