@@ -97,7 +97,7 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 # (profiles/wgrad_blocks_r2c.jsonl, one call): 512 -> 44.2/44.4k img/s, 384 44.2k,
 # 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k; at 1024 images per GPU 512 -> 46.6k,
 # 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl)
-_WGRAD_BLOCKS = 512
+_WGRAD_BLOCKS = int(os.environ.get("DMLAB_TUNE_WBLK", "512"))  # TEMP A/B (r4)
 _CUS = {}
 
 

@@ -43,6 +43,13 @@ class _EventHandle:
         torch.cuda.current_stream().wait_event(self.ev)
 
 
+class _Done:
+    """Handle of a transfer already ordered on the current stream (inline mode)."""
+
+    def wait(self):
+        pass
+
+
 class _ShapeCache:
     """One header per key, exchanged over the process group (host sync on the receiver
     the first time only)."""
@@ -153,6 +160,10 @@ class XGMITransport:
                 mine[i] = ("free", self.L.xgmi_get_handle(base), base)
         allh = [None] * dist.get_world_size(group)
         dist.all_gather_object(allh, {i: (k, h) for i, (k, h, _) in mine.items()}, group=group)
+        # inline: run the channel kernels on the CURRENT stream instead of per-channel streams
+        # (a captured pipeline step is then one linear chain in program order; see
+        # PipelineStage.capture)
+        self.inline = False
         self.chan = {}
         for i, (s, d) in enumerate(links):
             if self.rank not in (s, d):
@@ -180,6 +191,10 @@ class XGMITransport:
         t = t.contiguous()
         if t.numel() * t.element_size() % 16:
             raise ValueError("xGMI p2p: message bytes must be a multiple of 16")
+        if self.inline:
+            self.L.p2p_xgmi_send(t, c["ring"], c["full"], c["free"], self.cap, self.nslot,
+                                 c["state"])
+            return works
         st = c["stream"]
         st.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(st):
@@ -195,6 +210,10 @@ class XGMITransport:
         shape, dtype = self.hdr.recv(src, key, device)
         c = self.chan[(src, self.rank)]
         buf = torch.empty(shape, dtype=dtype, device=self.device)
+        if self.inline:
+            self.L.p2p_xgmi_recv(buf, c["ring"], c["full"], c["free"], self.cap, self.nslot,
+                                 c["state"])
+            return buf, _Done()
         st = c["stream"]
         st.wait_stream(torch.cuda.current_stream())  # buf's allocation is ordered first
         with torch.cuda.stream(st):

@@ -76,6 +76,9 @@ class PipelineStage:
         self.timing = timing and torch.cuda.is_available() and self.device.type == "cuda"
         self._events = []
         self.history = []  # (start, end, compute events) of every timed step
+        self._linear = False  # no receive posted ahead (captured steps)
+        self._graph = None
+        self._time_replays = False
 
     # -------------------------------------------------------------- pieces
     def _post_recv(self, tag, m, src, ahead=False):
@@ -86,7 +89,7 @@ class PipelineStage:
         k = (tag, m)
         if k in self._posted:
             return
-        if ahead and not self.p2p.known(k):
+        if ahead and (self._linear or not self.p2p.known(k)):
             return
         self._posted[k] = self.p2p.recv(src, k, self.device)
 
@@ -193,9 +196,63 @@ class PipelineStage:
             return torch.stack(losses).sum()
         return None
 
+    # -------------------------------------------------------------- hipGraph
+    def capture(self, x=None, y=None, n_micro: int = 1, warmup: int = 2):
+        """Capture one whole ``train_step`` (micro-batch schedule, channel kernels, backward,
+        optimiser) into a hipGraph; :meth:`replay` then runs a step as ONE graph launch, so
+        the per-micro-batch host work (a Python schedule, ~15 kernel launches and the
+        stream/event hops per message) is gone.  Needs the xGMI transport (its message
+        counters live on the device) and every rank capturing with the same ``n_micro`` and
+        ``warmup``.
+
+        The captured step is one linear chain in program order: the channel kernels run
+        inline on the step's stream and no receive is posted ahead.  A graph executes its
+        independent branches in an order of the runtime's choosing; with receives that spin
+        on a peer, a branch order other than program order could wait on a message the peer
+        sends only after this stage's skipped-over work (a cross-process deadlock that the
+        bounded waits would turn into a timeout).  Program order with blocking receives and
+        buffered sends is deadlock-free for GPipe and 1F1B."""
+        if not isinstance(self.p2p, XGMITransport):
+            raise ValueError("PipelineStage.capture needs transport='xgmi'")
+        self._linear, self.p2p.inline = True, True
+        self._sx = x.detach().clone() if self.first else None
+        self._sy = y.detach().clone() if self.first else None
+        self._n_micro = n_micro
+        timed, self.timing = self.timing, False
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):  # shapes negotiated, optimiser state allocated
+                loss = self.train_step(self._sx, self._sy, n_micro)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize(self.device)
+        self._graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self._graph):
+            self._gout = self.train_step(self._sx, self._sy, n_micro)
+        self._time_replays = timed
+        return loss  # of the last warm-up step (the warm-up steps are real updates)
+
+    def replay(self, x=None, y=None):
+        """One captured step on new data (first stage: ``x``/``y``; others: nothing).  With
+        ``timing`` the step is bracketed by events (no per-compute events inside a graph:
+        :meth:`step_stats` then reports the step time only)."""
+        if self.first:
+            self._sx.copy_(x, non_blocking=True)
+            self._sy.copy_(y, non_blocking=True)
+        if self._time_replays:
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+        self._graph.replay()
+        if self._time_replays:
+            t1.record()
+            self._step_events = (t0, t1, [])
+            self.history.append(self._step_events)
+        return self._gout
+
     def step_stats(self, skip=None):
         """(step ms, compute ms, bubble fraction): of the last timed step, or averaged over
-        the timed steps after the first ``skip`` (synchronises once)."""
+        the timed steps after the first ``skip`` (synchronises once).  Captured steps carry
+        no compute events: compute and bubble are None."""
         steps = [self._step_events] if skip is None else self.history[skip:]
         steps[-1][1].synchronize()
         tot = comp = 0.0
@@ -203,6 +260,8 @@ class PipelineStage:
             tot += t0.elapsed_time(t1)
             comp += sum(s.elapsed_time(e) for s, e in evs)
         n = len(steps)
+        if not any(evs for _, _, evs in steps):
+            return tot / n, None, None
         return tot / n, comp / n, (max(0.0, 1.0 - comp / tot) if tot > 0 else 0.0)
 
     @torch.no_grad()

@@ -50,6 +50,9 @@ def parse_args(argv=None):
     p.add_argument("--bench-json", default=None,
                    help="pipeline: write per-rank step ms, compute ms and bubble fraction "
                         "(HIP events) to <path>.rank<r>")
+    p.add_argument("--graph", action="store_true",
+                   help="pipeline (xgmi transport, GPU): capture each stage's whole step in a "
+                        "hipGraph after the first step and replay it")
     p.add_argument("--cu-partition", action="store_true",
                    help="pipeline on one shared GPU: every stage runs on its own equal CU "
                         "partition (a CU-masked stream), emulating one device per stage")
@@ -158,6 +161,7 @@ def _run_pipeline(a, dev, rank, ws):
                           transport=a.transport, timing=bool(a.bench_json), cap_bytes=cap)
     train_loader, test_loader = _data(a, dev, drop_last=True, test_batch=16) if rank == 0 \
         else (None, None)
+    graph = bool(a.graph) and a.transport == "xgmi" and dev.type == "cuda"
     nsteps = len(train_loader) if rank == 0 else 0
     nsteps = int(_bcast_scalar(nsteps, dev))
     print("Device {} starts training ...".format(rank))
@@ -170,7 +174,12 @@ def _run_pipeline(a, dev, rank, ws):
             it = iter(train_loader)
         for i in range(nsteps):
             x, y = next(it) if rank == 0 else (None, None)
-            loss = stage.train_step(x, y, n_micro=a.micro)
+            if graph and stage._graph is None:  # step 0 runs eagerly, then the capture
+                loss = stage.capture(x, y, n_micro=a.micro, warmup=1)
+            elif graph:
+                loss = stage.replay(x, y)
+            else:
+                loss = stage.train_step(x, y, n_micro=a.micro)
             step += 1
             if stage.last:
                 acc = acc + loss.detach()
@@ -198,7 +207,8 @@ def _run_pipeline(a, dev, rank, ws):
                "cu_partition": bool(a.cu_partition and dev.type == "cuda"),
                "n_micro": a.micro, "transport": a.transport, "batch": a.batch_size,
                "steps_timed": step - warm, "step_ms": round(step_ms, 4),
-               "compute_ms": round(comp_ms, 4), "bubble": round(bubble, 4),
+               "compute_ms": None if comp_ms is None else round(comp_ms, 4),
+               "bubble": None if bubble is None else round(bubble, 4), "graph": graph,
                "samples_per_s": round(a.batch_size / step_ms * 1e3, 1), "wall_s": round(dt, 3)}
         with open(f"{a.bench_json}.rank{rank}", "w") as f:
             json.dump(res, f)

@@ -195,7 +195,8 @@ def _entry(rank, ws, port, kind, q):
                 runs.append([p.detach().clone() for p in model.parameters()])
             err = max((a - b).abs().max().item() for a, b in zip(*runs))
             assert err == 0.0, err
-        elif kind in ("pipeline_xgmi", "pipeline_xgmi_gpipe", "pipeline_xgmi_cupart"):
+        elif kind in ("pipeline_xgmi", "pipeline_xgmi_gpipe", "pipeline_xgmi_cupart",
+                      "pipeline_xgmi_graph"):
             # the native xGMI stage transport (IPC ring, device flags; the two ranks share
             # the GPU here), prefetched receives, 1F1B / GPipe; ``cupart``: every stage on its
             # own half of the CUs (a CU-masked stream), as task4 --cu-partition
@@ -214,13 +215,23 @@ def _entry(rank, ws, port, kind, q):
             st = PipelineStage(mod, SGD(mod.parameters(), lr=0.1, momentum=0.9), CrossEntropyLoss(),
                                device=dev, transport="xgmi", timing=True,
                                schedule="gpipe" if kind.endswith("gpipe") else "1f1b")
-            for _ in range(3):
-                st.train_step(X if rank == 0 else None, Y if rank == 0 else None, n_micro=4)
+            xs, ys = (X, Y) if rank == 0 else (None, None)
+            for i in range(3):
+                if kind.endswith("graph"):  # step 0 eager + capture, then two replays
+                    if i == 0:
+                        st.capture(xs, ys, n_micro=4, warmup=1)
+                    else:
+                        st.replay(xs, ys)
+                else:
+                    st.train_step(xs, ys, n_micro=4)
                 ropt.zero_grad()
                 cross_entropy(ref(X), Y).backward()
                 ropt.step()
             step_ms, comp_ms, bubble = st.step_stats()
-            assert 0.0 <= bubble < 1.0 and comp_ms > 0.0
+            if kind.endswith("graph"):
+                assert step_ms > 0.0 and comp_ms is None
+            else:
+                assert 0.0 <= bubble < 1.0 and comp_ms > 0.0
             st.p2p.check()
             err = max((p - ref.get_parameter(n)).abs().max().item()
                       for n, p in mod.named_parameters())
@@ -254,7 +265,7 @@ def _entry(rank, ws, port, kind, q):
                                   "ddp_resnet_bf16", "pipeline",
                                   "xgmi", "xgmi_graph", "lenet_fused_ddp", "lenet_fused_ddp_xgmi",
                                   "ddp_xgmi_graph", "pipeline_xgmi", "pipeline_xgmi_gpipe",
-                                  "pipeline_xgmi_cupart"])
+                                  "pipeline_xgmi_cupart", "pipeline_xgmi_graph"])
 def test_two_ranks_one_gpu(kind):
     import torch.multiprocessing as mp
 

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--micro", default="1,4,8")
     ap.add_argument("--schedules", default="gpipe,1f1b")
     ap.add_argument("--out", default=None, help="append the JSON lines to this file")
+    ap.add_argument("--graph", action="store_true",
+                    help="capture each stage's step in a hipGraph (xgmi transport)")
     ap.add_argument("--cu-partition", action="store_true",
                     help="each stage on its own half of the CUs (one device per stage, emulated)")
     ap.add_argument("--epochs", type=int, default=0,
@@ -65,6 +67,8 @@ def main():
                        "--bench-json", str(js), "--no-test"]
                 if a.cu_partition:
                     cmd.append("--cu-partition")
+                if a.graph:
+                    cmd.append("--graph")
                 r = subprocess.run(cmd, cwd=str(ROOT), env=env, capture_output=True, text=True,
                                    timeout=600)
                 if r.returncode != 0:
@@ -74,6 +78,7 @@ def main():
             row = {"schedule": sch, "n_micro": m, "batch": a.batch, "device": a.device,
                    "transport": ranks[0]["transport"],
                    "cu_partition": ranks[0].get("cu_partition", False),
+                   "graph": ranks[0].get("graph", False),
                    "step_ms": max(x["step_ms"] for x in ranks),
                    "samples_per_s": round(a.batch / max(x["step_ms"] for x in ranks) * 1e3, 1),
                    "stage_compute_ms": [x["compute_ms"] for x in ranks],

@@ -62,7 +62,7 @@ def run(batch, steps, res, nbatches=4, lr=0.1, seed=0, classes=1000, log=print):
                 loss = F.cross_entropy(m(x), y)
             opts[k].zero_grad()
             loss.backward()
-            if s == steps - 1:  # gradient norms of the last step, before the update
+            if s in (0, steps - 1):  # gradient norms of the first / last step, before the update
                 rec[k + "_gnorm"] = {n: float(p.grad.float().norm())
                                      for n, p in m.named_parameters() if p.grad is not None}
             opts[k].step()
@@ -78,12 +78,15 @@ def summarize(models, hist):
     def dist(a, b):
         return max(abs(h[a] - h[b]) for h in hist)
 
-    last = hist[-1]
-    gn = {}
-    for n in last["fp32_gnorm"]:
-        ref = last["fp32_gnorm"][n]
-        gn[n] = (abs(last["native_gnorm"][n] - ref) / max(ref, 1e-12),
-                 abs(last["autocast_gnorm"][n] - ref) / max(ref, 1e-12))
+    def gnorm_err(rec):
+        out = {}
+        for n in rec["fp32_gnorm"]:
+            ref = rec["fp32_gnorm"][n]
+            out[n] = (abs(rec["native_gnorm"][n] - ref) / max(ref, 1e-12),
+                      abs(rec["autocast_gnorm"][n] - ref) / max(ref, 1e-12))
+        return out
+
+    gn, gn0 = gnorm_err(hist[-1]), gnorm_err(hist[0])
     bn = {}
     for (n, b_nat), (_, b_ac), (_, b_32) in zip(models["native"].named_buffers(),
                                                 models["autocast"].named_buffers(),
@@ -103,6 +106,13 @@ def summarize(models, hist):
         "gnorm_rel_err_median": {
             "native": sorted(v[0] for v in gn.values())[len(gn) // 2],
             "autocast": sorted(v[1] for v in gn.values())[len(gn) // 2]},
+        # step 0: same weights and batch in all three, so this isolates the kernels' numerics
+        # from the divergence of the trajectories
+        "step0_gnorm_rel_err_max": {"native": max(v[0] for v in gn0.values()),
+                                    "autocast": max(v[1] for v in gn0.values())},
+        "step0_gnorm_rel_err_median": {
+            "native": sorted(v[0] for v in gn0.values())[len(gn0) // 2],
+            "autocast": sorted(v[1] for v in gn0.values())[len(gn0) // 2]},
         "bn_running_rel_err_max": {"native": max(v[0] for v in bn.values()),
                                    "autocast": max(v[1] for v in bn.values())},
     }
