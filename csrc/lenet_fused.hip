@@ -30,7 +30,7 @@
 namespace dm {
 
 namespace {
-constexpr int LT = 512;  // threads per sample workgroup
+constexpr int LT = 1024;  // threads per sample workgroup (16 waves: the long phases split)
 // per-sample conv gradient partials: conv2 w (2400), conv2 b (16), conv1 w (150), conv1 b (6)
 constexpr int CS = 2400 + 16 + 150 + 6;
 
@@ -66,7 +66,8 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __shared__ short pos2[400];              // p1 offset of the argmax conv2 output
   __shared__ float h1[128], lg[16], dl[16], dh1[128], g2[400], g1[6 * 196];
   __shared__ float dc2[16 * 18 * 18];      // unpooled conv2 gradient, 4-pixel zero border
-  __shared__ float4 red4[5 * 100];
+  __shared__ float4 red4[10 * 100];        // cross-thread partials (fc1 dgrad, conv2, conv1 dw)
+  __shared__ float4 pd4[2 * 294];          // conv2 dgrad partials of output-channel groups 1, 2
   float* red = reinterpret_cast<float*>(red4);
 
   // ---- stage input and the small weights (fc1's 192 KB stream from L2 instead) ----
@@ -112,13 +113,15 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   }
   __syncthreads();
 
-  // ---- conv2 (6 -> 16, 5x5) + bias + ReLU + 2x2 max-pool ----
-  if (tid < 400) {
-    const int o = tid / 25, r = tid - o * 25, py = r / 5, px = r - py * 5;
+  // ---- conv2 (6 -> 16, 5x5) + bias + ReLU + 2x2 max-pool: channels 0-2 and 3-5 on two
+  //      thread halves, the second half's partial sums added in a fixed order ----
+  {
+    const int t4 = tid % 400, cg = tid / 400;
+    const int o = t4 / 25, r = t4 - o * 25, py = r / 5, px = r - py * 5;
     float acc[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) acc[a] = bb2[o];
-    for (int c = 0; c < 6; ++c) {
+    for (int a = 0; a < 4; ++a) acc[a] = cg == 0 ? bb2[o] : 0.f;
+    for (int c = 3 * cg; c < (cg < 2 ? 3 * cg + 3 : 0); ++c) {
       float win[6][6];
 #pragma unroll
       for (int i = 0; i < 6; ++i)
@@ -133,36 +136,47 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
           for (int a = 0; a < 4; ++a) acc[a] += win[(a >> 1) + kh][(a & 1) + kw] * w;
         }
     }
-    float best = 0.f;
-    int code = -1;
+    if (cg == 1) red4[t4] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (cg == 0) {
+      const float4 h = red4[t4];
+      acc[0] += h.x;
+      acc[1] += h.y;
+      acc[2] += h.z;
+      acc[3] += h.w;
+      float best = 0.f;
+      int code = -1;
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
-      if (acc[a] > best) {
-        best = acc[a];
-        code = a;
-      }
-    p2[tid] = best;
-    pos2[tid] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 14 + 2 * px + (code & 1));
+      for (int a = 0; a < 4; ++a)
+        if (acc[a] > best) {
+          best = acc[a];
+          code = a;
+        }
+      p2[t4] = best;
+      pos2[t4] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 14 + 2 * px + (code & 1));
+    }
   }
   __syncthreads();
 
-  // ---- fc1 (400 -> 120) + ReLU: 4 threads per output, each 25 independent float4 loads of
-  //      its quarter row (all in flight together), combined by lane shuffles ----
-  if (tid < 480) {
-    const int u = tid >> 2, part = tid & 3;
-    const float4* wr = reinterpret_cast<const float4*>(f1w + u * 400) + part * 25;
-    const float4* hr = reinterpret_cast<const float4*>(p2) + part * 25;
-    float4 wv[25];
+  // ---- fc1 (400 -> 120) + ReLU: 8 threads per output, thread p loading float4 columns
+  //      p, p+8, ... of the row (all 12-13 in flight together; the 8 threads of an output
+  //      read 128 contiguous bytes per step), combined by lane shuffles ----
+  if (tid < 960) {
+    const int u = tid >> 3, part = tid & 7;
+    const float4* wr = reinterpret_cast<const float4*>(f1w + u * 400);
+    const float4* hr = reinterpret_cast<const float4*>(p2);
+    float4 wv[13];
 #pragma unroll
-    for (int j = 0; j < 25; ++j) wv[j] = wr[j];
+    for (int j = 0; j < 13; ++j) wv[j] = part + 8 * j < 100 ? wr[part + 8 * j] : make_float4(0.f, 0.f, 0.f, 0.f);
     float acc = 0.f;
 #pragma unroll
-    for (int j = 0; j < 25; ++j) {
-      const float4 h = hr[j];
+    for (int j = 0; j < 13; ++j) {
+      const float4 h = part + 8 * j < 100 ? hr[part + 8 * j] : make_float4(0.f, 0.f, 0.f, 0.f);
       acc += wv[j].x * h.x + wv[j].y * h.y + wv[j].z * h.z + wv[j].w * h.w;
     }
     acc += __shfl_xor(acc, 1, 64);
     acc += __shfl_xor(acc, 2, 64);
+    acc += __shfl_xor(acc, 4, 64);
     if (part == 0) h1[u] = fmaxf(acc + f1b[u], 0.f);
   }
   __syncthreads();
@@ -197,16 +211,16 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   }
   __syncthreads();
 
-  // ---- fc1 data gradient: thread (k4, u-group of 24) streams coalesced float4 rows ----
-  if (tid < 500) {
+  // ---- fc1 data gradient: thread (k4, u-group of 12) streams coalesced float4 rows ----
+  if (tid < 1000) {
     const int k4 = tid % 100, ug = tid / 100;
-    float4 wv[24];
+    float4 wv[12];
 #pragma unroll
-    for (int j = 0; j < 24; ++j) wv[j] = reinterpret_cast<const float4*>(f1w + (ug * 24 + j) * 400)[k4];
+    for (int j = 0; j < 12; ++j) wv[j] = reinterpret_cast<const float4*>(f1w + (ug * 12 + j) * 400)[k4];
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int j = 0; j < 24; ++j) {
-      const float d = dh1[ug * 24 + j];
+    for (int j = 0; j < 12; ++j) {
+      const float d = dh1[ug * 12 + j];
       a.x += d * wv[j].x;
       a.y += d * wv[j].y;
       a.z += d * wv[j].z;
@@ -217,7 +231,9 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __syncthreads();
   float* r = rec + (long long)b * 656;  // per-sample record: h0 | h1 | dh1 | dl (+ pad)
   if (tid < 400) {
-    const float d = red[tid] + red[400 + tid] + red[800 + tid] + red[1200 + tid] + red[1600 + tid];
+    float d = 0.f;
+#pragma unroll
+    for (int g = 0; g < 10; ++g) d += red[g * 400 + tid];
     const int ps = pos2[tid];
     const float gv = ps >= 0 ? d : 0.f;
     g2[tid] = gv;
@@ -253,11 +269,14 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     cs[2400 + tid] = acc;
   }
   // ---- conv2 data gradient (full correlation with the flipped kernel over the unpooled
-  //      gradient), 2x2 outputs per thread sharing a 6x6 window, then unpool1 ----
-  if (tid >= 200 && tid < 200 + 294) {
-    const int q = tid - 200, c = q / 49, rr = q - c * 49, by = rr / 7, bx = rr - by * 7;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int o = 0; o < 16; ++o) {
+  //      gradient), 2x2 outputs per thread sharing a 6x6 window, output channels split in
+  //      three groups (0-5, 6-10, 11-15) summed in a fixed order, then unpool1 ----
+  float dacc[4] = {0.f, 0.f, 0.f, 0.f};
+  const int dq = tid % 294, dgp = tid / 294;  // dgp 3 (tid >= 882): idle
+  if (dgp < 3) {
+    const int c = dq / 49, rr = dq - c * 49, by = rr / 7, bx = rr - by * 7;
+    const int o0 = dgp == 0 ? 0 : dgp == 1 ? 6 : 11, o1 = dgp == 0 ? 6 : dgp == 1 ? 11 : 16;
+    for (int o = o0; o < o1; ++o) {
       float win[6][6];
 #pragma unroll
       for (int i = 0; i < 6; ++i)
@@ -269,33 +288,43 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
         for (int kw = 0; kw < 5; ++kw) {
           const float w = w2[o * 150 + c * 25 + kh * 5 + kw];
 #pragma unroll
-          for (int a = 0; a < 4; ++a) acc[a] += win[(a >> 1) + 4 - kh][(a & 1) + 4 - kw] * w;
+          for (int a = 0; a < 4; ++a) dacc[a] += win[(a >> 1) + 4 - kh][(a & 1) + 4 - kw] * w;
         }
     }
+    if (dgp > 0) pd4[(dgp - 1) * 294 + dq] = make_float4(dacc[0], dacc[1], dacc[2], dacc[3]);
+  }
+  __syncthreads();
+  if (dgp == 0) {
+    const int c = dq / 49, rr = dq - c * 49, by = rr / 7, bx = rr - by * 7;
+    const float4 e1 = pd4[dq], e2 = pd4[294 + dq];
+    const float s[4] = {dacc[0] + e1.x + e2.x, dacc[1] + e1.y + e2.y, dacc[2] + e1.z + e2.z,
+                        dacc[3] + e1.w + e2.w};
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int idx = c * 196 + (2 * by + (a >> 1)) * 14 + 2 * bx + (a & 1);
-      g1[idx] = pos1[idx] >= 0 ? acc[a] : 0.f;
+      g1[idx] = pos1[idx] >= 0 ? s[a] : 0.f;
     }
   }
   __syncthreads();
 
-  // ---- conv1 weight/bias gradient partials: 150 weights x 196 pooled positions, 3 threads
+  // ---- conv1 weight/bias gradient partials: 150 weights x 196 pooled positions, 6 threads
   //      per weight, combined in a fixed order ----
-  if (tid < 450) {
-    const int i = tid / 3, part = tid - i * 3;
+  if (tid < 900) {
+    const int i = tid / 6, part = tid - i * 6;
     const int c = i / 25, t = i - c * 25, kh = t / 5, kw = t - kh * 5;
     const float* xc = xs + kh * 32 + kw;
     float acc = 0.f;
 #pragma unroll 4
-    for (int j = part; j < 196; j += 3) {
+    for (int j = part; j < 196; j += 6) {
       const int ps = pos1[c * 196 + j];
       acc += g1[c * 196 + j] * xc[ps < 0 ? 0 : ps];
     }
     red[tid] = acc;
   }
   __syncthreads();
-  if (tid < 150) cs[2416 + tid] = red[3 * tid] + red[3 * tid + 1] + red[3 * tid + 2];
+  if (tid < 150)
+    cs[2416 + tid] = red[6 * tid] + red[6 * tid + 1] + red[6 * tid + 2] + red[6 * tid + 3] +
+                     red[6 * tid + 4] + red[6 * tid + 5];
   if (tid >= 192 && tid < 192 + 6 * 32) {  // conv1 bias: 6 channels x 32 lanes
     const int c = (tid - 192) >> 5, l = (tid - 192) & 31;
     float acc = 0.f;

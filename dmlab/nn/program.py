@@ -382,18 +382,9 @@ class Program(nn.Module):
         if st is None:
             # default priority (a higher-priority side stream measured -1.2 %:
             # profiles/bench_ab_side_stream_knobs_r3.jsonl)
-            _f = float(os.environ.get("DMLAB_TUNE_SIDEMASK", "0"))  # TEMP A/B (r4)
-            if _f > 0:
-                from dmlab.ops._native import lib
-
-                ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-                words = [0] * ((ncu + 31) // 32)
-                for c in range(int(ncu * _f)):
-                    words[c // 32] |= 1 << (c % 32)
-                st = self._side_streams[dev] = torch.cuda.ExternalStream(
-                    lib().cu_mask_stream(words), device=torch.device("cuda", dev))
-            else:
-                st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
+            # (a CU-masked side stream measured slower at 50-75 % of the CUs:
+            # profiles/wgrad_blocks_sidemask_ab_r4m.txt)
+            st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
         return st
 
     def prepare_native(self, x):

@@ -96,8 +96,10 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 # stream for the whole kernel and hold LDS the critical-path kernels need.  Measured
 # (profiles/wgrad_blocks_r2c.jsonl, one call): 512 -> 44.2/44.4k img/s, 384 44.2k,
 # 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k; at 1024 images per GPU 512 -> 46.6k,
-# 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl)
-_WGRAD_BLOCKS = int(os.environ.get("DMLAB_TUNE_WBLK", "512"))  # TEMP A/B (r4)
+# 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl); re-measured under
+# the high-priority step stream in round 4: 160-1024 blocks and CU-masked weight-gradient
+# streams all lose to 512 (profiles/wgrad_blocks_sidemask_ab_r4m.txt)
+_WGRAD_BLOCKS = 512
 _CUS = {}
 
 
@@ -290,7 +292,10 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C, W=OW if (OH, OW) == (H, W) else 0)
     pre_kw = {}
     if pre is not None:
-        if cfg in (39, 41, 42, 80, 90, 91, 92, 93):
+        _m = os.environ.get("DMLAB_TUNE_PIPEPRE", "1")  # TEMP A/B (r4)
+        _pp = (39, 41, 42, 80, 90, 91, 92, 93) if _m == "1" else (39, 41, 42, 80) if _m == "0" \
+            else (39, 41, 80)
+        if cfg in _pp:
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)
@@ -360,6 +365,8 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
     value at each window's argmax (ctx["yarg"]), as bn_bwd_reduce_masked does."""
     rl, rctx = red_for
     kernel_ok = cfg == 80 or 90 <= cfg <= 93 or cfg == 42
+    if 90 <= cfg <= 93 and os.environ.get("DMLAB_TUNE_PIPERED", "1") == "0":  # TEMP A/B (r4)
+        kernel_ok = False
     pool = getattr(rl, "pool_k", 0)
     y = rctx.get("yarg") if pool else rctx.get("y")
     if (stride != 1 or not kernel_ok or not rl.relu or y is None

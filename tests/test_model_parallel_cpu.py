@@ -44,8 +44,15 @@ def _pipeline(rank, ws, schedule):
     mod = SubNetConv() if rank == 0 else SubNetFC()
     sd = {k: v for k, v in full0.state_dict().items() if k.startswith("conv" if rank == 0 else "fc")}
     mod.load_state_dict(sd)
+    linear = schedule.endswith("_linear")
     stage = PipelineStage(mod, SGD(mod.parameters(), lr=0.1), CrossEntropyLoss(),
-                          schedule=schedule, device=torch.device("cpu"))
+                          schedule=schedule.replace("_linear", ""), device=torch.device("cpu"))
+    if linear:
+        # the program-order schedule of a captured step (no receive posted ahead); capture
+        # itself needs the device-side xGMI channel
+        stage._linear = True
+        with pytest.raises(ValueError):
+            stage.capture(X if rank == 0 else None, Y if rank == 0 else None)
     losses = []
     for _ in range(2):
         loss = stage.train_step(X if rank == 0 else None, Y if rank == 0 else None, n_micro=4)
@@ -58,7 +65,7 @@ def _pipeline(rank, ws, schedule):
         assert len(losses) == 2
 
 
-@pytest.mark.parametrize("schedule", ["gpipe", "1f1b"])
+@pytest.mark.parametrize("schedule", ["gpipe", "1f1b", "gpipe_linear", "1f1b_linear"])
 def test_pipeline_matches_single_process(schedule):
     run_dist(_pipeline, 2, schedule)
 

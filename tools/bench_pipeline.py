@@ -82,7 +82,8 @@ def main():
                    "step_ms": max(x["step_ms"] for x in ranks),
                    "samples_per_s": round(a.batch / max(x["step_ms"] for x in ranks) * 1e3, 1),
                    "stage_compute_ms": [x["compute_ms"] for x in ranks],
-                   "bubble": [x["bubble"] for x in ranks], "steps_timed": ranks[0]["steps_timed"]}
+                   "bubble": [x["bubble"] for x in ranks], "steps_timed": ranks[0]["steps_timed"],
+                   "wall_step_ms": max(x.get("wall_step_ms", float("nan")) for x in ranks)}
             print(json.dumps(row), flush=True)
             lines.append(row)
     if a.out:
