@@ -341,7 +341,8 @@ void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w
                       c10::optional<at::Tensor> mom, double lr, double momentum, double dampening,
                       double wd, double gscale, bool nesterov, bool first, at::Tensor loss,
                       c10::optional<at::Tensor> sidx, c10::optional<at::Tensor> cursor,
-                      int64_t batch, c10::optional<at::Tensor> loss_sum) {
+                      int64_t batch, c10::optional<at::Tensor> loss_sum,
+                      c10::optional<at::Tensor> probe) {
   CHECK_CUDA(x); CHECK_CONTIG(x);
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1 && x.size(2) == 28 && x.size(3) == 28,
               "x: [B, 1, 28, 28]");
@@ -398,6 +399,13 @@ void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w
     TORCH_CHECK(loss_sum->numel() == 1, "loss_sum: fp32 [1] on the device");
     lsum = loss_sum->data_ptr<float>();
   }
+  unsigned long long* pr = nullptr;
+  if (probe.has_value() && probe->defined()) {  // phase timestamps (tools/lenet_phases.py)
+    CHECK_CUDA(*probe); CHECK_CONTIG(*probe);
+    TORCH_CHECK(probe->scalar_type() == at::kLong && probe->numel() >= (int64_t)B * dm::lenet_probe_stamps(),
+                "probe: int64 [B * lenet_probe_stamps()]");
+    pr = reinterpret_cast<unsigned long long*>(probe->data_ptr<int64_t>());
+  }
   const DeviceGuard guard(x.device());
   dm::lenet_fused_step(x.data_ptr(), x.scalar_type() == at::kBFloat16,
                        reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()),
@@ -407,7 +415,7 @@ void lenet_fused_step(at::Tensor x, at::Tensor labels, std::vector<at::Tensor> w
                        first, pp != nullptr, loss.data_ptr<float>(),
                        indexed ? reinterpret_cast<const long long*>(sidx->data_ptr<int64_t>()) : nullptr,
                        indexed ? cursor->data_ptr<int>() : nullptr, x.size(0), nbatch, lsum,
-                       cur_stream());
+                       cur_stream(), pr);
 }
 
 int num_cus(int device) {
@@ -462,7 +470,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lr"), py::arg("momentum"), py::arg("dampening"), py::arg("wd"),
         py::arg("gscale"), py::arg("nesterov"), py::arg("first"), py::arg("loss"),
         py::arg("sidx") = py::none(), py::arg("cursor") = py::none(), py::arg("batch") = 0,
-        py::arg("loss_sum") = py::none());
+        py::arg("loss_sum") = py::none(), py::arg("probe") = py::none());
   m.def("lenet_record_floats", &dm::lenet_record_floats);
   m.def("lenet_slab_floats", &dm::lenet_slab_floats);
   m.attr("arch") = "gfx950";

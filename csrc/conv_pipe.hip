@@ -45,20 +45,18 @@ constexpr int PBK = 64;    // K per step (one 128-B LDS row per tile row)
 constexpr unsigned POOB = 0x80000000u;
 
 // BN output channels per tile (256 / 128 / 64); WM x WN waves, wave tile 256/WM x BN/WN;
-// MINW waves per SIMD the register budget is sized for; PRE: the operand is
-// relu(x * pre_sc + pre_sh) of the stored x (the previous conv's raw output): each thread
-// rewrites the 16-B chunks its own DMA landed, between its vmcnt wait and the barrier that
-// publishes the stage, skipping the zero rows of padding taps (the padding stays zero AFTER
-// the BatchNorm, as in the unfused conv)
+// MINW waves per SIMD the register budget is sized for.  (A PRE variant that applied the
+// previous BN + ReLU to the landed A chunks between the vmcnt wait and the barrier was removed
+// in round 4: materialising that BN output is 1.7 % faster per step on layers 3-4,
+// profiles/pipe_pre_materialise_ab_r4q.txt)
 // RED (data gradients): the backward reduction of the BatchNorm whose output gradient Y is
 // (kernels.h BnBwdRed) runs in the store loop -- each lane's 8 channels of the stored bf16
 // value against that BN's input y -- and leaves one [2][Ncols] row per M tile in red.part
-template <int BN, int WM, int WN, int MINW, bool PRE, bool RED = false>
+template <int BN, int WM, int WN, int MINW, bool RED = false>
 __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeomSet gs, unsigned xbytes, unsigned wbytes, int ntN,
-    int mtiles_max, int xcd, const float* __restrict__ pre_sc, const float* __restrict__ pre_sh,
-    BnBwdRed red) {
+    int mtiles_max, int xcd, BnBwdRed red) {
   // blockIdx.y selects one of up to four geometries sharing X / W / Y (the parity classes of a
   // stride-2 data gradient, which write disjoint output pixels); one geometry otherwise
   const ConvGeom g = gs.g[blockIdx.y];
@@ -138,11 +136,6 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   constexpr int ND = AI + BI;
   int icc = 0, ith = 0, itw = 0;
   unsigned doff[ND];
-  // PRE bookkeeping: which of this thread's A chunks hold real (non-padding) rows, and the
-  // 64-channel chunk, for the step prepared last (cur) and the one before it (land: the
-  // tile that lands at the next barrier)
-  unsigned vm_cur = 0, vm_land = 0;
-  int cc_cur = 0, cc_land = 0;
   auto prep = [&]() __attribute__((always_inline)) {
     const int cc = icc, th = ith, tw = itw;
     const int t = th * g.ntw + tw;
@@ -160,15 +153,6 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
         (unsigned)((((g.kh0 + th * g.khs) * g.KW + (g.kw0 + tw * g.kws)) * g.C + cc * PBK) * 2);
 #pragma unroll
     for (int j = 0; j < AI; ++j) doff[j] = live && ((amask[j] >> t) & 1u) ? abase[j] + tapd : POOB;
-    if constexpr (PRE) {
-      unsigned bits = 0;
-#pragma unroll
-      for (int j = 0; j < AI; ++j) bits |= (doff[j] != POOB ? 1u : 0u) << j;
-      vm_land = vm_cur;
-      cc_land = cc_cur;
-      vm_cur = bits;
-      cc_cur = cc;
-    }
 #pragma unroll
     for (int j = 0; j < BI; ++j) doff[AI + j] = live && bbase[j] != POOB ? bbase[j] + wko : POOB;
   };
@@ -231,49 +215,11 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
       if (RD && q < NRD) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     }
   };
-  // PRE: BN + ReLU of this thread's landed A chunks of stage st (scale/shift staged in LDS)
-  const float* psc = reinterpret_cast<const float*>(smem + 2 * STG);
-  const float* psh = psc + g.C;
-  auto transform = [&](int st) __attribute__((always_inline)) {
-    if constexpr (PRE) {
-      const int c0 = cc_land * PBK + dch * 8;
-      const float4 s0 = *reinterpret_cast<const float4*>(psc + c0);
-      const float4 s1 = *reinterpret_cast<const float4*>(psc + c0 + 4);
-      const float4 h0 = *reinterpret_cast<const float4*>(psh + c0);
-      const float4 h1 = *reinterpret_cast<const float4*>(psh + c0 + 4);
-      const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-      const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-#pragma unroll
-      for (int j = 0; j < AI; ++j) {
-        if (!((vm_land >> j) & 1u)) continue;
-        uint4* q = reinterpret_cast<uint4*>(smem + st * STG + (j * NW + wid) * 1024 + lane * 16);
-        const uint4 v = *q;
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        uint32_t o[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float lo = fmaxf(bf2f((bf16_t)(w[k] & 0xffff)) * sc[2 * k] + sh[2 * k], 0.f);
-          const float hi = fmaxf(bf2f((bf16_t)(w[k] >> 16)) * sc[2 * k + 1] + sh[2 * k + 1], 0.f);
-          o[k] = pack_bf2(lo, hi);
-        }
-        *q = make_uint4(o[0], o[1], o[2], o[3]);
-      }
-    }
-  };
   // tile of stage `nst` landed; publish it (every wave is done reading the other stage)
   auto barrier_vm0 = [&](int nst) __attribute__((always_inline)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    transform(nst);
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   };
-  if constexpr (PRE) {
-    float* s_sc = reinterpret_cast<float*>(smem + 2 * STG);
-    for (int c = tid; c < g.C; c += NT) {
-      s_sc[c] = pre_sc[c];
-      s_sc[g.C + c] = pre_sh[c];
-    }
-    __syncthreads();
-  }
 
   // ---- prologue: tiles 0 and 1 in flight, tile 0 published, its first fragments read ----
   // (with S == 1 the second DMA loads zeros into stage 1, which is never read)
@@ -288,7 +234,6 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   else if constexpr (ND == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   else if constexpr (ND == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  transform(0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   rdall(f0, 0, 0);
 
@@ -512,11 +457,10 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
 
 template <int BN, int WM, int WN, int MINW>
 void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                 const ConvGeomSet& gs, int ng, hipStream_t st, const float* pre_sc,
-                 const float* pre_sh, const BnBwdRed* red = nullptr) {
+                 const ConvGeomSet& gs, int ng, hipStream_t st, const BnBwdRed* red = nullptr) {
   const ConvGeom& g = gs.g[0];
   constexpr size_t STG = (size_t)PBM * PBK * 2 + (size_t)BN * PBK * 2;
-  const size_t sm_main = 2 * STG + (pre_sc ? (size_t)g.C * 8 : 0);
+  const size_t sm_main = 2 * STG;
   const size_t sm_epi = (size_t)WM * WN * 32 * (BN / WN + 4) * 4 + (red ? (size_t)WM * BN * 8 : 0);
   const size_t sm = sm_main > sm_epi ? sm_main : sm_epi;
   long long mmax = 0;
@@ -525,30 +469,26 @@ void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   const int ntN = (g.Ncols + BN - 1) / BN;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  if (red && (pre_sc || ng != 1))
+  if (red && ng != 1)
     throw std::runtime_error("conv_pipe: BN-backward reduction is for one-geometry data gradients");
-  auto k = red ? conv_pipe_kernel<BN, WM, WN, MINW, false, true>
-               : pre_sc ? conv_pipe_kernel<BN, WM, WN, MINW, true> : conv_pipe_kernel<BN, WM, WN, MINW, false>;
+  auto k = red ? conv_pipe_kernel<BN, WM, WN, MINW, true> : conv_pipe_kernel<BN, WM, WN, MINW, false>;
   const BnBwdRed rarg = red ? *red : BnBwdRed{};
   constexpr int NT = WM * WN * 64;
   set_smem_attr(k, sm);
   if (ntN > 1) {
     const unsigned mt8 = (unsigned)((mtiles + 7) / 8 * 8);
-    k<<<dim3(mt8 * ntN, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, ntN, mtiles, 1, pre_sc,
-                                           pre_sh, rarg);
+    k<<<dim3(mt8 * ntN, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, ntN, mtiles, 1, rarg);
   } else {
     k<<<dim3((unsigned)mtiles, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, 1, mtiles, 0,
-                                                  pre_sc, pre_sh, rarg);
+                                                  rarg);
   }
   DM_CHECK(hipGetLastError());
 }
 
 template <int BN, int WM, int WN, int MINW>
 void launch_pipe1(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                  const ConvGeom& g, hipStream_t st, const float* pre_sc, const float* pre_sh,
-                  const BnBwdRed* red) {
-  launch_pipe<BN, WM, WN, MINW>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1, st, pre_sc, pre_sh,
-                                red);
+                  const ConvGeom& g, hipStream_t st, const BnBwdRed* red) {
+  launch_pipe<BN, WM, WN, MINW>(X, Wp, Y, ADD, stats, ConvGeomSet::one(g), 1, st, red);
 }
 }  // namespace
 
@@ -564,15 +504,14 @@ bool conv_pipe_supported(const ConvGeom& g, int cfg) {
 }
 
 void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc,
-               const float* pre_sh, const BnBwdRed* red) {
+               const ConvGeom& g, int cfg, hipStream_t st, const BnBwdRed* red) {
   // 90: 256 x 256, 8 waves (2 x 4) of 128 x 64; 91: 256 x 128, 8 waves (4 x 2) of 64 x 64;
   // 92: 256 x 128, 4 waves (2 x 2) of 128 x 64; 93: 256 x 64, 4 waves (4 x 1) of 64 x 64,
   // two workgroups per CU (80 KB of LDS each)
-  if (cfg == 90) launch_pipe1<256, 2, 4, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
-  else if (cfg == 91) launch_pipe1<128, 4, 2, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
-  else if (cfg == 92) launch_pipe1<128, 2, 2, 1>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
-  else launch_pipe1<64, 4, 1, 2>(X, Wp, Y, ADD, stats, g, st, pre_sc, pre_sh, red);
+  if (cfg == 90) launch_pipe1<256, 2, 4, 1>(X, Wp, Y, ADD, stats, g, st, red);
+  else if (cfg == 91) launch_pipe1<128, 4, 2, 1>(X, Wp, Y, ADD, stats, g, st, red);
+  else if (cfg == 92) launch_pipe1<128, 2, 2, 1>(X, Wp, Y, ADD, stats, g, st, red);
+  else launch_pipe1<64, 4, 1, 2>(X, Wp, Y, ADD, stats, g, st, red);
 }
 
 // the parity classes of a stride-2 data gradient (no statistics) in one launch
@@ -581,10 +520,10 @@ bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t*
   if (ng < 1 || ng > 4) return false;
   for (int i = 0; i < ng; ++i)
     if (!conv_pipe_supported(gs.g[i], cfg)) return false;
-  if (cfg == 90) launch_pipe<256, 2, 4, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st, nullptr, nullptr);
-  else if (cfg == 91) launch_pipe<128, 4, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st, nullptr, nullptr);
-  else if (cfg == 92) launch_pipe<128, 2, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st, nullptr, nullptr);
-  else launch_pipe<64, 4, 1, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st, nullptr, nullptr);
+  if (cfg == 90) launch_pipe<256, 2, 4, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st);
+  else if (cfg == 91) launch_pipe<128, 4, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st);
+  else if (cfg == 92) launch_pipe<128, 2, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st);
+  else launch_pipe<64, 4, 1, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st);
   return true;
 }
 

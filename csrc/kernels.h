@@ -55,7 +55,9 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
                       const int* off, float* p, float* mom, float lr, float momentum,
                       float dampening, float wd, float gscale, bool nesterov, bool first,
                       bool do_sgd, float* loss, const long long* sidx, int* cursor,
-                      long long nrows, int nbatch, float* loss_sum, hipStream_t st);
+                      long long nrows, int nbatch, float* loss_sum, hipStream_t st,
+                      unsigned long long* probe = nullptr);
+int lenet_probe_stamps();
 }  // namespace dm
 
 namespace dm {
@@ -108,8 +110,7 @@ bool conv_pipe_supported(const ConvGeom& g, int cfg);
 bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
                      const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
 void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-               const ConvGeom& g, int cfg, hipStream_t st, const float* pre_sc = nullptr,
-               const float* pre_sh = nullptr, const BnBwdRed* red = nullptr);
+               const ConvGeom& g, int cfg, hipStream_t st, const BnBwdRed* red = nullptr);
 // conv_res64.hip: persistent register-resident-weight 3x3 conv, 64 -> 64 channels (cfg 80);
 // statistics rows = res64_grid(M) (one per workgroup)
 bool conv_res64_supported(const ConvGeom& g);

@@ -33,6 +33,7 @@ namespace {
 constexpr int LT = 1024;  // threads per sample workgroup (16 waves: the long phases split)
 // per-sample conv gradient partials: conv2 w (2400), conv2 b (16), conv1 w (150), conv1 b (6)
 constexpr int CS = 2400 + 16 + 150 + 6;
+constexpr int NPROBE = 16;
 
 template <typename XT>
 __device__ __forceinline__ float ldx(const XT* p);
@@ -41,15 +42,26 @@ __device__ __forceinline__ float ldx<float>(const float* p) { return *p; }
 template <>
 __device__ __forceinline__ float ldx<bf16_t>(const bf16_t* p) { return bf2f(*p); }
 
-template <typename XT>
+template <bool PROBE>
+__device__ __forceinline__ void probe_stamp(unsigned long long* probe, int b, int tid, int k) {
+  if constexpr (PROBE) {
+    if (tid == 0 && k < NPROBE) probe[(long long)b * NPROBE + k] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+template <typename XT, bool PROBE>
 __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     const XT* __restrict__ X, const long long* __restrict__ labels,
     const float* __restrict__ c1w, const float* __restrict__ c1b, const float* __restrict__ c2w,
     const float* __restrict__ c2b, const float* __restrict__ f1w, const float* __restrict__ f1b,
     const float* __restrict__ f2w, const float* __restrict__ f2b, float* __restrict__ rec,
     float* __restrict__ cslab, float* __restrict__ rowloss, float inv_b,
-    const long long* __restrict__ sidx, const int* __restrict__ cursor, long long nrows) {
+    const long long* __restrict__ sidx, const int* __restrict__ cursor, long long nrows,
+    unsigned long long* __restrict__ probe) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // probe (development, tools/lenet_phases.py; null otherwise): the 100 MHz real-time clock at
+  // the start and after every phase barrier, NPROBE stamps per sample
+  probe_stamp<PROBE>(probe, b, tid, 0);
   // device-resident loader: sample b of this step is dataset row sidx[cursor * B + b] (the
   // epoch's sampler order, uploaded once per epoch; the cursor advances on the device in the
   // gradient kernel, so a captured graph walks the epoch); clamped, never out of bounds
@@ -84,6 +96,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   if (tid < 16) bb2[tid] = c2b[tid];
   if (tid < 10) fb2[tid] = f2b[tid];
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 1);
 
   // ---- conv1 (1 -> 6, 5x5, pad 2) + bias + ReLU + 2x2 max-pool ----
   for (int q = tid; q < 1176; q += LT) {
@@ -112,6 +125,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     pos1[q] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 32 + 2 * px + (code & 1));
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 2);
 
   // ---- conv2 (6 -> 16, 5x5) + bias + ReLU + 2x2 max-pool: channels 0-2 and 3-5 on two
   //      thread halves, the second half's partial sums added in a fixed order ----
@@ -157,6 +171,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     }
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 3);
 
   // ---- fc1 (400 -> 120) + ReLU: 8 threads per output, thread p loading float4 columns
   //      p, p+8, ... of the row (all 12-13 in flight together; the 8 threads of an output
@@ -180,6 +195,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     if (part == 0) h1[u] = fmaxf(acc + f1b[u], 0.f);
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 4);
 
   // ---- fc2 (120 -> 10) from LDS, one wave per output ----
   for (int o = wid; o < 10; o += LT / 64) {
@@ -189,6 +205,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     if (lane == 0) lg[o] = acc + fb2[o];
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 5);
   // ---- softmax cross-entropy: loss and the (softmax - onehot) / B seed ----
   if (wid == 0) {
     const float z = lane < 10 ? lg[lane] : -INFINITY;
@@ -201,6 +218,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     if (lane == 0) rowloss[b] = mx + __logf(se) - zl;
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 6);
 
   // ---- fc2 data gradient, masked by fc1's ReLU ----
   if (tid < 120) {
@@ -210,6 +228,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     dh1[tid] = h1[tid] > 0.f ? acc : 0.f;
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 7);
 
   // ---- fc1 data gradient: thread (k4, u-group of 12) streams coalesced float4 rows ----
   if (tid < 1000) {
@@ -229,6 +248,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     red4[ug * 100 + k4] = a;
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 8);
   float* r = rec + (long long)b * 656;  // per-sample record: h0 | h1 | dh1 | dl (+ pad)
   if (tid < 400) {
     float d = 0.f;
@@ -249,6 +269,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   }
   if (tid < 10) r[640 + tid] = dl[tid];
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 9);
 
   float* cs = cslab + (long long)b * CS;
   // ---- conv2 weight/bias gradient partials over the 25 argmax positions of each channel ----
@@ -294,6 +315,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     if (dgp > 0) pd4[(dgp - 1) * 294 + dq] = make_float4(dacc[0], dacc[1], dacc[2], dacc[3]);
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 10);
   if (dgp == 0) {
     const int c = dq / 49, rr = dq - c * 49, by = rr / 7, bx = rr - by * 7;
     const float4 e1 = pd4[dq], e2 = pd4[294 + dq];
@@ -306,6 +328,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     }
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 11);
 
   // ---- conv1 weight/bias gradient partials: 150 weights x 196 pooled positions, 6 threads
   //      per weight, combined in a fixed order ----
@@ -322,6 +345,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     red[tid] = acc;
   }
   __syncthreads();
+  probe_stamp<PROBE>(probe, b, tid, 12);
   if (tid < 150)
     cs[2416 + tid] = red[6 * tid] + red[6 * tid + 1] + red[6 * tid + 2] + red[6 * tid + 3] +
                      red[6 * tid + 4] + red[6 * tid + 5];
@@ -333,6 +357,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
     for (int o = 16; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 32);
     if (l == 0) cs[2566 + c] = acc;
   }
+  probe_stamp<PROBE>(probe, b, tid, 13);
 }
 
 // Flat-buffer segment j (fc2.w, fc2.b, fc1.w, fc1.b, conv2.w, conv2.b, conv1.w, conv1.b in the
@@ -412,22 +437,26 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
 
 int lenet_record_floats() { return 656; }
 int lenet_slab_floats() { return CS; }
+int lenet_probe_stamps() { return NPROBE; }
 
 void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B,
                       const float* const* w, float* rec, float* cslab, float* rowloss, float* grad,
                       const int* off, float* p, float* mom, float lr, float momentum,
                       float dampening, float wd, float gscale, bool nesterov, bool first,
                       bool do_sgd, float* loss, const long long* sidx, int* cursor,
-                      long long nrows, int nbatch, float* loss_sum, hipStream_t st) {
+                      long long nrows, int nbatch, float* loss_sum, hipStream_t st,
+                      unsigned long long* probe) {
   const float inv_b = 1.f / (float)B;
-  if (x_bf16)
-    lenet_sample_kernel<bf16_t><<<B, LT, 0, st>>>((const bf16_t*)x, labels, w[0], w[1], w[2], w[3],
-                                                  w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b,
-                                                  sidx, cursor, nrows);
-  else
-    lenet_sample_kernel<float><<<B, LT, 0, st>>>((const float*)x, labels, w[0], w[1], w[2], w[3],
-                                                 w[4], w[5], w[6], w[7], rec, cslab, rowloss, inv_b,
-                                                 sidx, cursor, nrows);
+  // the probed variant is a separate instantiation: the normal kernel carries none of it
+  if (x_bf16) {
+    auto k = probe ? lenet_sample_kernel<bf16_t, true> : lenet_sample_kernel<bf16_t, false>;
+    k<<<B, LT, 0, st>>>((const bf16_t*)x, labels, w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7],
+                        rec, cslab, rowloss, inv_b, sidx, cursor, nrows, probe);
+  } else {
+    auto k = probe ? lenet_sample_kernel<float, true> : lenet_sample_kernel<float, false>;
+    k<<<B, LT, 0, st>>>((const float*)x, labels, w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7],
+                        rec, cslab, rowloss, inv_b, sidx, cursor, nrows, probe);
+  }
   DM_CHECK(hipGetLastError());
   LenetFlat fl;
   for (int j = 0; j < 8; ++j) fl.off[j] = off[j];

@@ -292,10 +292,11 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     cfg = _STEM_CFG if s2d else pick_cfg(M, cout, k, s, C, W=OW if (OH, OW) == (H, W) else 0)
     pre_kw = {}
     if pre is not None:
-        _m = os.environ.get("DMLAB_TUNE_PIPEPRE", "1")  # TEMP A/B (r4)
-        _pp = (39, 41, 42, 80, 90, 91, 92, 93) if _m == "1" else (39, 41, 42, 80) if _m == "0" \
-            else (39, 41, 80)
-        if cfg in _pp:
+        # the halo tiles (layer 2) and the layer-1 kernel normalise y1 on the fly; for the
+        # pipelined tiles of layers 3-4 (cfg 90-93) materialising relu(bn1(y1)) is 1.7 % faster
+        # per step than the in-LDS transform that delayed every pipeline stage (and layer 2
+        # measures the same either way: profiles/pipe_pre_materialise_ab_r4q.txt)
+        if cfg in (39, 41, 42, 80):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
             x = _materialise(x, pre)
@@ -365,8 +366,6 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
     value at each window's argmax (ctx["yarg"]), as bn_bwd_reduce_masked does."""
     rl, rctx = red_for
     kernel_ok = cfg == 80 or 90 <= cfg <= 93 or cfg == 42
-    if 90 <= cfg <= 93 and os.environ.get("DMLAB_TUNE_PIPERED", "1") == "0":  # TEMP A/B (r4)
-        kernel_ok = False
     pool = getattr(rl, "pool_k", 0)
     y = rctx.get("yarg") if pool else rctx.get("y")
     if (stride != 1 or not kernel_ok or not rl.relu or y is None
