@@ -473,5 +473,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("loss_sum") = py::none(), py::arg("probe") = py::none());
   m.def("lenet_record_floats", &dm::lenet_record_floats);
   m.def("lenet_slab_floats", &dm::lenet_slab_floats);
+  m.def("lenet_probe_stamps", &dm::lenet_probe_stamps);
   m.attr("arch") = "gfx950";
 }

@@ -295,7 +295,8 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
         # the halo tiles (layer 2) and the layer-1 kernel normalise y1 on the fly; for the
         # pipelined tiles of layers 3-4 (cfg 90-93) materialising relu(bn1(y1)) is 1.7 % faster
         # per step than the in-LDS transform that delayed every pipeline stage (and layer 2
-        # measures the same either way: profiles/pipe_pre_materialise_ab_r4q.txt)
+        # measures the same either way, as does layer 1: profiles/pipe_pre_materialise_ab_r4q.txt,
+        # profiles/layer12_pre_materialise_ab_r4u.txt)
         if cfg in (39, 41, 42, 80):
             pre_kw = dict(pre_scale=pre[0], pre_shift=pre[1])
         else:  # not a halo-kernel shape: materialise the previous BN output
