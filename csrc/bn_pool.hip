@@ -224,6 +224,71 @@ __global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// flat variant (TEMP A/B r4): block b covers U*256 consecutive chunks, no grid stride;
+// NT: non-temporal (streaming) loads and stores
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ uint4 ld16(const bf16_t* p, long long i) {
+  if constexpr (NT) {
+    const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(p) + i);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return reinterpret_cast<const uint4*>(p)[i];
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st16(bf16_t* p, long long i, const uint4& o) {
+  if constexpr (NT) {
+    u32x4v v;
+    v.x = o.x; v.y = o.y; v.z = o.z; v.w = o.w;
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4v*>(p) + i);
+  } else {
+    reinterpret_cast<uint4*>(p)[i] = o;
+  }
+}
+template <bool RES, bool RELU, int U, bool NT>
+__global__ void __launch_bounds__(256) bn_apply_flat_kernel(const bf16_t* __restrict__ y,
+                                                            const bf16_t* __restrict__ res,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            bf16_t* __restrict__ out, long long n8,
+                                                            int C, uint8_t* __restrict__ mask) {
+  extern __shared__ float sc_sh[];  // [2][C]
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    sc_sh[i] = scale[i];
+    sc_sh[C + i] = shift[i];
+  }
+  __syncthreads();
+  const long long i0 = (long long)blockIdx.x * (U * 256) + threadIdx.x;
+  const int C8 = C >> 3;
+  uint4 yr[U], rr[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = i0 + u * 256 < n8 ? i0 + u * 256 : 0;
+    yr[u] = ld16<NT>(y, i);
+    if (RES) rr[u] = ld16<NT>(res, i);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = i0 + u * 256;
+    if (i >= n8) continue;
+    const int c0 = (int)((unsigned long long)i & (unsigned)(C8 - 1)) * 8;
+    float f[8], r[8];
+    unpack8(yr[u], f);
+    if (RES) unpack8(rr[u], r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = f[j] * sc_sh[c0 + j] + sc_sh[C + c0 + j];
+      if (RES) v += r[j];
+      if (RELU) v = fmaxf(v, 0.f);
+      f[j] = v;
+    }
+    const uint4 o = pack8(f);
+    st16<NT>(out, i, o);
+    if (RELU && mask) mask[i] = (uint8_t)pos_bits8(o);
+  }
+}
+
 // ------------------------------------------------------------------ BN backward
 // dz = upstream grad with the ReLU mask; sources (template MODE):
 //   0  dout tensor, no ReLU
@@ -1085,6 +1150,27 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
   const long long n8 = n / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 2 * C;
+  static const int tune = getenv("DMLAB_TUNE_BNA") ? atoi(getenv("DMLAB_TUNE_BNA")) : 0;  // TEMP
+  if (tune) {
+#define DM_BNAF(U, NT)                                                                          \
+  {                                                                                             \
+    const int gf = (int)((n8 + U * 256 - 1) / (U * 256));                                       \
+    if (res) {                                                                                  \
+      if (relu) bn_apply_flat_kernel<true, true, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask); \
+      else bn_apply_flat_kernel<true, false, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr); \
+    } else {                                                                                    \
+      if (relu) bn_apply_flat_kernel<false, true, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask); \
+      else bn_apply_flat_kernel<false, false, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr); \
+    }                                                                                           \
+  }
+    if (tune == 1) DM_BNAF(4, false)
+    else if (tune == 2) DM_BNAF(4, true)
+    else if (tune == 3) DM_BNAF(2, false)
+    else if (tune == 4) DM_BNAF(8, false)
+    else DM_BNAF(2, true)
+#undef DM_BNAF
+    return;
+  }
   if (res) {
     if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
     else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);

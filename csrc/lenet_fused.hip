@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __shared__ float h1[128], lg[16], dl[16], dh1[128], g2[400], g1[6 * 196];
   __shared__ float dc2[16 * 18 * 18];      // unpooled conv2 gradient, 4-pixel zero border
   __shared__ float4 red4[10 * 100];        // cross-thread partials (fc1 dgrad, conv2, conv1 dw)
-  __shared__ float4 pd4[2 * 294];          // conv2 dgrad partials of output-channel groups 1, 2
+  __shared__ float pdg[4 * 1176];          // conv2 dgrad partials of the 4 output-channel groups
   float* red = reinterpret_cast<float*>(red4);
 
   // ---- stage input and the small weights (fc1's 192 KB stream from L2 instead) ----
@@ -272,60 +272,68 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   probe_stamp<PROBE>(probe, b, tid, 9);
 
   float* cs = cslab + (long long)b * CS;
-  // ---- conv2 weight/bias gradient partials over the 25 argmax positions of each channel ----
-  for (int i = tid; i < 2400; i += LT) {
-    const int o = i / 150, rr = i - o * 150, c = rr / 25, t = rr - c * 25, kh = t / 5, kw = t - kh * 5;
-    const float* pc = p1 + c * 196 + kh * 14 + kw;
-    float acc = 0.f;
+  // ---- conv2 data gradient (full correlation of the unpooled, zero-bordered gradient dc2
+  //      with the flipped kernel) on threads 0..671: thread (group og of 4 output channels,
+  //      channel c, row y, 7-column half) computes 7 outputs from a 5 x 11 window, one window
+  //      row at a time (55 + 25 LDS reads per output channel for 175 FMAs); the 4 group
+  //      partials are summed in a fixed order after the barrier ----
+  // ---- conv2 weight gradient on threads 672..1023: item (o, c, kh) = the 5 taps kw of one
+  //      kernel row, summed over the 25 argmax positions of channel o ----
+  if (tid < 672) {
+    const int og = tid / 168, r168 = tid - og * 168;
+    const int c = r168 / 28, r28 = r168 - c * 28, y0 = r28 >> 1, x0 = 7 * (r28 & 1);
+    float acc[7];
 #pragma unroll
-    for (int j = 0; j < 25; ++j) {
-      const int ps = pos2[o * 25 + j];
-      acc += g2[o * 25 + j] * pc[ps < 0 ? 0 : ps];
-    }
-    cs[i] = acc;
-  }
-  if (tid < 16) {
-    float acc = 0.f;
-    for (int j = 0; j < 25; ++j) acc += g2[tid * 25 + j];
-    cs[2400 + tid] = acc;
-  }
-  // ---- conv2 data gradient (full correlation with the flipped kernel over the unpooled
-  //      gradient), 2x2 outputs per thread sharing a 6x6 window, output channels split in
-  //      three groups (0-5, 6-10, 11-15) summed in a fixed order, then unpool1 ----
-  float dacc[4] = {0.f, 0.f, 0.f, 0.f};
-  const int dq = tid % 294, dgp = tid / 294;  // dgp 3 (tid >= 882): idle
-  if (dgp < 3) {
-    const int c = dq / 49, rr = dq - c * 49, by = rr / 7, bx = rr - by * 7;
-    const int o0 = dgp == 0 ? 0 : dgp == 1 ? 6 : 11, o1 = dgp == 0 ? 6 : dgp == 1 ? 11 : 16;
-    for (int o = o0; o < o1; ++o) {
-      float win[6][6];
+    for (int q = 0; q < 7; ++q) acc[q] = 0.f;
+    for (int o = 4 * og; o < 4 * og + 4; ++o) {
+      const float* wo = w2 + o * 150 + c * 25;
+      const float* d = dc2 + o * 324 + y0 * 18 + x0;
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+      for (int kh = 0; kh < 5; ++kh) {  // output row y0 reads window row 4 - kh
+        float row[11];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) win[i][j] = dc2[o * 324 + (2 * by + i) * 18 + 2 * bx + j];
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
+        for (int q = 0; q < 11; ++q) row[q] = d[(4 - kh) * 18 + q];
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const float w = w2[o * 150 + c * 25 + kh * 5 + kw];
+          const float wv = wo[kh * 5 + kw];
 #pragma unroll
-          for (int a = 0; a < 4; ++a) dacc[a] += win[(a >> 1) + 4 - kh][(a & 1) + 4 - kw] * w;
+          for (int q = 0; q < 7; ++q) acc[q] += row[q + 4 - kw] * wv;
         }
+      }
     }
-    if (dgp > 0) pd4[(dgp - 1) * 294 + dq] = make_float4(dacc[0], dacc[1], dacc[2], dacc[3]);
+    float* pg = pdg + og * 1176 + c * 196 + y0 * 14 + x0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) pg[q] = acc[q];
+  } else {
+    for (int i = tid - 672; i < 480; i += LT - 672) {
+      const int o = i / 30, r30 = i - o * 30, c = r30 / 5, kh = r30 - c * 5;
+      const float* pc = p1 + c * 196 + kh * 14;
+      float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 5
+      for (int j = 0; j < 25; ++j) {
+        const int ps = pos2[o * 25 + j];
+        const float gv = g2[o * 25 + j];
+        const float* q = pc + (ps < 0 ? 0 : ps);
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kw] += gv * q[kw];
+      }
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) cs[o * 150 + c * 25 + kh * 5 + kw] = acc[kw];
+    }
+    if (tid >= 1008) {  // conv2 bias: 16 channels
+      const int o = tid - 1008;
+      float acc = 0.f;
+      for (int j = 0; j < 25; ++j) acc += g2[o * 25 + j];
+      cs[2400 + o] = acc;
+    }
   }
   __syncthreads();
   probe_stamp<PROBE>(probe, b, tid, 10);
-  if (dgp == 0) {
-    const int c = dq / 49, rr = dq - c * 49, by = rr / 7, bx = rr - by * 7;
-    const float4 e1 = pd4[dq], e2 = pd4[294 + dq];
-    const float s[4] = {dacc[0] + e1.x + e2.x, dacc[1] + e1.y + e2.y, dacc[2] + e1.z + e2.z,
-                        dacc[3] + e1.w + e2.w};
+  for (int idx = tid; idx < 1176; idx += LT) {  // o-pair partials in order, unpool1 mask
+    float sacc = 0.f;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int idx = c * 196 + (2 * by + (a >> 1)) * 14 + 2 * bx + (a & 1);
-      g1[idx] = pos1[idx] >= 0 ? s[a] : 0.f;
-    }
+    for (int og = 0; og < 4; ++og) sacc += pdg[og * 1176 + idx];
+    g1[idx] = pos1[idx] >= 0 ? sacc : 0.f;
   }
   __syncthreads();
   probe_stamp<PROBE>(probe, b, tid, 11);

@@ -64,6 +64,7 @@ def main():
                           "MB": round(tensors * nb / 1e6, 1),
                           "TB/s": round(tensors * nb / us / 1e6, 2)}), flush=True)
 
+    rep("torch sum (1R)", timeit(lambda: y.sum(), a.reps), 1)
     rep("torch copy (1R1W)", timeit(lambda: o1.copy_(y), a.reps), 2)
     rep("torch add (2R1W)", timeit(lambda: torch.add(y, dz, out=o1), a.reps), 3)
     rep("bn_apply relu (1R1W)", timeit(lambda: L.bn_apply(y, None, scale, shift, o1, True), a.reps), 2)

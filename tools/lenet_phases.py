@@ -14,7 +14,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 import torch  # noqa: E402
 
-PHASES = ["stage input + weights", "conv1 + pool", "conv2 (channel halves)", "conv2 combine + pool",
+PHASES = ["stage input + weights", "conv1 + pool", "conv2 (channel halves) + combine + pool",
           "fc1", "fc2", "softmax CE", "fc2 dgrad", "fc1 dgrad", "records + unpool scatter",
           "conv2 dw + conv2 dgrad", "conv2 dgrad combine", "conv1 dw", "conv1 dw combine + bias"]
 
