@@ -375,6 +375,7 @@ struct BnBwdBatch {
   uint4 y[U], dout[U], out[U];
   uint32_t mk[U];
   bool ok[U];
+  template <bool NT = false>
   __device__ __forceinline__ void load(const BnBwdArgs& a, long long i0, long long stride,
                                        long long n8) {
 #pragma unroll
@@ -382,9 +383,9 @@ struct BnBwdBatch {
       const long long i = i0 + u * stride;
       ok[u] = i < n8;
       const long long ii = ok[u] ? i : 0;
-      y[u] = reinterpret_cast<const uint4*>(a.y)[ii];
-      if (MODE != 3) dout[u] = reinterpret_cast<const uint4*>(a.dout)[ii];
-      if (MODE == 1) out[u] = reinterpret_cast<const uint4*>(a.out)[ii];
+      y[u] = ld16<NT>(a.y, ii);
+      if (MODE != 3) dout[u] = ld16<NT>(a.dout, ii);
+      if (MODE == 1) out[u] = ld16<NT>(a.out, ii);
       if (MODE == 4) mk[u] = a.mask[ii];
     }
   }
@@ -412,7 +413,7 @@ struct BnBwdBatch {
 };
 
 // grid (G); block 256; thread t owns channel chunk t % C8 of the rows ≡ t / C8 (mod 256 / C8)
-template <int MODE, int UU = 4>
+template <int MODE, int UU = 4, bool NT = false>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* __restrict__ part) {
   constexpr int U = MODE == 3 ? 2 : UU;
   extern __shared__ float red[];  // [256][16] partials, then [2][C] scale/shift
@@ -443,7 +444,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
   const long long stride = rstride * C8;
   for (long long i0 = ((long long)blockIdx.x * RL + rl) * C8 + chunk; i0 < n8; i0 += U * stride) {
     BnBwdBatch<MODE, U> bt;
-    bt.load(a, i0, stride, n8);
+    bt.template load<NT>(a, i0, stride, n8);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!bt.ok[u]) continue;
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
 }
 
 // dy = a·dz + b·y + c ; optional dres = dz
-template <int MODE, bool DRES, int UU = 4>
+template <int MODE, bool DRES, int UU = 4, bool FLAT = false, bool NT = false>
 __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const float* __restrict__ coef,
                                                            bf16_t* __restrict__ dy,
                                                            bf16_t* __restrict__ dres) {
@@ -501,7 +502,8 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
     }
   __syncthreads();
   const long long n8 = a.M * C8;
-  const long long stride = (long long)gridDim.x * blockDim.x;
+  // FLAT: block b covers U*256 consecutive chunks (no grid stride); else grid-strided
+  const long long stride = FLAT ? (long long)blockDim.x : (long long)gridDim.x * blockDim.x;
   // With C8 | blockDim (C <= 2048) a thread's channel chunk never changes across the
   // grid-stride loop: its 24 coefficients live in registers instead of being re-read
   // from LDS per element (lanes 8 floats apart: the kernel's LDS bank conflicts).
@@ -516,9 +518,10 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
       kc[j] = cf[2 * C + c0 + j];
     }
   }
-  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
+  const long long ib = FLAT ? (long long)blockIdx.x * U * blockDim.x : (long long)blockIdx.x * blockDim.x;
+  for (long long i0 = ib + threadIdx.x; i0 < n8; i0 += FLAT ? n8 : U * stride) {
     BnBwdBatch<MODE, U> bt;
-    bt.load(a, i0, stride, n8);
+    bt.template load<NT>(a, i0, stride, n8);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (!bt.ok[u]) continue;
@@ -527,7 +530,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
       const int c0 = chunk * 8;
       float d[8], yv[8];
       bt.dz(a, u, i, chunk, C8, sc, sh, d, yv);
-      if (DRES) reinterpret_cast<uint4*>(dres)[i] = pack8(d);
+      if (DRES) st16<NT>(dres, i, pack8(d));
       float r[8];
       if (hoist) {
 #pragma unroll
@@ -537,7 +540,7 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(BnBwdArgs a, const fl
         for (int j = 0; j < 8; ++j)
           r[j] = cf[c0 + j] * d[j] + cf[C + c0 + j] * yv[j] + cf[2 * C + c0 + j];
       }
-      reinterpret_cast<uint4*>(dy)[i] = pack8(r);
+      st16<NT>(dy, i, pack8(r));
     }
   }
 }
@@ -1150,7 +1153,8 @@ void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const floa
   const long long n8 = n / 8;
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 2 * C;
-  static const int tune = getenv("DMLAB_TUNE_BNA") ? atoi(getenv("DMLAB_TUNE_BNA")) : 0;  // TEMP
+  static const int tuneb = getenv("DMLAB_TUNE_BN") ? atoi(getenv("DMLAB_TUNE_BN")) : 0;  // TEMP
+  const int tune = (tuneb & 1) ? ((tuneb & 2) ? 2 : 1) : 0;
   if (tune) {
 #define DM_BNAF(U, NT)                                                                          \
   {                                                                                             \
@@ -1210,6 +1214,7 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   float* coef = pre_part ? work : work + (long long)G * 2 * C;
   float* part2 = coef + 3 * C;
   const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
+  static const int tunr = getenv("DMLAB_TUNE_BN") ? atoi(getenv("DMLAB_TUNE_BN")) : 0;  // TEMP
   if (pre_part) {
   } else if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
   else switch (mode) {
@@ -1217,8 +1222,14 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     // forward apply, -1.2 % for the backward apply: profiles/bn_loads_in_flight_r2c.jsonl)
     case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
     case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
-    case 2: bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part); break;
-    case 4: bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part); break;
+    case 2:
+      if (tunr & 16) bn_bwd_reduce_kernel<2, 4, true><<<G, 256, shr, st>>>(a, part);
+      else bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part);
+      break;
+    case 4:
+      if (tunr & 16) bn_bwd_reduce_kernel<4, 4, true><<<G, 256, shr, st>>>(a, part);
+      else bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part);
+      break;
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
   const int G2 = colsum_groups(G);
@@ -1236,7 +1247,16 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   // profiles/bn_bwd_apply_grid_ab_r3s3.txt)
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;
-#define DM_BNB(MD, D) bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres)
+  static const int tuneb = getenv("DMLAB_TUNE_BN") ? atoi(getenv("DMLAB_TUNE_BN")) : 0;  // TEMP
+  const int gflat = (int)((n8 + 4 * 256 - 1) / (4 * 256));
+#define DM_BNB(MD, D)                                                                              \
+  do {                                                                                             \
+    if (MD != 3 && (tuneb & 4)) {                                                                  \
+      if (tuneb & 8) bn_bwd_apply_kernel<MD, D, 4, true, true><<<gflat, 256, sh, st>>>(a, coef, dy, dres); \
+      else bn_bwd_apply_kernel<MD, D, 4, true, false><<<gflat, 256, sh, st>>>(a, coef, dy, dres);  \
+    } else                                                                                         \
+      bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres);                        \
+  } while (0)
   if (quad) {
     bn_bwd_apply_quad_kernel<<<grid_for(n8 / 4, 256, 4096), 256, sh, st>>>(a, coef, dy);
     return;

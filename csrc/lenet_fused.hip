@@ -80,6 +80,7 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __shared__ float dc2[16 * 18 * 18];      // unpooled conv2 gradient, 4-pixel zero border
   __shared__ float4 red4[10 * 100];        // cross-thread partials (fc1 dgrad, conv2, conv1 dw)
   __shared__ float pdg[4 * 1176];          // conv2 dgrad partials of the 4 output-channel groups
+  __shared__ float pc2[6 * 1600];          // conv2 forward partials of the 6 input channels
   float* red = reinterpret_cast<float*>(red4);
 
   // ---- stage input and the small weights (fc1's 192 KB stream from L2 instead) ----
@@ -127,48 +128,51 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __syncthreads();
   probe_stamp<PROBE>(probe, b, tid, 2);
 
-  // ---- conv2 (6 -> 16, 5x5) + bias + ReLU + 2x2 max-pool: channels 0-2 and 3-5 on two
-  //      thread halves, the second half's partial sums added in a fixed order ----
-  {
-    const int t4 = tid % 400, cg = tid / 400;
-    const int o = t4 / 25, r = t4 - o * 25, py = r / 5, px = r - py * 5;
-    float acc[4];
+  // ---- conv2 (6 -> 16, 5x5): item (input channel c, output channel o, row oy) computes
+  //      the 10 outputs of one row from a 5 x 14 window read one row at a time (70 + 25 LDS
+  //      reads for 250 FMAs), partial sums per input channel into pc2 ----
+  if (tid < 960) {
+    const int c = tid / 160, r160 = tid - c * 160, o = r160 / 10, oy = r160 - o * 10;
+    const float* src = p1 + c * 196 + oy * 14;
+    const float* wo = w2 + o * 150 + c * 25;
+    float acc[10];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) acc[a] = cg == 0 ? bb2[o] : 0.f;
-    for (int c = 3 * cg; c < (cg < 2 ? 3 * cg + 3 : 0); ++c) {
-      float win[6][6];
+    for (int q = 0; q < 10; ++q) acc[q] = 0.f;
 #pragma unroll
-      for (int i = 0; i < 6; ++i)
+    for (int kh = 0; kh < 5; ++kh) {
+      float row[14];
 #pragma unroll
-        for (int j = 0; j < 6; ++j) win[i][j] = p1[c * 196 + (2 * py + i) * 14 + 2 * px + j];
+      for (int q = 0; q < 14; ++q) row[q] = src[kh * 14 + q];
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
+      for (int kw = 0; kw < 5; ++kw) {
+        const float wv = wo[kh * 5 + kw];
 #pragma unroll
-        for (int kw = 0; kw < 5; ++kw) {
-          const float w = w2[o * 150 + c * 25 + kh * 5 + kw];
-#pragma unroll
-          for (int a = 0; a < 4; ++a) acc[a] += win[(a >> 1) + kh][(a & 1) + kw] * w;
-        }
+        for (int q = 0; q < 10; ++q) acc[q] += row[q + kw] * wv;
+      }
     }
-    if (cg == 1) red4[t4] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    __syncthreads();
-    if (cg == 0) {
-      const float4 h = red4[t4];
-      acc[0] += h.x;
-      acc[1] += h.y;
-      acc[2] += h.z;
-      acc[3] += h.w;
-      float best = 0.f;
-      int code = -1;
+    float* dst = pc2 + c * 1600 + o * 100 + oy * 10;
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        if (acc[a] > best) {
-          best = acc[a];
-          code = a;
-        }
-      p2[t4] = best;
-      pos2[t4] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 14 + 2 * px + (code & 1));
+    for (int q = 0; q < 10; ++q) dst[q] = acc[q];
+  }
+  __syncthreads();
+  // ---- + bias (channel partials summed in a fixed order) + ReLU + 2x2 max-pool ----
+  if (tid < 400) {
+    const int o = tid / 25, r = tid - o * 25, py = r / 5, px = r - py * 5;
+    float best = 0.f;
+    int code = -1;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int e = o * 100 + (2 * py + (a >> 1)) * 10 + 2 * px + (a & 1);
+      float v = bb2[o];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) v += pc2[c * 1600 + e];
+      if (v > best) {  // first maximum; a window whose max is <= 0 passes no gradient
+        best = v;
+        code = a;
+      }
     }
+    p2[tid] = best;
+    pos2[tid] = code < 0 ? (short)-1 : (short)((2 * py + (code >> 1)) * 14 + 2 * px + (code & 1));
   }
   __syncthreads();
   probe_stamp<PROBE>(probe, b, tid, 3);
