@@ -179,53 +179,13 @@ __device__ __forceinline__ uint32_t pos_bits8(const uint4& v) {
   return b;
 }
 
-template <bool RES, bool RELU, int U = 4>  // U: loads of U grid-strided chunks in flight
-__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ y,
-                                                       const bf16_t* __restrict__ res,
-                                                       const float* __restrict__ scale,
-                                                       const float* __restrict__ shift,
-                                                       bf16_t* __restrict__ out, long long n8,
-                                                       int C, uint8_t* __restrict__ mask) {
-  extern __shared__ float sc_sh[];  // [2][C]
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    sc_sh[i] = scale[i];
-    sc_sh[C + i] = shift[i];
-  }
-  __syncthreads();
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const int C8 = C >> 3;
-  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n8; i0 += U * stride) {
-    uint4 yr[U], rr[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long i = i0 + u * stride < n8 ? i0 + u * stride : 0;
-      yr[u] = reinterpret_cast<const uint4*>(y)[i];
-      if (RES) rr[u] = reinterpret_cast<const uint4*>(res)[i];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long i = i0 + u * stride;
-      if (i >= n8) continue;
-      const int c0 = (int)((unsigned long long)i & (unsigned)(C8 - 1)) * 8;  // C8 | 256: power of 2
-      float f[8], r[8];
-      unpack8(yr[u], f);
-      if (RES) unpack8(rr[u], r);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float v = f[j] * sc_sh[c0 + j] + sc_sh[C + c0 + j];
-        if (RES) v += r[j];
-        if (RELU) v = fmaxf(v, 0.f);
-        f[j] = v;
-      }
-      const uint4 o = pack8(f);
-      reinterpret_cast<uint4*>(out)[i] = o;
-      if (RELU && mask) mask[i] = (uint8_t)pos_bits8(o);
-    }
-  }
-}
-
-// flat variant (TEMP A/B r4): block b covers U*256 consecutive chunks, no grid stride;
-// NT: non-temporal (streaming) loads and stores
+// Streaming passes: block b covers U*256 consecutive 16-B chunks (no grid stride: the
+// dispatcher balances the blocks) and the loads/stores are non-temporal (the activation
+// tensors of a batch-1024 step exceed the 256 MB MALL; keeping them out of L2/MALL leaves
+// those to the kernels that reuse data).  At 1024x56x56x64 the residual apply runs at
+// 6.4 TB/s against 4.5 for the earlier grid-strided, cached version (torch's add: 6.0), and
+// the step gains 1.9 % with the backward passes done the same way
+// (profiles/bn_apply_variants_r4x.jsonl, profiles/bn_stream_variants_ab_r4z.txt).
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 template <bool NT>
 __device__ __forceinline__ uint4 ld16(const bf16_t* p, long long i) {
@@ -246,8 +206,12 @@ __device__ __forceinline__ void st16(bf16_t* p, long long i, const uint4& o) {
     reinterpret_cast<uint4*>(p)[i] = o;
   }
 }
-template <bool RES, bool RELU, int U, bool NT>
-__global__ void __launch_bounds__(256) bn_apply_flat_kernel(const bf16_t* __restrict__ y,
+// out = [relu](y*scale + shift [+ res])
+// mask (optional, RELU only): one bit per element, (out > 0) of the stored bf16 value, one
+// byte per 8-channel chunk -- the BN backward's ReLU mask source for residual layers
+// (mode 4) at 1/16 of the bytes of re-reading `out`.
+template <bool RES, bool RELU, int U = 4, bool NT = true>
+__global__ void __launch_bounds__(256) bn_apply_kernel(const bf16_t* __restrict__ y,
                                                             const bf16_t* __restrict__ res,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
@@ -771,6 +735,7 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool_kernel(
 // adjacent pooled outputs (they share one input column: 15 loads instead of 18) and issues
 // all 15 16-B loads before any compare (the generic kernel's guarded loop keeps only a few
 // in flight).  Same scan order and strict '>' (first max wins), same codes and yarg.
+template <bool NT>
 __global__ void __launch_bounds__(256) bn_relu_maxpool3s2_kernel(
     const bf16_t* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
     bf16_t* __restrict__ out, uint8_t* __restrict__ idx, bf16_t* __restrict__ yarg, int N, int H,
@@ -837,8 +802,8 @@ __global__ void __launch_bounds__(256) bn_relu_maxpool3s2_kernel(
           }
         }
       const unsigned oi = (((unsigned)n * OH + oh) * OW + ow0 + o) * C8 + c8;
-      reinterpret_cast<uint4*>(out)[oi] = pack8(best);
-      if (yarg) reinterpret_cast<uint4*>(yarg)[oi] = pack8(raw);
+      st16<NT>(out, oi, pack8(best));
+      if (yarg) st16<NT>(yarg, oi, pack8(raw));
 #pragma unroll
       for (int j = 0; j < 8; ++j) arg[j] = best[j] > 0.f ? arg[j] : 15;
       uint2 a2;
@@ -1151,36 +1116,15 @@ void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, c
 void bn_apply(const bf16_t* y, const bf16_t* res, const float* scale, const float* shift,
               bf16_t* out, long long n, int C, bool relu, hipStream_t st, uint8_t* mask) {
   const long long n8 = n / 8;
-  const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 2 * C;
-  static const int tuneb = getenv("DMLAB_TUNE_BN") ? atoi(getenv("DMLAB_TUNE_BN")) : 0;  // TEMP
-  const int tune = (tuneb & 1) ? ((tuneb & 2) ? 2 : 1) : 0;
-  if (tune) {
-#define DM_BNAF(U, NT)                                                                          \
-  {                                                                                             \
-    const int gf = (int)((n8 + U * 256 - 1) / (U * 256));                                       \
-    if (res) {                                                                                  \
-      if (relu) bn_apply_flat_kernel<true, true, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask); \
-      else bn_apply_flat_kernel<true, false, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr); \
-    } else {                                                                                    \
-      if (relu) bn_apply_flat_kernel<false, true, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask); \
-      else bn_apply_flat_kernel<false, false, U, NT><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr); \
-    }                                                                                           \
-  }
-    if (tune == 1) DM_BNAF(4, false)
-    else if (tune == 2) DM_BNAF(4, true)
-    else if (tune == 3) DM_BNAF(2, false)
-    else if (tune == 4) DM_BNAF(8, false)
-    else DM_BNAF(2, true)
-#undef DM_BNAF
-    return;
-  }
+  constexpr int U = 4;
+  const int gf = (int)((n8 + U * 256 - 1) / (U * 256));
   if (res) {
-    if (relu) bn_apply_kernel<true, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
-    else bn_apply_kernel<true, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
+    if (relu) bn_apply_kernel<true, true><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
+    else bn_apply_kernel<true, false><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
   } else {
-    if (relu) bn_apply_kernel<false, true><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
-    else bn_apply_kernel<false, false><<<grid, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
+    if (relu) bn_apply_kernel<false, true><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, mask);
+    else bn_apply_kernel<false, false><<<gf, 256, sh, st>>>(y, res, scale, shift, out, n8, C, nullptr);
   }
 }
 
@@ -1214,22 +1158,17 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   float* coef = pre_part ? work : work + (long long)G * 2 * C;
   float* part2 = coef + 3 * C;
   const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
-  static const int tunr = getenv("DMLAB_TUNE_BN") ? atoi(getenv("DMLAB_TUNE_BN")) : 0;  // TEMP
   if (pre_part) {
   } else if (quad) bn_bwd_reduce_quad_kernel<<<G, 256, shr, st>>>(a, part);
   else switch (mode) {
     // 4 16-B chunks per operand in flight per thread (8 measured neutral for the reduce and
     // forward apply, -1.2 % for the backward apply: profiles/bn_loads_in_flight_r2c.jsonl)
-    case 0: bn_bwd_reduce_kernel<0><<<G, 256, shr, st>>>(a, part); break;
-    case 1: bn_bwd_reduce_kernel<1><<<G, 256, shr, st>>>(a, part); break;
-    case 2:
-      if (tunr & 16) bn_bwd_reduce_kernel<2, 4, true><<<G, 256, shr, st>>>(a, part);
-      else bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part);
-      break;
-    case 4:
-      if (tunr & 16) bn_bwd_reduce_kernel<4, 4, true><<<G, 256, shr, st>>>(a, part);
-      else bn_bwd_reduce_kernel<4><<<G, 256, shr, st>>>(a, part);
-      break;
+    // non-temporal loads: the reduce streams its inputs once (the apply pass re-reads them
+    // from HBM either way at these sizes)
+    case 0: bn_bwd_reduce_kernel<0, 4, true><<<G, 256, shr, st>>>(a, part); break;
+    case 1: bn_bwd_reduce_kernel<1, 4, true><<<G, 256, shr, st>>>(a, part); break;
+    case 2: bn_bwd_reduce_kernel<2, 4, true><<<G, 256, shr, st>>>(a, part); break;
+    case 4: bn_bwd_reduce_kernel<4, 4, true><<<G, 256, shr, st>>>(a, part); break;
     default: bn_bwd_reduce_kernel<3><<<G, 256, shr, st>>>(a, part); break;
   }
   const int G2 = colsum_groups(G);
@@ -1243,18 +1182,18 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
                                                                     (double)M, fb);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
-  // workgroup cap of the apply pass: 4096 (1024-8192 within noise,
+  // grid-strided mode 3: workgroup cap 4096 (1024-8192 within noise,
   // profiles/bn_bwd_apply_grid_ab_r3s3.txt)
   const int grid = grid_for(n8, 256, 4096);
   const size_t sh = sizeof(float) * 5 * C;
-  static const int tuneb = getenv("DMLAB_TUNE_BN") ? atoi(getenv("DMLAB_TUNE_BN")) : 0;  // TEMP
+  // streaming modes: flat blocks of 4 x 256 chunks, non-temporal (see bn_apply_kernel); the
+  // stem's pool-gather mode keeps its grid-strided loop
   const int gflat = (int)((n8 + 4 * 256 - 1) / (4 * 256));
 #define DM_BNB(MD, D)                                                                              \
   do {                                                                                             \
-    if (MD != 3 && (tuneb & 4)) {                                                                  \
-      if (tuneb & 8) bn_bwd_apply_kernel<MD, D, 4, true, true><<<gflat, 256, sh, st>>>(a, coef, dy, dres); \
-      else bn_bwd_apply_kernel<MD, D, 4, true, false><<<gflat, 256, sh, st>>>(a, coef, dy, dres);  \
-    } else                                                                                         \
+    if (MD != 3)                                                                                   \
+      bn_bwd_apply_kernel<MD, D, 4, true, true><<<gflat, 256, sh, st>>>(a, coef, dy, dres);        \
+    else                                                                                           \
       bn_bwd_apply_kernel<MD, D><<<grid, 256, sh, st>>>(a, coef, dy, dres);                        \
   } while (0)
   if (quad) {
@@ -1284,7 +1223,9 @@ void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf
   if (K == 3 && S == 2 && P == 1 && OH == (H - 1) / 2 + 1 && OW == (W - 1) / 2 + 1 &&
       (long long)N * H * W * C < (1LL << 31)) {
     const long long pairs = (long long)N * OH * ((OW + 1) / 2) * (C / 8);
-    bn_relu_maxpool3s2_kernel<<<grid_for(pairs, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
+    // non-temporal stores of out / yarg (+0.1-0.2 %, profiles/nt_pool_wgrad_reduce_ab_r4aa.txt);
+    // the overlapping window loads stay cached
+    bn_relu_maxpool3s2_kernel<true><<<grid_for(pairs, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
         y, scale, shift, out, idx, yarg, N, H, W, C, OH, OW);
     return;
   }
@@ -1302,7 +1243,7 @@ int bn_bwd_reduce_masked(const bf16_t* dout, const bf16_t* y, const float* mean,
               M, C, nullptr};
   const int G = bn_bwd_groups(M, C);
   const size_t shr = sizeof(float) * (256 * 16 + 2 * C);
-  bn_bwd_reduce_kernel<2><<<G, 256, shr, st>>>(a, part);
+  bn_bwd_reduce_kernel<2, 4, true><<<G, 256, shr, st>>>(a, part);
   return G;
 }
 

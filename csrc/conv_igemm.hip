@@ -406,6 +406,7 @@ __global__ void __launch_bounds__(256, 2) igemm_wgrad2_kernel(
 }
 
 // dw[co][ci][kh][kw] = beta*dw + Σ_s slab[s][co][(kh*KW+kw)*C + ci]   (ci < Cin)
+template <bool NT>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            int S, int Cout, int C, int Cin,
                                                            int KH, int KW,
@@ -428,7 +429,9 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     for (; i + 7 * lanes < S; i += 8 * lanes) {
       float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = src[(long long)(i + j * lanes) * plane];
+      for (int j = 0; j < 8; ++j)
+        v[j] = NT ? __builtin_nontemporal_load(src + (long long)(i + j * lanes) * plane)
+                  : src[(long long)(i + j * lanes) * plane];
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc += v[j];
     }
@@ -830,8 +833,9 @@ void wgrad_reduce(const float* slab, int S, int Cout, int C, int Cin, int KH, in
   int lanes = 1;  // split the S-sum over lanes so small gradients with many slabs stay parallel
   while (lanes < 16 && lanes * 8 < S) lanes *= 2;
   const int E = 256 / lanes;
-  wgrad_reduce_kernel<<<(unsigned)((total + E - 1) / E), 256, 0, st>>>(slab, S, Cout, C, Cin, KH,
-                                                                      KW, dw, beta, lanes);
+  // non-temporal slab loads: every slab is read once (profiles/nt_pool_wgrad_reduce_ab_r4aa.txt)
+  wgrad_reduce_kernel<true><<<(unsigned)((total + E - 1) / E), 256, 0, st>>>(slab, S, Cout, C, Cin,
+                                                                          KH, KW, dw, beta, lanes);
 }
 
 void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int Cpad, int KH,
