@@ -43,6 +43,7 @@ namespace {
 constexpr int PBM = 256;   // output pixels per tile
 constexpr int PBK = 64;    // K per step (one 128-B LDS row per tile row)
 constexpr unsigned POOB = 0x80000000u;
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
 
 // BN output channels per tile (256 / 128 / 64); WM x WN waves, wave tile 256/WM x BN/WN;
 // MINW waves per SIMD the register budget is sized for.  (A PRE variant that applied the
@@ -402,7 +403,11 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
       }
       const uint4 ov = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]),
                                   pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
-      *reinterpret_cast<uint4*>(Y + o) = ov;
+      {  // non-temporal store (profiles/conv_nt_stores_ab_r4ab.txt)
+        u32x4_nt v;
+        v.x = ov.x; v.y = ov.y; v.z = ov.z; v.w = ov.w;
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4_nt*>(Y + o));
+      }
       if constexpr (RED) {
         // dz = the stored gradient where the reduced BN's ReLU passed (1-bit mask, or
         // y*sc + sh > 0); Σdz and Σdz (y - mu) per channel

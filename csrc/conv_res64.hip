@@ -312,7 +312,9 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
         }
         const v4u32_t o = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]),
                            pack_bf2(v[6], v[7])};
-        __builtin_amdgcn_raw_buffer_store_b128(o, rsy, off, 0, 0);
+        // non-temporal (aux bit 1): the output streams past L2/MALL (+1.1 % per step with
+        // the other conv epilogues, profiles/conv_nt_stores_ab_r4ab.txt)
+        __builtin_amdgcn_raw_buffer_store_b128(o, rsy, off, 0, 2);
         if (RED && ADD) {  // the band keeps the stored values for the reduction below
           *reinterpret_cast<float4*>(cs + rr * R_LDC + cq * 8) = make_float4(v[0], v[1], v[2], v[3]);
           *reinterpret_cast<float4*>(cs + rr * R_LDC + cq * 8 + 4) = make_float4(v[4], v[5], v[6], v[7]);

@@ -248,7 +248,12 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
         tile_vals((tid + i * NT) / CPR, av[k], mb[k], v);
         const uint32_t ow[4] = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]),
                                 pack_bf2(v[6], v[7])};
-        *reinterpret_cast<uint4*>(Y + o[k]) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        {  // non-temporal store (profiles/conv_nt_stores_ab_r4ab.txt)
+          typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+          u32x4_nt v;
+          v.x = ow[0]; v.y = ow[1]; v.z = ow[2]; v.w = ow[3];
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4_nt*>(Y + o[k]));
+        }
         if constexpr (RED) {
           const uint32_t yw[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
 #pragma unroll
