@@ -1080,6 +1080,8 @@ void pack_input_s2d(const void* x, bool bf16, bf16_t* y, int N, int C, int H2, i
   const long long total = (long long)N * H2 * W2;
   if (!bf16 && C == 3 && Cp == 16 && sc == 1 && sw == 3 && sh == 3LL * 2 * W2 && W2 % 2 == 0 &&
       ((uintptr_t)x & 15) == 0 && sn % 4 == 0) {
+    // (non-temporal loads/stores measured slower here: the step's two alternating input
+    // batches partly stay in the MALL, profiles/nt_pack_stem_bwd_rejected_r4ad.txt)
     pack_input_s2d_cl3_kernel<<<grid_for(total / 2, 256, 8192), 256, 0, st>>>(
         (const float*)x, y, N, H2, W2, sn, idx, nsrc);
     return;

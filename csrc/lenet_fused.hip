@@ -79,8 +79,11 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   __shared__ float h1[128], lg[16], dl[16], dh1[128], g2[400], g1[6 * 196];
   __shared__ float dc2[16 * 18 * 18];      // unpooled conv2 gradient, 4-pixel zero border
   __shared__ float4 red4[10 * 100];        // cross-thread partials (fc1 dgrad, conv2, conv1 dw)
-  __shared__ float pdg[4 * 1176];          // conv2 dgrad partials of the 4 output-channel groups
-  __shared__ float pc2[6 * 1600];          // conv2 forward partials of the 6 input channels
+  // cross-thread partials: conv2 forward [6 input channels][16][10][10], later the conv2 data
+  // gradient [16 output channels][6][14][14] (the phases are separated by barriers)
+  __shared__ float big[16 * 1176];
+  float* pc2 = big;
+  float* pdq = big;
   float* red = reinterpret_cast<float*>(red4);
 
   // ---- stage input and the small weights (fc1's 192 KB stream from L2 instead) ----
@@ -277,39 +280,41 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
 
   float* cs = cslab + (long long)b * CS;
   // ---- conv2 data gradient (full correlation of the unpooled, zero-bordered gradient dc2
-  //      with the flipped kernel) on threads 0..671: thread (group og of 4 output channels,
-  //      channel c, row y, 7-column half) computes 7 outputs from a 5 x 11 window, one window
-  //      row at a time (55 + 25 LDS reads per output channel for 175 FMAs); the 4 group
-  //      partials are summed in a fixed order after the barrier ----
-  // ---- conv2 weight gradient on threads 672..1023: item (o, c, kh) = the 5 taps kw of one
+  //      with the flipped kernel) on threads 0..447: thread (output channel o, row y, 7-column
+  //      half) computes the 6 x 7 outputs of every input channel from one 5 x 11 window of
+  //      dc2[o], read one row at a time (55 window + 150 weight reads for 1050 FMAs); the 16
+  //      per-o partials are summed in a fixed order after the barrier ----
+  // ---- conv2 weight gradient on threads 448..1023: item (o, c, kh) = the 5 taps kw of one
   //      kernel row, summed over the 25 argmax positions of channel o ----
-  if (tid < 672) {
-    const int og = tid / 168, r168 = tid - og * 168;
-    const int c = r168 / 28, r28 = r168 - c * 28, y0 = r28 >> 1, x0 = 7 * (r28 & 1);
-    float acc[7];
+  if (tid < 448) {
+    const int o = tid / 28, r28 = tid - o * 28, y0 = r28 >> 1, x0 = 7 * (r28 & 1);
+    float acc[6][7];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) acc[q] = 0.f;
-    for (int o = 4 * og; o < 4 * og + 4; ++o) {
-      const float* wo = w2 + o * 150 + c * 25;
-      const float* d = dc2 + o * 324 + y0 * 18 + x0;
+    for (int c = 0; c < 6; ++c)
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh) {  // output row y0 reads window row 4 - kh
-        float row[11];
+      for (int q = 0; q < 7; ++q) acc[c][q] = 0.f;
+    const float* d = dc2 + o * 324 + y0 * 18 + x0;
+#pragma unroll 1
+    for (int kh = 0; kh < 5; ++kh) {  // output row y0 reads window row 4 - kh
+      float row[11];
 #pragma unroll
-        for (int q = 0; q < 11; ++q) row[q] = d[(4 - kh) * 18 + q];
+      for (int q = 0; q < 11; ++q) row[q] = d[(4 - kh) * 18 + q];
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const float wv = wo[kh * 5 + kw];
+          const float wv = w2[o * 150 + c * 25 + kh * 5 + kw];
 #pragma unroll
-          for (int q = 0; q < 7; ++q) acc[q] += row[q + 4 - kw] * wv;
+          for (int q = 0; q < 7; ++q) acc[c][q] += row[q + 4 - kw] * wv;
         }
-      }
     }
-    float* pg = pdg + og * 1176 + c * 196 + y0 * 14 + x0;
+    float* pg = pdq + o * 1176 + y0 * 14 + x0;
 #pragma unroll
-    for (int q = 0; q < 7; ++q) pg[q] = acc[q];
+    for (int c = 0; c < 6; ++c)
+#pragma unroll
+      for (int q = 0; q < 7; ++q) pg[c * 196 + q] = acc[c][q];
   } else {
-    for (int i = tid - 672; i < 480; i += LT - 672) {
+    for (int i = tid - 448; i < 480; i += LT - 448) {
       const int o = i / 30, r30 = i - o * 30, c = r30 / 5, kh = r30 - c * 5;
       const float* pc = p1 + c * 196 + kh * 14;
       float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
@@ -333,10 +338,10 @@ __global__ void __launch_bounds__(LT) lenet_sample_kernel(
   }
   __syncthreads();
   probe_stamp<PROBE>(probe, b, tid, 10);
-  for (int idx = tid; idx < 1176; idx += LT) {  // o-pair partials in order, unpool1 mask
+  for (int idx = tid; idx < 1176; idx += LT) {  // output-channel partials in order, unpool1
     float sacc = 0.f;
 #pragma unroll
-    for (int og = 0; og < 4; ++og) sacc += pdg[og * 1176 + idx];
+    for (int o = 0; o < 16; ++o) sacc += pdq[o * 1176 + idx];
     g1[idx] = pos1[idx] >= 0 ? sacc : 0.f;
   }
   __syncthreads();
