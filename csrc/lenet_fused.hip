@@ -395,90 +395,27 @@ __device__ __forceinline__ int seg_n(int s) {
   }
 }
 
-// fc1.w (48,000 of the 51,902 parameters) is reduced by tiles: a block owns 8 rows x 100
-// columns, stages dh1[b][8 rows] and h0[b][100 columns] of 32 samples at a time in LDS and
-// sums sample by sample in the same order as the per-parameter threads of the other segments
-// (bit-identical to a per-parameter loop); each thread owns 3-4 of the tile's 800 parameters.
-constexpr int GT_U = 8, GT_K = 100, GT_B = 32;
-constexpr int GT_BLOCKS = (120 / GT_U) * (400 / GT_K);
-constexpr int G_OTHER = 1200 + 10 + 120 + 2400 + 16 + 150 + 6;  // every segment but fc1.w
-constexpr int G_OTHER_BLOCKS = (G_OTHER + 255) / 256;
-
-struct LenetSgd {
-  float* grad;
-  float* p;
-  float* mom;
-  float lr, momentum, dampening, wd, gscale;
-  int nesterov, first, do_sgd;
-};
-
-__device__ __forceinline__ void grad_finish(const LenetSgd& s, int o, float g) {
-  s.grad[o] = g;
-  if (!s.do_sgd) return;
-  float d = g * s.gscale;
-  const float pv = s.p[o];
-  if (s.wd != 0.f) d += s.wd * pv;
-  if (s.momentum != 0.f) {
-    const float bv = s.first ? d : s.momentum * s.mom[o] + (1.f - s.dampening) * d;
-    s.mom[o] = bv;
-    d = s.nesterov ? d + s.momentum * bv : bv;
-  }
-  s.p[o] = pv - s.lr * d;
-}
-
 __global__ void __launch_bounds__(256) lenet_grad_kernel(
-    const float* __restrict__ rec, const float* __restrict__ cslab, int B, LenetFlat fl,
-    LenetSgd sg, const float* __restrict__ rowloss, float* __restrict__ loss,
-    int* __restrict__ cursor, int nbatch, float* __restrict__ loss_sum) {
-  const int tid = threadIdx.x;
-  if (blockIdx.x >= G_OTHER_BLOCKS) {  // ---- fc1.w tiles ----
-    __shared__ float sd[GT_B][GT_U], sh[GT_B][GT_K];
-    const int tile = blockIdx.x - G_OTHER_BLOCKS;
-    const int u0 = (tile / (400 / GT_K)) * GT_U, k0 = (tile % (400 / GT_K)) * GT_K;
-    float g[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int b0 = 0; b0 < B; b0 += GT_B) {
-      const int nb = B - b0 < GT_B ? B - b0 : GT_B;
-      for (int e = tid; e < nb * GT_U; e += 256)
-        sd[e / GT_U][e % GT_U] = rec[(long long)(b0 + e / GT_U) * 656 + 520 + u0 + e % GT_U];
-      for (int e = tid; e < nb * GT_K; e += 256)
-        sh[e / GT_K][e % GT_K] = rec[(long long)(b0 + e / GT_K) * 656 + k0 + e % GT_K];
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = tid + j * 256;
-        if (q < GT_U * GT_K) {
-          const int uu = q / GT_K, kk = q - uu * GT_K;
-          for (int bb = 0; bb < nb; ++bb) g[j] += sd[bb][uu] * sh[bb][kk];
-        }
-      }
-      __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = tid + j * 256;
-      if (q < GT_U * GT_K) {
-        const int uu = q / GT_K, kk = q - uu * GT_K;
-        grad_finish(sg, fl.off[2] + (u0 + uu) * 400 + k0 + kk, g[j]);
-      }
-    }
-    return;
-  }
-  if (blockIdx.x == 0 && tid < 64) {  // mean loss, fixed order
+    const float* __restrict__ rec, const float* __restrict__ cslab, int B, float* __restrict__ grad,
+    LenetFlat fl, float* __restrict__ p, float* __restrict__ mom, float lr, float momentum,
+    float dampening, float wd, float gscale, int nesterov, int first, int do_sgd,
+    const float* __restrict__ rowloss, float* __restrict__ loss, int* __restrict__ cursor,
+    int nbatch, float* __restrict__ loss_sum) {
+  int i = blockIdx.x * 256 + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // mean loss, fixed order
     float a = 0.f;
-    for (int j = tid; j < B; j += 64) a += rowloss[j];
+    for (int j = threadIdx.x; j < B; j += 64) a += rowloss[j];
     a = wave_sum(a);
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
       *loss = a / (float)B;
       if (loss_sum != nullptr) *loss_sum += a / (float)B;  // device-side running sum (logging)
       // next batch of the epoch (the sample kernel that read the cursor has finished)
       if (cursor != nullptr) *cursor = (*cursor + 1 >= nbatch) ? 0 : *cursor + 1;
     }
   }
-  // ---- every other segment: one thread per parameter ----
-  int i = blockIdx.x * 256 + tid;
   int seg = 0;
-  while (seg < 8 && i >= (seg == 2 ? 0 : seg_n(seg))) {
-    i -= seg == 2 ? 0 : seg_n(seg);
+  while (seg < 8 && i >= seg_n(seg)) {
+    i -= seg_n(seg);
     ++seg;
   }
   if (seg == 8) return;
@@ -489,6 +426,10 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + o] * rec[b * 656 + 400 + u];
   } else if (seg == 1) {
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + i];
+  } else if (seg == 2) {  // fc1.w[u][k] = sum_b dh1[b][u] h0[b][k]
+    const int u = i / 400, k = i - u * 400;
+#pragma unroll 16
+    for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + u] * rec[b * 656 + k];
   } else if (seg == 3) {
     for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + i];
   } else {
@@ -496,7 +437,18 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
 #pragma unroll 16
     for (int b = 0; b < B; ++b) g += cslab[(long long)b * CS + base + i];
   }
-  grad_finish(sg, fl.off[seg] + i, g);
+  const int o = fl.off[seg] + i;
+  grad[o] = g;
+  if (!do_sgd) return;
+  float d = g * gscale;
+  const float pv = p[o];
+  if (wd != 0.f) d += wd * pv;
+  if (momentum != 0.f) {
+    const float bv = first ? d : momentum * mom[o] + (1.f - dampening) * d;
+    mom[o] = bv;
+    d = nesterov ? d + momentum * bv : bv;
+  }
+  p[o] = pv - lr * d;
 }
 }  // namespace
 
@@ -525,10 +477,13 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
   DM_CHECK(hipGetLastError());
   LenetFlat fl;
   for (int j = 0; j < 8; ++j) fl.off[j] = off[j];
-  const LenetSgd sg{grad, p, mom, lr, momentum, dampening, wd, gscale, nesterov ? 1 : 0,
-                    first ? 1 : 0, do_sgd ? 1 : 0};
-  lenet_grad_kernel<<<G_OTHER_BLOCKS + GT_BLOCKS, 256, 0, st>>>(
-      rec, cslab, B, fl, sg, rowloss, loss, sidx != nullptr ? cursor : nullptr, nbatch, loss_sum);
+  const int total = 1200 + 10 + 48000 + 120 + 2400 + 16 + 150 + 6;
+  lenet_grad_kernel<<<(total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
+                                                         momentum, dampening, wd, gscale,
+                                                         nesterov ? 1 : 0, first ? 1 : 0,
+                                                         do_sgd ? 1 : 0, rowloss, loss,
+                                                         sidx != nullptr ? cursor : nullptr,
+                                                         nbatch, loss_sum);
   DM_CHECK(hipGetLastError());
 }
 
