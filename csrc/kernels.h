@@ -125,6 +125,10 @@ void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
                const float* pre_sc = nullptr, const float* pre_sh = nullptr,
                const BnBwdRed* red = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
+// stride-2 3x3 weight gradient over the four input parity planes (wgrad cfg 7)
+bool wgrad_s2_supported(const ConvGeom& g);
+void wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+              long long mchunk, hipStream_t st);
 // wgrad_res64.hip: row-streaming 64 -> 64 channel 3x3 weight gradient (wgrad cfg 8); S slabs
 bool wgrad_res64_supported(const ConvGeom& g);
 void wgrad_res64(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,

@@ -198,6 +198,188 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
       }
 }
 
+// ---------------------------------------------------------------- stride 2 (wgrad cfg 7)
+// 3x3 / stride-2 / pad-1 weight gradient of an even-sized input (the first conv of layers
+// 2-4).  Output pixel m = (n, y, x) reads input (2y + dy, 2x + dx), dy, dx in {-1, 0, 1}.
+// The input splits into four parity planes P(a, b) = pixels (2i + a, 2j + b), each indexed
+// exactly like the output (q = (n*Ho + i)*Wo + j), and tap (dy, dx) of pixel m reads plane
+// (dy & 1, dx & 1) at q = m + di*Wo + dj with di = (dy < 0 ? -1 : 0), dj likewise: per plane a
+// CONSTANT offset, as in the stride-1 kernel.  A step stages the 64 dY rows and, per plane,
+// the flattened range [m0 - lead, m0 + 64) its taps touch (lead 0, 1, Wo, Wo + 1 for planes
+// (0,0), (0,1), (1,0), (1,1): 258 + 2 Wo rows), and all 9 taps read B fragments from it.
+template <int HRN>
+__global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
+    ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes, int xy, int gx, int nz) {
+  constexpr int HROWS_MAX = HRN * 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][64][WPITCH] dY
+  bf16_t* Hs = As + 2 * WBK * WPITCH;                       // [2][HROWS_MAX][WPITCH] planes
+  bf16_t* Zr = Hs + 2 * HROWS_MAX * WPITCH;                 // one zero row
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (xy) {  // XCD-grouped 1-D grid, as the stride-1 kernel
+    const int b = blockIdx.x, j = b >> 3, t = j % xy;
+    bz = (j / xy) * 8 + (b & 7);
+    if (bz >= nz) return;
+    bx = t % gx;
+    by = t / gx;
+  }
+  const int co0 = bx * WBM;
+  const int cc0 = by * WBC;
+  const long long mb = (long long)bz * mchunk;
+  const long long me = min(g.M, mb + mchunk);
+  const int Wo = g.Wg, Ho = g.Hg, Wi = g.W, Hi = g.H;
+  // plane row bases in LDS and leads: plane p = a*2 + b
+  const int lead1 = 1, lead2 = Wo, lead3 = Wo + 1;
+  const int base1 = WBK, base2 = base1 + WBK + lead1, base3 = base2 + WBK + lead2;
+  const int hrows = base3 + WBK + lead3;
+  const long long NQ = g.M;  // plane positions (= output pixels)
+  if (tid < WPITCH / 8) *reinterpret_cast<uint4*>(Zr + tid * 8) = make_uint4(0, 0, 0, 0);
+
+  const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
+  const auto rsd = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, (int)dybytes, 0x00020000);
+  const int chunk = tid & 7, row0 = tid >> 3;
+
+  uint4 ra[2], rh[HRN];
+  auto load = [&](long long m0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long m = m0 + row0 + 32 * i;
+      const unsigned off = m < me ? (unsigned)((m * g.Ncols + co0 + chunk * 8) * 2) : WOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsd, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int j = 0; j < HRN; ++j) {
+      const int h = row0 + 32 * j;
+      int a, b;
+      long long q;
+      if (h < base1) { a = 0; b = 0; q = m0 + h; }
+      else if (h < base2) { a = 0; b = 1; q = m0 - lead1 + (h - base1); }
+      else if (h < base3) { a = 1; b = 0; q = m0 - lead2 + (h - base2); }
+      else { a = 1; b = 1; q = m0 - lead3 + (h - base3); }
+      unsigned off = WOOB;
+      if (h < hrows && q >= 0 && q < NQ) {
+        const unsigned t = fdiv((unsigned)q, g.wg_mul, g.wg_shr);
+        const int jj = (int)((unsigned)q - t * (unsigned)Wo);
+        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+        const int ii = (int)(t - n * (unsigned)Ho);
+        const int yi = 2 * ii + a, xi = 2 * jj + b;
+        if (yi < Hi && xi < Wi)
+          off = (unsigned)(((((long long)n * Hi + yi) * Wi + xi) * g.C + cc0 + chunk * 8) * 2);
+      }
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store = [&](int buf) {
+    bf16_t* as = As + buf * WBK * WPITCH;
+    bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
+#pragma unroll
+    for (int j = 0; j < HRN; ++j)
+      *reinterpret_cast<uint4*>(hs + (row0 + 32 * j) * WPITCH + chunk * 8) = rh[j];
+  };
+
+  f32x4 acc[4][9];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int grp = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int rbase = grp * 4 + q4;
+  const int nsteps = me > mb ? (int)((me - mb + WBK - 1) / WBK) : 0;
+  if (nsteps > 0) {
+    load(mb);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    const long long m0 = mb + (long long)s * WBK;
+    if (s + 1 < nsteps) load(m0 + WBK);
+    const bf16_t* as = As + buf * WBK * WPITCH;
+    const bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      int xr[2], yr[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const unsigned m = (unsigned)(m0 + ks * 32 + rbase + 16 * u);
+        const unsigned t = fdiv(m, g.wg_mul, g.wg_shr);
+        xr[u] = (int)(m - t * (unsigned)Wo);
+        const unsigned n = fdiv(t, g.hg_mul, g.hg_shr);
+        yr[u] = (int)(t - n * (unsigned)Ho);
+      }
+      bf16x8 af[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int col = i * 16 + 4 * p4;
+        const s4 lo = tr_read(as + (ks * 32 + rbase) * WPITCH + col);
+        const s4 hi = tr_read(as + (ks * 32 + rbase + 16) * WPITCH + col);
+        af[i] = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      const int bcol = wid * 16 + 4 * p4;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dy = t / 3 - 1, dx = t % 3 - 1;
+        const int a = dy & 1, b = dx & 1;
+        const int pbase = a ? (b ? base3 + lead3 : base2 + lead2) : (b ? base1 + lead1 : 0);
+        const int poff = (dy < 0 ? -Wo : 0) + (dx < 0 ? -1 : 0);
+        const bf16_t* src[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const bool ok = (unsigned)(2 * xr[u] + dx) < (unsigned)Wi &&
+                          (unsigned)(2 * yr[u] + dy) < (unsigned)Hi;
+          const int h = pbase + ks * 32 + rbase + 16 * u + poff;
+          src[u] = ok ? hs + h * WPITCH + bcol : Zr + 4 * p4;
+        }
+        const s4 lo = tr_read(src[0]);
+        const s4 hi = tr_read(src[1]);
+        const bf16x8 bfr = (bf16x8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][t], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nsteps) store(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = slab + (long long)bz * g.Ncols * g.K;
+  const int c = cc0 + wid * 16 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + i * 16 + (lane >> 4) * 4 + r;
+        if (co < g.Ncols) out[(long long)co * g.K + t * g.C + c] = acc[i][t][r];
+      }
+}
+
+template <int HRN>
+void launch_wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+                     long long mchunk, hipStream_t st) {
+  const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
+  dim3 grid((g.Ncols + WBM - 1) / WBM, g.C / WBC, S);
+  const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
+  const unsigned db = (unsigned)(g.M * g.Ncols * 2);
+  auto k = wgrad_s2_kernel<HRN>;
+  set_smem_attr(k, sm);
+  const int xy = (int)(grid.x * grid.y);
+  if (xy > 1 && S > 1) {
+    const unsigned z8 = (unsigned)((S + 7) / 8 * 8);
+    k<<<dim3(z8 * xy), 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, xy, (int)grid.x, S);
+    return;
+  }
+  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, 0, (int)grid.x, S);
+}
+
 template <int HRN, int NTY>
 void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                        long long mchunk, hipStream_t st, const float* pre_sc,
@@ -231,6 +413,26 @@ bool wgrad_halo_supported(const ConvGeom& g) {
   if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31) || g.M * g.Ncols * 2 >= (1LL << 31))
     return false;
   return WBK + 2 * g.W + 2 <= 6 * 32;
+}
+
+bool wgrad_s2_supported(const ConvGeom& g) {
+  // 3x3, stride 2, pad 1, even input (output = input / 2), tap order (kh, kw) row-major
+  if (g.isy != 2 || g.isx != 2 || g.H != 2 * g.Hg || g.W != 2 * g.Wg) return false;
+  if (g.nth != 3 || g.ntw != 3 || g.dy0 != -1 || g.dys != 1 || g.dx0 != -1 || g.dxs != 1) return false;
+  if (g.kh0 != 0 || g.khs != 1 || g.kw0 != 0 || g.kws != 1 || g.KW != 3) return false;
+  if (g.C % WBC != 0 || g.Ncols % 8 != 0 || g.K != 9 * g.C) return false;
+  if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31) || g.M * g.Ncols * 2 >= (1LL << 31))
+    return false;
+  return 4 * WBK + 2 * g.Wg + 2 <= 10 * 32;
+}
+
+void wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
+              long long mchunk, hipStream_t st) {
+  if (!wgrad_s2_supported(g)) throw std::runtime_error("wgrad_s2: unsupported geometry");
+  const int rows = 4 * WBK + 2 * g.Wg + 2;
+  if (rows <= 9 * 32) launch_wgrad_s2<9>(X, DY, slab, g, S, mchunk, st);
+  else launch_wgrad_s2<10>(X, DY, slab, g, S, mchunk, st);
+  DM_CHECK(hipGetLastError());
 }
 
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,

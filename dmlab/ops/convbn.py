@@ -112,13 +112,15 @@ def _cu_count():
     return _CUS[d]
 
 
-def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=False):
+def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=False,
+                even=False):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
     cfg 8: row-streaming 64 -> 64 channel 3x3 kernel (csrc/wgrad_res64.hip; ``W`` = image
     width <= 60, ``rows`` = N*H image rows, S = 5/8 of the CUs); cfg 4/5: halo-staged 3x3
-    unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per block; cfg 2/3/6: v2 igemm
-    tiles 128x128 / 64x128 / 64x256.
+    unit-stride kernel (csrc/wgrad_halo.hip) with 9 / 3 taps per block; cfg 7: the stride-2
+    3x3 kernel over the input's parity planes (same file); cfg 2/3/6: v2 igemm tiles
+    128x128 / 64x128 / 64x256.
     S splits the m reduction over blocks into fp32 slabs summed by a fixed-order reduce:
     ~2 blocks per CU, each split >= 8 row steps, slab bytes S*cout*K*4."""
     halo = k == 3 and stride == 1 and cin % 64 == 0 and cout % 8 == 0
@@ -133,8 +135,13 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # side stream, measure the same or slower: profiles/tail_wgrad_placement_ab_r4i.txt)
         S = _cu_count() if tail else max(1, _cu_count() * 5 // 8)
         return 8, max(1, min(rows, S))
+    # ``even``: a stride-2 3x3 conv whose output is exactly half the input in both dims
+    s2 = k == 3 and stride == 2 and cin % 64 == 0 and cout % 8 == 0 and even
     if force is not None:
         cfg = force
+    elif s2:
+        # stride-2 3x3 (first conv of layers 2-4): the parity-plane kernel, 9 taps per block
+        cfg = 7
     elif halo:
         # 9 taps per block share every dY fragment, but a layer with few (cout, cin)
         # tiles then needs many m-splits (slab traffic ~ S * cout * K); 3 taps per block
@@ -142,7 +149,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         cfg = 4 if math.ceil(cout / 64) * (cin // 64) >= 4 else 5
     else:
         cfg = 2 if cout % 128 == 0 else 3
-    if cfg in (4, 5):
+    if cfg in (4, 5, 7):
         tiles = max(1, math.ceil(cout / 64) * (cin // 64) * (3 if cfg == 5 else 1))
         max_split = max(1, M // 512)
     else:
@@ -467,8 +474,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     same = not s2d and (OH, OW) == tuple(x.shape[1:3])
     # red_for is the stem (a pooled ConvBN) only for the first block's c1: the step's last conv
     tail = red_for is not None and bool(getattr(red_for[0], "pool_k", 0))
+    even = not s2d and 2 * OH == x.shape[1] and 2 * OW == x.shape[2]
+    even = even and os.environ.get("DMLAB_TUNE_S2", "1") == "1"  # TEMP A/B (r4)
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
-                          tail=tail)
+                          tail=tail, even=even)
     dy = empty_nhwc(N, OH, OW, cout, y)
     masked_res = fused_skip and ctx["has_res"] and mode == 4
     dres = empty_nhwc(N, OH, OW, cout, y) if (ctx["has_res"] and not masked_res) else None

@@ -753,3 +753,29 @@ def _bits(keep):
     """1-bit mask layout of the kernels: bit j of byte i = element 8i + j (NHWC order)."""
     b = keep.reshape(-1, 8).to(torch.uint8) << torch.arange(8, device=keep.device, dtype=torch.uint8)
     return b.sum(1, dtype=torch.uint8)
+
+
+# stride-2 3x3 weight gradient over the input parity planes (wgrad cfg 7): the first conv of
+# layers 2-4, a small multi-image case (m-steps crossing images), partial last m-step
+WS2_GEOMS = [(2, 56, 64, 128, 3, 2, 1), (3, 28, 128, 256, 3, 2, 1), (2, 14, 256, 512, 3, 2, 1),
+             (5, 8, 64, 64, 3, 2, 1), (1, 6, 64, 64, 3, 2, 1)]
+
+
+@pytest.mark.parametrize("geom", WS2_GEOMS)
+@pytest.mark.parametrize("S", [1, 3, 16])
+def test_conv_wgrad_s2(dev, geom, S):
+    N, H, Cin, Cout, k, s, p = geom
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p, seed=7)
+    OH = H // 2
+    dy = torch.randn(N, Cout, OH, OH, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, p)
+    K = k * k * _cpad(Cin)
+    S = max(1, min(S, N * OH * OH // 64))
+    slab = torch.full((S * Cout * K,), float("nan"), device=dev)
+    d = torch.empty_like(w)
+    lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, 0.0, S, 7, False)
+    assert _rel(d, ref) < 2e-3
+    base = torch.randn_like(w)
+    d = base.clone()  # beta = 1: accumulate
+    lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, 1.0, S, 7, False)
+    assert _rel(d, ref + base) < 2e-3
