@@ -204,17 +204,18 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
 // The input splits into four parity planes P(a, b) = pixels (2i + a, 2j + b), each indexed
 // exactly like the output (q = (n*Ho + i)*Wo + j), and tap (dy, dx) of pixel m reads plane
 // (dy & 1, dx & 1) at q = m + di*Wo + dj with di = (dy < 0 ? -1 : 0), dj likewise: per plane a
-// CONSTANT offset, as in the stride-1 kernel.  A step stages the 64 dY rows and, per plane,
-// the flattened range [m0 - lead, m0 + 64) its taps touch (lead 0, 1, Wo, Wo + 1 for planes
-// (0,0), (0,1), (1,0), (1,1): 258 + 2 Wo rows), and all 9 taps read B fragments from it.
-template <int HRN>
-__global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
+// CONSTANT offset, as in the stride-1 kernel.  A step stages MR dY rows and, per plane, the
+// flattened range [m0 - lead, m0 + MR) its taps touch (lead 0, 1, Wo, Wo + 1 for planes
+// (0,0), (0,1), (1,0), (1,1): 4 MR + 2 Wo + 2 rows), and all 9 taps read B fragments from it.
+// MR: m rows per step (32: two workgroups per CU fit the LDS)
+template <int HRN, int MR>
+__global__ void __launch_bounds__(256, MR == 32 ? 2 : 1) wgrad_s2_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes, int xy, int gx, int nz) {
   constexpr int HROWS_MAX = HRN * 32;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][64][WPITCH] dY
-  bf16_t* Hs = As + 2 * WBK * WPITCH;                       // [2][HROWS_MAX][WPITCH] planes
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][MR][WPITCH] dY
+  bf16_t* Hs = As + 2 * MR * WPITCH;                        // [2][HROWS_MAX][WPITCH] planes
   bf16_t* Zr = Hs + 2 * HROWS_MAX * WPITCH;                 // one zero row
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
@@ -232,8 +233,8 @@ __global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
   const int Wo = g.Wg, Ho = g.Hg, Wi = g.W, Hi = g.H;
   // plane row bases in LDS and leads: plane p = a*2 + b
   const int lead1 = 1, lead2 = Wo, lead3 = Wo + 1;
-  const int base1 = WBK, base2 = base1 + WBK + lead1, base3 = base2 + WBK + lead2;
-  const int hrows = base3 + WBK + lead3;
+  const int base1 = MR, base2 = base1 + MR + lead1, base3 = base2 + MR + lead2;
+  const int hrows = base3 + MR + lead3;
   const long long NQ = g.M;  // plane positions (= output pixels)
   if (tid < WPITCH / 8) *reinterpret_cast<uint4*>(Zr + tid * 8) = make_uint4(0, 0, 0, 0);
 
@@ -241,10 +242,10 @@ __global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
   const auto rsd = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, (int)dybytes, 0x00020000);
   const int chunk = tid & 7, row0 = tid >> 3;
 
-  uint4 ra[2], rh[HRN];
+  uint4 ra[MR / 32], rh[HRN];
   auto load = [&](long long m0) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < MR / 32; ++i) {
       const long long m = m0 + row0 + 32 * i;
       const unsigned off = m < me ? (unsigned)((m * g.Ncols + co0 + chunk * 8) * 2) : WOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsd, off, 0, 0);
@@ -274,10 +275,10 @@ __global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
     }
   };
   auto store = [&](int buf) {
-    bf16_t* as = As + buf * WBK * WPITCH;
+    bf16_t* as = As + buf * MR * WPITCH;
     bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MR / 32; ++i)
       *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
 #pragma unroll
     for (int j = 0; j < HRN; ++j)
@@ -292,7 +293,7 @@ __global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
 
   const int grp = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   const int rbase = grp * 4 + q4;
-  const int nsteps = me > mb ? (int)((me - mb + WBK - 1) / WBK) : 0;
+  const int nsteps = me > mb ? (int)((me - mb + MR - 1) / MR) : 0;
   if (nsteps > 0) {
     load(mb);
     store(0);
@@ -300,12 +301,12 @@ __global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
-    const long long m0 = mb + (long long)s * WBK;
-    if (s + 1 < nsteps) load(m0 + WBK);
-    const bf16_t* as = As + buf * WBK * WPITCH;
+    const long long m0 = mb + (long long)s * MR;
+    if (s + 1 < nsteps) load(m0 + MR);
+    const bf16_t* as = As + buf * MR * WPITCH;
     const bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < MR / 32; ++ks) {
       int xr[2], yr[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -362,14 +363,14 @@ __global__ void __launch_bounds__(256, 1) wgrad_s2_kernel(
       }
 }
 
-template <int HRN>
+template <int HRN, int MR>
 void launch_wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                      long long mchunk, hipStream_t st) {
-  const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
+  const size_t sm = ((size_t)2 * MR * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
   dim3 grid((g.Ncols + WBM - 1) / WBM, g.C / WBC, S);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
-  auto k = wgrad_s2_kernel<HRN>;
+  auto k = wgrad_s2_kernel<HRN, MR>;
   set_smem_attr(k, sm);
   const int xy = (int)(grid.x * grid.y);
   if (xy > 1 && S > 1) {
@@ -423,15 +424,17 @@ bool wgrad_s2_supported(const ConvGeom& g) {
   if (g.C % WBC != 0 || g.Ncols % 8 != 0 || g.K != 9 * g.C) return false;
   if ((long long)g.N * g.H * g.W * g.C * 2 >= (1LL << 31) || g.M * g.Ncols * 2 >= (1LL << 31))
     return false;
-  return 4 * WBK + 2 * g.Wg + 2 <= 10 * 32;
+  return 4 * 32 + 2 * g.Wg + 2 <= 6 * 32;
 }
 
 void wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
               long long mchunk, hipStream_t st) {
   if (!wgrad_s2_supported(g)) throw std::runtime_error("wgrad_s2: unsupported geometry");
-  const int rows = 4 * WBK + 2 * g.Wg + 2;
-  if (rows <= 9 * 32) launch_wgrad_s2<9>(X, DY, slab, g, S, mchunk, st);
-  else launch_wgrad_s2<10>(X, DY, slab, g, S, mchunk, st);
+  // 32-row steps: 72 KB of LDS, two workgroups per CU (64-row steps, one per CU, lost 0.7 %:
+  // profiles/wgrad_s2_ab_r4al.txt, profiles/wgrad_s2_mr_ab_r4am.txt)
+  const int rows = 4 * 32 + 2 * g.Wg + 2;
+  if (rows <= 5 * 32) launch_wgrad_s2<5, 32>(X, DY, slab, g, S, mchunk, st);
+  else launch_wgrad_s2<6, 32>(X, DY, slab, g, S, mchunk, st);
   DM_CHECK(hipGetLastError());
 }
 

@@ -475,7 +475,6 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     # red_for is the stem (a pooled ConvBN) only for the first block's c1: the step's last conv
     tail = red_for is not None and bool(getattr(red_for[0], "pool_k", 0))
     even = not s2d and 2 * OH == x.shape[1] and 2 * OW == x.shape[2]
-    even = even and os.environ.get("DMLAB_TUNE_S2", "1") == "1"  # TEMP A/B (r4)
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
                           tail=tail, even=even)
     dy = empty_nhwc(N, OH, OW, cout, y)
