@@ -285,11 +285,12 @@ __global__ void __launch_bounds__(256, MR == 32 ? 2 : 1) wgrad_s2_kernel(
       *reinterpret_cast<uint4*>(hs + (row0 + 32 * j) * WPITCH + chunk * 8) = rh[j];
   };
 
-  f32x4 acc[4][9];
+  constexpr int NTAP = 9;
+  f32x4 acc[4][NTAP];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < NTAP; ++t) acc[i][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int grp = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   const int rbase = grp * 4 + q4;
@@ -326,7 +327,7 @@ __global__ void __launch_bounds__(256, MR == 32 ? 2 : 1) wgrad_s2_kernel(
       }
       const int bcol = wid * 16 + 4 * p4;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
+      for (int t = 0; t < NTAP; ++t) {
         const int dy = t / 3 - 1, dx = t % 3 - 1;
         const int a = dy & 1, b = dx & 1;
         const int pbase = a ? (b ? base3 + lead3 : base2 + lead2) : (b ? base1 + lead1 : 0);
@@ -355,7 +356,7 @@ __global__ void __launch_bounds__(256, MR == 32 ? 2 : 1) wgrad_s2_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < NTAP; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = co0 + i * 16 + (lane >> 4) * 4 + r;

@@ -113,7 +113,7 @@ def _cu_count():
 
 
 def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=False,
-                even=False):
+                even=0):
     """(cfg, S) for the weight-gradient GEMM dW[cout, K] = Σ_m dY[m, cout] X_col[m, K].
 
     cfg 8: row-streaming 64 -> 64 channel 3x3 kernel (csrc/wgrad_res64.hip; ``W`` = image
@@ -135,8 +135,11 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # side stream, measure the same or slower: profiles/tail_wgrad_placement_ab_r4i.txt)
         S = _cu_count() if tail else max(1, _cu_count() * 5 // 8)
         return 8, max(1, min(rows, S))
-    # ``even``: a stride-2 3x3 conv whose output is exactly half the input in both dims
-    s2 = k == 3 and stride == 2 and cin % 64 == 0 and cout % 8 == 0 and even
+    # ``even``: output width of a stride-2 conv whose output is exactly half the input in both
+    # dims (0 otherwise); the 3x3 plane staging holds rows up to a width of 31
+    # (1x1 projections on a one-tap variant of it measured slower than the igemm tile:
+    # profiles/wgrad_s2_1x1_rejected_r4ao.txt)
+    s2 = stride == 2 and k == 3 and cin % 64 == 0 and cout % 8 == 0 and 0 < even <= 31
     if force is not None:
         cfg = force
     elif s2:
@@ -474,7 +477,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     same = not s2d and (OH, OW) == tuple(x.shape[1:3])
     # red_for is the stem (a pooled ConvBN) only for the first block's c1: the step's last conv
     tail = red_for is not None and bool(getattr(red_for[0], "pool_k", 0))
-    even = not s2d and 2 * OH == x.shape[1] and 2 * OW == x.shape[2]
+    even = OW if (not s2d and 2 * OH == x.shape[1] and 2 * OW == x.shape[2]) else 0
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
                           tail=tail, even=even)
     dy = empty_nhwc(N, OH, OW, cout, y)

@@ -349,6 +349,19 @@ def test_wgrad_res64_plan():
     assert _wgrad_plan(1024 * 28 * 28, 128, 1152, 3, 1, 128, W=28, rows=1024 * 28)[0] != 8
 
 
+def test_wgrad_s2_plan():
+    """wgrad cfg 7 (the stride-2 parity-plane kernel) for 3x3/s2 layers whose output is half
+    the input and at most 31 wide; the igemm tile otherwise (1x1 projections included)."""
+    from dmlab.ops.convbn import _wgrad_plan
+    cfg, S = _wgrad_plan(1024 * 28 * 28, 128, 576, 3, 2, 64, even=28)
+    assert cfg == 7 and S >= 1
+    assert _wgrad_plan(1024 * 7 * 7, 512, 2304, 3, 2, 256, even=7)[0] == 7
+    assert _wgrad_plan(1024 * 28 * 28, 128, 64, 1, 2, 64, even=28)[0] != 7   # 1x1: igemm
+    assert _wgrad_plan(64 * 64 * 64, 128, 576, 3, 2, 64, even=64)[0] != 7   # too wide
+    assert _wgrad_plan(1024 * 28 * 28, 128, 576, 3, 2, 64)[0] != 7          # odd input
+    assert _wgrad_plan(1024 * 28 * 28, 128, 288, 3, 2, 32, even=28)[0] != 7  # channels
+
+
 def test_dgrad_red_selection():
     """Which data gradients reduce the consumer BN's backward sums in their epilogue
     (ops/convbn.py _dgrad_red): cfg 80 / 90-93 / 42, stride 1, a ReLU consumer of dx's shape;
