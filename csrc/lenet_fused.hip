@@ -401,7 +401,11 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
     float dampening, float wd, float gscale, int nesterov, int first, int do_sgd,
     const float* __restrict__ rowloss, float* __restrict__ loss, int* __restrict__ cursor,
     int nbatch, float* __restrict__ loss_sum) {
-  int i = blockIdx.x * 256 + threadIdx.x;
+  // two lanes per parameter: each sums half of the batch (16 loads in flight), the halves
+  // are added by a lane shuffle in a fixed order
+  const int half = threadIdx.x & 1;
+  int i = blockIdx.x * 128 + (threadIdx.x >> 1);
+  const int bh = (B + 1) >> 1, blo = half ? bh : 0, bhi = half ? B : bh;
   if (blockIdx.x == 0 && threadIdx.x < 64) {  // mean loss, fixed order
     float a = 0.f;
     for (int j = threadIdx.x; j < B; j += 64) a += rowloss[j];
@@ -423,20 +427,22 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
   if (seg == 0) {  // fc2.w[o][u] = sum_b dl[b][o] h1[b][u]
     const int o = i / 120, u = i - o * 120;
 #pragma unroll 16
-    for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + o] * rec[b * 656 + 400 + u];
+    for (int b = blo; b < bhi; ++b) g += rec[b * 656 + 640 + o] * rec[b * 656 + 400 + u];
   } else if (seg == 1) {
-    for (int b = 0; b < B; ++b) g += rec[b * 656 + 640 + i];
+    for (int b = blo; b < bhi; ++b) g += rec[b * 656 + 640 + i];
   } else if (seg == 2) {  // fc1.w[u][k] = sum_b dh1[b][u] h0[b][k]
     const int u = i / 400, k = i - u * 400;
 #pragma unroll 16
-    for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + u] * rec[b * 656 + k];
+    for (int b = blo; b < bhi; ++b) g += rec[b * 656 + 520 + u] * rec[b * 656 + k];
   } else if (seg == 3) {
-    for (int b = 0; b < B; ++b) g += rec[b * 656 + 520 + i];
+    for (int b = blo; b < bhi; ++b) g += rec[b * 656 + 520 + i];
   } else {
     const int base = seg == 4 ? 0 : seg == 5 ? 2400 : seg == 6 ? 2416 : 2566;
 #pragma unroll 16
-    for (int b = 0; b < B; ++b) g += cslab[(long long)b * CS + base + i];
+    for (int b = blo; b < bhi; ++b) g += cslab[(long long)b * CS + base + i];
   }
+  g += __shfl_xor(g, 1, 64);  // both lanes: first half + second half
+  if (half) return;
   const int o = fl.off[seg] + i;
   grad[o] = g;
   if (!do_sgd) return;
@@ -478,7 +484,7 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
   LenetFlat fl;
   for (int j = 0; j < 8; ++j) fl.off[j] = off[j];
   const int total = 1200 + 10 + 48000 + 120 + 2400 + 16 + 150 + 6;
-  lenet_grad_kernel<<<(total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
+  lenet_grad_kernel<<<(2 * total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
                                                          momentum, dampening, wd, gscale,
                                                          nesterov ? 1 : 0, first ? 1 : 0,
                                                          do_sgd ? 1 : 0, rowloss, loss,

@@ -161,6 +161,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # >= 8 row steps of 64 per split: the small-K layers (1x1/s2 downsample: K = Cin)
         # have one or two output tiles, so the m-split is their only parallelism
         max_split = max(1, M // 512)
+    # (2x / 4x more splits for cfg 7 measured -0.4 / -1.0 %: profiles/wgrad_s2_splits_ab_r4ap.txt)
     S = max(1, min(max_split, math.ceil(_WGRAD_BLOCKS / tiles)))
     return cfg, S
 
