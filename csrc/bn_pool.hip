@@ -1227,6 +1227,7 @@ void bn_relu_maxpool(const bf16_t* y, const float* scale, const float* shift, bf
     const long long pairs = (long long)N * OH * ((OW + 1) / 2) * (C / 8);
     // non-temporal stores of out / yarg (+0.1-0.2 %, profiles/nt_pool_wgrad_reduce_ab_r4aa.txt);
     // the overlapping window loads stay cached
+    // (an uncapped, one-pass grid measures the same: profiles/pool_pack_grid_ab_r4as.txt)
     bn_relu_maxpool3s2_kernel<true><<<grid_for(pairs, 256, 8192), 256, sizeof(float) * 2 * C, st>>>(
         y, scale, shift, out, idx, yarg, N, H, W, C, OH, OW);
     return;
