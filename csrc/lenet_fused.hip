@@ -401,11 +401,11 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
     float dampening, float wd, float gscale, int nesterov, int first, int do_sgd,
     const float* __restrict__ rowloss, float* __restrict__ loss, int* __restrict__ cursor,
     int nbatch, float* __restrict__ loss_sum) {
-  // four lanes per parameter: each sums a quarter of the batch (all its loads in flight at
-  // B = 32), the quarters are added by two lane shuffles (a fixed pairing)
-  const int qtr = threadIdx.x & 3;
-  int i = blockIdx.x * 64 + (threadIdx.x >> 2);
-  const int bq = (B + 3) >> 2, blo = min(B, qtr * bq), bhi = min(B, blo + bq);
+  // two lanes per parameter: each sums half of the batch (16 loads in flight), the halves
+  // are added by a lane shuffle in a fixed order
+  const int half = threadIdx.x & 1;
+  int i = blockIdx.x * 128 + (threadIdx.x >> 1);
+  const int bh = (B + 1) >> 1, blo = half ? bh : 0, bhi = half ? B : bh;
   if (blockIdx.x == 0 && threadIdx.x < 64) {  // mean loss, fixed order
     float a = 0.f;
     for (int j = threadIdx.x; j < B; j += 64) a += rowloss[j];
@@ -441,9 +441,8 @@ __global__ void __launch_bounds__(256) lenet_grad_kernel(
 #pragma unroll 16
     for (int b = blo; b < bhi; ++b) g += cslab[(long long)b * CS + base + i];
   }
-  g += __shfl_xor(g, 1, 64);
-  g += __shfl_xor(g, 2, 64);  // every lane of the four: (q0 + q1) + (q2 + q3)
-  if (qtr) return;
+  g += __shfl_xor(g, 1, 64);  // both lanes: first half + second half
+  if (half) return;
   const int o = fl.off[seg] + i;
   grad[o] = g;
   if (!do_sgd) return;
@@ -485,7 +484,7 @@ void lenet_fused_step(const void* x, bool x_bf16, const long long* labels, int B
   LenetFlat fl;
   for (int j = 0; j < 8; ++j) fl.off[j] = off[j];
   const int total = 1200 + 10 + 48000 + 120 + 2400 + 16 + 150 + 6;
-  lenet_grad_kernel<<<(4 * total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
+  lenet_grad_kernel<<<(2 * total + 255) / 256, 256, 0, st>>>(rec, cslab, B, grad, fl, p, mom, lr,
                                                          momentum, dampening, wd, gscale,
                                                          nesterov ? 1 : 0, first ? 1 : 0,
                                                          do_sgd ? 1 : 0, rowloss, loss,
