@@ -32,6 +32,7 @@
 #include "igemm_common.h"
 #include "kernels.h"
 
+#include <cstdint>
 #include <stdexcept>
 #include <string>
 
@@ -406,49 +407,59 @@ __global__ void __launch_bounds__(256, 2) igemm_wgrad2_kernel(
 }
 
 // dw[co][ci][kh][kw] = beta*dw + Σ_s slab[s][co][(kh*KW+kw)*C + ci]   (ci < Cin)
-template <bool NT>
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <bool NT, int V>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
                                                            int S, int Cout, int C, int Cin,
                                                            int KH, int KW,
                                                            float* __restrict__ dw, float beta,
                                                            int lanes) {
-  // block = (256 / lanes) consecutive slab elements x `lanes` split lanes; lane l sums the
-  // slabs l, l + lanes, ... (8 loads in flight), lanes combine in fixed order.  Reads follow
-  // the slab layout [S][Cout][K] (coalesced); the OIHW write is a permutation.
-  __shared__ float red[256];
+  // block = (256 / lanes) threads of V consecutive slab elements x `lanes` split lanes; lane l
+  // sums the slabs l, l + lanes, ... in order, up to 8 V-wide loads in flight (the last
+  // batch predicated, so a short S still issues its loads together), lanes combine in fixed
+  // order.  Reads follow the slab layout [S][Cout][K] (coalesced, V = 4 needs C % 4 == 0);
+  // the OIHW write is a permutation.
+  typedef typename std::conditional<V == 4, f32x4v, float>::type vec;
+  __shared__ vec red[256];
   const long long K = (long long)KH * KW * C;
   const long long total = (long long)Cout * K;
-  const long long plane = total;
+  const long long plane = total / V;
   const int E = 256 / lanes;
   const int el = threadIdx.x % E, ln = threadIdx.x / E;
-  const long long e = (long long)blockIdx.x * E + el;
-  float acc = 0.f;
+  const long long e = ((long long)blockIdx.x * E + el) * V;
+  vec acc = 0.f;
   if (e < total) {
-    const float* src = slab + e;
-    int i = ln;
-    for (; i + 7 * lanes < S; i += 8 * lanes) {
-      float v[8];
+    const vec* src = reinterpret_cast<const vec*>(slab + e);
+    for (int i = ln; i < S; i += 8 * lanes) {
+      vec v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const vec* a = src + (long long)(i + j * lanes) * plane;
+        v[j] = i + j * lanes < S ? (NT ? __builtin_nontemporal_load(a) : *a) : vec(0.f);
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        v[j] = NT ? __builtin_nontemporal_load(src + (long long)(i + j * lanes) * plane)
-                  : src[(long long)(i + j * lanes) * plane];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc += v[j];
+        if (i + j * lanes < S) acc += v[j];
     }
-    for (; i < S; i += lanes) acc += src[(long long)i * plane];
   }
   red[threadIdx.x] = acc;
   __syncthreads();
   if (ln != 0 || e >= total) return;
-  float sum = 0.f;
+  vec sum = 0.f;
   for (int l = 0; l < lanes; ++l) sum += red[l * E + el];
   const int co = (int)(e / K);
-  const int k = (int)(e - (long long)co * K);
-  const int tap = k / C, ci = k - tap * C;
-  if (ci >= Cin) return;  // channel padding of the packed input
+  const int k0 = (int)(e - (long long)co * K);
+  const int tap = k0 / C, ci0 = k0 - tap * C;  // V | C: the V elements share co and tap
   const int kh = tap / KW, kw = tap - kh * KW;
-  const long long o = (((long long)co * Cin + ci) * KH + kh) * KW + kw;
-  dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + sum;
+#pragma unroll
+  for (int u = 0; u < V; ++u) {
+    const int ci = ci0 + u;
+    if (ci >= Cin) break;  // channel padding of the packed input
+    const long long o = (((long long)co * Cin + ci) * KH + kh) * KW + kw;
+    float su;
+    if constexpr (V == 4) su = sum[u]; else su = sum;
+    dw[o] = (beta != 0.f ? beta * dw[o] : 0.f) + su;
+  }
 }
 
 // ------------------------------------------------------------------ weight packing
@@ -839,8 +850,16 @@ void wgrad_reduce(const float* slab, int S, int Cout, int C, int Cin, int KH, in
   while (lanes < 16 && lanes * 8 < S) lanes *= 2;
   const int E = 256 / lanes;
   // non-temporal slab loads: every slab is read once (profiles/nt_pool_wgrad_reduce_ab_r4aa.txt)
-  wgrad_reduce_kernel<true><<<(unsigned)((total + E - 1) / E), 256, 0, st>>>(slab, S, Cout, C, Cin,
-                                                                          KH, KW, dw, beta, lanes);
+  // 16-byte slab loads: isolated 0.333 -> 0.276 ms per ResNet-18 step, the step itself equal
+  // (profiles/wgrad_reduce_vec_ab_r4au.txt)
+  if (C % 4 == 0 && (reinterpret_cast<uintptr_t>(slab) & 15) == 0) {
+    const long long nv = total / 4;
+    wgrad_reduce_kernel<true, 4><<<(unsigned)((nv + E - 1) / E), 256, 0, st>>>(
+        slab, S, Cout, C, Cin, KH, KW, dw, beta, lanes);
+    return;
+  }
+  wgrad_reduce_kernel<true, 1><<<(unsigned)((total + E - 1) / E), 256, 0, st>>>(
+      slab, S, Cout, C, Cin, KH, KW, dw, beta, lanes);
 }
 
 void pack_weights(const float* w, bf16_t* wf, bf16_t* wd, int Cout, int Cin, int Cpad, int KH,
