@@ -87,6 +87,9 @@ def parse():
                     help="at one rank: initialise a 1-rank RCCL group and run DDP's full "
                          "communication path anyway (reducer, bucket hooks, every bucket's "
                          "all-reduce, buffer broadcasts) -- the multi-GPU code on one GPU")
+    ap.add_argument("--buffer-sync-every", type=int, default=1,
+                    help="DDP broadcast_buffers period in training forwards (1 = every step, "
+                         "as torch DDP; 0 = never)")
     ap.add_argument("--data", default="loader", choices=["loader", "resident"],
                     help="loader: MySampler + DeviceLoader over a device-resident synthetic "
                          "dataset (the task3 data path); resident: two fixed batches per rank")
@@ -171,7 +174,9 @@ def main():
     net = DDP(model, bucket_cap_mb=a.bucket_mb,
               comm_dtype=torch.bfloat16 if a.comm_dtype == "bf16" else None,
               small_allreduce="xgmi" if a.small_allreduce == "xgmi" else None,
-              small_cap_mb=a.xgmi_cap_mb, force_comm=bool(a.force_comm))
+              small_cap_mb=a.xgmi_cap_mb, force_comm=bool(a.force_comm),
+              broadcast_buffers=a.buffer_sync_every > 0,
+              buffer_sync_every=max(1, a.buffer_sync_every))
     net.fold_average_into(opt)
     if a.fused < 0:
         # the 2-dispatch fused step: 587k vs 205k img/s layer-wise at batch 32
@@ -359,6 +364,7 @@ def main():
                 "backend": a.backend,
                 "fused_step": bool(fused is not None),
                 "ddp_side_stream_hooks": (net.side_stream_hooks if comm else None),
+                "ddp_buffer_sync_every": (a.buffer_sync_every if comm else None),
                 "hip_graph": a.graph,
                 "stream_priority": a.stream_priority,
                 "sampler": ("MySampler(partition)" if loader is not None else None),

@@ -321,6 +321,30 @@ def test_ddp_broadcast_buffers():
     run_dist(_buffers_synced, 2, None)
 
 
+def _buffers_sync_every(rank, ws, path):
+    """buffer_sync_every=2 (bench.py --buffer-sync-every 2): the running statistics are
+    broadcast at the 1st, 3rd, ... training forward only, so the ranks agree after those
+    steps and differ (different batch per rank) after the others."""
+    from dmlab.parallel import DDP
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Conv2d(1, 4, 3), torch.nn.BatchNorm2d(4),
+                            torch.nn.ReLU(), torch.nn.Flatten(), torch.nn.Linear(4 * 26 * 26, 10))
+    ddp = DDP(m, broadcast_buffers=True, buffer_sync_every=2)
+    g = torch.Generator().manual_seed(40 + rank)
+    for step in range(4):
+        x = torch.rand(4, 1, 28, 28, generator=g) * (1 + rank)
+        F.cross_entropy(ddp(x), torch.zeros(4, dtype=torch.long)).backward()
+        rm = [torch.zeros_like(m[1].running_mean) for _ in range(ws)]
+        dist.all_gather(rm, m[1].running_mean)
+        same = all(torch.equal(rm[0], r) for r in rm)
+        assert same == (step % 2 == 0), (step, rm)
+
+
+def test_ddp_buffer_sync_every():
+    run_dist(_buffers_sync_every, 2, None)
+
+
 def _bf16_comm_side_hooks(rank, ws, path):
     """bf16 gradient communication through the persistent buffer equals the fp32
     communication within bf16 rounding, with the side-stream (stream_ok) hook path."""
