@@ -85,7 +85,8 @@ __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G
 // level-1 groups for a [T][2C] slab: none when the finalize block can sum it directly
 static inline int colsum_groups(int T) { return T <= 256 ? 0 : min(256, (T + 31) / 32); }
 
-// Per-channel finalize math shared by the separate and the fused (last-block) finalizes.
+// Per-channel finalize math of the forward / backward finalize kernels (the one-launch
+// last-block finalizes measured slower and were removed: docs/KERNELS.md round 2).
 struct FinFwd {
   const float* gamma;
   const float* beta;
