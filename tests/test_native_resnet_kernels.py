@@ -779,3 +779,23 @@ def test_conv_wgrad_s2(dev, geom, S):
     d = base.clone()  # beta = 1: accumulate
     lib().conv_wgrad(xn, _nhwc(dy), d, slab, Cin, k, k, s, p, 1.0, S, 7, False)
     assert _rel(d, ref + base) < 2e-3
+
+
+@pytest.mark.parametrize("S", [3, 11])
+def test_wgrad_reduce_vector_matches_scalar(dev, S):
+    """The slab reduce reads 16-byte vectors when the slab is 16-byte aligned and falls back
+    to 4-byte loads otherwise (a slab view at a one-float offset): same summation order, so
+    the two results are bit-identical (S = 11: split lanes and a predicated last batch)."""
+    N, H, Cin, Cout, k, s, p = (4, 20, 64, 128, 3, 1, 1)
+    x, w, xn, wf, wd = _setup(dev, N, H, Cin, Cout, k, s, p)
+    dy = torch.randn(N, Cout, H, H, device=dev).bfloat16()
+    ref = torch.nn.grad.conv2d_weight(x.float(), w.shape, dy.float(), s, p)
+    n = S * Cout * k * k * Cin
+    buf = torch.empty(n + 4, device=dev)
+    out = []
+    for off in (0, 1):
+        d = torch.empty_like(w)
+        lib().conv_wgrad(xn, _nhwc(dy), d, buf[off:off + n], Cin, k, k, s, p, 0.0, S, 4, False)
+        out.append(d)
+    assert torch.equal(out[0], out[1])
+    assert _rel(out[0], ref) < 2e-3
