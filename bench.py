@@ -107,6 +107,13 @@ def parse():
                     help="LeNet: the whole training step as 2 native dispatches "
                          "(dmlab.models.lenet_fused; 3 + the all-reduce with DDP); -1 = auto (on "
                          "for the native backend)")
+    ap.add_argument("--graph-steps", type=int, default=25,
+                    help="fused LeNet with --graph: training steps per captured graph (each one "
+                         "a complete step through the device cursor; the epoch's last steps "
+                         "replay the 1-step graph). The timed region runs every step it counts, "
+                         "plus up to graph-steps - 1 more (never fewer).  25 divides the "
+                         "1875-batch epoch: 1.035M vs 0.897M img/s at 1 step per graph "
+                         "(profiles/bench_lenet_graph_steps_ab_r4az.txt)")
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the whole step (fwd+bwd+all-reduce+opt) in a hipGraph; "
                          "-1 = auto: on for the launch-bound LeNet at any world size (RCCL "
@@ -232,6 +239,9 @@ def main():
 
     # ------------------------------------------------------------------ step sources
     batches = None
+
+    def step_reset():
+        pass
     if a.graph:
         from dmlab.utils.graph import CapturedStep
 
@@ -242,14 +252,37 @@ def main():
             ds = loader.dataset
             cap = CapturedStep(lambda x, y: train_step(x, y, cursor=cur),
                                [ds.images, ds.labels], warmup=3, bind_inputs=True)
-            state = {"step": 0, "epoch": 0}
+            kg = max(1, a.graph_steps)
+            capk = None
+            if kg > 1:
+                def multi(x, y):
+                    for _ in range(kg):
+                        out = train_step(x, y, cursor=cur)
+                    return out
+
+                cur.refill(0)
+                capk = CapturedStep(multi, [ds.images, ds.labels], warmup=1, bind_inputs=True)
+            # credit: steps a k-step replay already ran ahead of the caller's step count
+            state = {"step": 0, "epoch": 0, "credit": 0, "out": None}
 
             def step(i):
+                if state["credit"]:
+                    state["credit"] -= 1
+                    return state["out"]
                 if state["step"] and state["step"] % cur.nbatch == 0:
                     state["epoch"] += 1
                     cur.refill(state["epoch"])  # next epoch's shard order, same buffer
-                state["step"] += 1
-                return cap(ds.images, ds.labels)
+                left = cur.nbatch - state["step"] % cur.nbatch
+                if capk is not None and left >= kg:
+                    state["out"], n = capk(ds.images, ds.labels), kg
+                else:
+                    state["out"], n = cap(ds.images, ds.labels), 1
+                state["step"] += n
+                state["credit"] = n - 1
+                return state["out"]
+
+            def step_reset():  # the timed region starts on a fresh replay
+                state["credit"] = 0
 
             # restart the epoch after the capture warm-up advanced the cursor
             cur.refill(0)
@@ -298,6 +331,7 @@ def main():
     with run_ctx:
         for i in range(a.warmup):
             loss = step(i)
+        step_reset()
         torch.cuda.synchronize()
         env.barrier()
         torch.cuda.synchronize()
@@ -366,6 +400,8 @@ def main():
                 "ddp_side_stream_hooks": (net.side_stream_hooks if comm else None),
                 "ddp_buffer_sync_every": (a.buffer_sync_every if comm else None),
                 "hip_graph": a.graph,
+                "hip_graph_steps": (max(1, a.graph_steps) if (a.graph and fused is not None
+                                                            and loader is not None) else None),
                 "stream_priority": a.stream_priority,
                 "sampler": ("MySampler(partition)" if loader is not None else None),
             },

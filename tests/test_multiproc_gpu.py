@@ -420,3 +420,4 @@ def test_bench_lenet_two_ranks_graph(tmp_path):
     res = json.loads(line)
     assert res["n_gpus"] == 2 and res["config"]["hip_graph"] is True
     assert res["config"]["fused_step"] is True and res["value"] > 0
+    assert res["config"]["hip_graph_steps"] == 25 and res["replicas_in_sync"] is True

@@ -89,6 +89,7 @@ def test_bench_force_comm_lenet_graph():
     at ws > 1 on RCCL), batches drawn on the device through the sampler's epoch order."""
     res = _bench(["--model", "lenet", "--steps", "50", "--warmup", "5"])
     assert res["config"]["hip_graph"] is True and res["config"]["fused_step"] is True
+    assert res["config"]["hip_graph_steps"] == 25  # 25 steps (25 all-reduces) per replay
     assert res["replicas_in_sync"] is True and res["value"] > 0
 
 
