@@ -119,7 +119,7 @@ def _train_loop(model, loader, loss_fn, optimizer, num_epochs, stats, rank, aggr
 
 
 def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, log_every=20,
-                graph=True, graph_steps=20, max_steps=None, print_fn=print, writer=None):
+                graph=True, max_steps=None, print_fn=print, writer=None):
     """The lab-3 loop (codes/task3/model.py:39-64) on the GPU fast path: the reference LeNet
     step as the 2-dispatch fused kernel pair (:class:`~dmlab.models.lenet_fused.
     FusedLeNetStep`; with ``ddp`` the bucket all-reduce sits between them), its samples
@@ -128,16 +128,12 @@ def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, lo
     iteration.  Same console output as :func:`train`; the running loss is summed on the
     device and copied to pinned host memory every ``log_every`` steps, and each line prints
     once its copy has landed (at the next log point or the end) -- no host synchronisation
-    inside the loop.  ``graph_steps`` (a divisor of ``log_every``): complete steps per graph
-    replay, the epoch's tail and a ``max_steps`` cut on the 1-step graph (one replay per step
-    leaves ~5 us of launch latency per 31 us step: profiles/bench_lenet_graph_steps_ab_r4az.txt).
-    Returns the same stats dict as :func:`train`."""
+    inside the loop.  Returns the same stats dict as :func:`train`."""
     from dmlab.models.lenet_fused import FusedLeNetStep
 
     if rank is not None:
         print_fn("Device {} starts training ...".format(rank))
     net.train()
-    kg = graph_steps if (graph and graph_steps > 1 and log_every % graph_steps == 0) else 1
     step_fn = FusedLeNetStep(net, optimizer, ddp=ddp)
     cur = loader.cursor()
     ds = loader.dataset
@@ -154,24 +150,16 @@ def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, lo
         saved = [flat.data.clone()]
         runner = CapturedStep(lambda x, y: step_fn(x, y, cursor=cur), [ds.images, ds.labels],
                               warmup=2, bind_inputs=True)
-        runner_k = None
-        if kg > 1:
-            def multi(x, y):
-                for _ in range(kg):
-                    out = step_fn(x, y, cursor=cur)
-                return out
-
-            runner_k = CapturedStep(multi, [ds.images, ds.labels], warmup=1, bind_inputs=True)
         with torch.no_grad():
             flat.data.copy_(saved[0])
             flat.mark_updated()
             if getattr(optimizer, "buf", None) is not None:
                 optimizer.buf.zero_()
 
-        def run(n=1):
-            (runner_k if n > 1 else runner)(ds.images, ds.labels)
+        def run():
+            runner(ds.images, ds.labels)
     else:
-        def run(n=1):
+        def run():
             step_fn(ds.images, ds.labels, cursor=cur)
     stats = {"losses": [], "steps": 0, "samples": 0, "comm_time": 0.0}
     pending = []  # (epoch, iters, pinned copy, event) awaiting print
@@ -195,14 +183,10 @@ def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, lo
     for epoch in range(num_epochs):
         cur.refill(epoch)  # this epoch's shard order (set_epoch), cursor rewound
         step_fn.loss_sum.zero_()
-        i = 0  # steps done in this epoch
-        while i < cur.nbatch:
-            n = kg if (kg > 1 and i % kg == 0 and i + kg <= cur.nbatch
-                       and (max_steps is None or step + kg <= max_steps)) else 1
-            run(n)
-            i += n
-            step += n
-            if i % log_every == 0:  # a k-step block never straddles a log point (k | log_every)
+        for i in range(cur.nbatch):
+            run()
+            step += 1
+            if i % log_every == log_every - 1:
                 flush(False)
                 buf = host[nlog % len(host)]
                 if len(pending) >= len(host) - 1:
@@ -211,7 +195,7 @@ def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, lo
                 step_fn.loss_sum.zero_()
                 ev = torch.cuda.Event()
                 ev.record()
-                pending.append((epoch + 1, i, buf, ev))
+                pending.append((epoch + 1, i + 1, buf, ev))
                 nlog += 1
             if max_steps is not None and step >= max_steps:
                 done = True

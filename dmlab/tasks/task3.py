@@ -72,9 +72,6 @@ def parse_args(argv=None):
     p.add_argument("--fused", default="auto", choices=["auto", "0", "1"],
                    help="LeNet on the GPU: the fused 2-dispatch training step fed by the "
                         "device-side sampler cursor (auto: on for LeNet + DDP + SGD on a GPU)")
-    p.add_argument("--graph-steps", type=int, default=20,
-                   help="fused path with --graph: complete steps per graph replay (a divisor of "
-                        "the 20-step log interval; 1 = one replay per step)")
     p.add_argument("--graph", default="auto", choices=["auto", "0", "1"],
                    help="capture the fused step (with its all-reduce) in a hipGraph (auto: "
                         "on when --fused is, unless the group is gloo at ws > 1)")
@@ -137,8 +134,8 @@ def main(argv=None):
         graph = a.graph == "1" or (a.graph == "auto" and capturable)
         loader.drop_last = True  # fixed batch shape (the last partial batch of a shard drops)
         stats = train_fused(model, loader, opt, a.epochs, ddp=net, rank=rank, graph=graph,
-                            graph_steps=a.graph_steps, max_steps=a.max_steps)
-        stats.update(fused=True, hip_graph=graph, hip_graph_steps=a.graph_steps if graph else None)
+                            max_steps=a.max_steps)
+        stats.update(fused=True, hip_graph=graph)
     else:
         stats = train(net, loader, CrossEntropyLoss(), opt, a.epochs, rank=rank, aggregate=agg,
                       batch_size=a.batch_size, max_steps=a.max_steps)
