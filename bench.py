@@ -76,8 +76,12 @@ def parse():
                     help="after the timed run, N extra eager steps timed per phase with HIP "
                          "events (fwd, bwd compute, exposed comm, optimizer) -> 'phases_ms'; "
                          "-1 = auto (5 on the native backend)")
-    ap.add_argument("--small-allreduce", default="rccl", choices=["rccl", "xgmi"],
-                    help="buckets <= 4 MB via the one-shot xGMI peer-memory kernel")
+    ap.add_argument("--small-allreduce", default="auto", choices=["auto", "rccl", "xgmi"],
+                    help="buckets <= 4 MB via the one-shot xGMI peer-memory kernel.  auto: "
+                         "LeNet (207 KB of gradients, SURVEY 2.4's design point) uses it when "
+                         "the startup self-check (one xGMI call vs RCCL, exact) passes on every "
+                         "rank, else RCCL; ResNet-18 (25 MB buckets) always RCCL.  xgmi: the "
+                         "same self-check, RCCL on failure")
     ap.add_argument("--xgmi-cap-mb", type=float, default=4.0,
                     help="largest bucket sent through the xGMI kernel with --small-allreduce "
                          "xgmi; above the bucket size every bucket goes there (two-shot)")
@@ -165,6 +169,25 @@ def main():
     if a.gpus != ws:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={ws}", file=sys.stderr)
     comm = ws > 1 or bool(a.force_comm)
+
+    # device-path self-checks before anything is built or timed (dmlab.parallel.selfcheck):
+    # RCCL's all-reduce against a closed-form sum, and for LeNet the xGMI small-bucket kernel
+    # against RCCL; every rank takes the same path
+    checks = {}
+    if comm:
+        from dmlab.parallel import selfcheck
+
+        checks.update(selfcheck.allreduce_selfcheck(dev))
+        if checks["allreduce_selfcheck"] != "pass":
+            print(json.dumps({"error": "all-reduce self-check failed", **checks}), flush=True)
+            raise SystemExit(3)
+        if a.model == "lenet" and a.small_allreduce != "rccl" and dev.type == "cuda":
+            checks.update(selfcheck.xgmi_selfcheck(dev))
+        else:
+            checks.update(xgmi_selfcheck="skipped", small_allreduce_used="rccl")
+        a.small_allreduce = checks["small_allreduce_used"]
+    elif a.small_allreduce == "auto":
+        a.small_allreduce = "rccl"
 
     torch.manual_seed(0)
     if a.model == "resnet18":
@@ -347,6 +370,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     final_loss = float(loss)
+    # checksum of the flat fp32 parameters after the timed steps (float64 sums): equal bits
+    # give equal values, so two runs of the same step sequence can be compared exactly
+    pflat = model.flat.data if getattr(model, "flat", None) is not None else torch.cat(
+        [p.detach().reshape(-1) for p in model.parameters()])
+    pw = (torch.arange(pflat.numel(), device=pflat.device, dtype=torch.float64) % 251) + 1.0
+    param_checksum = [float(pflat.double().sum()), float((pflat.double() * pw).sum())]
     verify = verify_replicas(model, dev) if comm else None
     if a.phases < 0:
         a.phases = 5 if a.backend == "native" else 0
@@ -406,6 +435,7 @@ def main():
                 "sampler": ("MySampler(partition)" if loader is not None else None),
             },
             "final_loss": round(final_loss, 4),
+            "param_checksum": param_checksum,
             "peak_mem_gb": round(torch.cuda.max_memory_reserved() / 2**30, 1),
             "peak_alloc_gb": round(torch.cuda.max_memory_allocated() / 2**30, 1),
             # allocator retries (a failed hipMalloc frees the cache and synchronises): >0
@@ -414,6 +444,7 @@ def main():
         }
         if verify is not None:
             res.update(verify)
+        res.update(checks)
         if comm:
             res["buckets_launched"] = int(net.buckets_launched)
         if phases is not None:

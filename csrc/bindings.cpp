@@ -429,7 +429,13 @@ int num_cus(int device) {
 void register_resnet(pybind11::module_& m);
 void register_reducer(pybind11::module_& m);
 
+// generated per build by dmlab/_build.py (build/native/source_hash.cpp): sha256 of the csrc/
+// tree and build configuration this library was linked from
+extern "C" const char* dmlab_source_hash();
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("source_hash", []() { return std::string(dmlab_source_hash()); },
+        "sha256 of the csrc/ sources + build flags this extension was built from");
   register_resnet(m);
   register_reducer(m);
   m.doc() = "dmlab native HIP kernels for MI355X (gfx950)";

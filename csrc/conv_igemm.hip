@@ -809,7 +809,7 @@ void igemm_wgrad(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom&
   // 4 / 5: halo-staged 3x3 unit-stride kernel (wgrad_halo.hip) with 9 / 3 taps per block;
   // other shapes fall back to the v2 tiles: 2 = 128x128, 3 = 64x128, 6 = 64x256
   if (cfg == 8) return wgrad_res64(X, DY, slab, g, S, st);  // throws if unsupported
-  // 7: stride-2 parity-plane kernel (wgrad_halo.hip), 3x3 or 1x1
+  // 7: stride-2 parity-plane kernel (wgrad_halo.hip), 3x3 only (other shapes: v2 tiles)
   if (cfg == 7) {
     if (wgrad_s2_supported(g)) return wgrad_s2(X, DY, slab, g, S, mchunk, st);
     cfg = g.Ncols % 128 == 0 ? 2 : 3;

@@ -46,7 +46,9 @@ class DeviceCursor:
     For steps captured into a hipGraph: the graph reads batch ``cursor`` of ``order`` and
     advances the cursor itself (no per-step host work, not even an index copy).  ``refill``
     uploads the next epoch's order into the SAME buffer (captured pointers stay valid) and
-    rewinds the cursor."""
+    rewinds the cursor.  ``tail`` holds the shard's partial last batch (the indices past the
+    whole batches; empty when the shard size is a multiple of the batch), refreshed with the
+    order, for a loop that runs it as one uncaptured step (reference drop_last=False)."""
 
     def __init__(self, loader: "DeviceLoader"):
         self.loader = loader
@@ -54,12 +56,17 @@ class DeviceCursor:
         self.nbatch = len(loader.sampler if loader.sampler is not None else loader.dataset) // bs  # whole batches only (drop_last): a fixed batch shape
         if self.nbatch < 1:
             raise ValueError("the sampler's shard holds fewer than one batch")
-        self.order = loader._device_indices()[: self.nbatch * bs].contiguous()
+        idx = loader._device_indices()
+        self.order = idx[: self.nbatch * bs].contiguous()
+        self.tail = idx[self.nbatch * bs:].contiguous()
         self.cursor = torch.zeros(1, dtype=torch.int32, device=loader.device)
 
     def refill(self, epoch: int):
         self.loader.set_epoch(epoch)
-        self.order.copy_(self.loader._device_indices()[: self.order.numel()])
+        idx = self.loader._device_indices()
+        self.order.copy_(idx[: self.order.numel()])
+        if self.tail.numel():
+            self.tail.copy_(idx[self.order.numel(): self.order.numel() + self.tail.numel()])
         self.cursor.zero_()
 
 

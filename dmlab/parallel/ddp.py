@@ -40,7 +40,10 @@ task3/dist_utils.py:40-46).  Here:
   at the end of backward, so it overlaps backward instead of heading the next forward.
   ``num_batches_tracked`` advances identically on every rank and is not sent.  Nothing is broadcast when the wrapper switches to ``eval()`` (a rank-0-
   only evaluation must not enter a collective): to evaluate every rank with rank 0's final
-  statistics, call :meth:`sync_buffers` on every rank first.
+  statistics, call :meth:`sync_buffers` on every rank first (the task scripts do, before
+  their evaluation and checkpoint).  With ``buffer_sync_every > 1`` the statistics differ
+  between syncs, so that call is required there; such a step cannot be graph-captured (the
+  forward counter would not advance per replay: capture raises).
 * ``force_comm`` (or ``DMLAB_DDP_FORCE_COMM=1``): at world size 1 with an initialised
   process group (a 1-rank RCCL communicator), run the full multi-rank path anyway — native
   reducer, bucket hooks, one collective per bucket, buffer broadcasts — so the RCCL code is
@@ -478,6 +481,11 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *a, **kw):
         if self.broadcast_buffers and self._bcast_bufs and self.module.training and \
                 torch.is_grad_enabled():
+            if self.buffer_sync_every > 1 and torch.cuda.is_available() and \
+                    torch.cuda.is_current_stream_capturing():
+                # a captured graph replays whatever the capture recorded: the every-k-th
+                # forward counter would not advance per replay
+                raise ValueError("DDP buffer_sync_every > 1 cannot be graph-captured")
             if self._buf_state == "due" or self._buf_work is not None:
                 self._wait_buffer_sync()  # the previous forward never reached a backward
             if self._fwd_count % self.buffer_sync_every == 0:

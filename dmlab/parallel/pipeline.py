@@ -78,6 +78,22 @@ class PipelineStage:
         self.history = []  # (start, end, compute events) of every timed step
         self._linear = False  # no receive posted ahead (captured steps)
         self._graph = None
+
+    def selfcheck(self, corrupt=None) -> dict:
+        """One ping-pong per adjacent stage pair over this stage's transport, payloads checked
+        both ways (:func:`dmlab.parallel.selfcheck.p2p_selfcheck`); collective over the
+        default group.  Returns {"p2p_selfcheck": "pass" | "FAIL"}."""
+        from dmlab.parallel.selfcheck import p2p_selfcheck
+
+        res = "pass"
+        for i in range(self.P - 1):
+            a, b = self.ranks[i], self.ranks[i + 1]
+            peer = b if self.rank == a else a if self.rank == b else None
+            r = p2p_selfcheck(self.p2p, self.rank, peer, self.device, first=self.rank == a,
+                              corrupt=corrupt)
+            if r["p2p_selfcheck"] != "pass":
+                res = "FAIL"
+        return {"p2p_selfcheck": res}
         self._time_replays = False
 
     # -------------------------------------------------------------- pieces

@@ -69,22 +69,38 @@ class XGMIAllReduce:
         dist.all_gather_object(handles, handle, group=group)
         self._opened = []
         bases = []
-        for q, h in enumerate(handles):
-            if q == self.rank:
-                bases.append(self._base)
-            else:
-                p = L.xgmi_open_handle(h)
-                self._opened.append(p)
-                bases.append(p)
+        err = None
+        try:
+            for q, h in enumerate(handles):
+                if q == self.rank:
+                    bases.append(self._base)
+                else:
+                    p = L.xgmi_open_handle(h)
+                    self._opened.append(p)
+                    bases.append(p)
+        except Exception as e:  # reported to every rank below, so all fail together
+            err = f"rank {self.rank}: {type(e).__name__}: {e}"
         self._data = bases
         self._flags = [b + 8 * self.cap for b in bases]
         # ranks whose kernels share one physical GPU (1 on a node with one rank per GPU; the
         # single-GPU rehearsals run W ranks on one device): the spinning grids shrink by it so
         # every rank's blocks are resident together.  The kernels split the data by gridDim
         # and match flags by block index, so EVERY rank must launch the same grid: the divisor
-        # is the most crowded device's count, identical on all ranks
+        # is the most crowded device's count, identical on all ranks.  The same exchange
+        # carries each rank's handle-open status: one failed open fails every rank (no rank
+        # is left waiting in a later collective).
         keys = [None] * self.world
-        dist.all_gather_object(keys, _device_key(self.device), group=group)
+        dist.all_gather_object(keys, (_device_key(self.device), err), group=group)
+        errs = [e for _, e in keys if e]
+        if errs:
+            for p in self._opened:
+                L.xgmi_close_handle(p)
+            self._opened = []
+            dist.barrier(group=group)
+            L.xgmi_free(self._base)
+            self._base = 0
+            raise RuntimeError("xGMI all-reduce: peer memory mapping failed: " + "; ".join(errs))
+        keys = [k for k, _ in keys]
         self._share = max(1, max(keys.count(k) for k in keys))
         # [timeout flag, last published epoch, done-block counter, pad] (device side)
         self._state = torch.zeros(4, dtype=torch.int32, device=self.device)

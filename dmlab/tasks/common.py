@@ -119,94 +119,143 @@ def _train_loop(model, loader, loss_fn, optimizer, num_epochs, stats, rank, aggr
 
 
 def train_fused(net, loader, optimizer, num_epochs=2, *, ddp=None, rank=None, log_every=20,
-                graph=True, max_steps=None, print_fn=print, writer=None):
+                graph=True, graph_steps=20, max_steps=None, print_fn=print, writer=None,
+                drop_last=False):
     """The lab-3 loop (codes/task3/model.py:39-64) on the GPU fast path: the reference LeNet
     step as the 2-dispatch fused kernel pair (:class:`~dmlab.models.lenet_fused.
     FusedLeNetStep`; with ``ddp`` the bucket all-reduce sits between them), its samples
     gathered on the device through the sampler's epoch order (:class:`~dmlab.data.
-    DeviceCursor`), the whole step captured in ONE hipGraph (``graph``) and replayed per
-    iteration.  Same console output as :func:`train`; the running loss is summed on the
-    device and copied to pinned host memory every ``log_every`` steps, and each line prints
-    once its copy has landed (at the next log point or the end) -- no host synchronisation
-    inside the loop.  Returns the same stats dict as :func:`train`."""
+    DeviceCursor`), the whole step captured in a hipGraph (``graph``) and replayed.
+    ``graph_steps`` (a divisor of ``log_every``): complete steps per graph replay; blocks
+    that would cross the end of the epoch's whole batches or a ``max_steps`` cut run on the
+    1-step graph (one replay per step leaves ~5 us of launch latency per ~31 us step:
+    profiles/bench_lenet_graph_steps_ab_r4az.txt).  A shard whose size is not a multiple of
+    the batch ends each epoch with one eager fused step on its partial last batch, as the
+    reference DataLoader (drop_last=False) does; ``drop_last`` skips it.
+
+    Same console output as :func:`train`: the running loss is summed on the device, copied
+    to pinned host memory every ``log_every`` steps and printed once the copy has landed
+    (no host synchronisation inside the loop); like the reference loop (and :func:`train`)
+    the running sum is reset only after a printed line, so an epoch's tail carries into the
+    next epoch's first line.  Returns the same stats dict as :func:`train`."""
     from dmlab.models.lenet_fused import FusedLeNetStep
 
     if rank is not None:
         print_fn("Device {} starts training ...".format(rank))
     net.train()
+    kg = graph_steps if (graph and graph_steps > 1 and log_every % graph_steps == 0) else 1
     step_fn = FusedLeNetStep(net, optimizer, ddp=ddp)
     cur = loader.cursor()
     ds = loader.dataset
+    tail = 0 if drop_last else cur.tail.numel()
     if graph:
         from dmlab.utils.graph import CapturedStep
 
-        # the capture's eager warm-up steps must not count as training: snapshot the weights
-        # and the momentum buffer, restore them in place afterwards (the graph keeps the
-        # pointers).  The restored zero momentum with the captured not-first-step update is
-        # the first step's buf = grad (dampening 0, the labs' setting).
+        # the capture's eager warm-up steps must not count as training: snapshot the weights,
+        # the momentum buffer and the step counter, and restore them in place afterwards (the
+        # graphs keep the pointers).  The captured update is the not-first-step form
+        # buf = m*buf + grad (dampening 0, the labs' setting): with a fresh zero buffer that
+        # IS the first step's buf = grad, and a resumed run keeps its loaded momentum.
         if getattr(optimizer, "dampening", 0.0):
             raise ValueError("graph-captured fused step: SGD dampening != 0 is not supported")
         flat = net.flat
-        saved = [flat.data.clone()]
+        buf = getattr(optimizer, "buf", None)
+        saved = (flat.data.clone(), buf.clone() if buf is not None else None,
+                 getattr(optimizer, "step_count", 0))
+        if getattr(optimizer, "step_count", 0) == 0:
+            optimizer.step_count = 1  # capture the not-first-step update (see above)
         runner = CapturedStep(lambda x, y: step_fn(x, y, cursor=cur), [ds.images, ds.labels],
                               warmup=2, bind_inputs=True)
+        runner_k = None
+        if kg > 1:
+            def multi(x, y):
+                for _ in range(kg):
+                    out = step_fn(x, y, cursor=cur)
+                return out
+
+            runner_k = CapturedStep(multi, [ds.images, ds.labels], warmup=1, bind_inputs=True)
         with torch.no_grad():
             flat.data.copy_(saved[0])
             flat.mark_updated()
-            if getattr(optimizer, "buf", None) is not None:
-                optimizer.buf.zero_()
+            if buf is not None:
+                buf.copy_(saved[1])
+        optimizer.step_count = saved[2]
 
-        def run():
-            runner(ds.images, ds.labels)
+        def run(n=1):
+            (runner_k if n > 1 else runner)(ds.images, ds.labels)
+            optimizer.step_count += n  # the replays' updates (host-side count only)
     else:
-        def run():
+        def run(n=1):
             step_fn(ds.images, ds.labels, cursor=cur)
     stats = {"losses": [], "steps": 0, "samples": 0, "comm_time": 0.0}
-    pending = []  # (epoch, iters, pinned copy, event) awaiting print
+    pending = []  # (epoch, iters, step, pinned copy, event) awaiting print
     host = [torch.zeros(1, pin_memory=True) for _ in range(4)]
 
     def flush(block):
-        while pending and (block or pending[0][3].query()):
-            ep, it, buf, ev = pending.pop(0)
+        while pending and (block or pending[0][4].query()):
+            ep, it, st, hb, ev = pending.pop(0)
             ev.synchronize()
-            avg = float(buf[0]) / log_every
+            avg = float(hb[0]) / log_every
             stats["losses"].append(avg)
             if writer is not None:
-                writer.add_scalar("Train Loss", avg, stats["steps"])
+                writer.add_scalar("Train Loss", avg, st)
             print_fn('Device: %d epoch: %d, iters: %5d, loss: %.3f' % (rank or 0, ep, it, avg))
+
+    def log_point(epoch, it, step):
+        nonlocal nlog
+        flush(False)
+        hb = host[nlog % len(host)]
+        if len(pending) >= len(host) - 1:
+            flush(True)
+        hb.copy_(step_fn.loss_sum, non_blocking=True)
+        step_fn.loss_sum.zero_()
+        ev = torch.cuda.Event()
+        ev.record()
+        pending.append((epoch + 1, it, step, hb, ev))
+        nlog += 1
 
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     step = 0
     nlog = 0
+    samples = 0
     done = False
+    step_fn.loss_sum.zero_()  # once: the running sum carries across epochs (reference)
     for epoch in range(num_epochs):
         cur.refill(epoch)  # this epoch's shard order (set_epoch), cursor rewound
-        step_fn.loss_sum.zero_()
-        for i in range(cur.nbatch):
-            run()
-            step += 1
-            if i % log_every == log_every - 1:
-                flush(False)
-                buf = host[nlog % len(host)]
-                if len(pending) >= len(host) - 1:
-                    flush(True)
-                buf.copy_(step_fn.loss_sum, non_blocking=True)
-                step_fn.loss_sum.zero_()
-                ev = torch.cuda.Event()
-                ev.record()
-                pending.append((epoch + 1, i + 1, buf, ev))
-                nlog += 1
+        i = 0  # batches done in this epoch
+        while i < cur.nbatch:
+            n = kg if (kg > 1 and i % kg == 0 and i + kg <= cur.nbatch
+                       and (max_steps is None or step + kg <= max_steps)) else 1
+            run(n)
+            i += n
+            step += n
+            samples += n * loader.batch_size
+            if i % log_every == 0:  # a k-step block never straddles a log point (k | log_every)
+                log_point(epoch, i, step)
             if max_steps is not None and step >= max_steps:
                 done = True
                 break
+        if not done and tail:
+            # the shard's partial last batch: one eager fused step on the gathered rows
+            xt = ds.images.index_select(0, cur.tail)
+            yt = ds.labels.index_select(0, cur.tail)
+            step_fn(xt, yt)
+            i += 1
+            step += 1
+            samples += tail
+            if i % log_every == 0:
+                log_point(epoch, i, step)
+            if max_steps is not None and step >= max_steps:
+                done = True
         if done:
             break
     torch.cuda.synchronize()
     stats["train_time"] = time.perf_counter() - t0
     flush(True)
     stats["steps"] = step
-    stats["samples"] = step * loader.batch_size
+    stats["samples"] = samples
+    stats["graph_steps"] = kg if graph else None
     print_fn("Training Finished!")
     if writer is not None:
         writer.flush()

@@ -55,8 +55,11 @@ def parse_args(argv=None):
     p.add_argument("--lr", type=float, default=0.001)
     p.add_argument("--momentum", type=float, default=0.9)
     p.add_argument("--bucket-mb", type=float, default=25.0)
-    p.add_argument("--allreduce", default="rccl", choices=["rccl", "xgmi"],
-                   help="small-bucket all-reduce: RCCL ring or the one-shot xGMI kernel")
+    p.add_argument("--allreduce", default="auto", choices=["auto", "rccl", "xgmi"],
+                   help="small-bucket all-reduce: RCCL ring or the one-shot xGMI kernel.  At "
+                        "world size > 1 on GPUs a startup self-check runs one xGMI call against "
+                        "RCCL (exact); auto/xgmi use the kernel for LeNet only if it passes on "
+                        "every rank (RCCL otherwise); ResNet-18 stays on RCCL under auto")
     p.add_argument("--data", default="./data")
     p.add_argument("--synthetic", action="store_true")
     p.add_argument("--train-samples", type=int, default=None)
@@ -72,6 +75,9 @@ def parse_args(argv=None):
     p.add_argument("--fused", default="auto", choices=["auto", "0", "1"],
                    help="LeNet on the GPU: the fused 2-dispatch training step fed by the "
                         "device-side sampler cursor (auto: on for LeNet + DDP + SGD on a GPU)")
+    p.add_argument("--graph-steps", type=int, default=20,
+                   help="fused path with --graph: complete training steps per graph replay (a "
+                        "divisor of the 20-step log interval; 1 = one replay per step)")
     p.add_argument("--graph", default="auto", choices=["auto", "0", "1"],
                    help="capture the fused step (with its all-reduce) in a hipGraph (auto: "
                         "on when --fused is, unless the group is gloo at ws > 1)")
@@ -83,6 +89,24 @@ def main(argv=None):
     dev = env.init(a.n_devices, a.rank, a.master_addr, a.master_port, backend=a.backend,
                    device_type=a.device)
     rank, ws = env.get_rank(), env.get_world_size()
+    checks = {}
+    if ws > 1:
+        # the device paths this run depends on, proven before training (selfcheck module)
+        from dmlab.parallel import selfcheck
+
+        checks.update(selfcheck.allreduce_selfcheck(dev))
+        if checks["allreduce_selfcheck"] != "pass":
+            raise SystemExit(f"all-reduce self-check failed: {checks}")
+        want = a.allreduce == "xgmi" or (a.allreduce == "auto" and a.model == "lenet")
+        if want and dev.type == "cuda" and a.dp == "ddp":
+            checks.update(selfcheck.xgmi_selfcheck(dev))
+        else:
+            checks.update(xgmi_selfcheck="skipped", small_allreduce_used="rccl")
+        a.allreduce = checks["small_allreduce_used"]
+        if rank == 0:
+            print("self-check: " + ", ".join(f"{k}={v}" for k, v in checks.items()))
+    elif a.allreduce == "auto":
+        a.allreduce = "rccl"
     torch.manual_seed(4321 + rank)
     if a.model == "lenet":
         model = Net(1, 10).to(dev)
@@ -132,10 +156,11 @@ def main(argv=None):
 
         capturable = ws == 1 or dist_backend() == "nccl" or a.allreduce == "xgmi"
         graph = a.graph == "1" or (a.graph == "auto" and capturable)
-        loader.drop_last = True  # fixed batch shape (the last partial batch of a shard drops)
+        # whole batches replay the captured fixed-shape step; the shard's partial last batch
+        # (if any) runs as one eager fused step, as the reference DataLoader keeps it
         stats = train_fused(model, loader, opt, a.epochs, ddp=net, rank=rank, graph=graph,
-                            max_steps=a.max_steps)
-        stats.update(fused=True, hip_graph=graph)
+                            graph_steps=a.graph_steps, max_steps=a.max_steps)
+        stats.update(fused=True, hip_graph=graph, hip_graph_steps=stats.pop("graph_steps"))
     else:
         stats = train(net, loader, CrossEntropyLoss(), opt, a.epochs, rank=rank, aggregate=agg,
                       batch_size=a.batch_size, max_steps=a.max_steps)
@@ -143,12 +168,15 @@ def main(argv=None):
     if rank == 0:
         print("Throughput: {:.1f} samples/s (whole job, {} rank{})".format(
             stats["samples"] * ws / stats["train_time"], ws, "s" if ws > 1 else ""))
+    if hasattr(net, "sync_buffers"):
+        net.sync_buffers()  # every rank: rank 0's BN statistics for the save and the test
     if a.save:
         from dmlab.utils import checkpoint
 
         checkpoint.save(a.save, model, opt, epochs=a.epochs)
     if not a.no_test and rank == 0:
         stats["accuracy"] = test(model, DeviceLoader(test_set.to(dev, dtype=act), 32))
+    stats.update(checks)
     stats.update(rank=rank, world_size=ws, sampler=a.sampler, dp=a.dp,
                  samples_per_s=stats["samples"] * ws / stats["train_time"])
     if a.json and rank == 0:

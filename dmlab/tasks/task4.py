@@ -162,6 +162,23 @@ def _run_pipeline(a, dev, rank, ws):
     cap = max(1 << 20, a.batch_size * 400 * 4)
     stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
                           transport=a.transport, timing=bool(a.bench_json), cap_bytes=cap)
+    # one ping-pong per stage pair on the chosen transport before training (both directions,
+    # payload checked); the native xGMI channel falls back to torch.distributed P2P
+    checks = stage.selfcheck()
+    checks["transport_used"] = a.transport
+    if checks["p2p_selfcheck"] != "pass" and a.transport == "xgmi":
+        try:
+            stage.p2p.close()
+        except Exception:
+            pass
+        a.transport = "pg"
+        stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
+                              transport="pg", timing=bool(a.bench_json), cap_bytes=cap)
+        checks = dict(stage.selfcheck(), xgmi_p2p_selfcheck="FAIL", transport_used="pg")
+    if checks["p2p_selfcheck"] != "pass":
+        raise SystemExit(f"pipeline transport self-check failed: {checks}")
+    if rank == 0:
+        print("self-check: " + ", ".join(f"{k}={v}" for k, v in checks.items()))
     train_loader, test_loader = _data(a, dev, drop_last=True, test_batch=16) if rank == 0 \
         else (None, None)
     graph = bool(a.graph) and a.transport == "xgmi" and dev.type == "cuda"
@@ -214,7 +231,8 @@ def _run_pipeline(a, dev, rank, ws):
             step_ms, comp_ms, bubble = stage.step_stats(skip=warm)
         else:  # CPU: wall time only (no device events)
             warm, step_ms, comp_ms, bubble = 0, 1e3 * dt / max(step, 1), float("nan"), float("nan")
-        res = {"rank": rank, "stage": "conv" if rank == 0 else "fc", "schedule": a.schedule,
+        res = {**checks, "rank": rank, "stage": "conv" if rank == 0 else "fc",
+               "schedule": a.schedule,
                "cu_partition": bool(a.cu_partition and dev.type == "cuda"),
                "n_micro": a.micro, "transport": a.transport, "batch": a.batch_size,
                "steps_timed": step - warm, "step_ms": round(step_ms, 4),

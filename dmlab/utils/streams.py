@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 
 _STREAMS: dict[int, torch.cuda.Stream] = {}
+_PARTS: dict[tuple, torch.cuda.ExternalStream] = {}
 
 
 def compute_stream(device=None) -> torch.cuda.Stream:
@@ -31,12 +32,16 @@ def partition_stream(part: int, nparts: int, device=None) -> torch.cuda.External
     Processes sharing one GPU that each run on a different partition do not compete for CUs,
     so each sees a (smaller) device of its own: the lab-4 pipeline uses this to emulate
     one-GPU-per-stage on a one-GPU box (``task4 --cu-partition``).  The stream has its own
-    hardware queue carrying the mask (``hipExtStreamCreateWithCUMask``)."""
+    hardware queue carrying the mask (``hipExtStreamCreateWithCUMask``), created once per
+    (device, part, nparts) and reused: a new stream per call would leak hardware queues."""
     from dmlab.ops._native import lib
 
     if not 0 <= part < nparts:
         raise ValueError(f"partition {part} of {nparts}")
     dev = torch.cuda.current_device() if device is None else torch.device(device).index
+    key = (dev, part, nparts)
+    if key in _PARTS:
+        return _PARTS[key]
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     lo, hi = part * ncu // nparts, (part + 1) * ncu // nparts
     words = [0] * ((ncu + 31) // 32)
@@ -44,4 +49,5 @@ def partition_stream(part: int, nparts: int, device=None) -> torch.cuda.External
         words[c // 32] |= 1 << (c % 32)
     with torch.cuda.device(dev):
         ptr = lib().cu_mask_stream(words)
-    return torch.cuda.ExternalStream(ptr, device=torch.device("cuda", dev))
+    st = _PARTS[key] = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", dev))
+    return st

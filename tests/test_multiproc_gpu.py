@@ -364,6 +364,10 @@ def test_bench_two_ranks(tmp_path):
     assert res["replicas_in_sync"] is True and res["buckets_launched"] > 0
     assert set(res["phases_ms"]) == {"fwd", "bwd_compute", "comm_exposed", "opt"}
     assert res["config"]["sampler"] == "MySampler(partition)"
+    # startup device-path self-checks: the closed-form all-reduce ran; ResNet stays on the
+    # process group's all-reduce (no xGMI probe)
+    assert res["allreduce_selfcheck"] == "pass"
+    assert res["xgmi_selfcheck"] == "skipped" and res["small_allreduce_used"] == "rccl"
 
 
 @pytest.mark.parametrize("ws", [4, 8])
@@ -394,7 +398,8 @@ def test_xgmi_many_ranks_one_gpu(ws):
         assert err < 2e-4, (rank, err)
 
 
-def test_bench_lenet_two_ranks_graph(tmp_path):
+@pytest.mark.parametrize("corrupt", [None, "xgmi:1"])
+def test_bench_lenet_two_ranks_graph(tmp_path, corrupt):
     """bench.py --model lenet at 2 ranks (gloo process group on the shared GPU): with the
     xGMI all-reduce kernel the whole DDP step (fused LeNet step, all-reduce, SGD) is captured
     into a hipGraph at world size > 1 (hip_graph: true in the JSON line)."""
@@ -410,14 +415,25 @@ def test_bench_lenet_two_ranks_graph(tmp_path):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK="0", LOCAL_WORLD_SIZE="2",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), DMLAB_BACKEND="gloo",
                    OMP_NUM_THREADS="2")
+        if corrupt:  # a forced wrong xGMI sum on rank 1: both ranks must fall back together
+            env["DMLAB_SELFCHECK_CORRUPT"] = corrupt
         procs.append(subprocess.Popen(
             [sys.executable, str(root / "bench.py"), "--gpus", "2", "--model", "lenet", "--steps",
-             "20", "--warmup", "5", "--small-allreduce", "xgmi", "--fused", "1"], cwd=tmp_path,
+             "20", "--warmup", "5", "--fused", "1"], cwd=tmp_path,
             env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = [p.communicate(timeout=300) for p in procs]
     assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
     line = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")][-1]
     res = json.loads(line)
-    assert res["n_gpus"] == 2 and res["config"]["hip_graph"] is True
+    # on the fallback (gloo all-reduce, host-side) the step cannot be captured
+    assert res["n_gpus"] == 2 and res["config"]["hip_graph"] is (corrupt is None)
     assert res["config"]["fused_step"] is True and res["value"] > 0
-    assert res["config"]["hip_graph_steps"] == 25 and res["replicas_in_sync"] is True
+    assert res["config"]["hip_graph_steps"] == (None if corrupt else 25)
+    assert res["replicas_in_sync"] is True
+    # the small-bucket path was chosen by the startup self-check (one xGMI call vs the group's
+    # all-reduce on the same data, exact); a forced mismatch falls back on both ranks
+    assert res["allreduce_selfcheck"] == "pass"
+    if corrupt:
+        assert res["xgmi_selfcheck"] == "fail" and res["small_allreduce_used"] == "rccl"
+    else:
+        assert res["xgmi_selfcheck"] == "pass" and res["small_allreduce_used"] == "xgmi"
