@@ -634,6 +634,134 @@ void pack_input(at::Tensor x, at::Tensor y) {
 
 }  // namespace
 
+// ----------------------------------------------------------------- fused K-dense stem
+// img: the raw input as stored -- (N, 3, H, W) channels_last or (N, H, W, 3) contiguous, fp32 /
+// bf16 / u8; idx (optional int64 [B]): batch row -> image row (the loader's gather)
+struct ImgView {
+  const void* ptr;
+  int dtype, N, H, W;
+};
+ImgView img_view(const at::Tensor& img) {
+  TORCH_CHECK(img.is_cuda() && img.dim() == 4, "stem input must be a 4-D HIP tensor");
+  ImgView v{img.data_ptr(), 0, (int)img.size(0), 0, 0};
+  if (img.size(1) == 3 && img.size(3) != 3) {
+    TORCH_CHECK(img.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "stem input (N,3,H,W) must be channels_last");
+    v.H = img.size(2);
+    v.W = img.size(3);
+  } else {
+    TORCH_CHECK(img.size(3) == 3 && img.is_contiguous(), "stem input (N,H,W,3) must be contiguous");
+    v.H = img.size(1);
+    v.W = img.size(2);
+  }
+  const auto t = img.scalar_type();
+  TORCH_CHECK(t == at::kFloat || t == at::kBFloat16 || t == at::kByte,
+              "stem input must be fp32, bf16 or uint8");
+  v.dtype = t == at::kFloat ? 0 : t == at::kBFloat16 ? 1 : 2;
+  return v;
+}
+
+bool stem_fused_supported(int64_t Hin, int64_t Win) { return dm::stem_fused_supported(Hin, Win); }
+int64_t stem_fused_grid(int64_t N) { return dm::stem_fused_grid((int)N); }
+int64_t stem_slab_cols() { return dm::stem_slab_cols(); }
+
+const long long* idx_ptr(const c10::optional<at::Tensor>& idx, int B, int Nimg) {
+  if (!idx.has_value()) {
+    TORCH_CHECK(B <= Nimg, "stem: batch larger than the image tensor");
+    return nullptr;
+  }
+  TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == at::kLong && idx->is_contiguous() &&
+                  idx->numel() == B, "stem: idx must be a contiguous int64 HIP tensor of B rows");
+  return reinterpret_cast<const long long*>(idx->data_ptr());
+}
+
+void stem_fwd_fused(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<double> nsc,
+                    std::vector<double> nbi, at::Tensor wk, at::Tensor gamma, at::Tensor pext,
+                    at::Tensor code, c10::optional<at::Tensor> stats,
+                    c10::optional<at::Tensor> hslab, int64_t grid) {
+  const ImgView v = img_view(img);
+  TORCH_CHECK(dm::stem_fused_supported(v.H, v.W), "fused stem: unsupported input size");
+  need_bf16_nhwc(pext, "pext");
+  const int B = pext.size(0);
+  TORCH_CHECK(pext.size(1) == v.H / 4 && pext.size(2) == v.W / 4 && pext.size(3) == 64,
+              "pext must be [B, H/4, W/4, 64]");
+  TORCH_CHECK(code.is_cuda() && code.scalar_type() == at::kByte && code.is_contiguous() &&
+              code.numel() == pext.numel(), "code must be uint8 like pext");
+  TORCH_CHECK(wk.is_cuda() && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
+              wk.numel() == 64 * dm::stem_wk_cols(), "wk must be packed [64][176] bf16");
+  need_f32(gamma, "gamma", 64);
+  TORCH_CHECK(nsc.size() == 3 && nbi.size() == 3, "3 normalisation scales / biases");
+  TORCH_CHECK(grid >= 1 && grid <= B, "grid must be in [1, B]");
+  if (stats.has_value()) need_f32(*stats, "stats", grid * 128);
+  if (hslab.has_value()) need_f32(*hslab, "hslab", grid * 64 * dm::stem_slab_cols());
+  TORCH_CHECK(stats.has_value() || !hslab.has_value(), "hslab (gradients) needs batch stats");
+  const float s3[3] = {(float)nsc[0], (float)nsc[1], (float)nsc[2]};
+  const float b3[3] = {(float)nbi[0], (float)nbi[1], (float)nbi[2]};
+  const DeviceGuard guard(pext.device());
+  dm::stem_fwd_fused(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(wk), fp(gamma), bp(pext),
+                     (uint8_t*)code.data_ptr(), stats ? fp(*stats) : nullptr,
+                     hslab ? fp(*hslab) : nullptr, B, v.N, v.H, v.W, (int)grid, cur_stream());
+}
+
+void stem_pool_apply(at::Tensor pext, c10::optional<at::Tensor> code, at::Tensor scale,
+                     at::Tensor shift, at::Tensor out) {
+  need_bf16_nhwc(pext, "pext");
+  need_bf16_nhwc(out, "out");
+  TORCH_CHECK(out.numel() == pext.numel() && pext.size(3) == 64, "pooled shapes");
+  if (code.has_value())
+    TORCH_CHECK(code->scalar_type() == at::kByte && code->numel() == pext.numel(), "code");
+  need_f32(scale, "scale", 64);
+  need_f32(shift, "shift", 64);
+  const DeviceGuard guard(pext.device());
+  dm::stem_pool_apply(bp(pext), code ? (uint8_t*)code->data_ptr() : nullptr, fp(scale), fp(shift),
+                      bp(out), pext.numel(), cur_stream());
+}
+
+// BN-backward coefficients from the pooled-domain sums (pre_slab), the (a dz + cc) weight
+// gradient into dslab, then dW = beta dW + sum dslab + b * sum hslab
+void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<double> nsc,
+                     std::vector<double> nbi, at::Tensor pdy, at::Tensor code, at::Tensor mean,
+                     at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma, at::Tensor dbeta,
+                     double gbeta, at::Tensor pre_slab, int64_t pre_rows, at::Tensor hslab,
+                     int64_t hgrid, at::Tensor dw, double wbeta, at::Tensor work, at::Tensor dslab,
+                     int64_t grid) {
+  const ImgView v = img_view(img);
+  TORCH_CHECK(dm::stem_fused_supported(v.H, v.W), "fused stem: unsupported input size");
+  need_bf16_nhwc(pdy, "pdy");
+  const int B = pdy.size(0), C = 64;
+  TORCH_CHECK(pdy.size(1) == v.H / 4 && pdy.size(2) == v.W / 4 && pdy.size(3) == C, "pdy shape");
+  TORCH_CHECK(code.scalar_type() == at::kByte && code.numel() == pdy.numel(), "code");
+  const long long M = (long long)B * (v.H / 2) * (v.W / 2);
+  need_f32(work, "work", bn_bwd_work(M, C));
+  need_f32(pre_slab, "pre_slab", pre_rows * 2 * C);
+  need_f32(dw, "dw", (int64_t)C * 3 * 49);
+  need_f32(hslab, "hslab", hgrid * C * dm::stem_slab_cols());
+  TORCH_CHECK(grid >= 1 && grid <= B, "grid must be in [1, B]");
+  need_f32(dslab, "dslab", grid * C * dm::stem_slab_cols());
+  const float s3[3] = {(float)nsc[0], (float)nsc[1], (float)nsc[2]};
+  const float b3[3] = {(float)nbi[0], (float)nbi[1], (float)nbi[2]};
+  const DeviceGuard guard(pdy.device());
+  auto st = cur_stream();
+  // mode 3, dy = nullptr: coefficients only (work[0, 3C) = a, b, cc) + dgamma / dbeta
+  dm::bn_backward(nullptr, nullptr, nullptr, fp(mean), fp(invstd), fp(gamma), fp(dgamma), fp(dbeta),
+                  (float)gbeta, M, C, 3, nullptr, nullptr, nullptr, nullptr, v.H / 2, v.W / 2,
+                  v.H / 4, v.W / 4, 3, 2, 1, nullptr, nullptr, fp(work), st, fp(pre_slab),
+                  (int)pre_rows, nullptr);
+  dm::stem_bwd_fused2(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(pdy),
+                      (const uint8_t*)code.data_ptr(), fp(work), fp(dslab), B, v.N, v.H, v.W,
+                      (int)grid, st);
+  dm::stem_wreduce(fp(dslab), (int)grid, fp(hslab), (int)hgrid, fp(work), fp(dw), (float)wbeta, st);
+}
+
+void stem_pack_weights(at::Tensor w, at::Tensor wk) {
+  need_f32(w, "w", 64 * 3 * 49);
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3 && w.size(2) == 7 && w.size(3) == 7,
+              "stem weight must be [64][3][7][7]");
+  TORCH_CHECK(wk.scalar_type() == at::kBFloat16 && wk.numel() == 64 * dm::stem_wk_cols(), "wk");
+  const DeviceGuard guard(w.device());
+  dm::stem_pack_weights(fp(w), bp(wk), cur_stream());
+}
+
 void register_resnet(pybind11::module_& m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("wpack"), py::arg("y"), py::arg("stats"),
         py::arg("add"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
@@ -685,4 +813,18 @@ void register_resnet(pybind11::module_& m) {
   m.def("pack_input_s2d", &pack_input_s2d, py::arg("x"), py::arg("y"),
         py::arg("idx") = py::none());
   m.def("pack_weights_s2d", &pack_weights_s2d);
+  m.def("stem_fused_supported", &stem_fused_supported);
+  m.def("stem_fused_grid", &stem_fused_grid);
+  m.def("stem_slab_cols", &stem_slab_cols);
+  m.def("stem_fwd_fused", &stem_fwd_fused, py::arg("img"), py::arg("idx"), py::arg("nsc"),
+        py::arg("nbi"), py::arg("wk"), py::arg("gamma"), py::arg("pext"), py::arg("code"),
+        py::arg("stats"), py::arg("hslab"), py::arg("grid"));
+  m.def("stem_pool_apply", &stem_pool_apply, py::arg("pext"), py::arg("code"), py::arg("scale"),
+        py::arg("shift"), py::arg("out"));
+  m.def("stem_bwd_fused2", &stem_bwd_fused2, py::arg("img"), py::arg("idx"), py::arg("nsc"),
+        py::arg("nbi"), py::arg("pdy"), py::arg("code"), py::arg("mean"), py::arg("invstd"),
+        py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"),
+        py::arg("pre_slab"), py::arg("pre_rows"), py::arg("hslab"), py::arg("hgrid"),
+        py::arg("dw"), py::arg("wbeta"), py::arg("work"), py::arg("dslab"), py::arg("grid"));
+  m.def("stem_pack_weights", &stem_pack_weights);
 }

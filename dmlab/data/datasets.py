@@ -101,18 +101,46 @@ class SyntheticMNIST(TensorDataset):
         super().__init__(ds.images, labels)
 
 
+# uint8 images (what a decoded JPEG pipeline delivers) are normalised as ImageNet RGB:
+# x = (u / 255 - mean) / std per channel, by the first layer (the fused ResNet stem reads the
+# bytes and normalises on the fly: dmlab.ops.convbn); fp32 / bf16 images are used as stored
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def input_affine(dtype):
+    """(scale[3], bias[3]) with x = raw * scale + bias for an image tensor of ``dtype``."""
+    if dtype == torch.uint8:
+        return ([1.0 / (255.0 * s) for s in IMAGENET_STD],
+                [-m / s for m, s in zip(IMAGENET_MEAN, IMAGENET_STD)])
+    return [1.0, 1.0, 1.0], [0.0, 0.0, 0.0]
+
+
+def normalize_input(x: torch.Tensor, dtype=torch.float32) -> torch.Tensor:
+    """The reference-path equivalent of the stem's on-the-fly normalisation ((N,3,H,W))."""
+    if x.dtype != torch.uint8:
+        return x
+    sc, bi = input_affine(torch.uint8)
+    sc = torch.tensor(sc, device=x.device, dtype=torch.float32).view(1, 3, 1, 1)
+    bi = torch.tensor(bi, device=x.device, dtype=torch.float32).view(1, 3, 1, 1)
+    return (x.float() * sc + bi).to(dtype)
+
+
 class SyntheticImageNet(TensorDataset):
     """ImageNet-shaped synthetic data for the ResNet-18 benchmark.
 
     Generated directly on ``device`` (no host copy) with uniform pixels; the
     benchmark measures throughput, not accuracy (BASELINE.json: synthetic data,
-    random-init weights)."""
+    random-init weights).  ``dtype=torch.uint8`` stores decoded-image bytes (uniform in
+    0..255), normalised by the model's first layer (:func:`input_affine`)."""
 
     def __init__(self, n: int, res: int = 224, num_classes: int = 1000, device="cpu",
                  dtype=torch.float32, channels_last=True, seed: int = 0):
         g = torch.Generator(device=device).manual_seed(seed)
         fmt = torch.channels_last if channels_last else torch.contiguous_format
         im = torch.rand((n, 3, res, res), generator=g, device=device, dtype=torch.float32)
+        if dtype == torch.uint8:
+            im = (im * 256.0).floor_().clamp_(0, 255)
         im = im.to(dtype).contiguous(memory_format=fmt)
         lb = torch.randint(0, num_classes, (n,), generator=g, device=device)
         super().__init__(im, lb)

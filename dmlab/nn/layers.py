@@ -178,7 +178,9 @@ class ConvBNPool(ConvBN):
         self.pool_k, self.pool_s, self.pool_p = pool_k, pool_s, pool_p
 
     def torch_forward(self, x, residual=None):
-        y = super().torch_forward(x)
+        from dmlab.data import normalize_input
+
+        y = super().torch_forward(normalize_input(x, self.weight.dtype))  # u8 images: ImageNet norm
         return F.max_pool2d(y, self.pool_k, self.pool_s, self.pool_p)
 
 

@@ -205,6 +205,129 @@ def packed_weights_s2d(layer):
     return cache[1]
 
 
+def packed_weights_stem(layer):
+    """[64][176] bf16 K-dense stem weights (k = ky*24 + kx*3 + c), cached per weight version."""
+    prog = layer._prog
+    cache = getattr(layer, "_wcache_k176", None)
+    if cache is None or cache[0] != prog._wver:
+        wk = cache[1] if cache is not None else torch.empty(
+            (64, 176), device=layer.weight.device, dtype=torch.bfloat16)
+        lib().stem_pack_weights(layer.weight.detach(), wk)
+        cache = (prog._wver, wk)
+        object.__setattr__(layer, "_wcache_k176", cache)
+    return cache[1]
+
+
+def _stem_image(x):
+    """(images, idx) of a stem input: a loader batch by index (dmlab.data.Gathered) or an
+    image tensor ((N,3,H,W) channels_last or (N,H,W,3)); None if it is neither."""
+    if not isinstance(x, torch.Tensor):
+        return x.images, x.idx
+    if x.dim() == 4 and x.shape[1] == 3 and not getattr(x, "_dm_nhwc", False):
+        if not x.is_contiguous(memory_format=torch.channels_last):
+            x = x.contiguous(memory_format=torch.channels_last)
+        return x, None
+    return None
+
+
+_STEM_FUSED_DEFAULT = "0"  # until GPU-validated
+
+
+def stem_fused_ok(layer, x):
+    """The K-dense fused stem (csrc/stem_fused.hip) serves this layer and input:
+    7x7/s2/p3 conv 3 -> 64 + BN + ReLU + 3x3/s2/p1 max-pool, on a raw fp32 / bf16 / u8 image
+    batch whose size the kernel supports, BN in training mode or eval (not eval-BN with
+    gradients).  DMLAB_STEM_FUSED=0 selects the space-to-depth path (A/B)."""
+    if os.environ.get("DMLAB_STEM_FUSED", _STEM_FUSED_DEFAULT) == "0":
+        return False
+    if not (getattr(layer, "pool_k", 0) == 3 and layer.pool_s == 2 and layer.pool_p == 1
+            and layer.k == 7 and layer.stride == 2 and layer.padding == 3 and layer.cin == 3
+            and layer.cout == 64 and layer.relu):
+        return False
+    im = _stem_image(x)
+    if im is None:
+        return False
+    img = im[0]
+    if img.dtype not in (torch.float32, torch.bfloat16, torch.uint8) or not img.is_cuda:
+        return False
+    H, W = (img.shape[2], img.shape[3]) if img.shape[1] == 3 else (img.shape[1], img.shape[2])
+    return bool(lib().stem_fused_supported(H, W))
+
+
+def _stem_fused_fwd(layer, x, ctx, train):
+    """Fused stem forward: pooled BN-input extremum + window codes + BN statistics (+ the
+    weight-gradient helper H when training) in one kernel, then BN + ReLU on the pooled
+    tensor.  The conv output is never written."""
+    from dmlab.data import input_affine
+
+    L = lib()
+    img, idx = _stem_image(x)
+    B = idx.numel() if idx is not None else img.shape[0]
+    H, W = (img.shape[2], img.shape[3]) if img.shape[1] == 3 else (img.shape[1], img.shape[2])
+    PH, PW = H // 4, W // 4
+    dev = img.device
+    nsc, nbi = input_affine(img.dtype)
+    wk = packed_weights_stem(layer)
+    pext = empty_nhwc(B, PH, PW, 64, img)
+    code = torch.empty((B, PH, PW, 64), device=dev, dtype=torch.uint8)
+    grid = L.stem_fused_grid(B)
+    f32 = dict(device=dev, dtype=torch.float32)
+    scale = torch.empty(64, **f32)
+    shift = torch.empty(64, **f32)
+    use_batch = layer.training
+    stats = torch.empty(grid * 128, **f32) if use_batch else None
+    hslab = torch.empty(grid * 64 * L.stem_slab_cols(), **f32) if (use_batch and train) else None
+    L.stem_fwd_fused(img, idx, nsc, nbi, wk, layer.bn_weight.detach(), pext, code, stats, hslab,
+                     grid)
+    M = B * (H // 2) * (W // 2)
+    if use_batch:
+        mean = torch.empty(64, **f32)
+        invstd = torch.empty(64, **f32)
+        work = torch.empty(256 * 2 * 64, **f32)
+        L.bn_stats_finalize(stats, grid, float(M), layer.bn_weight.detach(),
+                            layer.bn_bias.detach(), layer.running_mean, layer.running_var,
+                            layer.momentum, layer.eps, scale, shift, mean, invstd, work,
+                            layer.num_batches_tracked)
+    else:
+        L.bn_eval_coeffs(layer.bn_weight.detach(), layer.bn_bias.detach(), layer.running_mean,
+                         layer.running_var, layer.eps, scale, shift)
+        mean = invstd = None
+    out = empty_nhwc(B, PH, PW, 64, img)
+    L.stem_pool_apply(pext, code if train else None, scale, shift, out)
+    if train:
+        ctx.update(fused_stem=True, img=img, gidx=idx, nsc=nsc, nbi=nbi, yarg=pext, idx=code,
+                   mean=mean, invstd=invstd, scale=scale, shift=shift, hslab=hslab, hgrid=grid,
+                   has_res=False, first=True, s2d=False, pre=None, y=pext, x=None, M=M)
+    return out
+
+
+def _stem_fused_bwd(layer, dout, ctx):
+    """Fused stem backward: BN-backward coefficients from the pooled-domain sums, the
+    (a*dz + cc) weight gradient over the raw input, and dW = that + b * H."""
+    L = lib()
+    dout = dout.contiguous()
+    pext, code = ctx["yarg"], ctx["idx"]
+    acc = 1.0 if layer.accumulate else 0.0
+    pre_sums = ctx.pop("pre_sums", None) or {}
+    if not pre_sums:
+        part = torch.empty(L.bn_bwd_rows(pext.numel() // 64, 64) * 2 * 64, device=dout.device,
+                           dtype=torch.float32)
+        rows = L.bn_bwd_reduce_masked(dout, pext, ctx["mean"], ctx["invstd"], ctx["scale"],
+                                      ctx["shift"], part)
+        pre_sums = dict(pre_slab=part, pre_rows=rows)
+    B = dout.shape[0]
+    grid = L.stem_fused_grid(B)
+    f32 = dict(device=dout.device, dtype=torch.float32)
+    work = torch.empty(L.bn_bwd_work(ctx["M"], 64), **f32)
+    dslab = torch.empty(grid * 64 * L.stem_slab_cols(), **f32)
+    L.stem_bwd_fused2(ctx["img"], ctx["gidx"], ctx["nsc"], ctx["nbi"], dout, code, ctx["mean"],
+                      ctx["invstd"], layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
+                      layer.grad_slot("bn_bias"), acc, pre_sums["pre_slab"],
+                      pre_sums["pre_rows"], ctx["hslab"], ctx["hgrid"],
+                      layer.grad_slot("weight"), acc, work, dslab, grid)
+    return None
+
+
 def packed_weights(layer, need_wd=True):
     prog = layer._prog
     ver = prog._wver
@@ -266,6 +389,9 @@ def _materialise(x, pre):
 
 def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     L = lib()
+    if (residual is None and not raw and pre is None and (layer.training or not train)
+            and stem_fused_ok(layer, x)):
+        return _stem_fused_fwd(layer, x, ctx, train)
     gidx = None
     if not isinstance(x, torch.Tensor):  # dmlab.data.Gathered: a loader batch by row index
         if use_s2d(layer, x.images) and x.images.dtype in (torch.float32, torch.bfloat16):
@@ -423,6 +549,8 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
                   dgrad kernel supports it (cfg 80), that BN's backward reduction (Σdz, Σdz·x̂)
                   runs in this dgrad's epilogue and is left in its ctx["pre_sums"], so its
                   own backward skips the pass that re-reads dx and y"""
+    if ctx.get("fused_stem"):
+        return _stem_fused_bwd(layer, dout, ctx)
     L = lib()
     x, y = ctx["x"], ctx["y"]
     N, OH, OW, cout = y.shape

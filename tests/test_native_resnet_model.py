@@ -79,6 +79,7 @@ def test_fused_stem_backward_matches_unfused(dev, res, monkeypatch):
     fp32 sums in another order), and every other gradient bit for bit."""
     import dmlab.ops.convbn as cb
 
+    monkeypatch.setenv("DMLAB_STEM_FUSED", "0")  # the space-to-depth stem path
     torch.manual_seed(3)
     a = ResNet18(num_classes=10).to(dev)
     x = torch.rand(4, 3, res, res, device=dev)

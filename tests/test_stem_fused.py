@@ -1,0 +1,201 @@
+"""The K-dense fused ResNet stem (csrc/stem_fused.hip) vs float64 PyTorch references:
+conv statistics, the pooled BN-input extremum and its window codes (both BN-scale signs),
+the weight-gradient helper H, and the whole stem backward (conv + BN + ReLU + max-pool)
+against autograd; u8 / fp32 / bf16 inputs through a gathered batch index."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from dmlab.data import input_affine
+from dmlab.ops._native import lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(dev, dtype, Nimg, H, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    u = torch.rand(Nimg, 3, H, H, device=dev, generator=g)
+    if dtype == torch.uint8:
+        img = (u * 256).floor().clamp(0, 255).to(torch.uint8)
+    else:
+        img = u.to(dtype)
+    return img.contiguous(memory_format=torch.channels_last)
+
+
+def _x_bf16(img):
+    """What the kernel computes on: the normalised input rounded to bf16 (float64 copy)."""
+    sc, bi = input_affine(img.dtype)
+    sc = torch.tensor(sc, device=img.device).view(1, 3, 1, 1)
+    bi = torch.tensor(bi, device=img.device).view(1, 3, 1, 1)
+    return (img.float() * sc + bi).to(torch.bfloat16).double()
+
+
+def _run_fwd(img, idx, w, gamma, train=True):
+    L = lib()
+    B = idx.numel() if idx is not None else img.shape[0]
+    H = img.shape[2]
+    dev = img.device
+    wk = torch.empty(64, 176, device=dev, dtype=torch.bfloat16)
+    L.stem_pack_weights(w.contiguous(), wk)
+    pext = torch.empty(B, H // 4, H // 4, 64, device=dev, dtype=torch.bfloat16)
+    code = torch.empty(B, H // 4, H // 4, 64, device=dev, dtype=torch.uint8)
+    grid = L.stem_fused_grid(B)
+    stats = torch.empty(grid * 128, device=dev) if train else None
+    hslab = torch.empty(grid * 64 * L.stem_slab_cols(), device=dev) if train else None
+    sc, bi = input_affine(img.dtype)
+    L.stem_fwd_fused(img, idx, sc, bi, wk, gamma, pext, code, stats, hslab, grid)
+    return pext, code, stats, hslab, grid
+
+
+def _codes_ref(z):
+    """max-pool 3x3/s2/p1 of z (N,C,H,W float64) -> values, window code kh*3+kw of the
+    first maximum in PyTorch's scan order."""
+    v, ind = F.max_pool2d(z, 3, 2, 1, return_indices=True)
+    H, W = z.shape[2], z.shape[3]
+    iy, ix = ind // W, ind % W
+    oy = torch.arange(v.shape[2], device=z.device).view(1, 1, -1, 1)
+    ox = torch.arange(v.shape[3], device=z.device).view(1, 1, 1, -1)
+    return v, (iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1))
+
+
+@pytest.mark.parametrize("dtype", [torch.uint8, torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [64, 224])
+def test_stem_fused_forward(dev, dtype, H):
+    torch.manual_seed(0)
+    img = _inputs(dev, dtype, 5, H, 1)
+    idx = torch.tensor([4, 0, 2], device=dev, dtype=torch.long)
+    w = torch.randn(64, 3, 7, 7, device=dev) * 0.08
+    gamma = torch.randn(64, device=dev)
+    gamma[3] = 0.0  # either extremum is right for a zero scale
+    pext, code, stats, hslab, grid = _run_fwd(img, idx, w, gamma)
+    xb = _x_bf16(img.index_select(0, idx)).cpu()
+    wb = w.to(torch.bfloat16).double().cpu()
+    y = F.conv2d(xb, wb, stride=2, padding=3)  # float64 reference of the conv
+    # BN statistics from the fp32 accumulators, one row per workgroup
+    st = stats.view(grid, 2, 64).double().sum(0).cpu()
+    torch.testing.assert_close(st[0], y.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[1], (y * y).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    # pooled extremum of the raw conv output: max where gamma >= 0, min where gamma < 0
+    sgn = torch.where(gamma.cpu() < 0, -1.0, 1.0).double().view(1, 64, 1, 1)
+    yb = y.to(torch.bfloat16).double()  # the kernel pools the bf16-rounded conv output
+    v, cref = _codes_ref(sgn * yb)
+    pref = (sgn * v).permute(0, 2, 3, 1)
+    got = pext.double().cpu()
+    assert (got - pref).abs().max().item() <= 2 ** -7 * pref.abs().max().item()
+    cref = cref.permute(0, 2, 3, 1)
+    agree = (code.cpu().long() == cref).double().mean().item()
+    assert agree > 0.995, agree  # ties / 1-ulp rounding differences may pick another pixel
+    # H[co][k] = sum_m y_bf16[m][co] * x_col[m][k]
+    xcol = F.unfold(xb, 7, padding=3, stride=2)  # [B, 3*49 (c, ky, kx), L]
+    href = torch.einsum("bcl,bkl->ck", yb.flatten(2), xcol)
+    hs = hslab.view(grid, 64, lib().stem_slab_cols()).double().sum(0).cpu()
+    ky, kx, c = torch.meshgrid(torch.arange(7), torch.arange(7), torch.arange(3), indexing="ij")
+    hk = hs[:, (ky * 24 + kx * 3 + c).flatten()]          # kernel order (ky, kx, c)
+    hr = href[:, (c * 49 + ky * 7 + kx).flatten()]       # unfold order (c, ky, kx)
+    assert ((hk - hr).norm() / hr.norm()).item() < 2e-3
+
+
+def test_stem_pool_apply_and_masked_codes(dev):
+    torch.manual_seed(2)
+    pext = torch.randn(2, 16, 16, 64, device=dev).to(torch.bfloat16)
+    code = torch.randint(0, 9, pext.shape, device=dev, dtype=torch.uint8)
+    scale = torch.randn(64, device=dev)
+    shift = torch.randn(64, device=dev) * 0.3
+    out = torch.empty_like(pext)
+    c2 = code.clone()
+    lib().stem_pool_apply(pext, c2, scale, shift, out)
+    z = pext.float() * scale + shift
+    torch.testing.assert_close(out.float(), z.clamp_min(0).to(torch.bfloat16).float(), rtol=0, atol=0)
+    assert torch.equal(c2, torch.where(z > 0, code, torch.full_like(code, 15)))
+
+
+@pytest.mark.parametrize("dtype,H", [(torch.uint8, 224), (torch.float32, 64)])
+def test_stem_fused_backward_matches_autograd(dev, dtype, H):
+    """stem = maxpool(relu(BN_train(conv(x)))): the native forward + backward (pooled-domain
+    BN sums, (a dz + cc) weight gradient, + b*H) against float64 autograd of the same
+    function on the same bf16-rounded input and weights."""
+    L = lib()
+    torch.manual_seed(1)
+    B = 3
+    img = _inputs(dev, dtype, B + 1, H, 5)
+    idx = torch.tensor([3, 1, 0], device=dev, dtype=torch.long)
+    w = torch.randn(64, 3, 7, 7, device=dev) * 0.08
+    gamma = torch.randn(64, device=dev)
+    beta = torch.randn(64, device=dev) * 0.2
+    pext, code, stats, hslab, grid = _run_fwd(img, idx, w, gamma)
+    M = B * (H // 2) ** 2
+    f = dict(device=dev, dtype=torch.float32)
+    scale, shift, mean, invstd = (torch.empty(64, **f) for _ in range(4))
+    rm, rv = torch.zeros(64, **f), torch.ones(64, **f)
+    L.bn_stats_finalize(stats, grid, float(M), gamma, beta, rm, rv, 0.1, 1e-5, scale, shift, mean,
+                        invstd, torch.empty(256 * 128, **f))
+    out = torch.empty_like(pext)
+    L.stem_pool_apply(pext, code, scale, shift, out)
+    g = torch.randn(out.shape, device=dev).to(torch.bfloat16)
+    part = torch.empty(L.bn_bwd_rows(pext.numel() // 64, 64) * 128, **f)
+    rows = L.bn_bwd_reduce_masked(g, pext, mean, invstd, scale, shift, part)
+    dgamma, dbeta = torch.zeros(64, **f), torch.zeros(64, **f)
+    dw = torch.zeros(64, 3, 7, 7, **f)
+    work = torch.empty(L.bn_bwd_work(M, 64), **f)
+    dslab = torch.empty(L.stem_fused_grid(B) * 64 * L.stem_slab_cols(), **f)
+    sc, bi = input_affine(img.dtype)
+    L.stem_bwd_fused2(img, idx, sc, bi, g, code, mean, invstd, gamma, dgamma, dbeta, 0.0, part,
+                      rows, hslab, grid, dw, 0.0, work, dslab, L.stem_fused_grid(B))
+    # float64 autograd reference
+    xb = _x_bf16(img.index_select(0, idx)).cpu()
+    wr = w.to(torch.bfloat16).double().cpu().requires_grad_(True)
+    gr = gamma.double().cpu().requires_grad_(True)
+    br = beta.double().cpu().requires_grad_(True)
+    y = F.conv2d(xb, wr, stride=2, padding=3)
+    z = F.relu(F.batch_norm(y, None, None, gr, br, training=True, eps=1e-5))
+    p = F.max_pool2d(z, 3, 2, 1)
+    (p * g.double().cpu().permute(0, 3, 1, 2)).sum().backward()
+    torch.testing.assert_close(out.double().cpu(), p.detach().permute(0, 2, 3, 1),
+                               rtol=2e-2, atol=2e-2)
+    for got, ref, n in ((dw, wr.grad, "dW"), (dgamma, gr.grad, "dgamma"), (dbeta, br.grad, "dbeta")):
+        err = ((got.double().cpu() - ref).norm() / ref.norm()).item()
+        assert err < 1e-2, (n, err)
+
+
+def test_resnet18_fused_stem_matches_s2d_stem(dev, monkeypatch):
+    """The whole model with the fused stem vs the space-to-depth stem (same weights, same
+    fp32 batch): the loss and every gradient agree to bf16 level."""
+    from dmlab.models import ResNet18
+    from dmlab.nn import cross_entropy
+
+    torch.manual_seed(4)
+    a = ResNet18(num_classes=10).to(dev)
+    x = torch.rand(8, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    res = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("DMLAB_STEM_FUSED", fused)
+        a.flat.grad.zero_()
+        loss = cross_entropy(a(x), y)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((loss.item(), {n: p.grad.detach().clone() for n, p in a.named_parameters()}))
+    (la, ga), (lb, gb) = res
+    assert abs(la - lb) < 1e-2 * max(1.0, abs(lb))
+    for n in ga:
+        e = ((ga[n] - gb[n]).norm() / (gb[n].norm() + 1e-12)).item()
+        assert e < 0.1, (n, e)
+
+
+def test_resnet18_u8_gathered_batch(dev, monkeypatch):
+    """A u8 dataset through the loader's gathered batch (the bench data path): the fused
+    stem reads the bytes by row index and normalises them; matches the model on the
+    normalised float batch."""
+    from dmlab.data import Gathered, normalize_input
+    from dmlab.models import ResNet18
+
+    monkeypatch.setenv("DMLAB_STEM_FUSED", "1")
+    torch.manual_seed(6)
+    a = ResNet18(num_classes=10).to(dev).eval()
+    img = _inputs(dev, torch.uint8, 6, 64, 9)
+    idx = torch.tensor([5, 2, 2, 0], device=dev, dtype=torch.long)
+    with torch.no_grad():
+        o1 = a(Gathered(img, idx)).float()
+        xf = normalize_input(img.index_select(0, idx)).contiguous(memory_format=torch.channels_last)
+        o2 = a(xf).float()
+    assert ((o1 - o2).norm() / o2.norm()).item() < 2e-2
