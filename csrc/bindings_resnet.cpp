@@ -677,8 +677,7 @@ const long long* idx_ptr(const c10::optional<at::Tensor>& idx, int B, int Nimg) 
 
 void stem_fwd_fused(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<double> nsc,
                     std::vector<double> nbi, at::Tensor wk, at::Tensor gamma, at::Tensor pext,
-                    at::Tensor code, c10::optional<at::Tensor> stats,
-                    c10::optional<at::Tensor> hslab, int64_t grid) {
+                    at::Tensor code, c10::optional<at::Tensor> stats, int64_t grid) {
   const ImgView v = img_view(img);
   TORCH_CHECK(dm::stem_fused_supported(v.H, v.W), "fused stem: unsupported input size");
   need_bf16_nhwc(pext, "pext");
@@ -693,14 +692,12 @@ void stem_fwd_fused(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<d
   TORCH_CHECK(nsc.size() == 3 && nbi.size() == 3, "3 normalisation scales / biases");
   TORCH_CHECK(grid >= 1 && grid <= B, "grid must be in [1, B]");
   if (stats.has_value()) need_f32(*stats, "stats", grid * 128);
-  if (hslab.has_value()) need_f32(*hslab, "hslab", grid * 64 * dm::stem_slab_cols());
-  TORCH_CHECK(stats.has_value() || !hslab.has_value(), "hslab (gradients) needs batch stats");
   const float s3[3] = {(float)nsc[0], (float)nsc[1], (float)nsc[2]};
   const float b3[3] = {(float)nbi[0], (float)nbi[1], (float)nbi[2]};
   const DeviceGuard guard(pext.device());
   dm::stem_fwd_fused(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(wk), fp(gamma), bp(pext),
-                     (uint8_t*)code.data_ptr(), stats ? fp(*stats) : nullptr,
-                     hslab ? fp(*hslab) : nullptr, B, v.N, v.H, v.W, (int)grid, cur_stream());
+                     (uint8_t*)code.data_ptr(), stats ? fp(*stats) : nullptr, B, v.N, v.H, v.W,
+                     (int)grid, cur_stream());
 }
 
 void stem_pool_apply(at::Tensor pext, c10::optional<at::Tensor> code, at::Tensor scale,
@@ -717,14 +714,13 @@ void stem_pool_apply(at::Tensor pext, c10::optional<at::Tensor> code, at::Tensor
                       bp(out), pext.numel(), cur_stream());
 }
 
-// BN-backward coefficients from the pooled-domain sums (pre_slab), the (a dz + cc) weight
-// gradient into dslab, then dW = beta dW + sum dslab + b * sum hslab
+// BN-backward coefficients from the pooled-domain sums (pre_slab), the weight gradient of
+// dy = a dz + b y + cc (y recomputed in the kernel) into dslab, then dW = beta dW + sum dslab
 void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<double> nsc,
-                     std::vector<double> nbi, at::Tensor pdy, at::Tensor code, at::Tensor mean,
-                     at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma, at::Tensor dbeta,
-                     double gbeta, at::Tensor pre_slab, int64_t pre_rows, at::Tensor hslab,
-                     int64_t hgrid, at::Tensor dw, double wbeta, at::Tensor work, at::Tensor dslab,
-                     int64_t grid) {
+                     std::vector<double> nbi, at::Tensor wk, at::Tensor pdy, at::Tensor code,
+                     at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
+                     at::Tensor dbeta, double gbeta, at::Tensor pre_slab, int64_t pre_rows,
+                     at::Tensor dw, double wbeta, at::Tensor work, at::Tensor dslab, int64_t grid) {
   const ImgView v = img_view(img);
   TORCH_CHECK(dm::stem_fused_supported(v.H, v.W), "fused stem: unsupported input size");
   need_bf16_nhwc(pdy, "pdy");
@@ -735,7 +731,8 @@ void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<
   need_f32(work, "work", bn_bwd_work(M, C));
   need_f32(pre_slab, "pre_slab", pre_rows * 2 * C);
   need_f32(dw, "dw", (int64_t)C * 3 * 49);
-  need_f32(hslab, "hslab", hgrid * C * dm::stem_slab_cols());
+  TORCH_CHECK(wk.is_cuda() && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
+              wk.numel() == 64 * dm::stem_wk_cols(), "wk must be packed [64][176] bf16");
   TORCH_CHECK(grid >= 1 && grid <= B, "grid must be in [1, B]");
   need_f32(dslab, "dslab", grid * C * dm::stem_slab_cols());
   const float s3[3] = {(float)nsc[0], (float)nsc[1], (float)nsc[2]};
@@ -747,10 +744,10 @@ void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<
                   (float)gbeta, M, C, 3, nullptr, nullptr, nullptr, nullptr, v.H / 2, v.W / 2,
                   v.H / 4, v.W / 4, 3, 2, 1, nullptr, nullptr, fp(work), st, fp(pre_slab),
                   (int)pre_rows, nullptr);
-  dm::stem_bwd_fused2(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(pdy),
+  dm::stem_bwd_fused2(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(wk), bp(pdy),
                       (const uint8_t*)code.data_ptr(), fp(work), fp(dslab), B, v.N, v.H, v.W,
                       (int)grid, st);
-  dm::stem_wreduce(fp(dslab), (int)grid, fp(hslab), (int)hgrid, fp(work), fp(dw), (float)wbeta, st);
+  dm::stem_wreduce(fp(dslab), (int)grid, fp(dw), (float)wbeta, st);
 }
 
 void stem_pack_weights(at::Tensor w, at::Tensor wk) {
@@ -818,13 +815,13 @@ void register_resnet(pybind11::module_& m) {
   m.def("stem_slab_cols", &stem_slab_cols);
   m.def("stem_fwd_fused", &stem_fwd_fused, py::arg("img"), py::arg("idx"), py::arg("nsc"),
         py::arg("nbi"), py::arg("wk"), py::arg("gamma"), py::arg("pext"), py::arg("code"),
-        py::arg("stats"), py::arg("hslab"), py::arg("grid"));
+        py::arg("stats"), py::arg("grid"));
   m.def("stem_pool_apply", &stem_pool_apply, py::arg("pext"), py::arg("code"), py::arg("scale"),
         py::arg("shift"), py::arg("out"));
   m.def("stem_bwd_fused2", &stem_bwd_fused2, py::arg("img"), py::arg("idx"), py::arg("nsc"),
-        py::arg("nbi"), py::arg("pdy"), py::arg("code"), py::arg("mean"), py::arg("invstd"),
-        py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"), py::arg("gbeta"),
-        py::arg("pre_slab"), py::arg("pre_rows"), py::arg("hslab"), py::arg("hgrid"),
-        py::arg("dw"), py::arg("wbeta"), py::arg("work"), py::arg("dslab"), py::arg("grid"));
+        py::arg("nbi"), py::arg("wk"), py::arg("pdy"), py::arg("code"), py::arg("mean"),
+        py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
+        py::arg("gbeta"), py::arg("pre_slab"), py::arg("pre_rows"), py::arg("dw"),
+        py::arg("wbeta"), py::arg("work"), py::arg("dslab"), py::arg("grid"));
   m.def("stem_pack_weights", &stem_pack_weights);
 }

@@ -93,22 +93,22 @@ void stem_wgrad_fused(const bf16_t* xs, const bf16_t* y, const bf16_t* pdy, cons
                       const float* coef, const float* sc, const float* sh, float* slab, int N,
                       int H, int W, int S, hipStream_t st);
 // stem_fused.hip: K-dense fused stem (raw-input gather + 7x7/s2 conv + BN statistics + pooled
-// extremum + wgrad helper H), pooled BN apply, backward (a dz + cc) wgrad, final reduce
+// extremum), pooled BN apply, backward (y recomputed, dy = a dz + b y + cc) wgrad, reduce
 bool stem_fused_supported(int Hin, int Win);
 int stem_fused_grid(int N);
 int stem_slab_cols();
 int stem_wk_cols();
 void stem_fwd_fused(const void* img, int dtype, const long long* idx, const float* nsc,
                     const float* nbi, const bf16_t* wk, const float* gamma, bf16_t* pext,
-                    uint8_t* code, float* stats, float* hslab, int N, int nimg, int Hin, int Win,
-                    int grid, hipStream_t st);
+                    uint8_t* code, float* stats, int N, int nimg, int Hin, int Win, int grid,
+                    hipStream_t st);
 void stem_pool_apply(const bf16_t* pext, uint8_t* code, const float* scale, const float* shift,
                      bf16_t* out, long long n, hipStream_t st);
 void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const float* nsc,
-                     const float* nbi, const bf16_t* pdy, const uint8_t* code, const float* coef,
-                     float* dslab, int N, int nimg, int Hin, int Win, int grid, hipStream_t st);
-void stem_wreduce(const float* dslab, int GD, const float* hslab, int GH, const float* coef,
-                  float* dw, float beta, hipStream_t st);
+                     const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code,
+                     const float* coef, float* dslab, int N, int nimg, int Hin, int Win, int grid,
+                     hipStream_t st);
+void stem_wreduce(const float* dslab, int GD, float* dw, float beta, hipStream_t st);
 void stem_pack_weights(const float* w, bf16_t* wk, hipStream_t st);
 // The BatchNorm backward reduction of the layer whose output gradient a data gradient
 // produces, done in that dgrad's epilogue: with dz = Y * relu-mask (mask from y*sc + sh > 0,

@@ -24,15 +24,19 @@
 //    batch 1024) never reaches memory.  A small pass then applies BN + ReLU to the pooled
 //    tensor and marks relu-masked windows (code 15).
 //  * BN statistics (sum, sum of squares) from the fp32 accumulators, one row per workgroup.
-//  * Weight-gradient helper H[co][k] = sum_m y[m][co] * x_col[m][k] (the y-term of the BN
-//    backward, see below), accumulated from the bf16 y tile and the E rows already in LDS.
 //
-// Backward (stem_bwd_kernel): the weight gradient of y = conv(x) with the BN backward
-//    dy = a*dz + b*y + cc  (dz: the pooled gradient routed to its window's selected pixel)
-// splits as dW = sum_m (a*dz + cc) x_col  +  b * H.  The kernel builds (a*dz + cc) per row
-// pair from the pooled gradient and codes (a 2x2 quad of pixels shares its 4 windows), never
-// needs y, and reduces it against the same E rows.  stem_wreduce_kernel sums both slab sets
-// in fixed order and writes the OIHW gradient.
+// Backward (stem_bwd_kernel), same walk: the weight gradient of y = conv(x) under the BN
+// backward  dy = a*dz + b*y + cc  (dz: the pooled gradient routed to its window's selected
+// pixel).  y is not stored, so the kernel RECOMPUTES it: per row pair, (1) a*dz from the
+// pooled gradient and codes (a 2x2 quad of pixels shares its 4 windows) into a bf16 tile,
+// (2) the conv MFMAs again (fp32 y in registers, the tile read/updated in place:
+// dy = a*dz + b*y + cc in fp32, then bf16 -- the mean-subtraction terms b*y + cc cancel in
+// fp32 per element, as in the unfused BN backward), (3) dW += dy^T x_col from the tile and
+// the E rows.  The 1.6 GB full-resolution y is neither written nor read: 1/3 more stem MFMA
+// work instead.  (Splitting dW = sum (a dz + cc) x_col + b * sum y x_col was built first and
+// rejected: the bf16 rounding of the large per-channel constant cc does not cancel against
+// b * sum y x_col -- 7-90 % gradient error on inputs with a large mean.)
+//  stem_wreduce_kernel sums the per-workgroup slabs in fixed order into the OIHW gradient.
 #include "common.h"
 #include "igemm_common.h"
 #include "kernels.h"
@@ -229,7 +233,6 @@ struct StemFwdArgs {
   bf16_t* pext;          // [N][PH][PW][64]
   uint8_t* code;         // [N][PH][PW][64]
   float* stats;          // [grid][2][64] or nullptr
-  float* hslab;          // [grid][64][SKH] or nullptr
   int N, nimg;           // batch rows, image rows (idx values are clamped to it)
   StemGeo G;
 };
@@ -244,7 +247,6 @@ __global__ void __launch_bounds__(SNT, 1) stem_fwd_kernel(StemFwdArgs a) {
   bf16_t* S = reinterpret_cast<bf16_t*>(Y + 2 * G.Wout * 128);  // [SROWS][SP]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const bool train = a.stats != nullptr;   // batch statistics
-  const bool wgh = a.hslab != nullptr;     // the backward's H (training with gradients)
 
   // zero everything once (S pads, E pad pixels are never read uninitialised)
   {
@@ -272,11 +274,6 @@ __global__ void __launch_bounds__(SNT, 1) stem_fwd_kernel(StemFwdArgs a) {
   for (int c = 0; c < 8; ++c) psg[c] = (pact && a.gamma[pc8 * 8 + c] < 0.f) ? -1.f : 1.f;
 
   float st_s[2] = {0.f, 0.f}, st_q[2] = {0.f, 0.f};
-  f32x16 hacc[3];
-#pragma unroll
-  for (int u = 0; u < 3; ++u)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) hacc[u][r] = 0.f;
 
   RawUnit ru[UPT];
   auto img_base = [&](int n) -> long long {
@@ -405,16 +402,15 @@ __global__ void __launch_bounds__(SNT, 1) stem_fwd_kernel(StemFwdArgs a) {
         __builtin_nontemporal_store((nt2){cd[0], cd[1]}, reinterpret_cast<nt2*>(a.code + po));
       }
       if (!last) e_build(E, S, G, 4 * i + 6, 4, 0, tid);
-      if (wgh) pair_wgrad(hacc, Y, E, G, i, wid, lane);
       __syncthreads();
-      if (last && more) {  // the next image's first rows: after this pair's wgrad reads of E
+      if (last && more) {  // the next image's first rows: after this pair's MFMA reads of E
         e_build(E, S, G, -3, 9, -3, tid);
         __syncthreads();
       }
     }
   }
   if (!train) return;
-  // ------------------------------------------------------------------ statistics + H slab
+  // ------------------------------------------------------------------ statistics
   float* red = reinterpret_cast<float*>(smem);  // reuse: [8 waves][2 halves][64][2]
   __syncthreads();
 #pragma unroll
@@ -430,8 +426,6 @@ __global__ void __launch_bounds__(SNT, 1) stem_fwd_kernel(StemFwdArgs a) {
     for (int k = 0; k < 16; ++k) s += red[(k * SCO + co) * 2 + which];
     a.stats[(long long)blockIdx.x * 2 * SCO + which * SCO + co] = s;
   }
-  __syncthreads();
-  if (wgh) write_wslab(hacc, red, a.hslab, wid, lane);
 }
 
 // out = relu(scale * pext + shift); code = 15 where that is <= 0 (no gradient flows)
@@ -472,6 +466,7 @@ struct StemBwdArgs2 {
   const void* img;
   const long long* idx;
   float nsc[3], nbi[3];
+  const bf16_t* wk;      // [64][SKP] packed weights (the forward's)
   const bf16_t* pdy;     // [N][PH][PW][64] pooled gradient
   const uint8_t* code;   // [N][PH][PW][64] window position, 15 = masked
   const float* coef;     // [3][64] a, b, cc
@@ -480,28 +475,33 @@ struct StemBwdArgs2 {
   StemGeo G;
 };
 
-constexpr int PRING = 4;  // pooled-row ring (rows i, i+1 in use, i+2 staged, i+3 in flight)
+constexpr int PRING = 3;  // pooled-row ring: rows i, i+1 in use, i+2 staged (i+3 in flight)
+constexpr int BROWS = 4;  // raw rows staged at once in the backward
 
 template <int DT>
 __global__ void __launch_bounds__(SNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const StemGeo G = a.G;
-  unsigned char* E = smem;                                   // [RING][Wout][24]
-  unsigned char* T = E + RING * G.ROWB;                      // [2][Wout][64] (a dz + cc)
-  bf16_t* S = reinterpret_cast<bf16_t*>(T + 2 * G.Wout * 128);  // [SROWS][SP]
+  unsigned char* Ws = smem;                                  // [64][SWP] bf16
+  unsigned char* E = Ws + SCO * SWP * 2;                     // [RING][Wout][24]
+  unsigned char* T = E + RING * G.ROWB;                      // [2][Wout][64]: a dz, then dy
+  bf16_t* S = reinterpret_cast<bf16_t*>(T + 2 * G.Wout * 128);  // [BROWS][SP]
   const int PRB = G.PW * SCO;                                // pooled row elements
-  bf16_t* Pg = S + SROWS * G.SP;                             // [PRING][PW][64] grads
+  bf16_t* Pg = S + BROWS * G.SP;                             // [PRING][PW][64] grads
   uint8_t* Pc = reinterpret_cast<uint8_t*>(Pg + PRING * PRB);  // [PRING][PW][64] codes
-  float* cf = reinterpret_cast<float*>(Pc + PRING * PRB);   // a, cc
+  float* cf = reinterpret_cast<float*>(Pc + PRING * PRB);   // a, b, cc
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   {
-    const int tot16 = (RING * G.ROWB + 2 * G.Wout * 128 + SROWS * G.SP * 2) / 16;
+    const int tot16 = (SCO * SWP * 2 + RING * G.ROWB + 2 * G.Wout * 128 + BROWS * G.SP * 2) / 16;
     for (int e = tid; e < tot16; e += SNT) reinterpret_cast<uint4*>(smem)[e] = make_uint4(0, 0, 0, 0);
   }
-  if (tid < SCO) {
-    cf[tid] = a.coef[tid];
-    cf[SCO + tid] = a.coef[2 * SCO + tid];
+  __syncthreads();
+  for (int e = tid; e < SCO * SKP / 8; e += SNT) {
+    const int co = e / (SKP / 8), ch = e - co * (SKP / 8);
+    *reinterpret_cast<uint4*>(Ws + co * SWP * 2 + ch * 16) =
+        *reinterpret_cast<const uint4*>(a.wk + co * SKP + ch * 8);
   }
+  if (tid < 3 * SCO) cf[tid] = a.coef[tid];
   f32x16 dacc[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u)
@@ -532,42 +532,39 @@ __global__ void __launch_bounds__(SNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
     *reinterpret_cast<uint4*>(Pg + s * PRB + tid * 8) = pg_r;
     *reinterpret_cast<uint2*>(Pc + s * PRB + tid * 8) = pc_r;
   };
-  __syncthreads();
-  int n = blockIdx.x;
-  if (n < a.N) {
-    raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, 0, SROWS, a.nsc, a.nbi, tid);
-    raw_store(ru, S, G.SP, G.Win, SROWS, tid);
-    for (int r = 0; r < 3; ++r) {
-      pload(n, r);
-      pstore(r);
-    }
-    pload(n, 3);
-  }
-  __syncthreads();
-  if (n < a.N) e_build(E, S, G, -3, 9, -3, tid);
-  __syncthreads();
+  // synchronous staging of raw rows iy0 .. iy0+nr-1 (nr <= BROWS) and E rows e0 .. iy0+nr-1
+  auto stage_sync = [&](int n, int iy0, int nr, int e0) {
+    raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, iy0, nr, a.nsc, a.nbi, tid);
+    raw_store(ru, S, G.SP, G.Win, nr, tid);
+    __syncthreads();
+    e_build(E, S, G, e0, iy0 + nr - e0, e0 - iy0, tid);
+    __syncthreads();
+  };
   // quad items: (qb, chunk) = pixels (2i + ddy, 2qb + ddx), ddy, ddx in {0, 1}, 8 channels
   const bool qact = tid < G.PW * 8;
   const int qb = tid >> 3, qc = tid & 7, c0 = qc * 8;
-  float ka[8], kc[8];
-  for (; n < a.N; n += gridDim.x) {
-    const int nnext = n + gridDim.x;
+  // y MFMA (recompute), C = W x E^T: [co][px] -- wave w: slot w >> 2, px block w & 3
+  const int yslot = wid >> 2, mb = wid & 3, hh = lane >> 5;
+  const bool yact = 32 * mb < G.Wout;
+  const int pxb = min(32 * mb + (lane & 31), G.Wout - 1);  // B column (pad lanes re-read W-1)
+  const int pxo = 32 * mb + (lane & 31);                     // the output pixel of this lane
+  __syncthreads();
+  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
+    // image prologue: E rows -3..5 (data rows 0..5 in two stagings), pooled rows 0, 1 + 2
+    pload(n, 0);
+    pstore(0);
+    pload(n, 1);
+    pstore(1);
+    pload(n, 2);
+    stage_sync(n, 0, 4, -3);
+    stage_sync(n, 4, 2, 4);
+    float ka[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      ka[j] = cf[c0 + j];
-      kc[j] = cf[SCO + c0 + j];
-    }
+    for (int j = 0; j < 8; ++j) ka[j] = cf[c0 + j];
     for (int i = 0; i < G.PH; ++i) {
       const bool last = i + 1 == G.PH;
-      // ---------------------------------------------------------------- phase A
-      int srows = 0;
-      if (!last) {
-        srows = 4;
-        raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, 4 * i + 6, 4, a.nsc, a.nbi, tid);
-      } else if (nnext < a.N) {
-        srows = SROWS;
-        raw_load<DT>(ru, a.img, img_base(nnext), G.Hin, G.Win, 0, SROWS, a.nsc, a.nbi, tid);
-      }
+      // ---------------------------------------------------------------- phase A: a dz
+      if (!last) raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, 4 * i + 6, 4, a.nsc, a.nbi, tid);
       if (qact) {
         // the quad's 4 windows: pooled rows i (+1), columns qb (+1)
         uint4 qg[4];
@@ -603,71 +600,87 @@ __global__ void __launch_bounds__(SNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
           }
           uint32_t o[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            o[k] = pack_bf2(ka[2 * k] * d[2 * k] + kc[2 * k], ka[2 * k + 1] * d[2 * k + 1] + kc[2 * k + 1]);
+          for (int k = 0; k < 4; ++k) o[k] = pack_bf2(ka[2 * k] * d[2 * k], ka[2 * k + 1] * d[2 * k + 1]);
           *reinterpret_cast<uint4*>(T + yoff(ddy, 2 * qb + ddx, qc, G.Wout)) = make_uint4(o[0], o[1], o[2], o[3]);
         }
       }
-      if (srows) raw_store(ru, S, G.SP, G.Win, srows, tid);
-      // pooled row i + 3 (loaded one pair ago) into the slot of row i - 1; load row i + 4
-      if (!last) {
-        pstore(i + 3);
-        pload(n, i + 4);
-      } else if (nnext < a.N) {
-        pload(nnext, 0);
-      }
+      // pooled row i + 2 (loaded one pair ago) into the slot of row i - 1; load row i + 3
+      pstore(i + 2);
+      pload(n, i + 3);
+      if (!last) raw_store(ru, S, G.SP, G.Win, 4, tid);
       __syncthreads();
-      // ---------------------------------------------------------------- phase B
+      // ---------------------------------------------------------------- phase B: dy
+      if (yact) {
+        const int oy = 2 * i + yslot;
+        const int rb = 2 * oy - 3;
+        f32x16 acc[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
+        const unsigned char* wa0 = Ws + (lane & 31) * SWP * 2 + 16 * hh;
+#pragma unroll
+        for (int s = 0; s < 11; ++s) {
+          const int j = 2 * s + hh;
+          int ky = j / 3;
+          const int part = j - 3 * ky;
+          if (ky > 6) ky = 6;  // k-step 10's upper half: zero weights, finite data
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(E + ring_of(rb + ky) * G.ROWB + pxb * 48 + part * 16);
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(wa0 + 32 * s);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wa0 + 32 * SWP * 2 + 32 * s);
+          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bfr, acc[0], 0, 0, 0);
+          acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bfr, acc[1], 0, 0, 0);
+        }
+        // C: col = px (lane & 31), row = co = 32 c + (r & 3) + 8 (r >> 2) + 4 hh
+        if (pxo < G.Wout) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const int co = 32 * c + 8 * g4 + 4 * hh;
+              unsigned char* tp = T + yoff(yslot, pxo, co >> 3, G.Wout) + 2 * (co & 7);
+              const uint2 t = *reinterpret_cast<const uint2*>(tp);
+              const float4 bv = *reinterpret_cast<const float4*>(cf + SCO + co);
+              const float4 cv = *reinterpret_cast<const float4*>(cf + 2 * SCO + co);
+              const float d0 = bf2f((bf16_t)(t.x & 0xffff)) + bv.x * acc[c][4 * g4 + 0] + cv.x;
+              const float d1 = bf2f((bf16_t)(t.x >> 16)) + bv.y * acc[c][4 * g4 + 1] + cv.y;
+              const float d2 = bf2f((bf16_t)(t.y & 0xffff)) + bv.z * acc[c][4 * g4 + 2] + cv.z;
+              const float d3 = bf2f((bf16_t)(t.y >> 16)) + bv.w * acc[c][4 * g4 + 3] + cv.w;
+              *reinterpret_cast<uint2*>(tp) = make_uint2(pack_bf2(d0, d1), pack_bf2(d2, d3));
+            }
+        }
+      }
       if (!last) e_build(E, S, G, 4 * i + 6, 4, 0, tid);
+      __syncthreads();
+      // ---------------------------------------------------------------- phase C: dW
       pair_wgrad(dacc, T, E, G, i, wid, lane);
       __syncthreads();
-      if (last && nnext < a.N) {
-        // the next image: E rows 0..5, pooled rows 0..2 (row 0 already loaded), 3 in flight
-        e_build(E, S, G, -3, 9, -3, tid);
-        pstore(0);
-        for (int r = 1; r < 3; ++r) {
-          pload(nnext, r);
-          pstore(r);
-        }
-        pload(nnext, 3);
-        __syncthreads();
-      }
     }
   }
   float* red = reinterpret_cast<float*>(smem);
-  __syncthreads();
   write_wslab(dacc, red, a.dslab, wid, lane);
 }
 
-// dW[co][c][ky][kx] = beta * dW + sum_g D'[g][co][k] + b[co] * sum_g H[g][co][k],
-// k = ky*24 + kx*3 + c.  One workgroup per output channel; each of the 4 lane groups sums a
-// quarter of the slabs in order, the quarters are combined in order (deterministic).
+// dW[co][c][ky][kx] = beta * dW + sum_g slab[g][co][k], k = ky*24 + kx*3 + c.  One
+// workgroup per output channel; each of the 4 lane groups sums a quarter of the slabs in
+// order, the quarters are combined in order (deterministic).
 __global__ void __launch_bounds__(256) stem_wreduce_kernel(const float* __restrict__ dslab, int GD,
-                                                           const float* __restrict__ hslab, int GH,
-                                                           const float* __restrict__ coef,
                                                            float* __restrict__ dw, float beta) {
-  __shared__ float part[2][4][SKH];
+  __shared__ float part[4][SKH];
   const int co = blockIdx.x, t = threadIdx.x, k = t & 63, gq = t >> 6;
 #pragma unroll
-  for (int src = 0; src < 2; ++src) {
-    const float* sl = src ? hslab : dslab;
-    const int G = src ? GH : GD;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      float s = 0.f;
-      for (int g = gq; g < G; g += 4) s += sl[((long long)g * SCO + co) * SKH + k + 64 * u];
-      part[src][gq][k + 64 * u] = s;
-    }
+  for (int u = 0; u < 3; ++u) {
+    float s = 0.f;
+    for (int g = gq; g < GD; g += 4) s += dslab[((long long)g * SCO + co) * SKH + k + 64 * u];
+    part[gq][k + 64 * u] = s;
   }
   __syncthreads();
-  const float b = coef[SCO + co];
   for (int e = t; e < 147; e += 256) {
     const int ky = e / 21, rem = e - 21 * ky, kx = rem / 3, c = rem - 3 * kx;
     const int kk = ky * 24 + kx * 3 + c;
-    const float d = ((part[0][0][kk] + part[0][1][kk]) + part[0][2][kk]) + part[0][3][kk];
-    const float h = ((part[1][0][kk] + part[1][1][kk]) + part[1][2][kk]) + part[1][3][kk];
+    const float d = ((part[0][kk] + part[1][kk]) + part[2][kk]) + part[3][kk];
     float* o = dw + ((co * 3 + c) * 7 + ky) * 7 + kx;
-    *o = (beta != 0.f ? beta * *o : 0.f) + d + b * h;
+    *o = (beta != 0.f ? beta * *o : 0.f) + d;
   }
 }
 
@@ -699,7 +712,8 @@ static StemGeo stem_geo(int Hin, int Win) {
 
 bool stem_fused_supported(int Hin, int Win) {
   // Wout a multiple of 16 (wgrad m-steps) and <= 128 (4 M-blocks); rows in 4-element units
-  // (LDS: the backward's 13 E rows + tile + staging + pooled-row ring fit 160 KB up to W 224)
+  // (LDS: the backward's weights + 13 E rows + tile + staging + pooled-row ring fit 160 KB
+  // up to W 224: 160,704 B there)
   return Hin >= 8 && Hin % 4 == 0 && Win % 32 == 0 && Win <= 224;
 }
 
@@ -708,8 +722,8 @@ static size_t fwd_smem(const StemGeo& G) {
          (size_t)SROWS * G.SP * 2;
 }
 static size_t bwd_smem(const StemGeo& G) {
-  return (size_t)RING * G.ROWB + (size_t)2 * G.Wout * 128 + (size_t)SROWS * G.SP * 2 +
-         (size_t)PRING * G.PW * SCO * 3 + 2 * SCO * 4;
+  return (size_t)SCO * SWP * 2 + (size_t)RING * G.ROWB + (size_t)2 * G.Wout * 128 +
+         (size_t)BROWS * G.SP * 2 + (size_t)PRING * G.PW * SCO * 3 + 3 * SCO * 4;
 }
 
 int stem_fused_grid(int N) {
@@ -724,8 +738,8 @@ int stem_fused_grid(int N) {
 
 void stem_fwd_fused(const void* img, int dtype, const long long* idx, const float* nsc,
                     const float* nbi, const bf16_t* wk, const float* gamma, bf16_t* pext,
-                    uint8_t* code, float* stats, float* hslab, int N, int nimg, int Hin, int Win,
-                    int grid, hipStream_t st) {
+                    uint8_t* code, float* stats, int N, int nimg, int Hin, int Win, int grid,
+                    hipStream_t st) {
   StemFwdArgs a;
   a.img = img;
   a.idx = idx;
@@ -738,7 +752,6 @@ void stem_fwd_fused(const void* img, int dtype, const long long* idx, const floa
   a.pext = pext;
   a.code = code;
   a.stats = stats;
-  a.hslab = hslab;
   a.N = N;
   a.nimg = nimg;
   a.G = stem_geo(Hin, Win);
@@ -764,8 +777,9 @@ void stem_pool_apply(const bf16_t* pext, uint8_t* code, const float* scale, cons
 }
 
 void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const float* nsc,
-                     const float* nbi, const bf16_t* pdy, const uint8_t* code, const float* coef,
-                     float* dslab, int N, int nimg, int Hin, int Win, int grid, hipStream_t st) {
+                     const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code,
+                     const float* coef, float* dslab, int N, int nimg, int Hin, int Win, int grid,
+                     hipStream_t st) {
   StemBwdArgs2 a;
   a.img = img;
   a.idx = idx;
@@ -773,6 +787,7 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
     a.nsc[c] = nsc[c];
     a.nbi[c] = nbi[c];
   }
+  a.wk = wk;
   a.pdy = pdy;
   a.code = code;
   a.coef = coef;
@@ -793,9 +808,8 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
   DM_CHECK(hipGetLastError());
 }
 
-void stem_wreduce(const float* dslab, int GD, const float* hslab, int GH, const float* coef,
-                  float* dw, float beta, hipStream_t st) {
-  stem_wreduce_kernel<<<SCO, 256, 0, st>>>(dslab, GD, hslab, GH, coef, dw, beta);
+void stem_wreduce(const float* dslab, int GD, float* dw, float beta, hipStream_t st) {
+  stem_wreduce_kernel<<<SCO, 256, 0, st>>>(dslab, GD, dw, beta);
   DM_CHECK(hipGetLastError());
 }
 

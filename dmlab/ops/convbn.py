@@ -255,9 +255,8 @@ def stem_fused_ok(layer, x):
 
 
 def _stem_fused_fwd(layer, x, ctx, train):
-    """Fused stem forward: pooled BN-input extremum + window codes + BN statistics (+ the
-    weight-gradient helper H when training) in one kernel, then BN + ReLU on the pooled
-    tensor.  The conv output is never written."""
+    """Fused stem forward: pooled BN-input extremum + window codes + BN statistics in one
+    kernel, then BN + ReLU on the pooled tensor.  The conv output is never written."""
     from dmlab.data import input_affine
 
     L = lib()
@@ -276,9 +275,7 @@ def _stem_fused_fwd(layer, x, ctx, train):
     shift = torch.empty(64, **f32)
     use_batch = layer.training
     stats = torch.empty(grid * 128, **f32) if use_batch else None
-    hslab = torch.empty(grid * 64 * L.stem_slab_cols(), **f32) if (use_batch and train) else None
-    L.stem_fwd_fused(img, idx, nsc, nbi, wk, layer.bn_weight.detach(), pext, code, stats, hslab,
-                     grid)
+    L.stem_fwd_fused(img, idx, nsc, nbi, wk, layer.bn_weight.detach(), pext, code, stats, grid)
     M = B * (H // 2) * (W // 2)
     if use_batch:
         mean = torch.empty(64, **f32)
@@ -295,15 +292,16 @@ def _stem_fused_fwd(layer, x, ctx, train):
     out = empty_nhwc(B, PH, PW, 64, img)
     L.stem_pool_apply(pext, code if train else None, scale, shift, out)
     if train:
-        ctx.update(fused_stem=True, img=img, gidx=idx, nsc=nsc, nbi=nbi, yarg=pext, idx=code,
-                   mean=mean, invstd=invstd, scale=scale, shift=shift, hslab=hslab, hgrid=grid,
-                   has_res=False, first=True, s2d=False, pre=None, y=pext, x=None, M=M)
+        ctx.update(fused_stem=True, img=img, gidx=idx, nsc=nsc, nbi=nbi, wk=wk, yarg=pext,
+                   idx=code, mean=mean, invstd=invstd, scale=scale, shift=shift, has_res=False,
+                   first=True, s2d=False, pre=None, y=pext, x=None, M=M)
     return out
 
 
 def _stem_fused_bwd(layer, dout, ctx):
-    """Fused stem backward: BN-backward coefficients from the pooled-domain sums, the
-    (a*dz + cc) weight gradient over the raw input, and dW = that + b * H."""
+    """Fused stem backward: BN-backward coefficients from the pooled-domain sums, then the
+    weight gradient of dy = a*dz + b*y + cc with y recomputed from the raw input (never
+    stored), reduced in fixed order into the OIHW gradient."""
     L = lib()
     dout = dout.contiguous()
     pext, code = ctx["yarg"], ctx["idx"]
@@ -320,11 +318,11 @@ def _stem_fused_bwd(layer, dout, ctx):
     f32 = dict(device=dout.device, dtype=torch.float32)
     work = torch.empty(L.bn_bwd_work(ctx["M"], 64), **f32)
     dslab = torch.empty(grid * 64 * L.stem_slab_cols(), **f32)
-    L.stem_bwd_fused2(ctx["img"], ctx["gidx"], ctx["nsc"], ctx["nbi"], dout, code, ctx["mean"],
-                      ctx["invstd"], layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
-                      layer.grad_slot("bn_bias"), acc, pre_sums["pre_slab"],
-                      pre_sums["pre_rows"], ctx["hslab"], ctx["hgrid"],
-                      layer.grad_slot("weight"), acc, work, dslab, grid)
+    L.stem_bwd_fused2(ctx["img"], ctx["gidx"], ctx["nsc"], ctx["nbi"], ctx["wk"], dout, code,
+                      ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
+                      layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,
+                      pre_sums["pre_slab"], pre_sums["pre_rows"], layer.grad_slot("weight"), acc,
+                      work, dslab, grid)
     return None
 
 

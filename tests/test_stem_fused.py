@@ -1,6 +1,6 @@
 """The K-dense fused ResNet stem (csrc/stem_fused.hip) vs float64 PyTorch references:
 conv statistics, the pooled BN-input extremum and its window codes (both BN-scale signs),
-the weight-gradient helper H, and the whole stem backward (conv + BN + ReLU + max-pool)
+and the whole stem backward (conv + BN + ReLU + max-pool, y recomputed in the kernel)
 against autograd; u8 / fp32 / bf16 inputs through a gathered batch index."""
 import pytest
 import torch
@@ -41,10 +41,9 @@ def _run_fwd(img, idx, w, gamma, train=True):
     code = torch.empty(B, H // 4, H // 4, 64, device=dev, dtype=torch.uint8)
     grid = L.stem_fused_grid(B)
     stats = torch.empty(grid * 128, device=dev) if train else None
-    hslab = torch.empty(grid * 64 * L.stem_slab_cols(), device=dev) if train else None
     sc, bi = input_affine(img.dtype)
-    L.stem_fwd_fused(img, idx, sc, bi, wk, gamma, pext, code, stats, hslab, grid)
-    return pext, code, stats, hslab, grid
+    L.stem_fwd_fused(img, idx, sc, bi, wk, gamma, pext, code, stats, grid)
+    return pext, code, stats, wk, grid
 
 
 def _codes_ref(z):
@@ -67,7 +66,7 @@ def test_stem_fused_forward(dev, dtype, H):
     w = torch.randn(64, 3, 7, 7, device=dev) * 0.08
     gamma = torch.randn(64, device=dev)
     gamma[3] = 0.0  # either extremum is right for a zero scale
-    pext, code, stats, hslab, grid = _run_fwd(img, idx, w, gamma)
+    pext, code, stats, wk, grid = _run_fwd(img, idx, w, gamma)
     xb = _x_bf16(img.index_select(0, idx)).cpu()
     wb = w.to(torch.bfloat16).double().cpu()
     y = F.conv2d(xb, wb, stride=2, padding=3)  # float64 reference of the conv
@@ -85,14 +84,6 @@ def test_stem_fused_forward(dev, dtype, H):
     cref = cref.permute(0, 2, 3, 1)
     agree = (code.cpu().long() == cref).double().mean().item()
     assert agree > 0.995, agree  # ties / 1-ulp rounding differences may pick another pixel
-    # H[co][k] = sum_m y_bf16[m][co] * x_col[m][k]
-    xcol = F.unfold(xb, 7, padding=3, stride=2)  # [B, 3*49 (c, ky, kx), L]
-    href = torch.einsum("bcl,bkl->ck", yb.flatten(2), xcol)
-    hs = hslab.view(grid, 64, lib().stem_slab_cols()).double().sum(0).cpu()
-    ky, kx, c = torch.meshgrid(torch.arange(7), torch.arange(7), torch.arange(3), indexing="ij")
-    hk = hs[:, (ky * 24 + kx * 3 + c).flatten()]          # kernel order (ky, kx, c)
-    hr = href[:, (c * 49 + ky * 7 + kx).flatten()]       # unfold order (c, ky, kx)
-    assert ((hk - hr).norm() / hr.norm()).item() < 2e-3
 
 
 def test_stem_pool_apply_and_masked_codes(dev):
@@ -104,8 +95,9 @@ def test_stem_pool_apply_and_masked_codes(dev):
     out = torch.empty_like(pext)
     c2 = code.clone()
     lib().stem_pool_apply(pext, c2, scale, shift, out)
-    z = pext.float() * scale + shift
-    torch.testing.assert_close(out.float(), z.clamp_min(0).to(torch.bfloat16).float(), rtol=0, atol=0)
+    z = pext.float() * scale + shift  # (the kernel fuses the multiply-add: 1 bf16 ulp at most)
+    torch.testing.assert_close(out.float(), z.clamp_min(0).to(torch.bfloat16).float(),
+                               rtol=2 ** -7, atol=1e-6)
     assert torch.equal(c2, torch.where(z > 0, code, torch.full_like(code, 15)))
 
 
@@ -122,7 +114,7 @@ def test_stem_fused_backward_matches_autograd(dev, dtype, H):
     w = torch.randn(64, 3, 7, 7, device=dev) * 0.08
     gamma = torch.randn(64, device=dev)
     beta = torch.randn(64, device=dev) * 0.2
-    pext, code, stats, hslab, grid = _run_fwd(img, idx, w, gamma)
+    pext, code, stats, wk, grid = _run_fwd(img, idx, w, gamma)
     M = B * (H // 2) ** 2
     f = dict(device=dev, dtype=torch.float32)
     scale, shift, mean, invstd = (torch.empty(64, **f) for _ in range(4))
@@ -139,8 +131,8 @@ def test_stem_fused_backward_matches_autograd(dev, dtype, H):
     work = torch.empty(L.bn_bwd_work(M, 64), **f)
     dslab = torch.empty(L.stem_fused_grid(B) * 64 * L.stem_slab_cols(), **f)
     sc, bi = input_affine(img.dtype)
-    L.stem_bwd_fused2(img, idx, sc, bi, g, code, mean, invstd, gamma, dgamma, dbeta, 0.0, part,
-                      rows, hslab, grid, dw, 0.0, work, dslab, L.stem_fused_grid(B))
+    L.stem_bwd_fused2(img, idx, sc, bi, wk, g, code, mean, invstd, gamma, dgamma, dbeta, 0.0,
+                      part, rows, dw, 0.0, work, dslab, L.stem_fused_grid(B))
     # float64 autograd reference
     xb = _x_bf16(img.index_select(0, idx)).cpu()
     wr = w.to(torch.bfloat16).double().cpu().requires_grad_(True)

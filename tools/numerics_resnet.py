@@ -28,7 +28,7 @@ import torch  # noqa: E402
 import torch.nn.functional as F  # noqa: E402
 
 
-def run(batch, steps, res, nbatches=4, lr=0.1, seed=0, classes=1000, log=print):
+def run(batch, steps, res, nbatches=4, lr=0.1, seed=0, classes=1000, log=print, table=None):
     from dmlab.models import ResNet18
     from dmlab.nn import cross_entropy
     from dmlab.optim import SGD
@@ -65,6 +65,9 @@ def run(batch, steps, res, nbatches=4, lr=0.1, seed=0, classes=1000, log=print):
             if s in (0, steps - 1):  # gradient norms of the first / last step, before the update
                 rec[k + "_gnorm"] = {n: float(p.grad.float().norm())
                                      for n, p in m.named_parameters() if p.grad is not None}
+            if s == 0 and table is not None:  # full step-0 gradients for the per-layer table
+                table[k] = {n: p.grad.detach().float().clone()
+                            for n, p in m.named_parameters() if p.grad is not None}
             opts[k].step()
             rec[k] = float(loss.detach())
         hist.append(rec)
@@ -118,6 +121,19 @@ def summarize(models, hist):
     }
 
 
+def layer_table(table):
+    """Per parameter, step 0 (same weights and batch for all three): the full-tensor relative
+    error ||g - g_fp32|| / ||g_fp32|| of native and autocast, and their ratio."""
+    rows = []
+    for n, ref in table["fp32"].items():
+        den = float(ref.norm()) + 1e-30
+        en = float((table["native"][n] - ref).norm()) / den
+        ea = float((table["autocast"][n] - ref).norm()) / den
+        rows.append({"param": n, "native_rel": round(en, 5), "autocast_rel": round(ea, 5),
+                     "ratio": round(en / max(ea, 1e-12), 3)})
+    return rows
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
@@ -125,6 +141,8 @@ def main():
     ap.add_argument("--res", type=int, default=224)
     ap.add_argument("--nbatches", type=int, default=4)
     ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--table", action="store_true",
+                    help="print the per-parameter step-0 gradient error table (full tensors)")
     a = ap.parse_args()
     # first steps of the PyTorch backends can sit in MIOpen's kernel search for minutes at
     # b1024: keep a heartbeat on stderr so a supervising runner does not take it as hung
@@ -139,7 +157,19 @@ def main():
             print(f"[numerics] alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
 
     threading.Thread(target=beat, daemon=True).start()
-    models, hist = run(a.batch, a.steps, a.res, a.nbatches, a.lr)
+    table = {} if a.table else None
+    models, hist = run(a.batch, a.steps, a.res, a.nbatches, a.lr, table=table)
+    if table is not None:
+        rows = layer_table(table)
+        del table
+        for r in rows:
+            print(json.dumps(r), flush=True)
+        med = sorted(r["native_rel"] for r in rows)[len(rows) // 2]
+        meda = sorted(r["autocast_rel"] for r in rows)[len(rows) // 2]
+        worst = max(rows, key=lambda r: r["native_rel"])
+        print(json.dumps({"table_summary": {"median_native_rel": med, "median_autocast_rel": meda,
+                                            "median_ratio": round(med / max(meda, 1e-12), 3),
+                                            "worst_native": worst}}), flush=True)
     s = summarize(models, hist)
     s.update(batch=a.batch, steps=a.steps, res=a.res, lr=a.lr, nbatches=a.nbatches)
     print(json.dumps({"summary": s}), flush=True)
