@@ -685,7 +685,7 @@ void stem_fwd_fused(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<d
   TORCH_CHECK(pext.size(1) == v.H / 4 && pext.size(2) == v.W / 4 && pext.size(3) == 64,
               "pext must be [B, H/4, W/4, 64]");
   TORCH_CHECK(code.is_cuda() && code.scalar_type() == at::kByte && code.is_contiguous() &&
-              code.numel() == pext.numel(), "code must be uint8 like pext");
+              code.numel() * 2 == pext.numel(), "code must be uint8 [N][PH][PW][32] (4-bit codes)");
   TORCH_CHECK(wk.is_cuda() && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
               wk.numel() == 64 * dm::stem_wk_cols(), "wk must be packed [64][176] bf16");
   need_f32(gamma, "gamma", 64);
@@ -700,24 +700,32 @@ void stem_fwd_fused(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<d
                      (int)grid, cur_stream());
 }
 
+// out = relu(scale * pext + shift); with code4: the backward's 4-bit window codes (15 where
+// the output is 0) from the forward's byte codes
 void stem_pool_apply(at::Tensor pext, c10::optional<at::Tensor> code, at::Tensor scale,
-                     at::Tensor shift, at::Tensor out) {
+                     at::Tensor shift, at::Tensor out, c10::optional<at::Tensor> code4) {
   need_bf16_nhwc(pext, "pext");
   need_bf16_nhwc(out, "out");
   TORCH_CHECK(out.numel() == pext.numel() && pext.size(3) == 64, "pooled shapes");
-  if (code.has_value())
-    TORCH_CHECK(code->scalar_type() == at::kByte && code->numel() == pext.numel(), "code");
+  TORCH_CHECK(code.has_value() == code4.has_value(), "code and code4 go together");
+  if (code.has_value()) {
+    TORCH_CHECK(code->is_cuda() && code->scalar_type() == at::kByte && code->is_contiguous() &&
+                    code->numel() * 2 == pext.numel(), "code must be uint8 [N][PH][PW][32]");
+    TORCH_CHECK(code4->is_cuda() && code4->scalar_type() == at::kByte && code4->is_contiguous() &&
+                    code4->numel() * 2 == pext.numel(), "code4 must be uint8 [N][PH][PW][32]");
+  }
   need_f32(scale, "scale", 64);
   need_f32(shift, "shift", 64);
   const DeviceGuard guard(pext.device());
-  dm::stem_pool_apply(bp(pext), code ? (uint8_t*)code->data_ptr() : nullptr, fp(scale), fp(shift),
-                      bp(out), pext.numel(), cur_stream());
+  dm::stem_pool_apply(bp(pext), code ? (const uint8_t*)code->data_ptr() : nullptr, fp(scale),
+                      fp(shift), bp(out), code4 ? (uint8_t*)code4->data_ptr() : nullptr,
+                      pext.numel(), cur_stream());
 }
 
 // BN-backward coefficients from the pooled-domain sums (pre_slab), the weight gradient of
 // dy = a dz + b y + cc (y recomputed in the kernel) into dslab, then dW = beta dW + sum dslab
 void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<double> nsc,
-                     std::vector<double> nbi, at::Tensor wk, at::Tensor pdy, at::Tensor code,
+                     std::vector<double> nbi, at::Tensor wk, at::Tensor pdy, at::Tensor code4,
                      at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
                      at::Tensor dbeta, double gbeta, at::Tensor pre_slab, int64_t pre_rows,
                      at::Tensor dw, double wbeta, at::Tensor work, at::Tensor dslab, int64_t grid) {
@@ -726,7 +734,8 @@ void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<
   need_bf16_nhwc(pdy, "pdy");
   const int B = pdy.size(0), C = 64;
   TORCH_CHECK(pdy.size(1) == v.H / 4 && pdy.size(2) == v.W / 4 && pdy.size(3) == C, "pdy shape");
-  TORCH_CHECK(code.scalar_type() == at::kByte && code.numel() == pdy.numel(), "code");
+  TORCH_CHECK(code4.is_cuda() && code4.scalar_type() == at::kByte && code4.is_contiguous() &&
+                  code4.numel() * 2 == pdy.numel(), "code4 must be uint8 [N][PH][PW][32]");
   const long long M = (long long)B * (v.H / 2) * (v.W / 2);
   need_f32(work, "work", bn_bwd_work(M, C));
   need_f32(pre_slab, "pre_slab", pre_rows * 2 * C);
@@ -745,7 +754,7 @@ void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<
                   v.H / 4, v.W / 4, 3, 2, 1, nullptr, nullptr, fp(work), st, fp(pre_slab),
                   (int)pre_rows, nullptr);
   dm::stem_bwd_fused2(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(wk), bp(pdy),
-                      (const uint8_t*)code.data_ptr(), fp(work), fp(dslab), B, v.N, v.H, v.W,
+                      (const uint8_t*)code4.data_ptr(), fp(work), fp(dslab), B, v.N, v.H, v.W,
                       (int)grid, st);
   dm::stem_wreduce(fp(dslab), (int)grid, fp(dw), (float)wbeta, st);
 }
@@ -817,9 +826,9 @@ void register_resnet(pybind11::module_& m) {
         py::arg("nbi"), py::arg("wk"), py::arg("gamma"), py::arg("pext"), py::arg("code"),
         py::arg("stats"), py::arg("grid"));
   m.def("stem_pool_apply", &stem_pool_apply, py::arg("pext"), py::arg("code"), py::arg("scale"),
-        py::arg("shift"), py::arg("out"));
+        py::arg("shift"), py::arg("out"), py::arg("code4") = py::none());
   m.def("stem_bwd_fused2", &stem_bwd_fused2, py::arg("img"), py::arg("idx"), py::arg("nsc"),
-        py::arg("nbi"), py::arg("wk"), py::arg("pdy"), py::arg("code"), py::arg("mean"),
+        py::arg("nbi"), py::arg("wk"), py::arg("pdy"), py::arg("code4"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("dgamma"), py::arg("dbeta"),
         py::arg("gbeta"), py::arg("pre_slab"), py::arg("pre_rows"), py::arg("dw"),
         py::arg("wbeta"), py::arg("work"), py::arg("dslab"), py::arg("grid"));

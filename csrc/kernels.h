@@ -102,10 +102,10 @@ void stem_fwd_fused(const void* img, int dtype, const long long* idx, const floa
                     const float* nbi, const bf16_t* wk, const float* gamma, bf16_t* pext,
                     uint8_t* code, float* stats, int N, int nimg, int Hin, int Win, int grid,
                     hipStream_t st);
-void stem_pool_apply(const bf16_t* pext, uint8_t* code, const float* scale, const float* shift,
-                     bf16_t* out, long long n, hipStream_t st);
+void stem_pool_apply(const bf16_t* pext, const uint8_t* code, const float* scale,
+                     const float* shift, bf16_t* out, uint8_t* code4, long long n, hipStream_t st);
 void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const float* nsc,
-                     const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code,
+                     const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code4,
                      const float* coef, float* dslab, int N, int nimg, int Hin, int Win, int grid,
                      hipStream_t st);
 void stem_wreduce(const float* dslab, int GD, float* dw, float beta, hipStream_t st);

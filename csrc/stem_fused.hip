@@ -4,8 +4,9 @@
 // Reference: the stem is not in the reference (SURVEY §2.5 "Extensions required by
 // BASELINE.json": ResNet-18-shaped CNN); it replaces cuDNN conv + BN + ReLU + max-pool.
 //
-// Forward (stem_fwd_kernel), one persistent 512-thread workgroup per CU walking whole images,
-// one conv-row PAIR (2i, 2i+1) per step:
+// Forward (stem_fwd_kernel), one persistent 768-thread workgroup per CU walking whole images,
+// one conv-row PAIR (2i, 2i+1) per step, warp-specialised: 4 MFMA waves, 8 VALU waves (raw
+// staging, E expansion, pooling), the two kinds a step apart on double-buffered tiles:
 //
 //  * K-dense operand.  Input row iy is expanded once in LDS into E[iy][ox][24]: the 7 x 3
 //    (kx, c) taps of output column ox (21 values + 3 zero pad, 48 B).  The A fragment of
@@ -36,6 +37,10 @@
 // work instead.  (Splitting dW = sum (a dz + cc) x_col + b * sum y x_col was built first and
 // rejected: the bf16 rounding of the large per-channel constant cc does not cancel against
 // b * sum y x_col -- 7-90 % gradient error on inputs with a large mean.)
+// Warp-specialised like the forward: 8 VALU waves do (1) and the E staging of pair i while the
+// 4 MFMA waves (their conv weights resident in registers) do (2) and (3) of pair i-1; the
+// window codes travel as 4-bit nibbles (the pooled-row ring then fits LDS beside the ring,
+// two tiles and the staging rows).
 //  stem_wreduce_kernel sums the per-workgroup slabs in fixed order into the OIHW gradient.
 #include "common.h"
 #include "igemm_common.h"
@@ -45,14 +50,10 @@ namespace dm {
 
 namespace {
 
-constexpr int SNT = 512;    // threads per workgroup (8 waves)
 constexpr int SCO = 64;     // output channels
 constexpr int SKP = 176;    // packed weight row: 7 ky x 24 + 8 pad
-constexpr int SWP = 184;    // weight row pitch in LDS (368 B: conflict-free B-fragment reads)
 constexpr int SKH = 192;    // H / D' columns per slab row (6 k-blocks of 32)
 constexpr int RING = 13;    // E-row ring
-constexpr int SROWS = 6;    // raw rows staged at once (image prologue: rows 0..5)
-constexpr int UPT = 3;      // raw 4-element units per thread per staging (<= 6 x 3*256/4 / 512)
 
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef unsigned int nt4 __attribute__((ext_vector_type(4)));
@@ -74,88 +75,117 @@ struct RawUnit {
 // E-ring row of input row iy (iy >= -5)
 __device__ __forceinline__ int ring_of(int iy) { return (iy + 13 * 8) % RING; }
 
-template <int DT>
-__device__ __forceinline__ void raw_load(RawUnit (&u)[UPT], const void* img, long long rowbase_elems,
-                                         int Hin, int Win, int iy0, int nrows, const float* nsc,
-                                         const float* nbi, int tid) {
-  // units of 4 consecutive row elements; unit e of the block: row e / (3W/4), k = e % (3W/4)
-  const int upr = 3 * Win / 4;
-  const int total = nrows * upr;
+// Division-free staging maps, computed once per thread (the loops then only add offsets).
+// Raw rows: a group of NT threads loads up to 4 rows = 3W units of 4 elements; thread t owns
+// units t, t + NT, ... (at most RU of them).  E rows: thread t < 3 Wout owns chunk (ox, part)
+// = (t / 3, t % 3) of every row it builds.
+template <int NT, int RU>
+struct RawMap {
+  int r[RU], k[RU];  // row within the staging, unit within the row (r = -1: none)
+  __device__ __forceinline__ void init(int t, int Win) {
+    const int upr = 3 * Win / 4;
 #pragma unroll
-  for (int t = 0; t < UPT; ++t) {
-    const int e = tid + SNT * t;
-    const int r = e / upr, k = e - r * upr;
-    const int iy = iy0 + r;
-    float x[4] = {0.f, 0.f, 0.f, 0.f};
-    if (e < total && iy >= 0 && iy < Hin) {
-      const long long off = rowbase_elems + (long long)iy * Win * 3 + 4LL * k;
-      if (DT == 0) {
-        const float4 f = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(img) + off);
-        x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
-      } else if (DT == 1) {
-        const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(img) + off);
-        x[0] = bf2f((bf16_t)(w.x & 0xffff)); x[1] = bf2f((bf16_t)(w.x >> 16));
-        x[2] = bf2f((bf16_t)(w.y & 0xffff)); x[3] = bf2f((bf16_t)(w.y >> 16));
-      } else {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(img) + off);
-        x[0] = (float)(w & 0xff); x[1] = (float)((w >> 8) & 0xff);
-        x[2] = (float)((w >> 16) & 0xff); x[3] = (float)(w >> 24);
-      }
-      // channel of element 4k + j is (4k + j) % 3 = (k + j) % 3
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = (k + j) % 3;
-        x[j] = x[j] * nsc[c] + nbi[c];
-      }
+    for (int u = 0; u < RU; ++u) {
+      const int e = t + NT * u;
+      r[u] = e < 4 * upr ? e / upr : -1;
+      k[u] = e - (e / upr) * upr;
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) u[t].v[j] = x[j];
   }
-}
-
-// S[row r][t], t = f + 9 (9 zero pad elements on the left, >= 15 on the right)
-__device__ __forceinline__ void raw_store(const RawUnit (&u)[UPT], bf16_t* S, int SP, int Win,
-                                          int nrows, int tid) {
-  const int upr = 3 * Win / 4;
-  const int total = nrows * upr;
+  template <int DT>
+  __device__ __forceinline__ void load(RawUnit (&ru)[RU], const void* img, long long rowbase, int Hin,
+                                       int Win, int iy0, int nrows, const float* nsc,
+                                       const float* nbi) const {
 #pragma unroll
-  for (int t = 0; t < UPT; ++t) {
-    const int e = tid + SNT * t;
-    if (e >= total) continue;
-    const int r = e / upr, k = e - r * upr;
-    bf16_t* p = S + r * SP + 4 * k + 9;  // odd element index
-    p[0] = f2bf(u[t].v[0]);
-    *reinterpret_cast<uint32_t*>(p + 1) = pack_bf2(u[t].v[1], u[t].v[2]);
-    p[3] = f2bf(u[t].v[3]);
-  }
-}
-
-// E rows iy0 .. iy0+nrows-1 from S rows srow0.. (rows outside [0, Hin) are written as zeros)
-__device__ __forceinline__ void e_build(unsigned char* E, const bf16_t* S, const StemGeo& G, int iy0,
-                                        int nrows, int srow0, int tid) {
-  const int per_row = 3 * G.Wout;
-  const int total = nrows * per_row;
-  for (int e = tid; e < total; e += SNT) {
-    const int q = e / per_row, rem = e - q * per_row;
-    const int ox = rem / 3, part = rem - ox * 3;
-    const int iy = iy0 + q;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (iy >= 0 && iy < G.Hin) {
-      const uint32_t* s = reinterpret_cast<const uint32_t*>(S + (srow0 + q) * G.SP + 6 * ox + 8 * part);
-      v = make_uint4(s[0], s[1], s[2], s[3]);
-      if (part == 2) {  // elements 21..23 of the expanded row are the zero pad
-        v.z &= 0xffffu;
-        v.w = 0;
+    for (int u = 0; u < RU; ++u) {
+      float x[4] = {0.f, 0.f, 0.f, 0.f};
+      const int iy = iy0 + r[u];
+      if (r[u] >= 0 && r[u] < nrows && iy >= 0 && iy < Hin) {
+        const long long off = rowbase + (long long)iy * Win * 3 + 4LL * k[u];
+        if (DT == 0) {
+          const float4 f = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(img) + off);
+          x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
+        } else if (DT == 1) {
+          const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(img) + off);
+          x[0] = bf2f((bf16_t)(w.x & 0xffff)); x[1] = bf2f((bf16_t)(w.x >> 16));
+          x[2] = bf2f((bf16_t)(w.y & 0xffff)); x[3] = bf2f((bf16_t)(w.y >> 16));
+        } else {
+          const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(img) + off);
+          x[0] = (float)(w & 0xff); x[1] = (float)((w >> 8) & 0xff);
+          x[2] = (float)((w >> 16) & 0xff); x[3] = (float)(w >> 24);
+        }
+        const int c0 = k[u] % 3;  // channel of element 4k + j is (k + j) % 3
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = (c0 + j) % 3;
+          x[j] = x[j] * nsc[c] + nbi[c];
+        }
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ru[u].v[j] = x[j];
     }
-    *reinterpret_cast<uint4*>(E + ring_of(iy) * G.ROWB + ox * 48 + part * 16) = v;
   }
+  __device__ __forceinline__ void store(const RawUnit (&ru)[RU], bf16_t* S, int SP, int nrows) const {
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      if (r[u] < 0 || r[u] >= nrows) continue;
+      bf16_t* p = S + r[u] * SP + 4 * k[u] + 9;  // odd element index
+      p[0] = f2bf(ru[u].v[0]);
+      *reinterpret_cast<uint32_t*>(p + 1) = pack_bf2(ru[u].v[1], ru[u].v[2]);
+      p[3] = f2bf(ru[u].v[3]);
+    }
+  }
+};
+
+struct EMap {
+  bool act;
+  int soff, eoff;  // S element offset 6 ox + 8 part, E byte offset 48 ox + 16 part
+  int part;
+  __device__ __forceinline__ void init(int t, int Wout) {
+    act = t < 3 * Wout;
+    const int ox = t / 3;
+    part = t - 3 * ox;
+    soff = 6 * ox + 8 * part;
+    eoff = 48 * ox + 16 * part;
+  }
+  // E rows iy0 .. iy0 + nrows - 1; S row of iy is srow0 + (iy - iy0) (rows outside [0, Hin):
+  // zeros, no S read)
+  __device__ __forceinline__ void build(unsigned char* E, const bf16_t* S, const StemGeo& G, int iy0,
+                                        int nrows, int srow0) const {
+    if (!act) return;
+    for (int q = 0; q < nrows; ++q) {
+      const int iy = iy0 + q;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (iy >= 0 && iy < G.Hin) {
+        const uint32_t* sp = reinterpret_cast<const uint32_t*>(S + (srow0 + q) * G.SP + soff);
+        v = make_uint4(sp[0], sp[1], sp[2], sp[3]);
+        if (part == 2) {  // elements 21..23 of the expanded row are the zero pad
+          v.z &= 0xffffu;
+          v.w = 0;
+        }
+      }
+      *reinterpret_cast<uint4*>(E + ring_of(iy) * G.ROWB + eoff) = v;
+    }
+  }
+};
+
+// Window code of pooling-window position (kh, kw): (2 - kh) << 2 | (2 - kw), the tie-break
+// rank of the forward's integer max (largest rank = first in PyTorch's scan order); 15 =
+// no gradient (the BN+ReLU output is 0).  Channel 2k in the low nibble of byte k.
+__host__ __device__ constexpr unsigned wcode(int kh, int kw) { return (unsigned)((2 - kh) << 2 | (2 - kw)); }
+
+// monotone 16-bit key of a bf16 bit pattern (signed int16 order = float order); involution
+__device__ __forceinline__ uint32_t mono2(uint32_t w) {  // two packed bf16 -> two keys
+  const uint32_t s = (w >> 15) & 0x00010001u;
+  return w ^ (s * 0x7fffu);
 }
 
-// Y-tile chunk swizzle: [2 slots][Wout px][8 chunks of 8 channels], chunk ^ (((px >> 1) & 1) << 2)
-// -> the 4-row x 32-channel transposed reads of the wgrad MFMAs are conflict-free
+// Y-tile chunk swizzle: [2 slots][Wout px][8 chunks of 8 channels], chunk ^ f(px) with
+// f = ((px >> 1) & 1) << 2 | ((px >> 2) & 3): the 4-row x 32-channel transposed reads of the
+// wgrad MFMAs stay conflict-free (bit 2 alternates over same-parity rows) and the 32-pixel
+// column accesses of the MFMA epilogues spread over all 8 chunk positions (2-way, the
+// minimum for 8-byte lanes; bit 2 alone left them 8-way)
 __device__ __forceinline__ int yoff(int slot, int px, int c8, int Wout) {
-  return ((slot * Wout + px) * 8 + (c8 ^ (((px >> 1) & 1) << 2))) * 16;
+  return ((slot * Wout + px) * 8 + (c8 ^ ((((px >> 1) & 1) << 2) | ((px >> 2) & 3)))) * 16;
 }
 
 // The wgrad MFMAs of one conv-row pair: acc[kb] (32 co x 32 k, 3 k-blocks per wave) +=
@@ -170,7 +200,9 @@ __device__ __forceinline__ void pair_wgrad(f32x16 (&acc)[3], const unsigned char
   const int oy = 2 * i + slot;
   // A: rows m = 16t + 4h + q (+8), channels co = 32cb + 16(g&1) + 4p .. +3
   const int c8 = 4 * cb + 2 * (g & 1) + (p >> 1);
+  // rows m and m + 8 (the swizzle is invariant under m + 16, not m + 8)
   const unsigned char* ta = T + yoff(slot, 4 * h + q, c8, G.Wout) + 8 * (p & 1);
+  const unsigned char* ta8 = T + yoff(slot, 4 * h + q + 8, c8, G.Wout) + 8 * (p & 1);
   // B: rows m (same), columns k = 32kb + 16(g&1) + 4p .. +3
   int boff[3];
 #pragma unroll
@@ -183,7 +215,7 @@ __device__ __forceinline__ void pair_wgrad(f32x16 (&acc)[3], const unsigned char
   const int nt = G.Wout >> 4;
   for (int t = 0; t < nt; ++t) {
     const int mo = 16 * t;
-    const s4v a0 = tr4(ta + mo * 128), a1 = tr4(ta + (mo + 8) * 128);
+    const s4v a0 = tr4(ta + mo * 128), a1 = tr4(ta8 + mo * 128);
     const bf16x8 af = (bf16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
@@ -191,34 +223,6 @@ __device__ __forceinline__ void pair_wgrad(f32x16 (&acc)[3], const unsigned char
       const bf16x8 bf = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
       acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[u], 0, 0, 0);
     }
-  }
-}
-
-// slab[blk][co][SKH]: the two slot groups' partials summed in fixed order through LDS
-__device__ __forceinline__ void write_wslab(const f32x16 (&acc)[3], float* red, float* slab, int wid,
-                                            int lane) {
-  const int slot = wid >> 2, cb = wid & 1, kq = (wid >> 1) & 1;
-  // C layout: col = lane & 31 (k), row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5) (co)
-  if (slot == 1) {
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int k = 32 * (3 * kq + u) + (lane & 31);
-        red[co * SKH + k] = acc[u][r];
-      }
-  }
-  __syncthreads();
-  if (slot == 0) {
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int k = 32 * (3 * kq + u) + (lane & 31);
-        slab[(long long)blockIdx.x * SCO * SKH + co * SKH + k] = acc[u][r] + red[co * SKH + k];
-      }
   }
 }
 
@@ -231,234 +235,283 @@ struct StemFwdArgs {
   const bf16_t* wk;      // [64][SKP]
   const float* gamma;    // BN weight: sign picks max / min pooling
   bf16_t* pext;          // [N][PH][PW][64]
-  uint8_t* code;         // [N][PH][PW][64]
+  uint8_t* code;         // [N][PH][PW][32]: window codes, 4 bits per channel (see wcode)
   float* stats;          // [grid][2][64] or nullptr
   int N, nimg;           // batch rows, image rows (idx values are clamped to it)
   StemGeo G;
 };
 
+// Warp-specialised forward: 4 MFMA waves compute pair i's conv into key tile Y[i & 1] while
+// 8 VALU waves pool pair i-1 from the other tile, expand the E rows pair i+1 needs and load
+// the raw rows of the step after; one barrier per step.  Per image the step stream is
+// [stage rows -3..3, stage rows 4..5, pair 0, ..., pair PH-1]; the last pair is pooled in the
+// next image's first step.  The tile holds monotone 16-bit keys of the bf16 conv output
+// (complemented where gamma < 0), so the pooled extremum and its first-in-scan-order window
+// position fall out of 32-bit integer max3s of (key << 16 | rank).
+constexpr int FNT = 768;                 // 12 waves: 0-3 MFMA, 4-11 VALU
+constexpr int FVT = FNT - 256;           // VALU threads
+constexpr int FRU = 2;                   // raw units per VALU thread per staging (4 rows)
+
 template <int DT>
-__global__ void __launch_bounds__(SNT, 1) stem_fwd_kernel(StemFwdArgs a) {
+__global__ void __launch_bounds__(FNT, 1) stem_fwd_kernel(StemFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const StemGeo G = a.G;
-  unsigned char* Ws = smem;                                  // [64][SWP] bf16
-  unsigned char* E = Ws + SCO * SWP * 2;                     // [RING][Wout][24] bf16
-  unsigned char* Y = E + RING * G.ROWB;                      // [2][Wout][64] bf16 (swizzled)
-  bf16_t* S = reinterpret_cast<bf16_t*>(Y + 2 * G.Wout * 128);  // [SROWS][SP]
+  const int YB = 2 * G.Wout * 128;       // one key tile: [2 slots][Wout][64]
+  const int SB = 4 * G.SP;               // one S buffer (elements)
+  unsigned char* E = smem;                                   // [RING][Wout][24] bf16
+  unsigned char* Y = E + RING * G.ROWB;                      // [2][YB]
+  bf16_t* S = reinterpret_cast<bf16_t*>(Y + 2 * YB);         // [2][4][SP]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const bool train = a.stats != nullptr;   // batch statistics
-
-  // zero everything once (S pads, E pad pixels are never read uninitialised)
+  const bool train = a.stats != nullptr;
   {
-    const int tot16 = (SCO * SWP * 2 + RING * G.ROWB + 2 * G.Wout * 128 + SROWS * G.SP * 2) / 16;
-    for (int e = tid; e < tot16; e += SNT) reinterpret_cast<uint4*>(smem)[e] = make_uint4(0, 0, 0, 0);
+    const int tot16 = (RING * G.ROWB + 2 * YB + 2 * SB * 2) / 16;
+    for (int e = tid; e < tot16; e += FNT) reinterpret_cast<uint4*>(smem)[e] = make_uint4(0, 0, 0, 0);
   }
   __syncthreads();
-  for (int e = tid; e < SCO * SKP / 8; e += SNT) {
-    const int co = e / (SKP / 8), ch = e - co * (SKP / 8);
-    *reinterpret_cast<uint4*>(Ws + co * SWP * 2 + ch * 16) =
-        *reinterpret_cast<const uint4*>(a.wk + co * SKP + ch * 8);
-  }
-
-  // ------------------------------------------------------------------ per-lane roles
-  // y MFMA: slot w >> 2 (conv row 2i + slot), M-block w & 3 (32 px), both co-blocks
-  const int yslot = wid >> 2, mb = wid & 3;
-  const int hh = lane >> 5;
-  const bool yact = 32 * mb < G.Wout;
-  const int pxa = min(32 * mb + (lane & 31), G.Wout - 1);  // A row (pad lanes re-read px W-1)
-  // pooling: thread (j, c8)
-  const bool pact = tid < G.PW * 8;
-  const int pj = tid >> 3, pc8 = tid & 7;
-  float psg[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) psg[c] = (pact && a.gamma[pc8 * 8 + c] < 0.f) ? -1.f : 1.f;
-
-  float st_s[2] = {0.f, 0.f}, st_q[2] = {0.f, 0.f};
-
-  RawUnit ru[UPT];
-  auto img_base = [&](int n) -> long long {
+  const int nimg = a.N > (int)blockIdx.x ? (a.N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int SPI = G.PH + 2;              // steps per image
+  const int nsteps = nimg * SPI;         // + 1 final pooling-only step
+  auto img_base = [&](int q) -> long long {
+    const int n = (int)blockIdx.x + q * (int)gridDim.x;
     long long row = a.idx ? a.idx[n] : (long long)n;
     row = row < 0 ? 0 : row >= a.nimg ? a.nimg - 1 : row;
     return row * G.Hin * G.Win * 3;
   };
-  // prologue: image blockIdx.x, rows 0..5 (rows -3..-1 are zero rows)
-  int n = blockIdx.x;
-  if (n < a.N) {
-    raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, 0, SROWS, a.nsc, a.nbi, tid);
-    raw_store(ru, S, G.SP, G.Win, SROWS, tid);
-  }
-  __syncthreads();
-  if (n < a.N) e_build(E, S, G, -3, 9, -3, tid);
-  __syncthreads();
-
-  for (; n < a.N; n += gridDim.x) {
-    const int nnext = n + gridDim.x;
-    float pv[8];
-    uint32_t pk = 0;  // previous odd row's horizontal extremum and kw (2 bits per channel)
+  const bool mw = wid < 4;
+  if (mw) {
+    // ================================================================ MFMA waves
+    // wave w: conv row 2i + (w >> 1) of the pair, output channels 32 (w & 1) .. +31, all
+    // pixel blocks.  C = W x E^T: lane = pixel (lane & 31), register r = channel
+    // 32cb + (r & 3) + 8 (r >> 2) + 4 hh -- 4 consecutive channels per register quad, one
+    // 8-byte key store each.  The weights (A) stay in registers.
+    const int slot = wid >> 1, cb = wid & 1, hh = lane >> 5;
+    bf16x8 wa[11];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) pv[c] = -INFINITY;
-    for (int i = 0; i < G.PH; ++i) {
-      // ---------------------------------------------------------------- phase A
-      // raw rows of the next step: pair i+1 needs rows 4i+6 .. 4i+9; after the image's last
-      // pair, the next image's rows 0..5
-      const bool last = i + 1 == G.PH;
-      const bool more = !last || nnext < a.N;
-      int srows = 0, siy = 0;
-      if (!last) {
-        srows = 4;
-        siy = 4 * i + 6;
-        raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, siy, 4, a.nsc, a.nbi, tid);
-      } else if (nnext < a.N) {
-        srows = SROWS;
-        siy = 0;
-        raw_load<DT>(ru, a.img, img_base(nnext), G.Hin, G.Win, 0, SROWS, a.nsc, a.nbi, tid);
+    for (int s = 0; s < 11; ++s)
+      wa[s] = *reinterpret_cast<const bf16x8*>(a.wk + (32 * cb + (lane & 31)) * SKP + 16 * s + 8 * hh);
+    uint32_t flm[4][2];  // complement masks (gamma < 0) of the register quads' channel pairs
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int co = 32 * cb + 8 * g4 + 4 * hh + 2 * h;
+        flm[g4][h] = (a.gamma[co] < 0.f ? 0xffffu : 0u) | (a.gamma[co + 1] < 0.f ? 0xffff0000u : 0u);
       }
-      if (yact) {
-        const int oy = 2 * i + yslot;
-        const int rb = 2 * oy - 3;
-        f32x16 acc[2];
+    float st_s[16], st_q[16];
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+    for (int r = 0; r < 16; ++r) st_s[r] = st_q[r] = 0.f;
+    for (int st = 0; st <= nsteps; ++st) {
+      __syncthreads();  // step boundary (the previous step's tile reads / E writes are done)
+      if (st == nsteps) break;
+      const int kk = st % SPI;
+      if (kk < 2) continue;
+      const int i = kk - 2;
+      unsigned char* Yt = Y + (st & 1) * YB;
+      const int ring0 = (4 * i - 3 + 2 * slot + 13 * 8) % RING;  // ring row of ky = 0
+#pragma unroll 1
+      for (int mb = 0; mb < 4; ++mb) {
+        if (32 * mb >= G.Wout) break;
+        const int px = 32 * mb + (lane & 31);
+        const int pxb = min(px, G.Wout - 1);
+        f32x16 acc;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
-        const unsigned char* wb = Ws + (lane & 31) * SWP * 2 + 16 * hh;
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int s = 0; s < 11; ++s) {
           const int j = 2 * s + hh;
           int ky = j / 3;
           const int part = j - 3 * ky;
           if (ky > 6) ky = 6;  // k-step 10's upper half: zero weights, finite data
-          const bf16x8 af = *reinterpret_cast<const bf16x8*>(E + ring_of(rb + ky) * G.ROWB + pxa * 48 + part * 16);
-          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(wb + 32 * s);
-          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(wb + 32 * SWP * 2 + 32 * s);
-          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc[1], 0, 0, 0);
+          int rr = ring0 + ky;
+          rr = rr >= RING ? rr - RING : rr;
+          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(E + rr * G.ROWB + pxb * 48 + part * 16);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], bfr, acc, 0, 0, 0);
         }
-        // C: col = co (lane & 31), row = px
+        const bool valid = px < G.Wout;
+        if (32 * mb + 32 > G.Wout) {  // partial block: drop the clamped duplicates
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int co = 32 * c + (lane & 31);
+          for (int r = 0; r < 16; ++r) acc[r] = valid ? acc[r] : 0.f;
+        }
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int px = 32 * mb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (px < G.Wout) {
-              const float v = acc[c][r];
-              st_s[c] += v;
-              st_q[c] += v * v;
-              *reinterpret_cast<bf16_t*>(Y + yoff(yslot, px, co >> 3, G.Wout) + 2 * (co & 7)) = f2bf(v);
-            }
+        for (int r = 0; r < 16; ++r) {
+          st_s[r] += acc[r];
+          st_q[r] = fmaf(acc[r], acc[r], st_q[r]);
+        }
+        if (valid) {
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const uint32_t k0 = mono2(pack_bf2(acc[4 * g4 + 0], acc[4 * g4 + 1])) ^ flm[g4][0];
+            const uint32_t k1 = mono2(pack_bf2(acc[4 * g4 + 2], acc[4 * g4 + 3])) ^ flm[g4][1];
+            *reinterpret_cast<uint2*>(Yt + yoff(slot, px, 4 * cb + g4, G.Wout) + 8 * hh) = make_uint2(k0, k1);
           }
         }
       }
-      if (srows) raw_store(ru, S, G.SP, G.Win, srows, tid);
-      __syncthreads();
-      // ---------------------------------------------------------------- phase B
-      if (pact) {
-        float hv[2][8];
-        uint32_t hk[2] = {0, 0};
+    }
+    if (!train) return;
+    // statistics: [wave][r][lane] partials -> per channel, summed in fixed order
+    float* red = reinterpret_cast<float*>(smem);  // 4 waves x 2 x 16 x 64 floats
+    __syncthreads();  // the VALU waves' last pooling reads of the tiles are done
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      red[((wid * 2 + 0) * 16 + r) * 64 + lane] = st_s[r];
+      red[((wid * 2 + 1) * 16 + r) * 64 + lane] = st_q[r];
+    }
+    __syncthreads();
+    if (tid < 2 * SCO) {
+      const int co = tid & 63, which = tid >> 6;
+      const int c = co >> 5, cl = co & 31, h = (cl >> 2) & 1, r = (cl & 3) + 4 * (cl >> 3);
+      float sum = 0.f;
+      for (int sl = 0; sl < 2; ++sl) {
+        const float* rp = red + (((2 * sl + c) * 2 + which) * 16 + r) * 64 + 32 * h;
+        for (int l = 0; l < 32; ++l) sum += rp[l];
+      }
+      a.stats[(long long)blockIdx.x * 2 * SCO + which * SCO + co] = sum;
+    }
+    return;
+  }
+  // ================================================================== VALU waves
+  const int vt = tid - 256;
+  RawMap<FVT, FRU> rm;
+  rm.init(vt, G.Win);
+  EMap em;
+  em.init(vt, G.Wout);
+  RawUnit ru[FRU];
+  // pooling thread (j, c8)
+  const bool pact = vt < G.PW * 8;
+  const int pj = vt >> 3, pc8 = vt & 7;
+  uint32_t pflip[4];  // per channel pair of this chunk: complement masks (gamma < 0)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = pc8 * 8 + 2 * k;
+    pflip[k] = (pact && a.gamma[c] < 0.f ? 0xffffu : 0u) |
+               (pact && a.gamma[c + 1] < 0.f ? 0xffff0000u : 0u);
+  }
+  int pv[8];  // previous odd row's horizontal max keys (key << 16 | 2 - kw)
+  // raw rows for step 0: image 0 rows 0..3
+  if (nimg > 0) {
+    rm.load<DT>(ru, a.img, img_base(0), G.Hin, G.Win, 0, 4, a.nsc, a.nbi);
+    rm.store(ru, S + 1 * SB, G.SP, 4);  // consumed by step 0 from S[(0 - 1) & 1] = S[1]
+  }
+  for (int st = 0; st <= nsteps; ++st) {
+    __syncthreads();
+    const int q = st / SPI, kk = st - q * SPI;
+    // (c) raw rows for the NEXT step's E build, issued first (consumed at this step's end)
+    int nrows = 0, niy = 0, nq = q;
+    if (st + 1 < nsteps) {
+      const int k1 = kk + 1 == SPI ? 0 : kk + 1;
+      if (k1 == 0) { nq = q + 1; nrows = 4; niy = 0; }
+      else if (k1 == 1) { nrows = 2; niy = 4; }
+      else if (k1 - 2 + 1 < G.PH) { nrows = 4; niy = 4 * (k1 - 2) + 6; }
+      if (nrows) rm.load<DT>(ru, a.img, img_base(nq), G.Hin, G.Win, niy, nrows, a.nsc, a.nbi);
+    }
+    // (a) pooling of the pair the MFMA waves computed in the previous step
+    if (st >= 1) {
+      const int ps = st - 1, pq = ps / SPI, pk = ps - pq * SPI;
+      if (pk >= 2 && pact) {
+        const int i = pk - 2;
+        const unsigned char* Yt = Y + (ps & 1) * YB;
+        if (i == 0) {
+#pragma unroll
+          for (int c = 0; c < 8; ++c) pv[c] = INT_MIN;
+        }
+        int hk[2][8];
 #pragma unroll
         for (int sl = 0; sl < 2; ++sl) {
-#pragma unroll
-          for (int c = 0; c < 8; ++c) hv[sl][c] = -INFINITY;
+          uint4 w[3];
 #pragma unroll
           for (int kw = 0; kw < 3; ++kw) {
             const int px = 2 * pj - 1 + kw;
-            if (px < 0 || px >= G.Wout) continue;
-            const uint4 w = *reinterpret_cast<const uint4*>(Y + yoff(sl, px, pc8, G.Wout));
-            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+            w[kw] = (px >= 0 && px < G.Wout) ? *reinterpret_cast<const uint4*>(Yt + yoff(sl, px, pc8, G.Wout))
+                                             : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+          }
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-              const float v = psg[c] * bf2f((bf16_t)((ww[c >> 1] >> (16 * (c & 1))) & 0xffff));
-              if (v > hv[sl][c]) {
-                hv[sl][c] = v;
-                hk[sl] = (hk[sl] & ~(3u << (2 * c))) | ((uint32_t)kw << (2 * c));
-              }
+          for (int c = 0; c < 8; ++c) {
+            const int sh = 16 * (c & 1);
+            int k3[3];
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw) {
+              const uint32_t ww[4] = {w[kw].x, w[kw].y, w[kw].z, w[kw].w};
+              const uint32_t d = ww[c >> 1];
+              k3[kw] = (int)((sh ? (d & 0xffff0000u) : (d << 16)) | (uint32_t)(2 - kw));
             }
+            hk[sl][c] = max(max(k3[0], k3[1]), k3[2]);
           }
         }
-        uint32_t o[4];
-        uint32_t cd[2] = {0, 0};
+        uint32_t o[4] = {0, 0, 0, 0}, cd = 0;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          float b = pv[c];
-          uint32_t code = (pk >> (2 * c)) & 3;  // kh = 0
-          if (hv[0][c] > b) {
-            b = hv[0][c];
-            code = 3 + ((hk[0] >> (2 * c)) & 3);
-          }
-          if (hv[1][c] > b) {
-            b = hv[1][c];
-            code = 6 + ((hk[1] >> (2 * c)) & 3);
-          }
-          const float val = psg[c] * b;  // exact: b is a bf16 value times +-1
-          if (c & 1) o[c >> 1] |= (uint32_t)f2bf(val) << 16;
-          else o[c >> 1] = f2bf(val);
-          cd[c >> 2] |= code << (8 * (c & 3));
-          pv[c] = hv[1][c];
+          const int v = max(max(pv[c] | 8, hk[0][c] | 4), hk[1][c]);  // kh rank 2 - kh in bits 2-3
+          cd |= ((uint32_t)v & 15u) << (4 * c);  // the rank nibble is the window code
+          o[c >> 1] |= ((uint32_t)v >> 16) << (16 * (c & 1));
+          pv[c] = hk[1][c];
         }
-        pk = hk[1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = mono2(o[k] ^ pflip[k]);  // keys -> bf16 bits
+        const int n = (int)blockIdx.x + pq * (int)gridDim.x;
         const long long po = (((long long)n * G.PH + i) * G.PW + pj) * SCO + pc8 * 8;
         __builtin_nontemporal_store((nt4){o[0], o[1], o[2], o[3]}, reinterpret_cast<nt4*>(a.pext + po));
-        __builtin_nontemporal_store((nt2){cd[0], cd[1]}, reinterpret_cast<nt2*>(a.code + po));
-      }
-      if (!last) e_build(E, S, G, 4 * i + 6, 4, 0, tid);
-      __syncthreads();
-      if (last && more) {  // the next image's first rows: after this pair's MFMA reads of E
-        e_build(E, S, G, -3, 9, -3, tid);
-        __syncthreads();
+        __builtin_nontemporal_store(cd, reinterpret_cast<uint32_t*>(a.code + po / 2));
       }
     }
+    // (b) E rows for the next step's MFMA, from the raw rows staged in the previous step
+    if (st < nsteps) {
+      const bf16_t* Sp = S + ((st - 1) & 1) * SB;
+      if (kk == 0) em.build(E, Sp, G, -3, 7, -3);
+      else if (kk == 1) em.build(E, Sp, G, 4, 2, 0);
+      else if (kk - 2 + 1 < G.PH) em.build(E, Sp, G, 4 * (kk - 2) + 6, 4, 0);
+    }
+    if (nrows) rm.store(ru, S + (st & 1) * SB, G.SP, nrows);
   }
-  if (!train) return;
-  // ------------------------------------------------------------------ statistics
-  float* red = reinterpret_cast<float*>(smem);  // reuse: [8 waves][2 halves][64][2]
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int co = 32 * c + (lane & 31);
-    red[((wid * 2 + hh) * SCO + co) * 2 + 0] = st_s[c];
-    red[((wid * 2 + hh) * SCO + co) * 2 + 1] = st_q[c];
-  }
-  __syncthreads();
-  if (tid < 2 * SCO) {
-    const int co = tid & 63, which = tid >> 6;
-    float s = 0.f;
-    for (int k = 0; k < 16; ++k) s += red[(k * SCO + co) * 2 + which];
-    a.stats[(long long)blockIdx.x * 2 * SCO + which * SCO + co] = s;
+  if (train) {  // the MFMA waves' statistics exchange (overwrites the tiles)
+    __syncthreads();
+    __syncthreads();
   }
 }
 
-// out = relu(scale * pext + shift); code = 15 where that is <= 0 (no gradient flows)
+// out = relu(scale * pext + shift); code4 (optional) = the forward's window codes with 15
+// where that output is <= 0 (no gradient flows).  Four 8-channel chunks per thread, all loads
+// issued first.
 __global__ void __launch_bounds__(256) stem_pool_apply_kernel(const bf16_t* __restrict__ pext,
-                                                              uint8_t* __restrict__ code,
+                                                              const uint32_t* __restrict__ code,
                                                               const float* __restrict__ scale,
                                                               const float* __restrict__ shift,
-                                                              bf16_t* __restrict__ out, long long n8) {
-  const long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n8) return;
-  const int c0 = (int)(e & 7) * 8;
-  const nt4 v = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(pext) + e);
-  uint2 cd = code ? reinterpret_cast<const uint2*>(code)[e] : make_uint2(0, 0);
-  const uint32_t w[4] = {v[0], v[1], v[2], v[3]};
-  uint32_t o[4];
-  uint32_t cw[2] = {cd.x, cd.y};
+                                                              bf16_t* __restrict__ out,
+                                                              uint32_t* __restrict__ code4,
+                                                              long long n8) {
+  constexpr int U = 4;
+  const long long b = (long long)blockIdx.x * 256 * U + threadIdx.x;
+  nt4 v[U];
+  uint32_t cd[U];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float r[2];
-#pragma unroll
-    for (int hlf = 0; hlf < 2; ++hlf) {
-      const int c = c0 + 2 * k + hlf;
-      const float z = bf2f((bf16_t)((w[k] >> (16 * hlf)) & 0xffff)) * scale[c] + shift[c];
-      r[hlf] = z > 0.f ? z : 0.f;
-      if (!(z > 0.f)) {
-        const int b = 2 * k + hlf;
-        cw[b >> 2] = (cw[b >> 2] & ~(0xffu << (8 * (b & 3)))) | (15u << (8 * (b & 3)));
-      }
+  for (int u = 0; u < U; ++u) {
+    const long long e = b + 256LL * u;
+    if (e < n8) {
+      v[u] = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(pext) + e);
+      cd[u] = code4 ? __builtin_nontemporal_load(code + e) : 0u;
     }
-    o[k] = pack_bf2(r[0], r[1]);
   }
-  __builtin_nontemporal_store((nt4){o[0], o[1], o[2], o[3]}, reinterpret_cast<nt4*>(out) + e);
-  if (code) reinterpret_cast<uint2*>(code)[e] = make_uint2(cw[0], cw[1]);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long e = b + 256LL * u;
+    if (e >= n8) continue;
+    const int c0 = (int)(e & 7) * 8;
+    const uint32_t w[4] = {v[u][0], v[u][1], v[u][2], v[u][3]};
+    uint32_t o[4], keep = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float r[2];
+#pragma unroll
+      for (int hlf = 0; hlf < 2; ++hlf) {
+        const int c = c0 + 2 * k + hlf;
+        const float z = bf2f((bf16_t)((w[k] >> (16 * hlf)) & 0xffff)) * scale[c] + shift[c];
+        r[hlf] = z > 0.f ? z : 0.f;
+        keep |= z > 0.f ? 15u << (4 * (2 * k + hlf)) : 0u;
+      }
+      o[k] = pack_bf2(r[0], r[1]);
+    }
+    __builtin_nontemporal_store((nt4){o[0], o[1], o[2], o[3]}, reinterpret_cast<nt4*>(out) + e);
+    if (code4) code4[e] = (cd[u] & keep) | ~keep;
+  }
 }
 
 // ------------------------------------------------------------------------------- backward
@@ -468,197 +521,259 @@ struct StemBwdArgs2 {
   float nsc[3], nbi[3];
   const bf16_t* wk;      // [64][SKP] packed weights (the forward's)
   const bf16_t* pdy;     // [N][PH][PW][64] pooled gradient
-  const uint8_t* code;   // [N][PH][PW][64] window position, 15 = masked
+  const uint8_t* code4;  // [N][PH][PW][32] window positions, 4 bits per channel, 15 = masked
   const float* coef;     // [3][64] a, b, cc
   float* dslab;          // [grid][64][SKH]
   int N, nimg;
   StemGeo G;
 };
 
-constexpr int PRING = 3;  // pooled-row ring: rows i, i+1 in use, i+2 staged (i+3 in flight)
-constexpr int BROWS = 4;  // raw rows staged at once in the backward
+constexpr int PRING = 3;  // pooled-row ring: rows i, i+1 in use, i+2 staged
+constexpr int BNT = 768;  // 12 waves: 0-3 MFMA, 4-11 VALU
+constexpr int BVT = BNT - 256;
 
+// Warp-specialised backward.  Step stream per image: [stage E rows -3..3 + pooled rows 0..2,
+// stage rows 4..5, pair 0, ..., pair PH-1, (drain)]; the VALU waves build pair i's a*dz tile
+// T[i & 1] (and stage pair i+1's E rows) while the MFMA waves process pair i-1: recompute
+// its conv output y (weights resident in registers, C = [co][px]), turn T into
+// dy = a*dz + b*y + cc in place, then reduce dy^T x_col.  Two barriers per step: the y pass
+// of every MFMA wave completes before any wgrad read of T, and the VALU waves' S reads before
+// the raw rows of the next step overwrite it.
 template <int DT>
-__global__ void __launch_bounds__(SNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
+__global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const StemGeo G = a.G;
-  unsigned char* Ws = smem;                                  // [64][SWP] bf16
-  unsigned char* E = Ws + SCO * SWP * 2;                     // [RING][Wout][24]
-  unsigned char* T = E + RING * G.ROWB;                      // [2][Wout][64]: a dz, then dy
-  bf16_t* S = reinterpret_cast<bf16_t*>(T + 2 * G.Wout * 128);  // [BROWS][SP]
+  const int TB = 2 * G.Wout * 128;                           // one tile: [2 slots][Wout][64]
+  unsigned char* E = smem;                                   // [RING][Wout][24]
+  unsigned char* T = E + RING * G.ROWB;                      // [2][TB]
+  bf16_t* S = reinterpret_cast<bf16_t*>(T + 2 * TB);         // [4][SP]
   const int PRB = G.PW * SCO;                                // pooled row elements
-  bf16_t* Pg = S + BROWS * G.SP;                             // [PRING][PW][64] grads
-  uint8_t* Pc = reinterpret_cast<uint8_t*>(Pg + PRING * PRB);  // [PRING][PW][64] codes
-  float* cf = reinterpret_cast<float*>(Pc + PRING * PRB);   // a, b, cc
+  bf16_t* Pg = S + 4 * G.SP;                                 // [PRING][PW][64] grads
+  uint8_t* Pc = reinterpret_cast<uint8_t*>(Pg + PRING * PRB);  // [PRING][PW][32] 4-bit codes
+  float* cf = reinterpret_cast<float*>(Pc + PRING * PRB / 2);  // a, b, cc
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   {
-    const int tot16 = (SCO * SWP * 2 + RING * G.ROWB + 2 * G.Wout * 128 + BROWS * G.SP * 2) / 16;
-    for (int e = tid; e < tot16; e += SNT) reinterpret_cast<uint4*>(smem)[e] = make_uint4(0, 0, 0, 0);
-  }
-  __syncthreads();
-  for (int e = tid; e < SCO * SKP / 8; e += SNT) {
-    const int co = e / (SKP / 8), ch = e - co * (SKP / 8);
-    *reinterpret_cast<uint4*>(Ws + co * SWP * 2 + ch * 16) =
-        *reinterpret_cast<const uint4*>(a.wk + co * SKP + ch * 8);
+    const int tot16 = (RING * G.ROWB + 2 * TB + 4 * G.SP * 2) / 16;
+    for (int e = tid; e < tot16; e += BNT) reinterpret_cast<uint4*>(smem)[e] = make_uint4(0, 0, 0, 0);
   }
   if (tid < 3 * SCO) cf[tid] = a.coef[tid];
-  f32x16 dacc[3];
-#pragma unroll
-  for (int u = 0; u < 3; ++u)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dacc[u][r] = 0.f;
-  RawUnit ru[UPT];
-  auto img_base = [&](int n) -> long long {
-    long long row = a.idx ? a.idx[n] : (long long)n;
+  const int nimg = a.N > (int)blockIdx.x ? (a.N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int SPI = G.PH + 2;
+  const int nsteps = nimg * SPI;  // + 1 drain step (the last pair's MFMA work)
+  auto img_of = [&](int q) { return (int)blockIdx.x + q * (int)gridDim.x; };
+  auto img_base = [&](int q) -> long long {
+    long long row = a.idx ? a.idx[img_of(q)] : (long long)img_of(q);
     row = row < 0 ? 0 : row >= a.nimg ? a.nimg - 1 : row;
     return row * G.Hin * G.Win * 3;
   };
-  // pooled rows: PW * 8 chunks of (8 grads, 8 codes) per row; thread tid < PW*8 owns one
-  const bool pl = tid < G.PW * 8;
-  uint4 pg_r;
-  uint2 pc_r;
-  auto pload = [&](int n, int r) {
+  if (wid < 4) {
+    // ================================================================ MFMA waves
+    // y pass: wave w owns co-block cb = w & 1 and px-blocks (w >> 1) * 2 + {0, 1} of BOTH
+    // slots (4 units); its A fragments (the weights of its 32 channels, 11 k-steps) stay in
+    // registers.  wgrad pass: pair_wgrad's wave roles with w and w + 4 of the 8-wave layout
+    // (slot, co-block, k-blocks) folded onto 4 waves: wave w does roles w and w + 4.
+    const int cb = wid & 1, hh = lane >> 5;
+    bf16x8 wa[11];
+#pragma unroll
+    for (int s = 0; s < 11; ++s)
+      wa[s] = *reinterpret_cast<const bf16x8*>(a.wk + (32 * cb + (lane & 31)) * SKP + 16 * s + 8 * hh);
+    f32x16 dacc[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dacc[u][r] = 0.f;
+    __syncthreads();  // cf, zeroed LDS
+    for (int st = 0; st <= nsteps; ++st) {
+      __syncthreads();  // step start: T[(st-1) & 1] (a dz of the pair) and its E rows are ready
+      const int ps = st - 1;
+      const int pk = ps >= 0 ? ps % SPI : -1;
+      const bool work = ps >= 0 && pk >= 2;
+      const int i = pk - 2;
+      unsigned char* Tt = T + (ps & 1) * TB;
+      if (work) {
+        const int ring0 = (4 * i - 3 + 13 * 8) % RING;  // ring row of iy = 4i - 3
+#pragma unroll 1
+        for (int u = 0; u < 4; ++u) {
+          const int slot = u >> 1, mb = 2 * (wid >> 1) + (u & 1);
+          if (32 * mb >= G.Wout) continue;
+          const int pxb = min(32 * mb + (lane & 31), G.Wout - 1);
+          const int pxo = 32 * mb + (lane & 31);
+          f32x16 acc;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+          for (int s = 0; s < 11; ++s) {
+            const int j = 2 * s + hh;
+            int ky = j / 3;
+            const int part = j - 3 * ky;
+            if (ky > 6) ky = 6;
+            int rr = ring0 + 2 * slot + ky;  // iy = 2 oy - 3 + ky, oy = 2i + slot
+            rr = rr >= RING ? rr - RING : rr;
+            rr = rr >= RING ? rr - RING : rr;
+            const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(E + rr * G.ROWB + pxb * 48 + part * 16);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], bfr, acc, 0, 0, 0);
+          }
+          // C: col = px (lane & 31), row = co = 32 cb + (r & 3) + 8 (r >> 2) + 4 hh
+          if (pxo < G.Wout) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const int co = 32 * cb + 8 * g4 + 4 * hh;
+              unsigned char* tp = Tt + yoff(slot, pxo, co >> 3, G.Wout) + 2 * (co & 7);
+              const uint2 t = *reinterpret_cast<const uint2*>(tp);
+              const float4 bv = *reinterpret_cast<const float4*>(cf + SCO + co);
+              const float4 cv = *reinterpret_cast<const float4*>(cf + 2 * SCO + co);
+              const float d0 = bf2f((bf16_t)(t.x & 0xffff)) + bv.x * acc[4 * g4 + 0] + cv.x;
+              const float d1 = bf2f((bf16_t)(t.x >> 16)) + bv.y * acc[4 * g4 + 1] + cv.y;
+              const float d2 = bf2f((bf16_t)(t.y & 0xffff)) + bv.z * acc[4 * g4 + 2] + cv.z;
+              const float d3 = bf2f((bf16_t)(t.y >> 16)) + bv.w * acc[4 * g4 + 3] + cv.w;
+              *reinterpret_cast<uint2*>(tp) = make_uint2(pack_bf2(d0, d1), pack_bf2(d2, d3));
+            }
+          }
+        }
+      }
+      __syncthreads();  // mid-step: every wave's dy is in T
+      if (work) {
+        pair_wgrad(dacc, Tt, E, G, i, wid, lane);      // slot 0
+        pair_wgrad(dacc, Tt, E, G, i, wid + 4, lane);  // slot 1
+      }
+    }
+    // slab: both slots' partials are in dacc (same co / k positions)
+    const int kq = (wid >> 1) & 1;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int k = 32 * (3 * kq + u) + (lane & 31);
+        a.dslab[(long long)blockIdx.x * SCO * SKH + co * SKH + k] = dacc[u][r];
+      }
+    return;
+  }
+  // ================================================================== VALU waves
+  // Per image (SPI = PH + 2 steps): kk = 0 stages raw rows 0..1 and pooled rows 0..2 (the
+  // MFMA waves finish the previous image's last pair); kk = 1 expands E rows -3..1; kk = i + 2
+  // expands rows 4i+2..4i+5 (the new rows of pair i) and gathers pair i's a*dz into T.  The
+  // MFMA waves read pair i-1's rows 4i-7..4i+1 meanwhile: 13 live rows, the ring's size.
+  // Raw rows are stored into S after the mid-step barrier (the step's S reads are done) and
+  // expanded the step after.
+  const int vt = tid - 256;
+  RawMap<BVT, FRU> rm;
+  rm.init(vt, G.Win);
+  EMap em;
+  em.init(vt, G.Wout);
+  RawUnit ru[FRU];
+  // pooled rows: PW * 8 chunks of (8 grads, 8 4-bit codes) per row; thread vt < PW*8 owns one
+  const bool pl = vt < G.PW * 8;
+  uint4 pg_r = make_uint4(0, 0, 0, 0);
+  uint32_t pc_r = 0xffffffffu;
+  auto pload = [&](int q, int r) {
     pg_r = make_uint4(0, 0, 0, 0);
-    pc_r = make_uint2(0x0f0f0f0fu, 0x0f0f0f0fu);  // rows past the image: masked windows
+    pc_r = 0xffffffffu;  // rows past the image: masked windows
     if (pl && r < G.PH) {
-      const long long o = (((long long)n * G.PH + r) * G.PW) * SCO + tid * 8;
+      const long long o = (((long long)img_of(q) * G.PH + r) * G.PW) * SCO + vt * 8;
       pg_r = *reinterpret_cast<const uint4*>(a.pdy + o);
-      pc_r = *reinterpret_cast<const uint2*>(a.code + o);
+      pc_r = *reinterpret_cast<const uint32_t*>(a.code4 + o / 2);
     }
   };
   auto pstore = [&](int r) {
     if (!pl) return;
-    const int s = r % PRING;
-    *reinterpret_cast<uint4*>(Pg + s * PRB + tid * 8) = pg_r;
-    *reinterpret_cast<uint2*>(Pc + s * PRB + tid * 8) = pc_r;
+    const int sl = r % PRING;
+    *reinterpret_cast<uint4*>(Pg + sl * PRB + vt * 8) = pg_r;
+    *reinterpret_cast<uint32_t*>(Pc + (sl * PRB + vt * 8) / 2) = pc_r;
   };
-  // synchronous staging of raw rows iy0 .. iy0+nr-1 (nr <= BROWS) and E rows e0 .. iy0+nr-1
-  auto stage_sync = [&](int n, int iy0, int nr, int e0) {
-    raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, iy0, nr, a.nsc, a.nbi, tid);
-    raw_store(ru, S, G.SP, G.Win, nr, tid);
-    __syncthreads();
-    e_build(E, S, G, e0, iy0 + nr - e0, e0 - iy0, tid);
-    __syncthreads();
+  const int qb = vt >> 3, qc = vt & 7, c0 = qc * 8;
+  __syncthreads();  // cf, zeroed LDS
+  float ka[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ka[j] = cf[c0 + j];
+  uint4 qg[4];     // the quad's windows: 8 pooled grads each
+  uint32_t qi[4];  // and their codes (15 everywhere for a window outside the image)
+  // a*dz of quad pixel pp = (ddy, ddx): the sum of the grads of the covering windows whose
+  // code names this pixel (window (wa, wb) sees it at kh = ddy ? (wa ? 0 : 2) : 1, same for kw)
+  auto gpix = [&](unsigned char* Tt, int pp) {
+    const int ddy = pp >> 1, ddx = pp & 1;
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int wa = w >> 1, wb = w & 1;
+      if ((wa && !ddy) || (wb && !ddx)) continue;
+      const uint32_t gw[4] = {qg[w].x, qg[w].y, qg[w].z, qg[w].w};
+      const unsigned code = wcode(ddy ? (wa ? 0 : 2) : 1, ddx ? (wb ? 0 : 2) : 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t g = gw[j >> 1];
+        const float gf = __uint_as_float((j & 1) ? (g & 0xffff0000u) : (g << 16));
+        d[j] += (qi[w] & (15u << (4 * j))) == (code << (4 * j)) ? gf : 0.f;
+      }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = pack_bf2(ka[2 * k] * d[2 * k], ka[2 * k + 1] * d[2 * k + 1]);
+    *reinterpret_cast<uint4*>(Tt + yoff(ddy, 2 * qb + ddx, qc, G.Wout)) = make_uint4(o[0], o[1], o[2], o[3]);
   };
-  // quad items: (qb, chunk) = pixels (2i + ddy, 2qb + ddx), ddy, ddx in {0, 1}, 8 channels
-  const bool qact = tid < G.PW * 8;
-  const int qb = tid >> 3, qc = tid & 7, c0 = qc * 8;
-  // y MFMA (recompute), C = W x E^T: [co][px] -- wave w: slot w >> 2, px block w & 3
-  const int yslot = wid >> 2, mb = wid & 3, hh = lane >> 5;
-  const bool yact = 32 * mb < G.Wout;
-  const int pxb = min(32 * mb + (lane & 31), G.Wout - 1);  // B column (pad lanes re-read W-1)
-  const int pxo = 32 * mb + (lane & 31);                     // the output pixel of this lane
-  __syncthreads();
-  for (int n = blockIdx.x; n < a.N; n += gridDim.x) {
-    // image prologue: E rows -3..5 (data rows 0..5 in two stagings), pooled rows 0, 1 + 2
-    pload(n, 0);
-    pstore(0);
-    pload(n, 1);
-    pstore(1);
-    pload(n, 2);
-    stage_sync(n, 0, 4, -3);
-    stage_sync(n, 4, 2, 4);
-    float ka[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ka[j] = cf[c0 + j];
-    for (int i = 0; i < G.PH; ++i) {
-      const bool last = i + 1 == G.PH;
-      // ---------------------------------------------------------------- phase A: a dz
-      if (!last) raw_load<DT>(ru, a.img, img_base(n), G.Hin, G.Win, 4 * i + 6, 4, a.nsc, a.nbi, tid);
-      if (qact) {
-        // the quad's 4 windows: pooled rows i (+1), columns qb (+1)
-        uint4 qg[4];
-        uint2 qi[4];
-        unsigned ok = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const int wa = w >> 1, wb = w & 1;
-          ok |= (i + wa < G.PH && qb + wb < G.PW) ? 1u << w : 0u;
-          const int s = (i + wa) % PRING, col = qb + wb < G.PW ? qb + wb : qb;
-          qg[w] = *reinterpret_cast<const uint4*>(Pg + s * PRB + col * SCO + c0);
-          qi[w] = *reinterpret_cast<const uint2*>(Pc + s * PRB + col * SCO + c0);
-        }
-#pragma unroll
-        for (int pp = 0; pp < 4; ++pp) {
-          const int ddy = pp >> 1, ddx = pp & 1;
-          float d[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  if (nimg > 0) rm.load<DT>(ru, a.img, img_base(0), G.Hin, G.Win, 0, 2, a.nsc, a.nbi);
+  for (int st = 0; st <= nsteps; ++st) {
+    const int q = st / SPI, kk = st - q * SPI;
+    __syncthreads();  // (MFMA waves: step start)
+    // ---- phase 1 (MFMA waves: y pass of the previous step's pair)
+    if (st < nsteps) {
+      if (kk == 0) {
+        rm.store(ru, S, G.SP, 2);  // rows 0..1
+        pload(q, 0);
+        pstore(0);
+        pload(q, 1);
+        pstore(1);
+        pload(q, 2);
+        pstore(2);
+        pload(q, 3);
+        rm.load<DT>(ru, a.img, img_base(q), G.Hin, G.Win, 2, 4, a.nsc, a.nbi);
+      } else if (kk == 1) {
+        em.build(E, S, G, -3, 5, -3);
+      } else {
+        const int i = kk - 2;
+        em.build(E, S, G, 4 * i + 2, 4, 0);
+        if (pl) {
+          // the quad's 4 windows: pooled rows i (+1), columns qb (+1); pixels (0,0), (1,1) now,
+          // (0,1), (1,0) after the mid-step barrier (5 + 4 window tests: balances the phases)
 #pragma unroll
           for (int w = 0; w < 4; ++w) {
             const int wa = w >> 1, wb = w & 1;
-            if (wa == 1 && ddy == 0) continue;
-            if (wb == 1 && ddx == 0) continue;
-            if (!(ok & (1u << w))) continue;
-            const uint32_t gw[4] = {qg[w].x, qg[w].y, qg[w].z, qg[w].w};
-            const uint32_t aw[2] = {qi[w].x, qi[w].y};
-            const unsigned code = (unsigned)((ddy ? (wa ? 0 : 2) : 1) * 3 + (ddx ? (wb ? 0 : 2) : 1));
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (((aw[j >> 2] >> (8 * (j & 3))) & 0xff) == code)
-                d[j] += bf2f((bf16_t)((gw[j >> 1] >> (16 * (j & 1))) & 0xffff));
+            const bool okw = i + wa < G.PH && qb + wb < G.PW;
+            const int sl = (i + wa) % PRING, col = okw ? qb + wb : qb;
+            qg[w] = *reinterpret_cast<const uint4*>(Pg + sl * PRB + col * SCO + c0);
+            qi[w] = okw ? *reinterpret_cast<const uint32_t*>(Pc + (sl * PRB + col * SCO + c0) / 2)
+                        : 0xffffffffu;
           }
-          uint32_t o[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) o[k] = pack_bf2(ka[2 * k] * d[2 * k], ka[2 * k + 1] * d[2 * k + 1]);
-          *reinterpret_cast<uint4*>(T + yoff(ddy, 2 * qb + ddx, qc, G.Wout)) = make_uint4(o[0], o[1], o[2], o[3]);
+          gpix(T + (st & 1) * TB, 0);
+          gpix(T + (st & 1) * TB, 3);
         }
       }
-      // pooled row i + 2 (loaded one pair ago) into the slot of row i - 1; load row i + 3
-      pstore(i + 2);
-      pload(n, i + 3);
-      if (!last) raw_store(ru, S, G.SP, G.Win, 4, tid);
-      __syncthreads();
-      // ---------------------------------------------------------------- phase B: dy
-      if (yact) {
-        const int oy = 2 * i + yslot;
-        const int rb = 2 * oy - 3;
-        f32x16 acc[2];
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[c][r] = 0.f;
-        const unsigned char* wa0 = Ws + (lane & 31) * SWP * 2 + 16 * hh;
-#pragma unroll
-        for (int s = 0; s < 11; ++s) {
-          const int j = 2 * s + hh;
-          int ky = j / 3;
-          const int part = j - 3 * ky;
-          if (ky > 6) ky = 6;  // k-step 10's upper half: zero weights, finite data
-          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(E + ring_of(rb + ky) * G.ROWB + pxb * 48 + part * 16);
-          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(wa0 + 32 * s);
-          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(wa0 + 32 * SWP * 2 + 32 * s);
-          acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bfr, acc[0], 0, 0, 0);
-          acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bfr, acc[1], 0, 0, 0);
+    }
+    __syncthreads();  // (MFMA waves: mid-step) this step's S and pooled-ring reads are done
+    // ---- phase 2 (MFMA waves: wgrad of the previous step's pair)
+    if (st < nsteps) {
+      if (kk == 1) {
+        rm.store(ru, S, G.SP, 4);  // rows 2..5
+        if (G.PH > 1) rm.load<DT>(ru, a.img, img_base(q), G.Hin, G.Win, 6, 4, a.nsc, a.nbi);
+      } else if (kk >= 2) {
+        const int i = kk - 2;
+        if (pl) {
+          gpix(T + (st & 1) * TB, 1);
+          gpix(T + (st & 1) * TB, 2);
         }
-        // C: col = px (lane & 31), row = co = 32 c + (r & 3) + 8 (r >> 2) + 4 hh
-        if (pxo < G.Wout) {
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-              const int co = 32 * c + 8 * g4 + 4 * hh;
-              unsigned char* tp = T + yoff(yslot, pxo, co >> 3, G.Wout) + 2 * (co & 7);
-              const uint2 t = *reinterpret_cast<const uint2*>(tp);
-              const float4 bv = *reinterpret_cast<const float4*>(cf + SCO + co);
-              const float4 cv = *reinterpret_cast<const float4*>(cf + 2 * SCO + co);
-              const float d0 = bf2f((bf16_t)(t.x & 0xffff)) + bv.x * acc[c][4 * g4 + 0] + cv.x;
-              const float d1 = bf2f((bf16_t)(t.x >> 16)) + bv.y * acc[c][4 * g4 + 1] + cv.y;
-              const float d2 = bf2f((bf16_t)(t.y & 0xffff)) + bv.z * acc[c][4 * g4 + 2] + cv.z;
-              const float d3 = bf2f((bf16_t)(t.y >> 16)) + bv.w * acc[c][4 * g4 + 3] + cv.w;
-              *reinterpret_cast<uint2*>(tp) = make_uint2(pack_bf2(d0, d1), pack_bf2(d2, d3));
-            }
+        if (i + 1 < G.PH) {
+          rm.store(ru, S, G.SP, 4);  // rows 4i+6..4i+9 (pair i+1's new rows)
+          pstore(i + 3);             // row i's slot: its last reader was this step's gather
+          pload(q, i + 4);
         }
+        if (i + 2 < G.PH) rm.load<DT>(ru, a.img, img_base(q), G.Hin, G.Win, 4 * i + 10, 4, a.nsc, a.nbi);
+        else if (i + 2 == G.PH && q + 1 < nimg)
+          rm.load<DT>(ru, a.img, img_base(q + 1), G.Hin, G.Win, 0, 2, a.nsc, a.nbi);
       }
-      if (!last) e_build(E, S, G, 4 * i + 6, 4, 0, tid);
-      __syncthreads();
-      // ---------------------------------------------------------------- phase C: dW
-      pair_wgrad(dacc, T, E, G, i, wid, lane);
-      __syncthreads();
     }
   }
-  float* red = reinterpret_cast<float*>(smem);
-  write_wslab(dacc, red, a.dslab, wid, lane);
 }
 
 // dW[co][c][ky][kx] = beta * dW + sum_g slab[g][co][k], k = ky*24 + kx*3 + c.  One
@@ -718,12 +833,12 @@ bool stem_fused_supported(int Hin, int Win) {
 }
 
 static size_t fwd_smem(const StemGeo& G) {
-  return (size_t)SCO * SWP * 2 + (size_t)RING * G.ROWB + (size_t)2 * G.Wout * 128 +
-         (size_t)SROWS * G.SP * 2;
+  return (size_t)RING * G.ROWB + (size_t)2 * 2 * G.Wout * 128 + (size_t)2 * 4 * G.SP * 2;
 }
 static size_t bwd_smem(const StemGeo& G) {
-  return (size_t)SCO * SWP * 2 + (size_t)RING * G.ROWB + (size_t)2 * G.Wout * 128 +
-         (size_t)BROWS * G.SP * 2 + (size_t)PRING * G.PW * SCO * 3 + 3 * SCO * 4;
+  // E ring + 2 tiles + S (4 rows) + pooled ring (bf16 grads + 4-bit codes) + coefficients
+  return (size_t)RING * G.ROWB + (size_t)2 * 2 * G.Wout * 128 + (size_t)4 * G.SP * 2 +
+         (size_t)PRING * G.PW * SCO * 2 + (size_t)PRING * G.PW * SCO / 2 + 3 * SCO * 4;
 }
 
 int stem_fused_grid(int N) {
@@ -759,7 +874,7 @@ void stem_fwd_fused(const void* img, int dtype, const long long* idx, const floa
 #define DM_SF(DT)                                              \
   do {                                                         \
     set_smem_attr(stem_fwd_kernel<DT>, sm);                    \
-    stem_fwd_kernel<DT><<<grid, SNT, sm, st>>>(a);             \
+    stem_fwd_kernel<DT><<<grid, FNT, sm, st>>>(a);             \
   } while (0)
   if (dtype == 0) DM_SF(0);
   else if (dtype == 1) DM_SF(1);
@@ -768,16 +883,17 @@ void stem_fwd_fused(const void* img, int dtype, const long long* idx, const floa
   DM_CHECK(hipGetLastError());
 }
 
-void stem_pool_apply(const bf16_t* pext, uint8_t* code, const float* scale, const float* shift,
-                     bf16_t* out, long long n, hipStream_t st) {
+void stem_pool_apply(const bf16_t* pext, const uint8_t* code, const float* scale,
+                     const float* shift, bf16_t* out, uint8_t* code4, long long n, hipStream_t st) {
   const long long n8 = n / 8;
-  stem_pool_apply_kernel<<<(unsigned)((n8 + 255) / 256), 256, 0, st>>>(pext, code, scale, shift,
-                                                                       out, n8);
+  stem_pool_apply_kernel<<<(unsigned)((n8 + 1023) / 1024), 256, 0, st>>>(
+      pext, reinterpret_cast<const uint32_t*>(code), scale, shift, out,
+      reinterpret_cast<uint32_t*>(code4), n8);
   DM_CHECK(hipGetLastError());
 }
 
 void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const float* nsc,
-                     const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code,
+                     const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code4,
                      const float* coef, float* dslab, int N, int nimg, int Hin, int Win, int grid,
                      hipStream_t st) {
   StemBwdArgs2 a;
@@ -789,7 +905,7 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
   }
   a.wk = wk;
   a.pdy = pdy;
-  a.code = code;
+  a.code4 = code4;
   a.coef = coef;
   a.dslab = dslab;
   a.N = N;
@@ -799,7 +915,7 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
 #define DM_SB(DT)                                              \
   do {                                                         \
     set_smem_attr(stem_bwd_kernel<DT>, sm);                    \
-    stem_bwd_kernel<DT><<<grid, SNT, sm, st>>>(a);             \
+    stem_bwd_kernel<DT><<<grid, BNT, sm, st>>>(a);             \
   } while (0)
   if (dtype == 0) DM_SB(0);
   else if (dtype == 1) DM_SB(1);

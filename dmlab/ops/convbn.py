@@ -268,7 +268,7 @@ def _stem_fused_fwd(layer, x, ctx, train):
     nsc, nbi = input_affine(img.dtype)
     wk = packed_weights_stem(layer)
     pext = empty_nhwc(B, PH, PW, 64, img)
-    code = torch.empty((B, PH, PW, 64), device=dev, dtype=torch.uint8)
+    code = torch.empty((B, PH, PW, 32), device=dev, dtype=torch.uint8)
     grid = L.stem_fused_grid(B)
     f32 = dict(device=dev, dtype=torch.float32)
     scale = torch.empty(64, **f32)
@@ -290,10 +290,11 @@ def _stem_fused_fwd(layer, x, ctx, train):
                          layer.running_var, layer.eps, scale, shift)
         mean = invstd = None
     out = empty_nhwc(B, PH, PW, 64, img)
-    L.stem_pool_apply(pext, code if train else None, scale, shift, out)
+    code4 = torch.empty((B, PH, PW, 32), device=dev, dtype=torch.uint8) if train else None
+    L.stem_pool_apply(pext, code if train else None, scale, shift, out, code4)
     if train:
         ctx.update(fused_stem=True, img=img, gidx=idx, nsc=nsc, nbi=nbi, wk=wk, yarg=pext,
-                   idx=code, mean=mean, invstd=invstd, scale=scale, shift=shift, has_res=False,
+                   idx=code4, mean=mean, invstd=invstd, scale=scale, shift=shift, has_res=False,
                    first=True, s2d=False, pre=None, y=pext, x=None, M=M)
     return out
 
