@@ -664,6 +664,11 @@ ImgView img_view(const at::Tensor& img) {
 bool stem_fused_supported(int64_t Hin, int64_t Win) { return dm::stem_fused_supported(Hin, Win); }
 int64_t stem_fused_grid(int64_t N) { return dm::stem_fused_grid((int)N); }
 int64_t stem_slab_cols() { return dm::stem_slab_cols(); }
+// floats of the backward's slab workspace for `grid` workgroups: D and G partials + their sums
+int64_t stem_bwd_slab_len(int64_t grid) {
+  const int64_t gk = dm::stem_gram_cols();
+  return grid * (64 * dm::stem_slab_cols() + gk * gk) + dm::stem_sums_len();
+}
 
 const long long* idx_ptr(const c10::optional<at::Tensor>& idx, int B, int Nimg) {
   if (!idx.has_value()) {
@@ -722,8 +727,8 @@ void stem_pool_apply(at::Tensor pext, c10::optional<at::Tensor> code, at::Tensor
                       pext.numel(), cur_stream());
 }
 
-// BN-backward coefficients from the pooled-domain sums (pre_slab), the weight gradient of
-// dy = a dz + b y + cc (y recomputed in the kernel) into dslab, then dW = beta dW + sum dslab
+// BN-backward coefficients (a, b, cc) from the pooled-domain sums (pre_slab); the per-workgroup
+// D = dz^T X and G = X^T X partials into dslab; dW = beta dW + a D + b W G + cc colsum(X)
 void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<double> nsc,
                      std::vector<double> nbi, at::Tensor wk, at::Tensor pdy, at::Tensor code4,
                      at::Tensor mean, at::Tensor invstd, at::Tensor gamma, at::Tensor dgamma,
@@ -743,7 +748,7 @@ void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<
   TORCH_CHECK(wk.is_cuda() && wk.scalar_type() == at::kBFloat16 && wk.is_contiguous() &&
               wk.numel() == 64 * dm::stem_wk_cols(), "wk must be packed [64][176] bf16");
   TORCH_CHECK(grid >= 1 && grid <= B, "grid must be in [1, B]");
-  need_f32(dslab, "dslab", grid * C * dm::stem_slab_cols());
+  need_f32(dslab, "dslab", stem_bwd_slab_len(grid));
   const float s3[3] = {(float)nsc[0], (float)nsc[1], (float)nsc[2]};
   const float b3[3] = {(float)nbi[0], (float)nbi[1], (float)nbi[2]};
   const DeviceGuard guard(pdy.device());
@@ -753,10 +758,13 @@ void stem_bwd_fused2(at::Tensor img, c10::optional<at::Tensor> idx, std::vector<
                   (float)gbeta, M, C, 3, nullptr, nullptr, nullptr, nullptr, v.H / 2, v.W / 2,
                   v.H / 4, v.W / 4, 3, 2, 1, nullptr, nullptr, fp(work), st, fp(pre_slab),
                   (int)pre_rows, nullptr);
+  float* d_part = fp(dslab);
+  float* g_part = d_part + grid * C * dm::stem_slab_cols();
+  float* sums = g_part + grid * dm::stem_gram_cols() * dm::stem_gram_cols();
   dm::stem_bwd_fused2(v.ptr, v.dtype, idx_ptr(idx, B, v.N), s3, b3, bp(wk), bp(pdy),
-                      (const uint8_t*)code4.data_ptr(), fp(work), fp(dslab), B, v.N, v.H, v.W,
+                      (const uint8_t*)code4.data_ptr(), d_part, g_part, B, v.N, v.H, v.W,
                       (int)grid, st);
-  dm::stem_wreduce(fp(dslab), (int)grid, fp(dw), (float)wbeta, st);
+  dm::stem_wcombine(d_part, g_part, (int)grid, bp(wk), fp(work), sums, fp(dw), (float)wbeta, st);
 }
 
 void stem_pack_weights(at::Tensor w, at::Tensor wk) {
@@ -822,6 +830,7 @@ void register_resnet(pybind11::module_& m) {
   m.def("stem_fused_supported", &stem_fused_supported);
   m.def("stem_fused_grid", &stem_fused_grid);
   m.def("stem_slab_cols", &stem_slab_cols);
+  m.def("stem_bwd_slab_len", &stem_bwd_slab_len);
   m.def("stem_fwd_fused", &stem_fwd_fused, py::arg("img"), py::arg("idx"), py::arg("nsc"),
         py::arg("nbi"), py::arg("wk"), py::arg("gamma"), py::arg("pext"), py::arg("code"),
         py::arg("stats"), py::arg("grid"));

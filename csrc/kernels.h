@@ -106,9 +106,12 @@ void stem_pool_apply(const bf16_t* pext, const uint8_t* code, const float* scale
                      const float* shift, bf16_t* out, uint8_t* code4, long long n, hipStream_t st);
 void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const float* nsc,
                      const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code4,
-                     const float* coef, float* dslab, int N, int nimg, int Hin, int Win, int grid,
+                     float* dslab, float* gslab, int N, int nimg, int Hin, int Win, int grid,
                      hipStream_t st);
-void stem_wreduce(const float* dslab, int GD, float* dw, float beta, hipStream_t st);
+void stem_wcombine(const float* dslab, const float* gslab, int GD, const bf16_t* wk,
+                   const float* coef, float* sums, float* dw, float beta, hipStream_t st);
+int stem_gram_cols();
+int stem_sums_len();
 void stem_pack_weights(const float* w, bf16_t* wk, hipStream_t st);
 // The BatchNorm backward reduction of the layer whose output gradient a data gradient
 // produces, done in that dgrad's epilogue: with dz = Y * relu-mask (mask from y*sc + sh > 0,

@@ -42,6 +42,11 @@
 // window codes travel as 4-bit nibbles (the pooled-row ring then fits LDS beside the ring,
 // two tiles and the staging rows).
 //  stem_wreduce_kernel sums the per-workgroup slabs in fixed order into the OIHW gradient.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "common.h"
 #include "igemm_common.h"
 #include "kernels.h"
@@ -69,8 +74,24 @@ struct StemGeo {
 };
 
 struct RawUnit {
-  float v[4];
+  uint4 w;  // the raw bits of 4 consecutive row elements (u8: .x, bf16: .x .y, fp32: all)
 };
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not its
+// global loads (__syncthreads' fence drains vmcnt too, which would expose the raw-row and
+// pooled-row prefetches -- issued a step ahead -- at every step boundary).
+// s_memtime stamp (timing experiments: DMLAB_STEM_TRACE); one asm statement with its wait
+__device__ __forceinline__ unsigned long long stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 // E-ring row of input row iy (iy >= -5)
 __device__ __forceinline__ int ring_of(int iy) { return (iy + 13 * 8) % RING; }
@@ -82,56 +103,76 @@ __device__ __forceinline__ int ring_of(int iy) { return (iy + 13 * 8) % RING; }
 template <int NT, int RU>
 struct RawMap {
   int r[RU], k[RU];  // row within the staging, unit within the row (r = -1: none)
-  __device__ __forceinline__ void init(int t, int Win) {
+  unsigned valid;    // bit u: unit u of the last load lies inside the image
+  float sc[RU][4], bi[RU][4];  // normalisation of the unit's 4 elements (channel (k + j) % 3)
+  __device__ __forceinline__ void init(int t, int Win, const float (&nsc)[3], const float (&nbi)[3]) {
     const int upr = 3 * Win / 4;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int e = t + NT * u;
       r[u] = e < 4 * upr ? e / upr : -1;
       k[u] = e - (e / upr) * upr;
+      // register selects of the (scalar) kernel arguments: no memory reads, so no vmcnt
+      // wait on the in-flight prefetches where the values are used
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = (k[u] + j) % 3;
+        sc[u][j] = c == 0 ? nsc[0] : c == 1 ? nsc[1] : nsc[2];
+        bi[u][j] = c == 0 ? nbi[0] : c == 1 ? nbi[1] : nbi[2];
+      }
     }
   }
+  // issue the loads only: the conversion waits for them in store(), a step later.  Every
+  // lane loads (out-of-range units read a clamped in-image address and are zeroed in store()):
+  // a conditionally loaded register would be merged with a copy at the branch join, and that
+  // copy waits for the load on the spot.
   template <int DT>
   __device__ __forceinline__ void load(RawUnit (&ru)[RU], const void* img, long long rowbase, int Hin,
-                                       int Win, int iy0, int nrows, const float* nsc,
-                                       const float* nbi) const {
+                                       int Win, int iy0, int nrows) {
+    valid = 0;
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
-      float x[4] = {0.f, 0.f, 0.f, 0.f};
       const int iy = iy0 + r[u];
-      if (r[u] >= 0 && r[u] < nrows && iy >= 0 && iy < Hin) {
-        const long long off = rowbase + (long long)iy * Win * 3 + 4LL * k[u];
-        if (DT == 0) {
-          const float4 f = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(img) + off);
-          x[0] = f.x; x[1] = f.y; x[2] = f.z; x[3] = f.w;
-        } else if (DT == 1) {
-          const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(img) + off);
-          x[0] = bf2f((bf16_t)(w.x & 0xffff)); x[1] = bf2f((bf16_t)(w.x >> 16));
-          x[2] = bf2f((bf16_t)(w.y & 0xffff)); x[3] = bf2f((bf16_t)(w.y >> 16));
-        } else {
-          const uint32_t w = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(img) + off);
-          x[0] = (float)(w & 0xff); x[1] = (float)((w >> 8) & 0xff);
-          x[2] = (float)((w >> 16) & 0xff); x[3] = (float)(w >> 24);
-        }
-        const int c0 = k[u] % 3;  // channel of element 4k + j is (k + j) % 3
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = (c0 + j) % 3;
-          x[j] = x[j] * nsc[c] + nbi[c];
-        }
+      const bool ok = r[u] >= 0 && r[u] < nrows && iy >= 0 && iy < Hin;
+      valid |= ok ? 1u << u : 0u;
+      const int iyc = min(max(iy, 0), Hin - 1);
+      const long long off = rowbase + (long long)iyc * Win * 3 + 4LL * (r[u] >= 0 ? k[u] : 0);
+      if (DT == 0) {
+        ru[u].w = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(img) + off);
+      } else if (DT == 1) {
+        const uint2 w = *reinterpret_cast<const uint2*>(reinterpret_cast<const bf16_t*>(img) + off);
+        ru[u].w = make_uint4(w.x, w.y, 0, 0);
+      } else {
+        ru[u].w = make_uint4(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(img) + off), 0, 0, 0);
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ru[u].v[j] = x[j];
     }
   }
+  // normalise (x = raw * nsc[c] + nbi[c]; rows outside the image stay 0), round to bf16, write
+  // S[row r][t], t = f + 9 (9 zero pad elements on the left, >= 15 on the right)
+  template <int DT>
   __device__ __forceinline__ void store(const RawUnit (&ru)[RU], bf16_t* S, int SP, int nrows) const {
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       if (r[u] < 0 || r[u] >= nrows) continue;
+      float x[4];
+      const uint4 w = ru[u].w;
+      if (DT == 0) {
+        x[0] = __uint_as_float(w.x); x[1] = __uint_as_float(w.y);
+        x[2] = __uint_as_float(w.z); x[3] = __uint_as_float(w.w);
+      } else if (DT == 1) {
+        x[0] = __uint_as_float(w.x << 16); x[1] = __uint_as_float(w.x & 0xffff0000u);
+        x[2] = __uint_as_float(w.y << 16); x[3] = __uint_as_float(w.y & 0xffff0000u);
+      } else {
+        x[0] = (float)(w.x & 0xff); x[1] = (float)((w.x >> 8) & 0xff);
+        x[2] = (float)((w.x >> 16) & 0xff); x[3] = (float)(w.x >> 24);
+      }
+      const bool ok = (valid >> u) & 1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = ok ? fmaf(x[j], sc[u][j], bi[u][j]) : 0.f;
       bf16_t* p = S + r[u] * SP + 4 * k[u] + 9;  // odd element index
-      p[0] = f2bf(ru[u].v[0]);
-      *reinterpret_cast<uint32_t*>(p + 1) = pack_bf2(ru[u].v[1], ru[u].v[2]);
-      p[3] = f2bf(ru[u].v[3]);
+      p[0] = f2bf(x[0]);
+      *reinterpret_cast<uint32_t*>(p + 1) = pack_bf2(x[1], x[2]);
+      p[3] = f2bf(x[3]);
     }
   }
 };
@@ -158,8 +199,8 @@ struct EMap {
       if (iy >= 0 && iy < G.Hin) {
         const uint32_t* sp = reinterpret_cast<const uint32_t*>(S + (srow0 + q) * G.SP + soff);
         v = make_uint4(sp[0], sp[1], sp[2], sp[3]);
-        if (part == 2) {  // elements 21..23 of the expanded row are the zero pad
-          v.z &= 0xffffu;
+        if (part == 2) {  // elements 21..23 of the expanded row: 1.0 (the backward's all-ones
+          v.z = (v.z & 0xffffu) | 0x3f800000u;  // X column, zero weight), 0, 0
           v.w = 0;
         }
       }
@@ -188,41 +229,98 @@ __device__ __forceinline__ int yoff(int slot, int px, int c8, int Wout) {
   return ((slot * Wout + px) * 8 + (c8 ^ ((((px >> 1) & 1) << 2) | ((px >> 2) & 3)))) * 16;
 }
 
-// The wgrad MFMAs of one conv-row pair: acc[kb] (32 co x 32 k, 3 k-blocks per wave) +=
-// T[slot][m][co]^T * E[m][k] over the slot's Wout pixels.  Wave w: slot w >> 2, co-block w & 1,
-// k-blocks 3*((w >> 1) & 1) + 0..2.  T is the bf16 tile (y in the forward, a*dz + cc in the
-// backward), E the ring rows of the pair (base = ring row of iy = 4i - 3).
+// One 32-channel x 32-pixel conv tile: acc = W (registers, 11 k-steps of 16) x E^T, the E
+// fragment of k-step s at byte rowoff[ky] + 16 part + pxoff with (ky, part) = divmod(2s + hh, 3)
+// (ky clamped to 6: k-step 10's upper half has zero weights).  rowoff is wave-uniform, so a
+// k-step's address is one select between two scalar sums; the reads run PF k-steps ahead of
+// the MFMAs.
+template <int PF>
+__device__ __forceinline__ f32x16 conv_tile(const bf16x8 (&wa)[11], const unsigned char* E,
+                                            const int (&rowoff)[7], int pxoff, bool hh) {
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  bf16x8 bq[11];
+#pragma unroll
+  for (int s = 0; s < 11 + PF; ++s) {
+    if (s < 11) {
+      const int j0 = 2 * s, j1 = 2 * s + 1;
+      const int k0 = j0 / 3 > 6 ? 6 : j0 / 3, k1 = j1 / 3 > 6 ? 6 : j1 / 3;
+      const int a0 = rowoff[k0] + 16 * (j0 % 3), a1 = rowoff[k1] + 16 * (j1 % 3);
+      bq[s] = *reinterpret_cast<const bf16x8*>(E + (hh ? a1 : a0) + pxoff);
+    }
+    if (s >= PF) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s - PF], bq[s - PF], acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// byte offsets of the ring rows of input rows iy0 + r, r = 0..6 (iy0 >= -5)
+__device__ __forceinline__ void ring_rows(int (&ro)[7], int iy0, int ROWB) {
+  const int r0 = ring_of(iy0);
+#pragma unroll
+  for (int r = 0; r < 7; ++r) {
+    const int x = r0 + r;
+    ro[r] = (x >= RING ? x - RING : x) * ROWB;
+  }
+}
+
+// The wgrad MFMAs of one conv-row pair: acc[kb] (32 co x 32 k, 3 k-blocks) += T[slot][m][co]^T *
+// E[m][k] over both slots' Wout pixels.  Wave w (0..3): co-block w & 1, k-blocks
+// 3*((w >> 1) & 1) + 0..2.  T is the bf16 dy tile, E the ring rows of the pair.  The 8
+// transposed reads of each (t, slot) stage are issued one stage ahead of its 3 MFMAs.
 __device__ __forceinline__ void pair_wgrad(f32x16 (&acc)[3], const unsigned char* T,
                                            const unsigned char* E, const StemGeo& G, int i,
                                            int wid, int lane) {
-  const int slot = wid >> 2, cb = wid & 1, kq = (wid >> 1) & 1;
+  const int cb = wid & 1, kq = (wid >> 1) & 1;
   const int g = lane >> 4, h = g >> 1, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
-  const int oy = 2 * i + slot;
   // A: rows m = 16t + 4h + q (+8), channels co = 32cb + 16(g&1) + 4p .. +3
   const int c8 = 4 * cb + 2 * (g & 1) + (p >> 1);
   // rows m and m + 8 (the swizzle is invariant under m + 16, not m + 8)
-  const unsigned char* ta = T + yoff(slot, 4 * h + q, c8, G.Wout) + 8 * (p & 1);
-  const unsigned char* ta8 = T + yoff(slot, 4 * h + q + 8, c8, G.Wout) + 8 * (p & 1);
-  // B: rows m (same), columns k = 32kb + 16(g&1) + 4p .. +3
-  int boff[3];
+  int ta[2], ta8[2], boff[2][3];
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int k = 32 * (3 * kq + u) + 16 * (g & 1) + 4 * p;
-    int ky = k / 24, kk = k - 24 * ky;
-    if (ky > 6) ky = 6;  // the pad columns k >= 168 read finite data (their results are unused)
-    boff[u] = ring_of(2 * oy - 3 + ky) * G.ROWB + (4 * h + q) * 48 + 2 * kk;
-  }
-  const int nt = G.Wout >> 4;
-  for (int t = 0; t < nt; ++t) {
-    const int mo = 16 * t;
-    const s4v a0 = tr4(ta + mo * 128), a1 = tr4(ta8 + mo * 128);
-    const bf16x8 af = (bf16x8){a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+  for (int sl = 0; sl < 2; ++sl) {
+    ta[sl] = yoff(sl, 4 * h + q, c8, G.Wout) + 8 * (p & 1);
+    ta8[sl] = yoff(sl, 4 * h + q + 8, c8, G.Wout) + 8 * (p & 1);
+    const int oy = 2 * i + sl;
+    // B: rows m (same), columns k = 32kb + 16(g&1) + 4p .. +3
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
-      const s4v b0 = tr4(E + boff[u] + mo * 48), b1 = tr4(E + boff[u] + (mo + 8) * 48);
-      const bf16x8 bf = (bf16x8){b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+      const int k = 32 * (3 * kq + u) + 16 * (g & 1) + 4 * p;
+      int ky = k / 24, kk = k - 24 * ky;
+      if (ky > 6) ky = 6;  // the pad columns k >= 168 read finite data (their results are unused)
+      boff[sl][u] = ring_of(2 * oy - 3 + ky) * G.ROWB + (4 * h + q) * 48 + 2 * kk;
+    }
+  }
+  struct Stage {
+    s4v a0, a1, b0[3], b1[3];
+  };
+  auto load = [&](Stage& S, int t, int sl) {
+    const int mo = 16 * t;
+    S.a0 = tr4(T + ta[sl] + mo * 128);
+    S.a1 = tr4(T + ta8[sl] + mo * 128);
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      S.b0[u] = tr4(E + boff[sl][u] + mo * 48);
+      S.b1[u] = tr4(E + boff[sl][u] + (mo + 8) * 48);
+    }
+  };
+  auto mma = [&](const Stage& S) {
+    const bf16x8 af = (bf16x8){S.a0[0], S.a0[1], S.a0[2], S.a0[3], S.a1[0], S.a1[1], S.a1[2], S.a1[3]};
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const bf16x8 bf = (bf16x8){S.b0[u][0], S.b0[u][1], S.b0[u][2], S.b0[u][3],
+                                 S.b1[u][0], S.b1[u][1], S.b1[u][2], S.b1[u][3]};
       acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, bf, acc[u], 0, 0, 0);
     }
+  };
+  const int nt = G.Wout >> 4;
+  Stage s0, s1;
+  load(s0, 0, 0);
+  for (int t = 0; t < nt; ++t) {
+    load(s1, t, 1);
+    mma(s0);
+    if (t + 1 < nt) load(s0, t + 1, 0);
+    mma(s1);
   }
 }
 
@@ -238,6 +336,7 @@ struct StemFwdArgs {
   uint8_t* code;         // [N][PH][PW][32]: window codes, 4 bits per channel (see wcode)
   float* stats;          // [grid][2][64] or nullptr
   int N, nimg;           // batch rows, image rows (idx values are clamped to it)
+  int ablate;            // timing experiments only (DMLAB_STEM_ABLATE): skip parts of the work
   StemGeo G;
 };
 
@@ -301,32 +400,20 @@ __global__ void __launch_bounds__(FNT, 1) stem_fwd_kernel(StemFwdArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) st_s[r] = st_q[r] = 0.f;
     for (int st = 0; st <= nsteps; ++st) {
-      __syncthreads();  // step boundary (the previous step's tile reads / E writes are done)
+      lds_barrier();  // step boundary (the previous step's tile reads / E writes are done)
       if (st == nsteps) break;
       const int kk = st % SPI;
       if (kk < 2) continue;
       const int i = kk - 2;
       unsigned char* Yt = Y + (st & 1) * YB;
-      const int ring0 = (4 * i - 3 + 2 * slot + 13 * 8) % RING;  // ring row of ky = 0
-#pragma unroll 1
+      int ro[7];
+      ring_rows(ro, 4 * i - 3 + 2 * slot, G.ROWB);  // conv row 2i + slot: input rows 2oy-3 ..
+#pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
-        if (32 * mb >= G.Wout) break;
+        if (32 * mb >= G.Wout || (a.ablate & 1)) break;
         const int px = 32 * mb + (lane & 31);
         const int pxb = min(px, G.Wout - 1);
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 11; ++s) {
-          const int j = 2 * s + hh;
-          int ky = j / 3;
-          const int part = j - 3 * ky;
-          if (ky > 6) ky = 6;  // k-step 10's upper half: zero weights, finite data
-          int rr = ring0 + ky;
-          rr = rr >= RING ? rr - RING : rr;
-          const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(E + rr * G.ROWB + pxb * 48 + part * 16);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], bfr, acc, 0, 0, 0);
-        }
+        f32x16 acc = conv_tile<4>(wa, E, ro, pxb * 48, hh);
         const bool valid = px < G.Wout;
         if (32 * mb + 32 > G.Wout) {  // partial block: drop the clamped duplicates
 #pragma unroll
@@ -372,7 +459,7 @@ __global__ void __launch_bounds__(FNT, 1) stem_fwd_kernel(StemFwdArgs a) {
   // ================================================================== VALU waves
   const int vt = tid - 256;
   RawMap<FVT, FRU> rm;
-  rm.init(vt, G.Win);
+  rm.init(vt, G.Win, a.nsc, a.nbi);
   EMap em;
   em.init(vt, G.Wout);
   RawUnit ru[FRU];
@@ -388,26 +475,51 @@ __global__ void __launch_bounds__(FNT, 1) stem_fwd_kernel(StemFwdArgs a) {
   }
   int pv[8];  // previous odd row's horizontal max keys (key << 16 | 2 - kw)
   // raw rows for step 0: image 0 rows 0..3
+  // dataset row bases of the current and the next image, read once per image (a per-step
+  // index read is a vector load whose wait would drain the in-flight prefetches and stores)
+  long long bcur = nimg > 0 ? img_base(0) : 0, bnext = nimg > 1 ? img_base(1) : 0;
+  int bq = 0;  // image of bcur
+  auto base = [&](int qq) {
+    if (qq != bq) {  // advance (images are visited in order)
+      bcur = bnext;
+      bq = qq;
+      bnext = qq + 1 < nimg ? img_base(qq + 1) : 0;
+    }
+    return bcur;
+  };
+  // raw rows expanded at step t (stored into S[(t - 1) & 1] at the top of step t - 1, loaded
+  // during step t - 2: a whole step in flight)
+  auto plan = [&](int t, int& pq, int& piy) -> int {
+    if (t >= nsteps) return 0;
+    pq = t / SPI;
+    const int k = t - pq * SPI;
+    if (k == 0) { piy = 0; return 4; }
+    if (k == 1) { piy = 4; return 2; }
+    if (k - 2 + 1 < G.PH) { piy = 4 * (k - 2) + 6; return 4; }
+    return 0;
+  };
+  int pend = 0;  // rows in flight in ru (for step st + 1)
   if (nimg > 0) {
-    rm.load<DT>(ru, a.img, img_base(0), G.Hin, G.Win, 0, 4, a.nsc, a.nbi);
-    rm.store(ru, S + 1 * SB, G.SP, 4);  // consumed by step 0 from S[(0 - 1) & 1] = S[1]
+    rm.load<DT>(ru, a.img, bcur, G.Hin, G.Win, 0, 4);
+    rm.store<DT>(ru, S + 1 * SB, G.SP, 4);  // consumed by step 0 from S[(0 - 1) & 1] = S[1]
+    int pq = 0, piy = 0;
+    pend = plan(1, pq, piy);
+    if (pend) rm.load<DT>(ru, a.img, base(pq), G.Hin, G.Win, piy, pend);
   }
   for (int st = 0; st <= nsteps; ++st) {
-    __syncthreads();
+    lds_barrier();
     const int q = st / SPI, kk = st - q * SPI;
-    // (c) raw rows for the NEXT step's E build, issued first (consumed at this step's end)
-    int nrows = 0, niy = 0, nq = q;
-    if (st + 1 < nsteps) {
-      const int k1 = kk + 1 == SPI ? 0 : kk + 1;
-      if (k1 == 0) { nq = q + 1; nrows = 4; niy = 0; }
-      else if (k1 == 1) { nrows = 2; niy = 4; }
-      else if (k1 - 2 + 1 < G.PH) { nrows = 4; niy = 4 * (k1 - 2) + 6; }
-      if (nrows) rm.load<DT>(ru, a.img, img_base(nq), G.Hin, G.Win, niy, nrows, a.nsc, a.nbi);
+    // (c) the rows of step st + 1 into S, then the loads of step st + 2's
+    if (pend) rm.store<DT>(ru, S + (st & 1) * SB, G.SP, pend);
+    {
+      int pq = 0, piy = 0;
+      pend = plan(st + 2, pq, piy);
+      if (pend) rm.load<DT>(ru, a.img, base(pq), G.Hin, G.Win, piy, pend);
     }
     // (a) pooling of the pair the MFMA waves computed in the previous step
     if (st >= 1) {
       const int ps = st - 1, pq = ps / SPI, pk = ps - pq * SPI;
-      if (pk >= 2 && pact) {
+      if (pk >= 2 && pact && !(a.ablate & 4)) {
         const int i = pk - 2;
         const unsigned char* Yt = Y + (ps & 1) * YB;
         if (i == 0) {
@@ -454,13 +566,12 @@ __global__ void __launch_bounds__(FNT, 1) stem_fwd_kernel(StemFwdArgs a) {
       }
     }
     // (b) E rows for the next step's MFMA, from the raw rows staged in the previous step
-    if (st < nsteps) {
+    if (st < nsteps && !(a.ablate & 8)) {
       const bf16_t* Sp = S + ((st - 1) & 1) * SB;
       if (kk == 0) em.build(E, Sp, G, -3, 7, -3);
       else if (kk == 1) em.build(E, Sp, G, 4, 2, 0);
       else if (kk - 2 + 1 < G.PH) em.build(E, Sp, G, 4 * (kk - 2) + 6, 4, 0);
     }
-    if (nrows) rm.store(ru, S + (st & 1) * SB, G.SP, nrows);
   }
   if (train) {  // the MFMA waves' statistics exchange (overwrites the tiles)
     __syncthreads();
@@ -515,6 +626,111 @@ __global__ void __launch_bounds__(256) stem_pool_apply_kernel(const bf16_t* __re
 }
 
 // ------------------------------------------------------------------------------- backward
+// ------------------------------------------------------------------ backward MFMA plans
+// dW = a*D + b*(W G) + cc*colsum(X), with D = dz^T X (dz: the routed pooled gradient, bf16
+// tile T) and G = X^T X (X: the im2col rows of the conv, straight from the E ring), both
+// fp32 MFMA accumulations over the workgroup's images.  y = X W^T never exists: b * sum y X
+// is W G, exactly, in the combine kernel (the mean-subtraction terms cancel in fp32 there).
+// colsum(X) is row 93 of G: E element 21 of every in-image row is 1.0 (X column 3*24 + 21,
+// centre kernel row, zero weight).  6 k-blocks of 32: G's 21 upper-triangle tiles and D's
+// 12 tiles over 8 MFMA waves; a wave loads the X fragments of its blocks (and the T
+// fragment of its co-block) once per 16-row m-step and feeds all its tiles.
+constexpr int GK = 192;   // G rows / columns (6 k-blocks)
+constexpr int GONE = 93;  // the all-ones X column
+struct WavePlan {
+  int nb, blk[4];         // X blocks loaded
+  int tcb;                // T co-block loaded (-1: none)
+  int nt, kind[5], x[5], y[5];  // tiles: kind 0 = G(blk[x], blk[y]), 1 = D(tcb, blk[y])
+};
+__device__ constexpr WavePlan kPlans[8] = {
+    {2, {0, 1, 0, 0}, 0, 5, {0, 0, 0, 1, 1}, {0, 0, 1, 0, 0}, {0, 1, 1, 0, 1}},
+    {2, {2, 3, 0, 0}, 0, 5, {0, 0, 0, 1, 1}, {0, 0, 1, 0, 0}, {0, 1, 1, 0, 1}},
+    {2, {4, 5, 0, 0}, 0, 5, {0, 0, 0, 1, 1}, {0, 0, 1, 0, 0}, {0, 1, 1, 0, 1}},
+    {4, {0, 1, 2, 3}, -1, 4, {0, 0, 0, 0, 0}, {0, 0, 1, 1, 0}, {2, 3, 2, 3, 0}},
+    {4, {0, 1, 4, 5}, -1, 4, {0, 0, 0, 0, 0}, {0, 0, 1, 1, 0}, {2, 3, 2, 3, 0}},
+    {4, {2, 3, 4, 5}, -1, 4, {0, 0, 0, 0, 0}, {0, 0, 1, 1, 0}, {2, 3, 2, 3, 0}},
+    {3, {0, 1, 2, 0}, 1, 3, {1, 1, 1, 0, 0}, {0, 0, 0, 0, 0}, {0, 1, 2, 0, 0}},
+    {3, {3, 4, 5, 0}, 1, 3, {1, 1, 1, 0, 0}, {0, 0, 0, 0, 0}, {0, 1, 2, 0, 0}},
+};
+
+struct BwdFrags {
+  bf16x8 xf[4], tf;
+};
+
+// MFMA work of m-steps [t0, t1) of one slot (conv row 2i + slot) of a pair for wave W
+template <int W>
+__device__ __forceinline__ void gram_slot(f32x16 (&acc)[5], const unsigned char* T,
+                                          const unsigned char* E, const StemGeo& G, int i,
+                                          int slot, int t0, int t1, int lane) {
+  constexpr WavePlan P = kPlans[W];
+  const int g = lane >> 4, h = g >> 1, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  const int oy = 2 * i + slot;
+  int boff[4];
+#pragma unroll
+  for (int b = 0; b < P.nb; ++b) {
+    const int k = 32 * P.blk[b] + 16 * (g & 1) + 4 * p;
+    int ky = k / 24;
+    const int kk = k - 24 * ky;
+    if (ky > 6) ky = 6;  // pad columns k >= 168: finite data, unused results
+    boff[b] = ring_of(2 * oy - 3 + ky) * G.ROWB + (4 * h + q) * 48 + 2 * kk;
+  }
+  int ta = 0, ta8 = 0;
+  if (P.tcb >= 0) {
+    const int c8 = 4 * P.tcb + 2 * (g & 1) + (p >> 1);
+    ta = yoff(slot, 4 * h + q, c8, G.Wout) + 8 * (p & 1);
+    ta8 = yoff(slot, 4 * h + q + 8, c8, G.Wout) + 8 * (p & 1);  // swizzle: m + 16 invariant only
+  }
+  auto load = [&](BwdFrags& F, int t) {
+    const int mo = 16 * t;
+#pragma unroll
+    for (int b = 0; b < P.nb; ++b) {
+      const s4v v0 = tr4(E + boff[b] + mo * 48), v1 = tr4(E + boff[b] + (mo + 8) * 48);
+      F.xf[b] = (bf16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+    if (P.tcb >= 0) {
+      const s4v v0 = tr4(T + ta + mo * 128), v1 = tr4(T + ta8 + mo * 128);
+      F.tf = (bf16x8){v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+  };
+  auto mma = [&](const BwdFrags& F) {
+#pragma unroll
+    for (int j = 0; j < P.nt; ++j)
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(P.kind[j] ? F.tf : F.xf[P.x[j]], F.xf[P.y[j]],
+                                                       acc[j], 0, 0, 0);
+  };
+  // (two MFMA waves per SIMD cover each other's fragment-read latency)
+  for (int t = t0; t < t1; ++t) {
+    BwdFrags f;
+    load(f, t);
+    mma(f);
+  }
+}
+
+template <int W>
+__device__ __forceinline__ void gram_store(const f32x16 (&acc)[5], float* dslab, float* gslab,
+                                           int lane) {
+  constexpr WavePlan P = kPlans[W];
+#pragma unroll
+  for (int j = 0; j < P.nt; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int col = 32 * P.blk[P.y[j]] + (lane & 31);
+      if (P.kind[j])
+        dslab[(long long)blockIdx.x * SCO * SKH + (32 * P.tcb + row) * SKH + col] = acc[j][r];
+      else
+        gslab[(long long)blockIdx.x * GK * GK + (32 * P.blk[P.x[j]] + row) * GK + col] = acc[j][r];
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void gram_zero(f32x16 (&acc)[5]) {
+#pragma unroll
+  for (int j = 0; j < 5; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+}
+
 struct StemBwdArgs2 {
   const void* img;
   const long long* idx;
@@ -522,23 +738,26 @@ struct StemBwdArgs2 {
   const bf16_t* wk;      // [64][SKP] packed weights (the forward's)
   const bf16_t* pdy;     // [N][PH][PW][64] pooled gradient
   const uint8_t* code4;  // [N][PH][PW][32] window positions, 4 bits per channel, 15 = masked
-  const float* coef;     // [3][64] a, b, cc
-  float* dslab;          // [grid][64][SKH]
+  float* dslab;          // [grid][64][SKH]: D = dz^T X partials
+  float* gslab;          // [grid][GK][GK]: G = X^T X partials (upper-triangle tiles)
   int N, nimg;
+  int ablate;            // timing experiments only (DMLAB_STEM_ABLATE)
+  int split;             // m-steps of a pair's MFMA work before the mid-step barrier
+  unsigned long long* trace;  // timing experiments: [step][8] stamps of workgroup 0
   StemGeo G;
 };
 
 constexpr int PRING = 3;  // pooled-row ring: rows i, i+1 in use, i+2 staged
-constexpr int BNT = 768;  // 12 waves: 0-3 MFMA, 4-11 VALU
-constexpr int BVT = BNT - 256;
+constexpr int BNT = 1024;  // 16 waves: 0-7 MFMA, 8-15 VALU
+constexpr int BMW = 8;     // MFMA waves
+constexpr int BVT = BNT - 64 * BMW;
 
-// Warp-specialised backward.  Step stream per image: [stage E rows -3..3 + pooled rows 0..2,
-// stage rows 4..5, pair 0, ..., pair PH-1, (drain)]; the VALU waves build pair i's a*dz tile
-// T[i & 1] (and stage pair i+1's E rows) while the MFMA waves process pair i-1: recompute
-// its conv output y (weights resident in registers, C = [co][px]), turn T into
-// dy = a*dz + b*y + cc in place, then reduce dy^T x_col.  Two barriers per step: the y pass
-// of every MFMA wave completes before any wgrad read of T, and the VALU waves' S reads before
-// the raw rows of the next step overwrite it.
+// Warp-specialised backward.  Step stream per image: [stage raw rows 0..1 + pooled rows 0..2,
+// expand E rows -3..1, pair 0, ..., pair PH-1, (drain)]; the VALU waves route pair i's pooled
+// gradient into the dz tile T[i & 1] (and stage its E rows) while the MFMA waves accumulate
+// pair i-1's D and G tiles (slot 0 before the mid-step barrier, slot 1 after).  The barriers:
+// T and E hand-offs (step start) and the VALU waves' S reads before the next raw rows
+// overwrite it (mid-step).
 template <int DT>
 __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -550,13 +769,11 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
   const int PRB = G.PW * SCO;                                // pooled row elements
   bf16_t* Pg = S + 4 * G.SP;                                 // [PRING][PW][64] grads
   uint8_t* Pc = reinterpret_cast<uint8_t*>(Pg + PRING * PRB);  // [PRING][PW][32] 4-bit codes
-  float* cf = reinterpret_cast<float*>(Pc + PRING * PRB / 2);  // a, b, cc
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   {
     const int tot16 = (RING * G.ROWB + 2 * TB + 4 * G.SP * 2) / 16;
     for (int e = tid; e < tot16; e += BNT) reinterpret_cast<uint4*>(smem)[e] = make_uint4(0, 0, 0, 0);
   }
-  if (tid < 3 * SCO) cf[tid] = a.coef[tid];
   const int nimg = a.N > (int)blockIdx.x ? (a.N - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
   const int SPI = G.PH + 2;
   const int nsteps = nimg * SPI;  // + 1 drain step (the last pair's MFMA work)
@@ -566,87 +783,49 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
     row = row < 0 ? 0 : row >= a.nimg ? a.nimg - 1 : row;
     return row * G.Hin * G.Win * 3;
   };
-  if (wid < 4) {
+  if (wid < BMW) {
     // ================================================================ MFMA waves
-    // y pass: wave w owns co-block cb = w & 1 and px-blocks (w >> 1) * 2 + {0, 1} of BOTH
-    // slots (4 units); its A fragments (the weights of its 32 channels, 11 k-steps) stay in
-    // registers.  wgrad pass: pair_wgrad's wave roles with w and w + 4 of the 8-wave layout
-    // (slot, co-block, k-blocks) folded onto 4 waves: wave w does roles w and w + 4.
-    const int cb = wid & 1, hh = lane >> 5;
-    bf16x8 wa[11];
-#pragma unroll
-    for (int s = 0; s < 11; ++s)
-      wa[s] = *reinterpret_cast<const bf16x8*>(a.wk + (32 * cb + (lane & 31)) * SKP + 16 * s + 8 * hh);
-    f32x16 dacc[3];
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dacc[u][r] = 0.f;
-    __syncthreads();  // cf, zeroed LDS
-    for (int st = 0; st <= nsteps; ++st) {
-      __syncthreads();  // step start: T[(st-1) & 1] (a dz of the pair) and its E rows are ready
-      const int ps = st - 1;
-      const int pk = ps >= 0 ? ps % SPI : -1;
-      const bool work = ps >= 0 && pk >= 2;
-      const int i = pk - 2;
-      unsigned char* Tt = T + (ps & 1) * TB;
-      if (work) {
-        const int ring0 = (4 * i - 3 + 13 * 8) % RING;  // ring row of iy = 4i - 3
-#pragma unroll 1
-        for (int u = 0; u < 4; ++u) {
-          const int slot = u >> 1, mb = 2 * (wid >> 1) + (u & 1);
-          if (32 * mb >= G.Wout) continue;
-          const int pxb = min(32 * mb + (lane & 31), G.Wout - 1);
-          const int pxo = 32 * mb + (lane & 31);
-          f32x16 acc;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-          for (int s = 0; s < 11; ++s) {
-            const int j = 2 * s + hh;
-            int ky = j / 3;
-            const int part = j - 3 * ky;
-            if (ky > 6) ky = 6;
-            int rr = ring0 + 2 * slot + ky;  // iy = 2 oy - 3 + ky, oy = 2i + slot
-            rr = rr >= RING ? rr - RING : rr;
-            rr = rr >= RING ? rr - RING : rr;
-            const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(E + rr * G.ROWB + pxb * 48 + part * 16);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], bfr, acc, 0, 0, 0);
-          }
-          // C: col = px (lane & 31), row = co = 32 cb + (r & 3) + 8 (r >> 2) + 4 hh
-          if (pxo < G.Wout) {
-#pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-              const int co = 32 * cb + 8 * g4 + 4 * hh;
-              unsigned char* tp = Tt + yoff(slot, pxo, co >> 3, G.Wout) + 2 * (co & 7);
-              const uint2 t = *reinterpret_cast<const uint2*>(tp);
-              const float4 bv = *reinterpret_cast<const float4*>(cf + SCO + co);
-              const float4 cv = *reinterpret_cast<const float4*>(cf + 2 * SCO + co);
-              const float d0 = bf2f((bf16_t)(t.x & 0xffff)) + bv.x * acc[4 * g4 + 0] + cv.x;
-              const float d1 = bf2f((bf16_t)(t.x >> 16)) + bv.y * acc[4 * g4 + 1] + cv.y;
-              const float d2 = bf2f((bf16_t)(t.y & 0xffff)) + bv.z * acc[4 * g4 + 2] + cv.z;
-              const float d3 = bf2f((bf16_t)(t.y >> 16)) + bv.w * acc[4 * g4 + 3] + cv.w;
-              *reinterpret_cast<uint2*>(tp) = make_uint2(pack_bf2(d0, d1), pack_bf2(d2, d3));
-            }
-          }
+    f32x16 acc[5];
+    gram_zero<0>(acc);
+    __syncthreads();  // zeroed LDS
+    auto run = [&](auto wtag) {
+      constexpr int W = decltype(wtag)::value;
+      const bool tr = a.trace && blockIdx.x == 0 && W == 0;
+      for (int st = 0; st <= nsteps; ++st) {
+        if (tr) a.trace[st * 8 + 4] = stamp();
+        lds_barrier();  // step start: T[(st-1) & 1] (dz of the pair) and its E rows are ready
+        if (tr) a.trace[st * 8 + 5] = stamp();
+        const int ps = st - 1;
+        const int pk = ps >= 0 ? ps % SPI : -1;
+        const bool work = ps >= 0 && pk >= 2 && !(a.ablate & 1);
+        const unsigned char* Tt = T + (ps & 1) * TB;
+        // the VALU waves' gather runs before the mid-step barrier, their staging after it:
+        // m-steps [0, split) of the 2 * Wout / 16 before, the rest after
+        const int nt = G.Wout >> 4, split = min(a.split, 2 * nt);
+        if (work) {
+          gram_slot<W>(acc, Tt, E, G, pk - 2, 0, 0, min(split, nt), lane);
+          if (split > nt) gram_slot<W>(acc, Tt, E, G, pk - 2, 1, 0, split - nt, lane);
+        }
+        if (tr) a.trace[st * 8 + 6] = stamp();
+        lds_barrier();  // mid-step
+        if (tr) a.trace[st * 8 + 7] = stamp();
+        if (work) {
+          if (split < nt) gram_slot<W>(acc, Tt, E, G, pk - 2, 0, split, nt, lane);
+          gram_slot<W>(acc, Tt, E, G, pk - 2, 1, max(split - nt, 0), nt, lane);
         }
       }
-      __syncthreads();  // mid-step: every wave's dy is in T
-      if (work) {
-        pair_wgrad(dacc, Tt, E, G, i, wid, lane);      // slot 0
-        pair_wgrad(dacc, Tt, E, G, i, wid + 4, lane);  // slot 1
-      }
+      gram_store<W>(acc, a.dslab, a.gslab, lane);
+    };
+    switch (wid) {
+      case 0: run(std::integral_constant<int, 0>{}); break;
+      case 1: run(std::integral_constant<int, 1>{}); break;
+      case 2: run(std::integral_constant<int, 2>{}); break;
+      case 3: run(std::integral_constant<int, 3>{}); break;
+      case 4: run(std::integral_constant<int, 4>{}); break;
+      case 5: run(std::integral_constant<int, 5>{}); break;
+      case 6: run(std::integral_constant<int, 6>{}); break;
+      default: run(std::integral_constant<int, 7>{}); break;
     }
-    // slab: both slots' partials are in dacc (same co / k positions)
-    const int kq = (wid >> 1) & 1;
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = 32 * cb + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int k = 32 * (3 * kq + u) + (lane & 31);
-        a.dslab[(long long)blockIdx.x * SCO * SKH + co * SKH + k] = dacc[u][r];
-      }
     return;
   }
   // ================================================================== VALU waves
@@ -656,147 +835,180 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
   // MFMA waves read pair i-1's rows 4i-7..4i+1 meanwhile: 13 live rows, the ring's size.
   // Raw rows are stored into S after the mid-step barrier (the step's S reads are done) and
   // expanded the step after.
-  const int vt = tid - 256;
+  const int vt = tid - 64 * BMW;
   RawMap<BVT, FRU> rm;
-  rm.init(vt, G.Win);
+  rm.init(vt, G.Win, a.nsc, a.nbi);
   EMap em;
   em.init(vt, G.Wout);
   RawUnit ru[FRU];
   // pooled rows: PW * 8 chunks of (8 grads, 8 4-bit codes) per row; thread vt < PW*8 owns one
   const bool pl = vt < G.PW * 8;
-  uint4 pg_r = make_uint4(0, 0, 0, 0);
-  uint32_t pc_r = 0xffffffffu;
+  uint4 pg_r;
+  uint32_t pc_r;
+  bool p_ok = false;
+  // branch-free like RawMap::load: clamped addresses, validity applied at the store
   auto pload = [&](int q, int r) {
-    pg_r = make_uint4(0, 0, 0, 0);
-    pc_r = 0xffffffffu;  // rows past the image: masked windows
-    if (pl && r < G.PH) {
-      const long long o = (((long long)img_of(q) * G.PH + r) * G.PW) * SCO + vt * 8;
-      pg_r = *reinterpret_cast<const uint4*>(a.pdy + o);
-      pc_r = *reinterpret_cast<const uint32_t*>(a.code4 + o / 2);
-    }
+    p_ok = pl && r < G.PH;
+    const int rc = min(r, G.PH - 1), vc = pl ? vt : 0;
+    const long long o = (((long long)img_of(min(q, nimg - 1)) * G.PH + rc) * G.PW) * SCO + vc * 8;
+    pg_r = *reinterpret_cast<const uint4*>(a.pdy + o);
+    pc_r = *reinterpret_cast<const uint32_t*>(a.code4 + o / 2);
   };
   auto pstore = [&](int r) {
     if (!pl) return;
     const int sl = r % PRING;
-    *reinterpret_cast<uint4*>(Pg + sl * PRB + vt * 8) = pg_r;
-    *reinterpret_cast<uint32_t*>(Pc + (sl * PRB + vt * 8) / 2) = pc_r;
+    *reinterpret_cast<uint4*>(Pg + sl * PRB + vt * 8) = p_ok ? pg_r : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint32_t*>(Pc + (sl * PRB + vt * 8) / 2) = p_ok ? pc_r : 0xffffffffu;
   };
   const int qb = vt >> 3, qc = vt & 7, c0 = qc * 8;
-  __syncthreads();  // cf, zeroed LDS
-  float ka[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ka[j] = cf[c0 + j];
-  uint4 qg[4];     // the quad's windows: 8 pooled grads each
-  uint32_t qi[4];  // and their codes (15 everywhere for a window outside the image)
-  // a*dz of quad pixel pp = (ddy, ddx): the sum of the grads of the covering windows whose
-  // code names this pixel (window (wa, wb) sees it at kh = ddy ? (wa ? 0 : 2) : 1, same for kw)
-  auto gpix = [&](unsigned char* Tt, int pp) {
-    const int ddy = pp >> 1, ddx = pp & 1;
-    float d[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+  __syncthreads();  // zeroed LDS
+  // dz of quad pixel pp = (ddy, ddx), channels c0 + 4 hf .. +3: the sum of the grads of the
+  // covering windows whose code names this pixel (window (wa, wb) sees it at
+  // kh = ddy ? (wa ? 0 : 2) : 1, same for kw).  Half a chunk at a time keeps the live set small.
+  auto gquad = [&](unsigned char* Tt, int i, int hf) {
+    uint2 qg[4];     // the quad's windows: 4 pooled grads each
+    uint32_t qi[4];  // and their codes (15 everywhere for a window outside the image)
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const int wa = w >> 1, wb = w & 1;
-      if ((wa && !ddy) || (wb && !ddx)) continue;
-      const uint32_t gw[4] = {qg[w].x, qg[w].y, qg[w].z, qg[w].w};
-      const unsigned code = wcode(ddy ? (wa ? 0 : 2) : 1, ddx ? (wb ? 0 : 2) : 1);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t g = gw[j >> 1];
-        const float gf = __uint_as_float((j & 1) ? (g & 0xffff0000u) : (g << 16));
-        d[j] += (qi[w] & (15u << (4 * j))) == (code << (4 * j)) ? gf : 0.f;
-      }
+      const bool okw = i + wa < G.PH && qb + wb < G.PW;
+      const int sl = (i + wa) % PRING, col = okw ? qb + wb : qb;
+      qg[w] = *reinterpret_cast<const uint2*>(Pg + sl * PRB + col * SCO + c0 + 4 * hf);
+      qi[w] = okw ? *reinterpret_cast<const uint16_t*>(Pc + (sl * PRB + col * SCO + c0) / 2 + 2 * hf)
+                  : 0xffffu;
     }
-    uint32_t o[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = pack_bf2(ka[2 * k] * d[2 * k], ka[2 * k + 1] * d[2 * k + 1]);
-    *reinterpret_cast<uint4*>(Tt + yoff(ddy, 2 * qb + ddx, qc, G.Wout)) = make_uint4(o[0], o[1], o[2], o[3]);
+    for (int pp = 0; pp < 4; ++pp) {
+      const int ddy = pp >> 1, ddx = pp & 1;
+      float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int wa = w >> 1, wb = w & 1;
+        if ((wa && !ddy) || (wb && !ddx)) continue;
+        const uint32_t gw[2] = {qg[w].x, qg[w].y};
+        const unsigned code = wcode(ddy ? (wa ? 0 : 2) : 1, ddx ? (wb ? 0 : 2) : 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t g = gw[j >> 1];
+          const float gf = __uint_as_float((j & 1) ? (g & 0xffff0000u) : (g << 16));
+          d[j] += (qi[w] & (15u << (4 * j))) == (code << (4 * j)) ? gf : 0.f;
+        }
+      }
+      *reinterpret_cast<uint2*>(Tt + yoff(ddy, 2 * qb + ddx, qc, G.Wout) + 8 * hf) =
+          make_uint2(pack_bf2(d[0], d[1]), pack_bf2(d[2], d[3]));
+    }
   };
-  if (nimg > 0) rm.load<DT>(ru, a.img, img_base(0), G.Hin, G.Win, 0, 2, a.nsc, a.nbi);
+
+  // dataset row bases of the current and the next image, read once per image (a per-step
+  // index read is a vector load whose wait would drain the in-flight prefetches)
+  long long bcur = nimg > 0 ? img_base(0) : 0, bnext = nimg > 1 ? img_base(1) : 0;
+  int bq = 0;
+  auto base = [&](int qq) {
+    if (qq != bq) {
+      bcur = bnext;
+      bq = qq;
+      bnext = qq + 1 < nimg ? img_base(qq + 1) : 0;
+    }
+    return bcur;
+  };
+  if (nimg > 0) rm.load<DT>(ru, a.img, bcur, G.Hin, G.Win, 0, 2);
+  const bool trv = a.trace && blockIdx.x == 0 && vt < 64;
   for (int st = 0; st <= nsteps; ++st) {
     const int q = st / SPI, kk = st - q * SPI;
-    __syncthreads();  // (MFMA waves: step start)
+    if (trv) a.trace[st * 8 + 0] = stamp();
+    lds_barrier();  // (MFMA waves: step start)
+    if (trv) a.trace[st * 8 + 1] = stamp();
     // ---- phase 1 (MFMA waves: y pass of the previous step's pair)
     if (st < nsteps) {
       if (kk == 0) {
-        rm.store(ru, S, G.SP, 2);  // rows 0..1
+        rm.store<DT>(ru, S, G.SP, 2);  // rows 0..1
         pload(q, 0);
         pstore(0);
         pload(q, 1);
         pstore(1);
-        pload(q, 2);
-        pstore(2);
-        pload(q, 3);
-        rm.load<DT>(ru, a.img, img_base(q), G.Hin, G.Win, 2, 4, a.nsc, a.nbi);
+        pload(q, 2);  // stored at pair 0
+        rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 2, 4);
       } else if (kk == 1) {
         em.build(E, S, G, -3, 5, -3);
       } else {
         const int i = kk - 2;
-        em.build(E, S, G, 4 * i + 2, 4, 0);
-        if (pl) {
-          // the quad's 4 windows: pooled rows i (+1), columns qb (+1); pixels (0,0), (1,1) now,
-          // (0,1), (1,0) after the mid-step barrier (5 + 4 window tests: balances the phases)
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const int wa = w >> 1, wb = w & 1;
-            const bool okw = i + wa < G.PH && qb + wb < G.PW;
-            const int sl = (i + wa) % PRING, col = okw ? qb + wb : qb;
-            qg[w] = *reinterpret_cast<const uint4*>(Pg + sl * PRB + col * SCO + c0);
-            qi[w] = okw ? *reinterpret_cast<const uint32_t*>(Pc + (sl * PRB + col * SCO + c0) / 2)
-                        : 0xffffffffu;
-          }
-          gpix(T + (st & 1) * TB, 0);
-          gpix(T + (st & 1) * TB, 3);
-        }
+        // pooled ring: rows i, i+1 are gathered this step (both phases); row i+2 goes into
+        // the slot of row i-1 (last read in the previous step); row i+3 is loaded
+        pstore(i + 2);
+        pload(q, i + 3);
+        if (!(a.ablate & 8)) em.build(E, S, G, 4 * i + 2, 4, 0);
+        // the quad's 4 windows: pooled rows i (+1), columns qb (+1); channels 0..3 of the
+        // chunk now, 4..7 after the mid-step barrier (each half reloads its windows)
+        if (pl && !(a.ablate & 4)) gquad(T + (st & 1) * TB, i, 0);
       }
     }
-    __syncthreads();  // (MFMA waves: mid-step) this step's S and pooled-ring reads are done
+    if (trv) a.trace[st * 8 + 2] = stamp();
+    lds_barrier();  // (MFMA waves: mid-step) this step's S and pooled-ring reads are done
+    if (trv) a.trace[st * 8 + 3] = stamp();
     // ---- phase 2 (MFMA waves: wgrad of the previous step's pair)
     if (st < nsteps) {
       if (kk == 1) {
-        rm.store(ru, S, G.SP, 4);  // rows 2..5
-        if (G.PH > 1) rm.load<DT>(ru, a.img, img_base(q), G.Hin, G.Win, 6, 4, a.nsc, a.nbi);
+        rm.store<DT>(ru, S, G.SP, 4);  // rows 2..5
+        if (G.PH > 1) rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 6, 4);
       } else if (kk >= 2) {
         const int i = kk - 2;
-        if (pl) {
-          gpix(T + (st & 1) * TB, 1);
-          gpix(T + (st & 1) * TB, 2);
-        }
-        if (i + 1 < G.PH) {
-          rm.store(ru, S, G.SP, 4);  // rows 4i+6..4i+9 (pair i+1's new rows)
-          pstore(i + 3);             // row i's slot: its last reader was this step's gather
-          pload(q, i + 4);
-        }
-        if (i + 2 < G.PH) rm.load<DT>(ru, a.img, img_base(q), G.Hin, G.Win, 4 * i + 10, 4, a.nsc, a.nbi);
+        if (pl && !(a.ablate & 4)) gquad(T + (st & 1) * TB, i, 1);
+        if (trv) a.trace[16384 + st * 4 + 0] = stamp();
+        if (i + 1 < G.PH) rm.store<DT>(ru, S, G.SP, 4);  // rows 4i+6..4i+9 (pair i+1's new rows)
+        if (trv) a.trace[16384 + st * 4 + 1] = stamp();
+        if (trv) a.trace[16384 + st * 4 + 2] = stamp();
+        if (i + 2 < G.PH) rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 4 * i + 10, 4);
         else if (i + 2 == G.PH && q + 1 < nimg)
-          rm.load<DT>(ru, a.img, img_base(q + 1), G.Hin, G.Win, 0, 2, a.nsc, a.nbi);
+          rm.load<DT>(ru, a.img, bnext, G.Hin, G.Win, 0, 2);
       }
     }
   }
 }
 
-// dW[co][c][ky][kx] = beta * dW + sum_g slab[g][co][k], k = ky*24 + kx*3 + c.  One
-// workgroup per output channel; each of the 4 lane groups sums a quarter of the slabs in
-// order, the quarters are combined in order (deterministic).
-__global__ void __launch_bounds__(256) stem_wreduce_kernel(const float* __restrict__ dslab, int GD,
-                                                           float* __restrict__ dw, float beta) {
-  __shared__ float part[4][SKH];
-  const int co = blockIdx.x, t = threadIdx.x, k = t & 63, gq = t >> 6;
+// Fixed-order sums of the per-workgroup D and G slabs (one thread per element, 4 partial
+// chains combined in order): dsum [64][SKH], gsum [GK][GK] (upper-triangle tiles meaningful)
+__global__ void __launch_bounds__(256) stem_slab_reduce_kernel(const float* __restrict__ dslab,
+                                                               const float* __restrict__ gslab,
+                                                               int GD, float* __restrict__ dsum,
+                                                               float* __restrict__ gsum) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const int nd = SCO * SKH, ng = GK * GK;
+  if (e >= nd + ng) return;
+  const float* src = e < nd ? dslab + e : gslab + (e - nd);
+  const long long stride = e < nd ? nd : ng;
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  int gi = 0;
+  for (; gi + 4 <= GD; gi += 4)
 #pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    float s = 0.f;
-    for (int g = gq; g < GD; g += 4) s += dslab[((long long)g * SCO + co) * SKH + k + 64 * u];
-    part[gq][k + 64 * u] = s;
-  }
+    for (int u = 0; u < 4; ++u) s4[u] += src[(long long)(gi + u) * stride];
+  for (; gi < GD; ++gi) s4[0] += src[(long long)gi * stride];
+  const float v = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  if (e < nd) dsum[e] = v;
+  else gsum[e - nd] = v;
+}
+
+// dW[co][c][ky][kx] = beta * dW + a D[co][k] + b (W G)[co][k] + cc G[GONE][k], k = ky*24 + kx*3 + c
+__global__ void __launch_bounds__(256) stem_wcombine_kernel(const float* __restrict__ dsum,
+                                                            const float* __restrict__ gsum,
+                                                            const bf16_t* __restrict__ wk,
+                                                            const float* __restrict__ coef,
+                                                            float* __restrict__ dw, float beta) {
+  __shared__ float wrow[SKP];
+  const int co = blockIdx.x, t = threadIdx.x;
+  for (int k = t; k < SKP; k += 256) wrow[k] = bf2f(wk[co * SKP + k]);
   __syncthreads();
-  for (int e = t; e < 147; e += 256) {
-    const int ky = e / 21, rem = e - 21 * ky, kx = rem / 3, c = rem - 3 * kx;
-    const int kk = ky * 24 + kx * 3 + c;
-    const float d = ((part[0][kk] + part[1][kk]) + part[2][kk]) + part[3][kk];
-    float* o = dw + ((co * 3 + c) * 7 + ky) * 7 + kx;
-    *o = (beta != 0.f ? beta * *o : 0.f) + d;
+  if (t >= 147) return;
+  const int ky = t / 21, rem = t - 21 * ky, kx = rem / 3, c = rem - 3 * kx;
+  const int k = ky * 24 + kx * 3 + c;
+  float wg = 0.f;
+  for (int j = 0; j < SKP; ++j) {
+    const float gv = j <= k ? gsum[j * GK + k] : gsum[k * GK + j];  // symmetric: upper tiles
+    wg = fmaf(wrow[j], gv, wg);
   }
+  const float colsum = GONE <= k ? gsum[GONE * GK + k] : gsum[k * GK + GONE];
+  const float d = coef[co] * dsum[co * SKH + k] + coef[SCO + co] * wg + coef[2 * SCO + co] * colsum;
+  float* o = dw + ((co * 3 + c) * 7 + ky) * 7 + kx;
+  *o = (beta != 0.f ? beta * *o : 0.f) + d;
 }
 
 // OIHW fp32 [64][3][7][7] -> [64][SKP] bf16, k = ky*24 + kx*3 + c (pads zero)
@@ -836,9 +1048,20 @@ static size_t fwd_smem(const StemGeo& G) {
   return (size_t)RING * G.ROWB + (size_t)2 * 2 * G.Wout * 128 + (size_t)2 * 4 * G.SP * 2;
 }
 static size_t bwd_smem(const StemGeo& G) {
-  // E ring + 2 tiles + S (4 rows) + pooled ring (bf16 grads + 4-bit codes) + coefficients
+  // E ring + 2 dz tiles + S (4 rows) + pooled ring (bf16 grads + 4-bit codes)
   return (size_t)RING * G.ROWB + (size_t)2 * 2 * G.Wout * 128 + (size_t)4 * G.SP * 2 +
-         (size_t)PRING * G.PW * SCO * 2 + (size_t)PRING * G.PW * SCO / 2 + 3 * SCO * 4;
+         (size_t)PRING * G.PW * SCO * 2 + (size_t)PRING * G.PW * SCO / 2;
+}
+
+// DMLAB_STEM_ABLATE=<bits>: timing experiments (wrong results): 1 conv MFMAs, 2 wgrad MFMAs,
+// 4 pooling / gather, 8 E expansion
+static int stem_ablate() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DMLAB_STEM_ABLATE");
+    v = e ? atoi(e) : 0;
+  }
+  return v;
 }
 
 int stem_fused_grid(int N) {
@@ -870,6 +1093,7 @@ void stem_fwd_fused(const void* img, int dtype, const long long* idx, const floa
   a.N = N;
   a.nimg = nimg;
   a.G = stem_geo(Hin, Win);
+  a.ablate = stem_ablate();
   const size_t sm = fwd_smem(a.G);
 #define DM_SF(DT)                                              \
   do {                                                         \
@@ -894,7 +1118,7 @@ void stem_pool_apply(const bf16_t* pext, const uint8_t* code, const float* scale
 
 void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const float* nsc,
                      const float* nbi, const bf16_t* wk, const bf16_t* pdy, const uint8_t* code4,
-                     const float* coef, float* dslab, int N, int nimg, int Hin, int Win, int grid,
+                     float* dslab, float* gslab, int N, int nimg, int Hin, int Win, int grid,
                      hipStream_t st) {
   StemBwdArgs2 a;
   a.img = img;
@@ -906,11 +1130,28 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
   a.wk = wk;
   a.pdy = pdy;
   a.code4 = code4;
-  a.coef = coef;
   a.dslab = dslab;
+  a.gslab = gslab;
   a.N = N;
   a.nimg = nimg;
   a.G = stem_geo(Hin, Win);
+  a.ablate = stem_ablate();
+  {
+    static int sp = -1;
+    if (sp < 0) {
+      const char* e = getenv("DMLAB_STEM_SPLIT");  // tuning: default 10 of 14 at W 224
+      sp = e ? atoi(e) : 0;
+    }
+    a.split = sp > 0 ? sp : (2 * (a.G.Wout >> 4) * 5 + 6) / 7;
+  }
+  static unsigned long long* trace_buf = nullptr;
+  const bool trace = getenv("DMLAB_STEM_TRACE") != nullptr;
+  const int nst = ((N + grid - 1) / grid) * (a.G.PH + 2) + 1;
+  if (trace && !trace_buf) {
+    DM_CHECK(hipMalloc(&trace_buf, 8 * 8 * 4096));
+    DM_CHECK(hipMemset(trace_buf, 0, 8 * 8 * 4096));
+  }
+  a.trace = trace && nst <= 4096 ? trace_buf : nullptr;
   const size_t sm = bwd_smem(a.G);
 #define DM_SB(DT)                                              \
   do {                                                         \
@@ -922,12 +1163,59 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
   else DM_SB(2);
 #undef DM_SB
   DM_CHECK(hipGetLastError());
+  if (a.trace) {  // per-step medians of workgroup 0's phases (s_memtime units)
+    std::vector<unsigned long long> h((size_t)nst * 8), h2((size_t)nst * 4);
+    DM_CHECK(hipStreamSynchronize(st));
+    DM_CHECK(hipMemcpy(h.data(), a.trace, h.size() * 8, hipMemcpyDeviceToHost));
+    DM_CHECK(hipMemcpy(h2.data(), a.trace + 16384, h2.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> col[12];
+    for (int s2 = 1; s2 + 1 < nst; ++s2) {
+      const unsigned long long* r = &h[(size_t)s2 * 8];
+      const unsigned long long* nx = &h[(size_t)(s2 + 1) * 8];
+      const unsigned long long* r2 = &h2[(size_t)s2 * 4];
+      col[0].push_back((double)(r[2] - r[1]));   // VALU phase 1
+      col[1].push_back((double)(r[3] - r[2]));   // VALU mid wait
+      col[2].push_back((double)(nx[0] - r[3]));  // VALU phase 2
+      col[3].push_back((double)(nx[1] - nx[0])); // VALU step-start wait
+      col[4].push_back((double)(r[6] - r[5]));   // MFMA phase 1
+      col[5].push_back((double)(r[7] - r[6]));
+      col[6].push_back((double)(nx[4] - r[7]));
+      col[7].push_back((double)(nx[5] - nx[4]));
+      col[8].push_back((double)(nx[0] - r[0]));  // whole step
+      if (r2[0] >= r[3] && r2[2] <= nx[0] && r2[0]) {
+        col[9].push_back((double)(r2[0] - r[3]));
+        col[10].push_back((double)(r2[2] - r2[0]));
+        col[11].push_back((double)(nx[0] - r2[2]));
+      }
+    }
+    auto med = [](std::vector<double> v) {
+      if (v.empty()) return 0.0;
+      std::sort(v.begin(), v.end());
+      return v[v.size() / 2];
+    };
+    const double tot = (double)(h[(size_t)(nst - 1) * 8] - h[8]) / (nst - 2);
+    fprintf(stderr,
+            "stem_bwd trace (medians, units/step; mean step %.0f): step %.0f | VALU p1 %.0f wait %.0f "
+            "p2 %.0f wait %.0f [p2: gather %.0f raw %.0f rest %.0f] | MFMA p1 %.0f wait %.0f p2 %.0f "
+            "wait %.0f\n",
+            tot, med(col[8]), med(col[0]), med(col[1]), med(col[2]), med(col[3]), med(col[9]),
+            med(col[10]), med(col[11]), med(col[4]), med(col[5]), med(col[6]), med(col[7]));
+  }
+
 }
 
-void stem_wreduce(const float* dslab, int GD, float* dw, float beta, hipStream_t st) {
-  stem_wreduce_kernel<<<SCO, 256, 0, st>>>(dslab, GD, dw, beta);
+void stem_wcombine(const float* dslab, const float* gslab, int GD, const bf16_t* wk,
+                   const float* coef, float* sums, float* dw, float beta, hipStream_t st) {
+  const int n = SCO * SKH + GK * GK;
+  float* dsum = sums;
+  float* gsum = sums + SCO * SKH;
+  stem_slab_reduce_kernel<<<(n + 255) / 256, 256, 0, st>>>(dslab, gslab, GD, dsum, gsum);
+  DM_CHECK(hipGetLastError());
+  stem_wcombine_kernel<<<SCO, 256, 0, st>>>(dsum, gsum, wk, coef, dw, beta);
   DM_CHECK(hipGetLastError());
 }
+int stem_gram_cols() { return GK; }
+int stem_sums_len() { return SCO * SKH + GK * GK; }
 
 void stem_pack_weights(const float* w, bf16_t* wk, hipStream_t st) {
   stem_pack_weights_kernel<<<(SCO * SKP + 255) / 256, 256, 0, st>>>(w, wk);

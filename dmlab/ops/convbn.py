@@ -318,7 +318,7 @@ def _stem_fused_bwd(layer, dout, ctx):
     grid = L.stem_fused_grid(B)
     f32 = dict(device=dout.device, dtype=torch.float32)
     work = torch.empty(L.bn_bwd_work(ctx["M"], 64), **f32)
-    dslab = torch.empty(grid * 64 * L.stem_slab_cols(), **f32)
+    dslab = torch.empty(L.stem_bwd_slab_len(grid), **f32)
     L.stem_bwd_fused2(ctx["img"], ctx["gidx"], ctx["nsc"], ctx["nbi"], ctx["wk"], dout, code,
                       ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
                       layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc,

@@ -151,7 +151,7 @@ def test_stem_fused_backward_matches_autograd(dev, dtype, H):
     dgamma, dbeta = torch.zeros(64, **f), torch.zeros(64, **f)
     dw = torch.zeros(64, 3, 7, 7, **f)
     work = torch.empty(L.bn_bwd_work(M, 64), **f)
-    dslab = torch.empty(L.stem_fused_grid(B) * 64 * L.stem_slab_cols(), **f)
+    dslab = torch.empty(L.stem_bwd_slab_len(L.stem_fused_grid(B)), **f)
     sc, bi = input_affine(img.dtype)
     L.stem_bwd_fused2(img, idx, sc, bi, wk, g, code4, mean, invstd, gamma, dgamma, dbeta, 0.0,
                       part, rows, dw, 0.0, work, dslab, L.stem_fused_grid(B))

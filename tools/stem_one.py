@@ -55,7 +55,7 @@ def main():
     dgamma, dbeta = torch.zeros(64, **f), torch.zeros(64, **f)
     dw = torch.zeros(64, 3, 7, 7, **f)
     work = torch.empty(L.bn_bwd_work(M, 64), **f)
-    dslab = torch.empty(grid * 64 * L.stem_slab_cols(), **f)
+    dslab = torch.empty(L.stem_bwd_slab_len(grid), **f)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     tt = [0.0] * 4
     for it in range(a.iters + 2):
