@@ -196,10 +196,13 @@ def test_stem_fused_backward_matches_autograd(dev, dtype, H):
 
 def test_resnet18_fused_stem_matches_s2d_stem(dev, monkeypatch):
     """The whole model with the fused stem vs the space-to-depth stem (same weights, same
-    fp32 batch): the loss and every gradient downstream of the stem agree to bf16 level.
-    (The stem's own gradients are compared against float64 above: the two paths break
-    max-pool near-ties differently -- bf16 y vs bf16 BN output -- so their routing of the
-    pooled gradient differs by design.)"""
+    fp32 batch).  A randomly initialised ResNet-18 in training mode at a small batch is
+    ill-conditioned: BatchNorm over a few elements per channel in the deep layers amplifies
+    bf16-level differences (measured: a 2^-8 relative input perturbation moves the layer-1
+    weight gradient by ~50 % on the s2d path itself).  So the check is relative to that
+    sensitivity: the fused-vs-s2d difference of every downstream gradient stays within
+    twice what the s2d path shows between the batch and a 2^-8-perturbed copy, and the loss
+    agrees to 1 %.  (The stem's own gradients are compared against float64 above.)"""
     from dmlab.models import ResNet18
     from dmlab.nn import cross_entropy
 
@@ -207,21 +210,27 @@ def test_resnet18_fused_stem_matches_s2d_stem(dev, monkeypatch):
     a = ResNet18(num_classes=10).to(dev)
     x = torch.rand(8, 3, 64, 64, device=dev)
     y = torch.randint(0, 10, (8,), device=dev)
-    res = []
-    for fused in ("1", "0"):
+    xp = x * (1 + 2 ** -8 * torch.randn_like(x))
+
+    def run(fused, xx):
         monkeypatch.setenv("DMLAB_STEM_FUSED", fused)
         a.flat.grad.zero_()
-        loss = cross_entropy(a(x), y)
+        loss = cross_entropy(a(xx), y)
         loss.backward()
         torch.cuda.synchronize()
-        res.append((loss.item(), {n: p.grad.detach().clone() for n, p in a.named_parameters()}))
-    (la, ga), (lb, gb) = res
+        return loss.item(), {n: p.grad.detach().clone() for n, p in a.named_parameters()}
+
+    (la, ga), (lb, gb), (_, gp) = run("1", x), run("0", x), run("0", xp)
     assert abs(la - lb) < 1e-2 * max(1.0, abs(lb))
+
+    def rel(u, v):
+        return ((u - v).norm() / (v.norm() + 1e-12)).item()
+
     for n in ga:
         if n.startswith("stem."):
             continue
-        e = ((ga[n] - gb[n]).norm() / (gb[n].norm() + 1e-12)).item()
-        assert e < 0.1, (n, e)
+        e, base = rel(ga[n], gb[n]), rel(gp[n], gb[n])
+        assert e < 2 * base + 0.02, (n, e, base)
 
 
 def test_resnet18_u8_gathered_batch(dev, monkeypatch):
