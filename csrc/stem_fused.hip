@@ -190,19 +190,34 @@ struct EMap {
   }
   // E rows iy0 .. iy0 + nrows - 1; S row of iy is srow0 + (iy - iy0) (rows outside [0, Hin):
   // zeros, no S read)
+  // (all the rows' S reads are issued before the first E write: one LDS round trip, not nrows)
   __device__ __forceinline__ void build(unsigned char* E, const bf16_t* S, const StemGeo& G, int iy0,
                                         int nrows, int srow0) const {
     if (!act) return;
-    for (int q = 0; q < nrows; ++q) {
+    if (nrows == 4) build_n<4>(E, S, G, iy0, srow0);
+    else if (nrows == 2) build_n<2>(E, S, G, iy0, srow0);
+    else for (int q = 0; q < nrows; ++q) build_n<1>(E, S, G, iy0 + q, srow0 + q);
+  }
+  template <int NR>
+  __device__ __forceinline__ void build_n(unsigned char* E, const bf16_t* S, const StemGeo& G,
+                                          int iy0, int srow0) const {
+    uint32_t w[NR][4];
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      // rows outside the image read a clamped in-buffer row (zeroed below: no branch joins)
+      const int sr = min(max(srow0 + q, 0), 3);
+      const uint32_t* sp = reinterpret_cast<const uint32_t*>(S + sr * G.SP + soff);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[q][j] = sp[j];
+    }
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
       const int iy = iy0 + q;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (iy >= 0 && iy < G.Hin) {
-        const uint32_t* sp = reinterpret_cast<const uint32_t*>(S + (srow0 + q) * G.SP + soff);
-        v = make_uint4(sp[0], sp[1], sp[2], sp[3]);
-        if (part == 2) {  // elements 21..23 of the expanded row: 1.0 (the backward's all-ones
-          v.z = (v.z & 0xffffu) | 0x3f800000u;  // X column, zero weight), 0, 0
-          v.w = 0;
-        }
+      const bool in = iy >= 0 && iy < G.Hin;
+      uint4 v = make_uint4(in ? w[q][0] : 0u, in ? w[q][1] : 0u, in ? w[q][2] : 0u, in ? w[q][3] : 0u);
+      if (part == 2) {  // elements 21..23 of the expanded row: 1.0 (the backward's all-ones
+        v.z = in ? (v.z & 0xffffu) | 0x3f800000u : 0u;  // X column, zero weight), 0, 0
+        v.w = 0;
       }
       *reinterpret_cast<uint4*>(E + ring_of(iy) * G.ROWB + eoff) = v;
     }
@@ -865,17 +880,26 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
   // dz of quad pixel pp = (ddy, ddx), channels c0 + 4 hf .. +3: the sum of the grads of the
   // covering windows whose code names this pixel (window (wa, wb) sees it at
   // kh = ddy ? (wa ? 0 : 2) : 1, same for kw).  Half a chunk at a time keeps the live set small.
-  auto gquad = [&](unsigned char* Tt, int i, int hf) {
+  // per-thread constants of the gather: the quad's two window columns (clamped; a column past
+  // the row is masked by its code) and its 4 pixels' tile offsets
+  const bool colok = qb + 1 < G.PW;
+  const int ocol0 = qb * SCO + c0, ocol1 = (colok ? qb + 1 : qb) * SCO + c0;
+  int toff[4];
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) toff[pp] = yoff(pp >> 1, 2 * qb + (pp & 1), qc, G.Wout);
+  uint2 gres[4];  // channels 0..3 of the 4 pixels, held across the mid-step barrier
+  auto gquad = [&](uint2 (&res)[4], int i, int hf) {
     uint2 qg[4];     // the quad's windows: 4 pooled grads each
     uint32_t qi[4];  // and their codes (15 everywhere for a window outside the image)
+    const int sl0 = i % PRING, sl1 = sl0 + 1 == PRING ? 0 : sl0 + 1;  // rows i, i+1 (uniform)
+    const bool rowok = i + 1 < G.PH;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       const int wa = w >> 1, wb = w & 1;
-      const bool okw = i + wa < G.PH && qb + wb < G.PW;
-      const int sl = (i + wa) % PRING, col = okw ? qb + wb : qb;
-      qg[w] = *reinterpret_cast<const uint2*>(Pg + sl * PRB + col * SCO + c0 + 4 * hf);
-      qi[w] = okw ? *reinterpret_cast<const uint16_t*>(Pc + (sl * PRB + col * SCO + c0) / 2 + 2 * hf)
-                  : 0xffffu;
+      const int o = (wa ? sl1 : sl0) * PRB + (wb ? ocol1 : ocol0);
+      qg[w] = *reinterpret_cast<const uint2*>(Pg + o + 4 * hf);
+      const uint32_t c = *reinterpret_cast<const uint16_t*>(Pc + o / 2 + 2 * hf);
+      qi[w] = ((wa && !rowok) || (wb && !colok)) ? 0xffffu : c;
     }
 #pragma unroll
     for (int pp = 0; pp < 4; ++pp) {
@@ -894,10 +918,10 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
           d[j] += (qi[w] & (15u << (4 * j))) == (code << (4 * j)) ? gf : 0.f;
         }
       }
-      *reinterpret_cast<uint2*>(Tt + yoff(ddy, 2 * qb + ddx, qc, G.Wout) + 8 * hf) =
-          make_uint2(pack_bf2(d[0], d[1]), pack_bf2(d[2], d[3]));
+      res[pp] = make_uint2(pack_bf2(d[0], d[1]), pack_bf2(d[2], d[3]));
     }
   };
+
 
   // dataset row bases of the current and the next image, read once per image (a per-step
   // index read is a vector load whose wait would drain the in-flight prefetches)
@@ -939,7 +963,7 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
         if (!(a.ablate & 8)) em.build(E, S, G, 4 * i + 2, 4, 0);
         // the quad's 4 windows: pooled rows i (+1), columns qb (+1); channels 0..3 of the
         // chunk now, 4..7 after the mid-step barrier (each half reloads its windows)
-        if (pl && !(a.ablate & 4)) gquad(T + (st & 1) * TB, i, 0);
+        if (pl && !(a.ablate & 4)) gquad(gres, i, 0);
       }
     }
     if (trv) a.trace[st * 8 + 2] = stamp();
@@ -952,7 +976,16 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
         if (G.PH > 1) rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 6, 4);
       } else if (kk >= 2) {
         const int i = kk - 2;
-        if (pl && !(a.ablate & 4)) gquad(T + (st & 1) * TB, i, 1);
+        if (pl && !(a.ablate & 4)) {
+          uint2 r1[4];
+          gquad(r1, i, 1);
+          // whole 16-byte chunks: 8-lane groups of ds_write_b128 fill a pixel row, conflict-free
+          // (half-chunk 8-byte writes of same-parity pixels were 4-way bank conflicts)
+          unsigned char* Tt = T + (st & 1) * TB;
+#pragma unroll
+          for (int pp = 0; pp < 4; ++pp)
+            *reinterpret_cast<uint4*>(Tt + toff[pp]) = make_uint4(gres[pp].x, gres[pp].y, r1[pp].x, r1[pp].y);
+        }
         if (trv) a.trace[16384 + st * 4 + 0] = stamp();
         if (i + 1 < G.PH) rm.store<DT>(ru, S, G.SP, 4);  // rows 4i+6..4i+9 (pair i+1's new rows)
         if (trv) a.trace[16384 + st * 4 + 1] = stamp();
