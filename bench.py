@@ -273,6 +273,16 @@ def main():
             # samples through it and advances the cursor itself (no per-step host work)
             cur = loader.cursor()
             ds = loader.dataset
+            # the captures' eager warm-up steps are not part of the run: snapshot the weights,
+            # the momentum buffer and the step counter, restore them in place afterwards (as
+            # dmlab.tasks.common.train_fused does), so every --graph-steps value trains the
+            # same step sequence from the same state
+            flat = model.flat
+            buf = getattr(opt, "buf", None)
+            saved = (flat.data.clone(), buf.clone() if buf is not None else None,
+                     getattr(opt, "step_count", 0))
+            if getattr(opt, "step_count", 0) == 0:
+                opt.step_count = 1  # capture the not-first-step update: buf = m*0 + g = g
             cap = CapturedStep(lambda x, y: train_step(x, y, cursor=cur),
                                [ds.images, ds.labels], warmup=3, bind_inputs=True)
             kg = max(1, a.graph_steps)
@@ -307,6 +317,12 @@ def main():
             def step_reset():  # the timed region starts on a fresh replay
                 state["credit"] = 0
 
+            with torch.no_grad():
+                flat.data.copy_(saved[0])
+                flat.mark_updated()
+                if buf is not None:
+                    buf.copy_(saved[1])
+            opt.step_count = saved[2]
             # restart the epoch after the capture warm-up advanced the cursor
             cur.refill(0)
         else:
