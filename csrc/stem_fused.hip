@@ -803,6 +803,8 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
     f32x16 acc[5];
     gram_zero<0>(acc);
     __syncthreads();  // zeroed LDS
+    EMap em;  // the E expansion runs here, after the step's Gram work (the VALU waves are the
+    em.init(tid, G.Wout);  // busier side): rows of pair kk-2 from the S rows stored this step
     auto run = [&](auto wtag) {
       constexpr int W = decltype(wtag)::value;
       const bool tr = a.trace && blockIdx.x == 0 && W == 0;
@@ -828,6 +830,13 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
           if (split < nt) gram_slot<W>(acc, Tt, E, G, pk - 2, 0, split, nt, lane);
           gram_slot<W>(acc, Tt, E, G, pk - 2, 1, max(split - nt, 0), nt, lane);
         }
+        // E rows: kk = 1 -> rows -3..1 (S rows 0..1), kk = i + 2 -> rows 4i+2..4i+5 (pair i's
+        // new rows; pair i-1's 4i-7..4i+1 are being read: 13 live rows, the ring)
+        if (st < nsteps && !(a.ablate & 8)) {
+          const int kk = st % SPI;
+          if (kk == 1) em.build(E, S, G, -3, 5, -3);
+          else if (kk >= 2) em.build(E, S, G, 4 * (kk - 2) + 2, 4, 0);
+        }
       }
       gram_store<W>(acc, a.dslab, a.gslab, lane);
     };
@@ -844,17 +853,14 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
     return;
   }
   // ================================================================== VALU waves
-  // Per image (SPI = PH + 2 steps): kk = 0 stages raw rows 0..1 and pooled rows 0..2 (the
-  // MFMA waves finish the previous image's last pair); kk = 1 expands E rows -3..1; kk = i + 2
-  // expands rows 4i+2..4i+5 (the new rows of pair i) and gathers pair i's a*dz into T.  The
-  // MFMA waves read pair i-1's rows 4i-7..4i+1 meanwhile: 13 live rows, the ring's size.
-  // Raw rows are stored into S after the mid-step barrier (the step's S reads are done) and
-  // expanded the step after.
+  // Per image (SPI = PH + 2 steps): kk = 0 stages pooled rows 0..2 (the MFMA waves finish the
+  // previous image's last pair); kk = 1 stores raw rows 0..1 (expanded to E rows -3..1 by the
+  // MFMA waves after the mid-step barrier); kk = i + 2 stores rows 4i+2..4i+5 (pair i's new
+  // rows) and routes pair i's pooled gradient into the dz tile T.  The MFMA waves read pair
+  // i-1's rows 4i-7..4i+1 meanwhile: 13 live rows, the ring's size.
   const int vt = tid - 64 * BMW;
   RawMap<BVT, FRU> rm;
   rm.init(vt, G.Win, a.nsc, a.nbi);
-  EMap em;
-  em.init(vt, G.Wout);
   RawUnit ru[FRU];
   // pooled rows: PW * 8 chunks of (8 grads, 8 4-bit codes) per row; thread vt < PW*8 owns one
   const bool pl = vt < G.PW * 8;
@@ -935,32 +941,31 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
     }
     return bcur;
   };
-  if (nimg > 0) rm.load<DT>(ru, a.img, bcur, G.Hin, G.Win, 0, 2);
   const bool trv = a.trace && blockIdx.x == 0 && vt < 64;
+  // raw rows: stored into S before the mid-step barrier of step kk (the MFMA waves expand them
+  // after it), loaded during step kk - 1: kk = 1 rows 0..1, kk = i + 2 rows 4i+2..4i+5
   for (int st = 0; st <= nsteps; ++st) {
     const int q = st / SPI, kk = st - q * SPI;
     if (trv) a.trace[st * 8 + 0] = stamp();
     lds_barrier();  // (MFMA waves: step start)
     if (trv) a.trace[st * 8 + 1] = stamp();
-    // ---- phase 1 (MFMA waves: y pass of the previous step's pair)
+    // ---- phase 1 (MFMA waves: the first m-steps of the previous step's pair)
     if (st < nsteps) {
       if (kk == 0) {
-        rm.store<DT>(ru, S, G.SP, 2);  // rows 0..1
         pload(q, 0);
         pstore(0);
         pload(q, 1);
         pstore(1);
         pload(q, 2);  // stored at pair 0
-        rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 2, 4);
       } else if (kk == 1) {
-        em.build(E, S, G, -3, 5, -3);
+        rm.store<DT>(ru, S, G.SP, 2);  // rows 0..1
       } else {
         const int i = kk - 2;
         // pooled ring: rows i, i+1 are gathered this step (both phases); row i+2 goes into
         // the slot of row i-1 (last read in the previous step); row i+3 is loaded
         pstore(i + 2);
         pload(q, i + 3);
-        if (!(a.ablate & 8)) em.build(E, S, G, 4 * i + 2, 4, 0);
+        rm.store<DT>(ru, S, G.SP, 4);  // rows 4i+2..4i+5
         // the quad's 4 windows: pooled rows i (+1), columns qb (+1); channels 0..3 of the
         // chunk now, 4..7 after the mid-step barrier (each half reloads its windows)
         if (pl && !(a.ablate & 4)) gquad(gres, i, 0);
@@ -969,12 +974,13 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
     if (trv) a.trace[st * 8 + 2] = stamp();
     lds_barrier();  // (MFMA waves: mid-step) this step's S and pooled-ring reads are done
     if (trv) a.trace[st * 8 + 3] = stamp();
-    // ---- phase 2 (MFMA waves: wgrad of the previous step's pair)
+    // ---- phase 2 (MFMA waves: the rest of the pair, then the E expansion)
     if (st < nsteps) {
-      if (kk == 1) {
-        rm.store<DT>(ru, S, G.SP, 4);  // rows 2..5
-        if (G.PH > 1) rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 6, 4);
-      } else if (kk >= 2) {
+      if (kk == 0) {
+        rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 0, 2);
+      } else if (kk == 1) {
+        rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 2, 4);
+      } else {
         const int i = kk - 2;
         if (pl && !(a.ablate & 4)) {
           uint2 r1[4];
@@ -987,12 +993,9 @@ __global__ void __launch_bounds__(BNT, 1) stem_bwd_kernel(StemBwdArgs2 a) {
             *reinterpret_cast<uint4*>(Tt + toff[pp]) = make_uint4(gres[pp].x, gres[pp].y, r1[pp].x, r1[pp].y);
         }
         if (trv) a.trace[16384 + st * 4 + 0] = stamp();
-        if (i + 1 < G.PH) rm.store<DT>(ru, S, G.SP, 4);  // rows 4i+6..4i+9 (pair i+1's new rows)
         if (trv) a.trace[16384 + st * 4 + 1] = stamp();
         if (trv) a.trace[16384 + st * 4 + 2] = stamp();
-        if (i + 2 < G.PH) rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 4 * i + 10, 4);
-        else if (i + 2 == G.PH && q + 1 < nimg)
-          rm.load<DT>(ru, a.img, bnext, G.Hin, G.Win, 0, 2);
+        if (i + 1 < G.PH) rm.load<DT>(ru, a.img, base(q), G.Hin, G.Win, 4 * i + 6, 4);
       }
     }
   }
