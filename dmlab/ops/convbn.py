@@ -520,7 +520,8 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
     # dgrad_bn_reduce_ab_r3s3.txt, red9); ``allow_res64_add`` (tests) opts in.  The STEM's
     # pooled-grid sums in the last layer-1 dgrad do pay: +0.5 % (the separate pooled reduce ran
     # next to the full-CU tail weight gradient at ~2 TB/s; profiles/side_stream_sweep_r4f.txt)
-    if cfg == 80 and mask is not None and not pool and not allow_res64_add:
+    if (cfg == 80 and mask is not None and not pool and not allow_res64_add
+            and os.environ.get("DMLAB_RES64_RED_ADD", "0") != "1"):
         return {}
     N, H, W, C = dx.shape
     rows = L.conv_stats_rows(N * H * W, cfg, C)
