@@ -1081,7 +1081,9 @@ bool stem_fused_supported(int Hin, int Win) {
 }
 
 static size_t fwd_smem(const StemGeo& G) {
-  return (size_t)RING * G.ROWB + (size_t)2 * 2 * G.Wout * 128 + (size_t)2 * 4 * G.SP * 2;
+  const size_t tiles = (size_t)RING * G.ROWB + (size_t)2 * 2 * G.Wout * 128 + (size_t)2 * 4 * G.SP * 2;
+  const size_t red = (size_t)4 * 2 * 16 * 64 * 4;  // the statistics exchange at exit (32 KB)
+  return tiles > red ? tiles : red;
 }
 static size_t bwd_smem(const StemGeo& G) {
   // E ring + 2 dz tiles + S (4 rows) + pooled ring (bf16 grads + 4-bit codes)

@@ -74,7 +74,7 @@ def _pack4(c):
 
 
 @pytest.mark.parametrize("dtype", [torch.uint8, torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("H", [64, 224])
+@pytest.mark.parametrize("H", [32, 64, 224])
 def test_stem_fused_forward(dev, dtype, H):
     torch.manual_seed(0)
     img = _inputs(dev, dtype, 5, H, 1)
@@ -122,7 +122,7 @@ def test_stem_pool_apply_and_masked_codes(dev):
     assert torch.equal(out2, out)
 
 
-@pytest.mark.parametrize("dtype,H", [(torch.uint8, 224), (torch.float32, 64)])
+@pytest.mark.parametrize("dtype,H", [(torch.uint8, 224), (torch.float32, 64), (torch.bfloat16, 32)])
 def test_stem_fused_backward_matches_autograd(dev, dtype, H):
     """stem = maxpool(relu(BN_train(conv(x)))): the native forward + backward (pooled-domain
     BN sums, (a dz + cc) weight gradient, + b*H) against float64 autograd of the same
