@@ -12,9 +12,9 @@ from dmlab.ops._native import lib
 pytestmark = pytest.mark.gpu
 
 
-def _inputs(dev, dtype, Nimg, H, seed):
+def _inputs(dev, dtype, Nimg, H, seed, W=None):
     g = torch.Generator(device=dev).manual_seed(seed)
-    u = torch.rand(Nimg, 3, H, H, device=dev, generator=g)
+    u = torch.rand(Nimg, 3, H, W or H, device=dev, generator=g)
     if dtype == torch.uint8:
         img = (u * 256).floor().clamp(0, 255).to(torch.uint8)
     else:
@@ -33,12 +33,12 @@ def _x_bf16(img):
 def _run_fwd(img, idx, w, gamma, train=True):
     L = lib()
     B = idx.numel() if idx is not None else img.shape[0]
-    H = img.shape[2]
+    H, W = img.shape[2], img.shape[3]
     dev = img.device
     wk = torch.empty(64, 176, device=dev, dtype=torch.bfloat16)
     L.stem_pack_weights(w.contiguous(), wk)
-    pext = torch.empty(B, H // 4, H // 4, 64, device=dev, dtype=torch.bfloat16)
-    code = torch.empty(B, H // 4, H // 4, 32, device=dev, dtype=torch.uint8)
+    pext = torch.empty(B, H // 4, W // 4, 64, device=dev, dtype=torch.bfloat16)
+    code = torch.empty(B, H // 4, W // 4, 32, device=dev, dtype=torch.uint8)
     grid = L.stem_fused_grid(B)
     stats = torch.empty(grid * 128, device=dev) if train else None
     sc, bi = input_affine(img.dtype)
@@ -250,3 +250,65 @@ def test_resnet18_u8_gathered_batch(dev, monkeypatch):
         xf = normalize_input(img.index_select(0, idx)).contiguous(memory_format=torch.channels_last)
         o2 = a(xf).float()
     assert ((o1 - o2).norm() / o2.norm()).item() < 2e-2
+
+
+def test_stem_fused_non_square(dev):
+    """48 x 96 input (PH != PW, Wout = 48: one full and one half pixel block): forward values,
+    codes and statistics, and the weight gradient, against float64 references."""
+    L = lib()
+    torch.manual_seed(7)
+    H, W, B = 48, 96, 3
+    img = _inputs(dev, torch.float32, B, H, 11, W=W)
+    w = torch.randn(64, 3, 7, 7, device=dev) * 0.08
+    gamma = torch.randn(64, device=dev)
+    beta = torch.randn(64, device=dev) * 0.2
+    pext, code, stats, wk, grid = _run_fwd(img, None, w, gamma)
+    xb = _x_bf16(img).cpu()
+    y = F.conv2d(xb, w.to(torch.bfloat16).double().cpu(), stride=2, padding=3)
+    st = stats.view(grid, 2, 64).double().sum(0).cpu()
+    torch.testing.assert_close(st[0], y.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(st[1], (y * y).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    sgn = torch.where(gamma.cpu() < 0, -1.0, 1.0).double().view(1, 64, 1, 1)
+    v, cref = _codes_ref(sgn * y.to(torch.bfloat16).double())
+    pref = (sgn * v).permute(0, 2, 3, 1)
+    assert (pext.double().cpu() - pref).abs().max().item() <= 2 ** -7 * pref.abs().max().item()
+    assert (_unpack4(code).cpu().long() == cref.permute(0, 2, 3, 1)).double().mean().item() > 0.995
+    # backward: dW vs float64 autograd routed through the kernel's codes
+    M = B * (H // 2) * (W // 2)
+    f = dict(device=dev, dtype=torch.float32)
+    scale, shift, mean, invstd = (torch.empty(64, **f) for _ in range(4))
+    L.bn_stats_finalize(stats, grid, float(M), gamma, beta, torch.zeros(64, **f),
+                        torch.ones(64, **f), 0.1, 1e-5, scale, shift, mean, invstd,
+                        torch.empty(256 * 128, **f))
+    out = torch.empty_like(pext)
+    code4 = torch.empty_like(code)
+    L.stem_pool_apply(pext, code, scale, shift, out, code4)
+    g = torch.randn(out.shape, device=dev).to(torch.bfloat16)
+    part = torch.empty(L.bn_bwd_rows(pext.numel() // 64, 64) * 128, **f)
+    rows = L.bn_bwd_reduce_masked(g, pext, mean, invstd, scale, shift, part)
+    dw = torch.zeros(64, 3, 7, 7, **f)
+    sc, bi = input_affine(img.dtype)
+    L.stem_bwd_fused2(img, None, sc, bi, wk, g, code4, mean, invstd, gamma, torch.zeros(64, **f),
+                      torch.zeros(64, **f), 0.0, part, rows, dw, 0.0,
+                      torch.empty(L.bn_bwd_work(M, 64), **f),
+                      torch.empty(L.stem_bwd_slab_len(grid), **f), grid)
+    gd = g.double().cpu().permute(0, 3, 1, 2)
+    cd = _unpack4(code4).long().cpu().permute(0, 3, 1, 2)
+    dz = torch.zeros_like(y)
+    PHh, PWw = gd.shape[2], gd.shape[3]
+    ii = torch.arange(PHh).view(1, 1, -1, 1).expand_as(cd)
+    jj = torch.arange(PWw).view(1, 1, 1, -1).expand_as(cd)
+    valid = cd != 15
+    nn_ = torch.arange(B).view(-1, 1, 1, 1).expand_as(cd)[valid]
+    cc_ = torch.arange(64).view(1, -1, 1, 1).expand_as(cd)[valid]
+    dz.index_put_((nn_, cc_, (2 * ii - 1 + cd // 3)[valid], (2 * jj - 1 + cd % 3)[valid]),
+                  gd[valid], accumulate=True)
+    mu = y.mean((0, 2, 3), keepdim=True)
+    inv = 1.0 / torch.sqrt(y.var((0, 2, 3), unbiased=False, keepdim=True) + 1e-5)
+    xh = (y - mu) * inv
+    ga = gamma.double().cpu().view(1, -1, 1, 1)
+    dy = ga * inv * (dz - dz.sum((0, 2, 3), keepdim=True) / M
+                     - xh * (dz * xh).sum((0, 2, 3), keepdim=True) / M)
+    dwr = torch.nn.grad.conv2d_weight(xb, (64, 3, 7, 7), dy, stride=2, padding=3)
+    err = ((dw.double().cpu() - dwr).norm() / dwr.norm()).item()
+    assert err < 1e-2, err
