@@ -1108,6 +1108,8 @@ int stem_fused_grid(int N) {
     int dev = 0;
     DM_CHECK(hipGetDevice(&dev));
     DM_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const char* e = getenv("DMLAB_STEM_GRID");  // tuning: workgroups (default one per CU)
+    if (e && atoi(e) > 0 && atoi(e) < cus) cus = atoi(e);
   }
   return N < cus ? N : cus;
 }
