@@ -20,28 +20,25 @@
 //  * Pool in the epilogue.  BN is a per-channel affine with scale gamma * invstd, whose sign
 //    is the sign of gamma, known before the batch statistics: max-pool(relu(s*y + t)) =
 //    relu(s * ext(y) + t) with ext = max for s >= 0, min for s < 0.  The kernel writes the
-//    pooled extremum of the RAW conv output and its window position (code kh*3 + kw, the
-//    first extremum in PyTorch's scan order); the full-resolution conv output (1.6 GB at
-//    batch 1024) never reaches memory.  A small pass then applies BN + ReLU to the pooled
-//    tensor and marks relu-masked windows (code 15).
+//    pooled extremum of the RAW conv output and its 4-bit window code (the tie-break rank
+//    (2-kh) << 2 | (2-kw) of an integer max: the first extremum in PyTorch's scan order); the
+//    full-resolution conv output (1.6 GB at batch 1024) never reaches memory.  A small pass
+//    then applies BN + ReLU to the pooled tensor and masks the codes of zero outputs (15).
 //  * BN statistics (sum, sum of squares) from the fp32 accumulators, one row per workgroup.
 //
-// Backward (stem_bwd_kernel), same walk: the weight gradient of y = conv(x) under the BN
-// backward  dy = a*dz + b*y + cc  (dz: the pooled gradient routed to its window's selected
-// pixel).  y is not stored, so the kernel RECOMPUTES it: per row pair, (1) a*dz from the
-// pooled gradient and codes (a 2x2 quad of pixels shares its 4 windows) into a bf16 tile,
-// (2) the conv MFMAs again (fp32 y in registers, the tile read/updated in place:
-// dy = a*dz + b*y + cc in fp32, then bf16 -- the mean-subtraction terms b*y + cc cancel in
-// fp32 per element, as in the unfused BN backward), (3) dW += dy^T x_col from the tile and
-// the E rows.  The 1.6 GB full-resolution y is neither written nor read: 1/3 more stem MFMA
-// work instead.  (Splitting dW = sum (a dz + cc) x_col + b * sum y x_col was built first and
-// rejected: the bf16 rounding of the large per-channel constant cc does not cancel against
-// b * sum y x_col -- 7-90 % gradient error on inputs with a large mean.)
-// Warp-specialised like the forward: 8 VALU waves do (1) and the E staging of pair i while the
-// 4 MFMA waves (their conv weights resident in registers) do (2) and (3) of pair i-1; the
-// window codes travel as 4-bit nibbles (the pooled-row ring then fits LDS beside the ring,
-// two tiles and the staging rows).
-//  stem_wreduce_kernel sums the per-workgroup slabs in fixed order into the OIHW gradient.
+// Backward (stem_bwd_kernel), same walk, 16 waves: with the BN backward dy = a*dz + b*y + cc
+// (dz: the pooled gradient routed to its window's selected pixel),
+//     dW = a * dz^T X + b * W (X^T X) + cc * colsum(X)
+// (X: the im2col rows).  8 VALU waves route pair i's pooled gradient into a bf16 dz tile (a
+// 2x2 quad of conv pixels shares its 4 windows: 9 code tests per channel) and stage the raw
+// rows; 8 MFMA waves accumulate pair i-1's D = dz^T X and G = X^T X tiles in fp32 and expand
+// the E rows.  y never exists in the backward, and the mean-subtraction terms b*W G and
+// cc*colsum cancel in fp32 in stem_wcombine_kernel (colsum(X) is row 93 of G: E element 21
+// of every in-image row is 1.0, a zero-weight column).  Rejected on the way (docs/KERNELS.md
+// "Round 5"): (a dz + cc) x_col with cc rounded to bf16 per element (7-90 % gradient error),
+// and recomputing y for an in-place dy tile (slower: a conflicted read-modify-write epilogue).
+// stem_slab_reduce_kernel + stem_wcombine_kernel sum the per-workgroup slabs in fixed order
+// and form the OIHW gradient.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
