@@ -61,18 +61,40 @@ __global__ void __launch_bounds__(256) slab_colsum_kernel(const float* __restric
                                            red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment): 16 row lanes
-// x 16 channels per 256-thread block, 8 loads in flight per lane, lanes combined in fixed
-// order; the result is valid in threads 0..15 (channel blockIdx.x*16 + threadIdx.x).
+// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment): NT/16 row
+// lanes x 16 channels per block, 8 loads in flight per lane, lanes combined in a fixed order
+// (groups of 4 lanes, then the groups); the result is valid in threads 0..15 (channel
+// blockIdx.x*16 + threadIdx.x).  NT = 1024 (64 row lanes) sums up to kFinDirect rows without
+// the slab_colsum pre-pass: one dependent launch fewer per finalize.
 constexpr int FIN_CH = 16;
+template <int NT>
 __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G, int C, int c,
                                            double& s, double& q) {
-  __shared__ double red[2][16][FIN_CH];
+  constexpr int RLN = NT / FIN_CH;
+  __shared__ double red[2][RLN][FIN_CH];
   const int rl = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH;
   const long long W = 2LL * C;
-  red[0][rl][cl] = c < C ? sum_rows8(part + c, rl, G, 16, W) : 0.0;
-  red[1][rl][cl] = c < C ? sum_rows8(part + C + c, rl, G, 16, W) : 0.0;
+  red[0][rl][cl] = c < C ? sum_rows8(part + c, rl, G, RLN, W) : 0.0;
+  red[1][rl][cl] = c < C ? sum_rows8(part + C + c, rl, G, RLN, W) : 0.0;
   __syncthreads();
+  if constexpr (RLN > 16) {
+    // first level: 16 groups of RLN/16 consecutive lanes, in order
+    constexpr int PER = RLN / 16;
+    double a = 0.0, b = 0.0;
+    if (threadIdx.x < 16 * FIN_CH) {
+#pragma unroll
+      for (int l = 0; l < PER; ++l) {
+        a += red[0][rl * PER + l][cl];
+        b += red[1][rl * PER + l][cl];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x < 16 * FIN_CH) {
+      red[0][rl][cl] = a;
+      red[1][rl][cl] = b;
+    }
+    __syncthreads();
+  }
   s = 0.0;
   q = 0.0;
   if (threadIdx.x < FIN_CH)
@@ -82,8 +104,20 @@ __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G
     }
 }
 
+// rows a 1024-thread finalize sums directly (DMLAB_FIN_DIRECT, default 2048; 256 = the
+// round-4 path: slab_colsum pre-pass above 256 rows)
+static int fin_direct_rows() {
+  static const int v = [] {
+    const char* e = getenv("DMLAB_FIN_DIRECT");
+    return e ? atoi(e) : 2048;
+  }();
+  return v;
+}
+
 // level-1 groups for a [T][2C] slab: none when the finalize block can sum it directly
-static inline int colsum_groups(int T) { return T <= 256 ? 0 : min(256, (T + 31) / 32); }
+static inline int colsum_groups(int T) {
+  return (T <= 256 || T <= fin_direct_rows()) ? 0 : min(256, (T + 31) / 32);
+}
 
 // Per-channel finalize math of the forward / backward finalize kernels (the one-launch
 // last-block finalizes measured slower and were removed: docs/KERNELS.md round 2).
@@ -142,12 +176,13 @@ __device__ __forceinline__ void fin_bwd_channel(const FinBwd& f, int c, int C, d
 
 // stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
 // grid ceil(C/16) x 256 threads
-__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int G,
-                                                          int C, double count, FinFwd f) {
+template <int NT>
+__global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ part, int G,
+                                                         int C, double count, FinFwd f) {
   const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
   if (f.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *f.num_batches += 1;
   double s, q;
-  block_sum2(part, G, C, c, s, q);
+  block_sum2<NT>(part, G, C, c, s, q);
   if (threadIdx.x >= FIN_CH || c >= C) return;
   fin_fwd_channel(f, c, s, q, count);
 }
@@ -439,12 +474,13 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
 
 // finalize: Σ over G partials -> dgamma, dbeta (written with beta-accumulate into grad
 // slots) and the affine dy coefficients a, b, c.  grid ceil(C/16) x 256 threads.
-__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ part,
-                                                              int G, int C, double count,
-                                                              FinBwd f) {
+template <int NT>
+__global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ part,
+                                                             int G, int C, double count,
+                                                             FinBwd f) {
   const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
   double s, q;
-  block_sum2(part, G, C, c, s, q);
+  block_sum2<NT>(part, G, C, c, s, q);
   if (threadIdx.x >= FIN_CH || c >= C) return;
   fin_bwd_channel(f, c, C, s, q, count);
 }
@@ -1107,7 +1143,11 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
     slab_colsum_kernel<<<dim3((W + 63) / 64, G), 256, 0, st>>>(stats, T, W, work);
     fin = work;
   }
-  bn_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G ? G : T, C, count, f);
+  const int rows = G ? G : T;
+  if (rows > 256)
+    bn_finalize_kernel<1024><<<(C + FIN_CH - 1) / FIN_CH, 1024, 0, st>>>(fin, rows, C, count, f);
+  else
+    bn_finalize_kernel<256><<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, rows, C, count, f);
 }
 
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
@@ -1181,8 +1221,13 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
     slab_colsum_kernel<<<dim3((2 * C + 63) / 64, G2), 256, 0, st>>>(part, G, 2 * C, part2);
     fin = part2;
   }
-  bn_bwd_finalize_kernel<<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, G2 ? G2 : G, C,
-                                                                    (double)M, fb);
+  const int rows = G2 ? G2 : G;
+  if (rows > 256)
+    bn_bwd_finalize_kernel<1024><<<(C + FIN_CH - 1) / FIN_CH, 1024, 0, st>>>(fin, rows, C,
+                                                                          (double)M, fb);
+  else
+    bn_bwd_finalize_kernel<256><<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, rows, C,
+                                                                        (double)M, fb);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
   // grid-strided mode 3: workgroup cap 4096 (1024-8192 within noise,
