@@ -61,18 +61,19 @@ __global__ void __launch_bounds__(256) slab_colsum_kernel(const float* __restric
                                            red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
-// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment): NT/16 row
-// lanes x 16 channels per block, 8 loads in flight per lane, lanes combined in a fixed order
-// (groups of 4 lanes, then the groups); the result is valid in threads 0..15 (channel
-// blockIdx.x*16 + threadIdx.x).  NT = 1024 (64 row lanes) sums up to kFinDirect rows without
-// the slab_colsum pre-pass: one dependent launch fewer per finalize.
+// Σ over the G rows of part[G][2C] for channels c (Σ) and C+c (second moment): NT/CH row
+// lanes x CH channels per block, 8 loads in flight per lane, lanes combined in a fixed order
+// (groups of RLN/16 lanes, then the 16 groups); the result is valid in threads 0..CH-1
+// (channel blockIdx.x*CH + threadIdx.x).  CH = 4 (64 row lanes) sums up to fin_direct_rows()
+// rows without the slab_colsum pre-pass: one dependent launch fewer per finalize, in 4-wave
+// blocks (a 1024-thread block waited for a whole free CU next to the side stream: 23 us)
 constexpr int FIN_CH = 16;
-template <int NT>
+template <int NT, int CH>
 __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G, int C, int c,
                                            double& s, double& q) {
-  constexpr int RLN = NT / FIN_CH;
-  __shared__ double red[2][RLN][FIN_CH];
-  const int rl = threadIdx.x / FIN_CH, cl = threadIdx.x % FIN_CH;
+  constexpr int RLN = NT / CH;
+  __shared__ double red[2][RLN][CH];
+  const int rl = threadIdx.x / CH, cl = threadIdx.x % CH;
   const long long W = 2LL * C;
   red[0][rl][cl] = c < C ? sum_rows8(part + c, rl, G, RLN, W) : 0.0;
   red[1][rl][cl] = c < C ? sum_rows8(part + C + c, rl, G, RLN, W) : 0.0;
@@ -81,7 +82,7 @@ __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G
     // first level: 16 groups of RLN/16 consecutive lanes, in order
     constexpr int PER = RLN / 16;
     double a = 0.0, b = 0.0;
-    if (threadIdx.x < 16 * FIN_CH) {
+    if (threadIdx.x < 16 * CH) {
 #pragma unroll
       for (int l = 0; l < PER; ++l) {
         a += red[0][rl * PER + l][cl];
@@ -89,7 +90,7 @@ __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G
       }
     }
     __syncthreads();
-    if (threadIdx.x < 16 * FIN_CH) {
+    if (threadIdx.x < 16 * CH) {
       red[0][rl][cl] = a;
       red[1][rl][cl] = b;
     }
@@ -97,14 +98,14 @@ __device__ __forceinline__ void block_sum2(const float* __restrict__ part, int G
   }
   s = 0.0;
   q = 0.0;
-  if (threadIdx.x < FIN_CH)
+  if (threadIdx.x < CH)
     for (int l = 0; l < 16; ++l) {
       s += red[0][l][cl];
       q += red[1][l][cl];
     }
 }
 
-// rows a 1024-thread finalize sums directly (DMLAB_FIN_DIRECT, default 2048; 256 = the
+// rows a 4-channel finalize block sums directly (DMLAB_FIN_DIRECT, default 2048; 256 = the
 // round-4 path: slab_colsum pre-pass above 256 rows)
 static int fin_direct_rows() {
   static const int v = [] {
@@ -176,14 +177,14 @@ __device__ __forceinline__ void fin_bwd_channel(const FinBwd& f, int c, int C, d
 
 // stats: [G][2][C] partial (Σy, Σy²) -> scale/shift, mean/invstd; running stats update.
 // grid ceil(C/16) x 256 threads
-template <int NT>
+template <int NT, int CH>
 __global__ void __launch_bounds__(NT) bn_finalize_kernel(const float* __restrict__ part, int G,
                                                          int C, double count, FinFwd f) {
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
+  const int c = blockIdx.x * CH + (threadIdx.x % CH);
   if (f.num_batches && blockIdx.x == 0 && threadIdx.x == 0) *f.num_batches += 1;
   double s, q;
-  block_sum2<NT>(part, G, C, c, s, q);
-  if (threadIdx.x >= FIN_CH || c >= C) return;
+  block_sum2<NT, CH>(part, G, C, c, s, q);
+  if (threadIdx.x >= CH || c >= C) return;
   fin_fwd_channel(f, c, s, q, count);
 }
 
@@ -474,14 +475,14 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(BnBwdArgs a, float* 
 
 // finalize: Σ over G partials -> dgamma, dbeta (written with beta-accumulate into grad
 // slots) and the affine dy coefficients a, b, c.  grid ceil(C/16) x 256 threads.
-template <int NT>
+template <int NT, int CH>
 __global__ void __launch_bounds__(NT) bn_bwd_finalize_kernel(const float* __restrict__ part,
                                                              int G, int C, double count,
                                                              FinBwd f) {
-  const int c = blockIdx.x * FIN_CH + (threadIdx.x % FIN_CH);
+  const int c = blockIdx.x * CH + (threadIdx.x % CH);
   double s, q;
-  block_sum2<NT>(part, G, C, c, s, q);
-  if (threadIdx.x >= FIN_CH || c >= C) return;
+  block_sum2<NT, CH>(part, G, C, c, s, q);
+  if (threadIdx.x >= CH || c >= C) return;
   fin_bwd_channel(f, c, C, s, q, count);
 }
 
@@ -1145,9 +1146,9 @@ void bn_stats_finalize(const float* stats, int T, int C, double count, const flo
   }
   const int rows = G ? G : T;
   if (rows > 256)
-    bn_finalize_kernel<1024><<<(C + FIN_CH - 1) / FIN_CH, 1024, 0, st>>>(fin, rows, C, count, f);
+    bn_finalize_kernel<256, 4><<<(C + 3) / 4, 256, 0, st>>>(fin, rows, C, count, f);
   else
-    bn_finalize_kernel<256><<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, rows, C, count, f);
+    bn_finalize_kernel<256, FIN_CH><<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, rows, C, count, f);
 }
 
 void bn_eval_coeffs(const float* gamma, const float* beta, const float* rmean, const float* rvar,
@@ -1223,11 +1224,10 @@ void bn_backward(const bf16_t* dout, const bf16_t* out, const bf16_t* y, const f
   }
   const int rows = G2 ? G2 : G;
   if (rows > 256)
-    bn_bwd_finalize_kernel<1024><<<(C + FIN_CH - 1) / FIN_CH, 1024, 0, st>>>(fin, rows, C,
-                                                                          (double)M, fb);
+    bn_bwd_finalize_kernel<256, 4><<<(C + 3) / 4, 256, 0, st>>>(fin, rows, C, (double)M, fb);
   else
-    bn_bwd_finalize_kernel<256><<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, rows, C,
-                                                                        (double)M, fb);
+    bn_bwd_finalize_kernel<256, FIN_CH><<<(C + FIN_CH - 1) / FIN_CH, 256, 0, st>>>(fin, rows, C,
+                                                                            (double)M, fb);
   if (!dy) return;  // coefficients only (a consumer kernel applies dy = a·dz + b·y + c itself)
   const long long n8 = M * C / 8;
   // grid-strided mode 3: workgroup cap 4096 (1024-8192 within noise,
