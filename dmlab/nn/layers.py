@@ -161,11 +161,11 @@ class ConvBN(Layer):
         return CB.convbn_fwd(self, x, ctx, train, residual, raw=raw, pre=pre)
 
     def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
-                   red_for=None):
+                   red_for=None, phase=0):
         from dmlab.ops import convbn as CB
 
         return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into,
-                             fused_skip=fused_skip, red_for=red_for)
+                             fused_skip=fused_skip, red_for=red_for, phase=phase)
 
 
 class ConvBNPool(ConvBN):
@@ -257,10 +257,29 @@ class BasicBlock(Layer):
                 red_for = nxt
             return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None,
                                       red_for=red_for)
+        aux = self._bn_stream() if need_dx else None
+        if aux is not None:
+            # the shortcut's BN backward (reduce + apply: memory-bound passes over the block's
+            # output gradient) only needs dres: it runs on a second high-priority stream next
+            # to c1's BN backward and stride-2 data gradient instead of after them
+            main = torch.cuda.current_stream()
+            aux.wait_stream(main)
+            with torch.cuda.stream(aux):
+                self.down.native_bwd(dres, ctx["cd"], need_dx, phase=1)
+            dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
+            main.wait_stream(aux)
+            self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx, phase=2)
+            return dx
         dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
         # projection skip: its dgrad (one parity class of the 1x1/s2 conv) accumulates in place
         self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx)
         return dx
+
+    def _bn_stream(self):
+        prog = getattr(self, "_prog", None)
+        if prog is None or not prog._native_active:
+            return None
+        return prog._aux_stream()
 
 
 class MaxPool(Layer):

@@ -387,5 +387,19 @@ class Program(nn.Module):
             st = self._side_streams[dev] = torch.cuda.Stream(device=dev)
         return st
 
+    def _aux_stream(self):
+        """Third HIP stream, at the step stream's high priority, for critical-path work that
+        can run beside the main chain (a projection shortcut's BN backward); None when
+        disabled (``DMLAB_AUX_STREAM=0``) or without a side stream."""
+        if self._side_stream() is None or os.environ.get("DMLAB_AUX_STREAM", "1") == "0":
+            return None
+        dev = torch.cuda.current_device()
+        key = ("aux", dev)
+        st = self._side_streams.get(key)
+        if st is None:
+            lo, hi = torch.cuda.Stream.priority_range()
+            st = self._side_streams[key] = torch.cuda.Stream(device=dev, priority=min(lo, hi))
+        return st
+
     def prepare_native(self, x):
         """Hook for subclasses: convert input layout / refresh packed weights."""

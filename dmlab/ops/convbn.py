@@ -535,7 +535,7 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
 
 
 def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
-               red_for=None):
+               red_for=None, phase=0):
     """Returns dx (or (dx, dres) when the forward had a residual input).
 
     ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient), or
@@ -548,7 +548,10 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     ``red_for``  : (layer, ctx) of the ConvBN + ReLU whose output gradient dx is.  When the
                   dgrad kernel supports it (cfg 80), that BN's backward reduction (Σdz, Σdz·x̂)
                   runs in this dgrad's epilogue and is left in its ctx["pre_sums"], so its
-                  own backward skips the pass that re-reads dx and y"""
+                  own backward skips the pass that re-reads dx and y
+    ``phase``    : 0 = the whole backward; 1 = only the BatchNorm backward (dy kept in ctx),
+                  on the caller's current stream; 2 = the weight and data gradients from
+                  phase 1's dy (the caller has made the current stream wait for phase 1)"""
     if ctx.get("fused_stem"):
         return _stem_fused_bwd(layer, dout, ctx)
     L = lib()
@@ -566,9 +569,13 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
         _, dout, in_mask = dout
         assert not layer.relu and not ctx["has_res"], "masked upstream gradient: linear BN only"
     dout = dout.contiguous()
-    work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
-    pre_sums = ctx.pop("pre_sums", None) or {}
     pool = getattr(layer, "pool_k", 0)
+    if phase == 2:
+        assert not pool, "phase 2: a plain ConvBN"
+        work, pre_sums = None, {}
+    else:
+        work = torch.empty(L.bn_bwd_work(M, cout), device=y.device, dtype=torch.float32)
+        pre_sums = ctx.pop("pre_sums", None) or {}
     if pool and ctx.get("yarg") is not None and not pre_sums:
         # stem: Σdz, Σdz·x̂ over the pooled grid (pooled grad masked at the argmax, x̂ from
         # y at the argmax) -- reads 2 pooled-size tensors instead of y + grad + codes
@@ -609,15 +616,26 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     even = OW if (not s2d and 2 * OH == x.shape[1] and 2 * OW == x.shape[2]) else 0
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
                           tail=tail, even=even)
-    dy = empty_nhwc(N, OH, OW, cout, y)
     masked_res = fused_skip and ctx["has_res"] and mode == 4
-    dres = empty_nhwc(N, OH, OW, cout, y) if (ctx["has_res"] and not masked_res) else None
-    L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
-                  layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
-                  layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
-                  dout if pool else None, ctx.get("idx"),
-                  getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
-                  getattr(layer, "pool_p", 1), dy, dres, work, mask=in_mask if in_mask is not None else ctx.get("mask"), **pre_sums)
+    if phase == 2:
+        dy, dres = ctx.pop("_bn_out")
+        # allocated on the phase-1 stream, read here and on the weight-gradient stream
+        dy.record_stream(torch.cuda.current_stream())
+        if dres is not None:
+            dres.record_stream(torch.cuda.current_stream())
+    else:
+        dy = empty_nhwc(N, OH, OW, cout, y)
+        dres = empty_nhwc(N, OH, OW, cout, y) if (ctx["has_res"] and not masked_res) else None
+        L.bn_backward(None if pool else dout, ctx.get("out"), y, ctx["mean"], ctx["invstd"],
+                      layer.bn_weight.detach(), layer.grad_slot("bn_weight"),
+                      layer.grad_slot("bn_bias"), acc, mode, ctx["scale"], ctx["shift"],
+                      dout if pool else None, ctx.get("idx"),
+                      getattr(layer, "pool_k", 3), getattr(layer, "pool_s", 2),
+                      getattr(layer, "pool_p", 1), dy, dres, work,
+                      mask=in_mask if in_mask is not None else ctx.get("mask"), **pre_sums)
+        if phase == 1:
+            ctx["_bn_out"] = (dy, dres)
+            return None
     # weight gradient: on the Program's side stream when it has one (off the critical
     # path; overlaps the following dgrad / BN-backward chain).  Tensors it reads that the
     # main stream allocated are recorded on the side stream so the caching allocator does
