@@ -143,3 +143,28 @@ def test_resnet18_training_trajectory_224(dev):
     assert med["native"] <= 2.0 * med["autocast"] + 0.1, s
     bn = s["bn_running_rel_err_max"]
     assert bn["native"] <= 2.0 * bn["autocast"] + 0.05, s
+
+
+def test_resnet18_aux_stream_bit_identical(dev, monkeypatch):
+    """The projection shortcuts' BN backward on the aux stream (BasicBlock.native_bwd,
+    convbn_bwd phase 1/2) computes exactly what the serial order does: every gradient and
+    running statistic bit-identical, over two steps so that stream-ordered memory reuse
+    between steps is exercised too."""
+    torch.manual_seed(5)
+    base = ResNet18(num_classes=10).to(dev)
+    x = torch.rand(8, 3, 64, 64, device=dev)
+    y = torch.randint(0, 10, (8,), device=dev)
+    grads, stats = {}, {}
+    for aux in ("1", "0"):
+        monkeypatch.setenv("DMLAB_AUX_STREAM", aux)
+        m = copy.deepcopy(base)
+        for _ in range(2):
+            m.zero_grad()
+            cross_entropy(m(x), y).backward()
+        torch.cuda.synchronize()
+        grads[aux] = [p.grad.clone() for p in m.parameters()]
+        stats[aux] = [b.clone() for b in m.buffers()]
+    for ga, gb in zip(grads["1"], grads["0"]):
+        assert torch.equal(ga, gb)
+    for sa, sb in zip(stats["1"], stats["0"]):
+        assert torch.equal(sa, sb)
