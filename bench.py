@@ -114,8 +114,8 @@ def parse():
     ap.add_argument("--graph-steps", type=int, default=25,
                     help="fused LeNet with --graph: training steps per captured graph (each one "
                          "a complete step through the device cursor; the epoch's last steps "
-                         "replay the 1-step graph). The timed region runs every step it counts, "
-                         "plus up to graph-steps - 1 more (never fewer).  25 divides the "
+                         "and a remainder of --steps replay the 1-step graph; capped at "
+                         "--steps). The timed region runs exactly --steps steps.  25 divides the "
                          "1875-batch epoch: 1.035M vs 0.897M img/s at 1 step per graph "
                          "(profiles/bench_lenet_graph_steps_ab_r4az.txt)")
     ap.add_argument("--graph", type=int, default=-1,
@@ -181,7 +181,11 @@ def main():
         if checks["allreduce_selfcheck"] != "pass":
             print(json.dumps({"error": "all-reduce self-check failed", **checks}), flush=True)
             raise SystemExit(3)
-        if a.model == "lenet" and a.small_allreduce != "rccl" and dev.type == "cuda":
+        # auto: LeNet only (its 207 KB of gradients are the one-shot kernel's design point);
+        # an explicit --small-allreduce xgmi runs the same self-check for any model
+        want_xgmi = (a.small_allreduce == "xgmi"
+                     or (a.small_allreduce == "auto" and a.model == "lenet"))
+        if want_xgmi and dev.type == "cuda":
             checks.update(selfcheck.xgmi_selfcheck(dev))
         else:
             checks.update(xgmi_selfcheck="skipped", small_allreduce_used="rccl")
@@ -285,7 +289,9 @@ def main():
                 opt.step_count = 1  # capture the not-first-step update: buf = m*0 + g = g
             cap = CapturedStep(lambda x, y: train_step(x, y, cursor=cur),
                                [ds.images, ds.labels], warmup=3, bind_inputs=True)
-            kg = max(1, a.graph_steps)
+            # a k-step replay never runs past the steps the caller asked for: the timed
+            # region executes EXACTLY --steps training steps (k = min(graph-steps, steps))
+            kg = max(1, min(a.graph_steps, a.steps))
             capk = None
             if kg > 1:
                 def multi(x, y):
@@ -296,7 +302,7 @@ def main():
                 cur.refill(0)
                 capk = CapturedStep(multi, [ds.images, ds.labels], warmup=1, bind_inputs=True)
             # credit: steps a k-step replay already ran ahead of the caller's step count
-            state = {"step": 0, "epoch": 0, "credit": 0, "out": None}
+            state = {"step": 0, "epoch": 0, "credit": 0, "out": None, "budget": a.warmup}
 
             def step(i):
                 if state["credit"]:
@@ -306,16 +312,18 @@ def main():
                     state["epoch"] += 1
                     cur.refill(state["epoch"])  # next epoch's shard order, same buffer
                 left = cur.nbatch - state["step"] % cur.nbatch
-                if capk is not None and left >= kg:
+                if capk is not None and left >= kg and state["budget"] >= kg:
                     state["out"], n = capk(ds.images, ds.labels), kg
                 else:
                     state["out"], n = cap(ds.images, ds.labels), 1
                 state["step"] += n
+                state["budget"] -= n
                 state["credit"] = n - 1
                 return state["out"]
 
             def step_reset():  # the timed region starts on a fresh replay
                 state["credit"] = 0
+                state["budget"] = a.steps
 
             with torch.no_grad():
                 flat.data.copy_(saved[0])

@@ -1188,7 +1188,8 @@ void stem_bwd_fused2(const void* img, int dtype, const long long* idx, const flo
     DM_CHECK(hipMalloc(&trace_buf, 8 * 8 * 4096));
     DM_CHECK(hipMemset(trace_buf, 0, 8 * 8 * 4096));
   }
-  a.trace = trace && nst <= 4096 ? trace_buf : nullptr;
+  // [0, nst*8) per-step stamps, [16384, 16384 + nst*4) the second region: disjoint for nst <= 2048
+  a.trace = trace && nst <= 2048 ? trace_buf : nullptr;
   const size_t sm = bwd_smem(a.G);
 #define DM_SB(DT)                                              \
   do {                                                         \

@@ -136,9 +136,7 @@ class XGMITransport:
     message), ``nslot``: ring depth."""
 
     def __init__(self, links, cap_bytes=1 << 20, nslot=4, group=None, device=None):
-        from dmlab.ops._native import lib
-
-        self.L = lib()
+        self.L = None
         self.rank = dist.get_rank()
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.cap = (int(cap_bytes) + 255) // 256 * 256
@@ -149,38 +147,84 @@ class XGMITransport:
         self._owned, self._opened = [], []
         flag_bytes = 256
         mine = {}
-        for i, (s, d) in enumerate(links):
-            if d == self.rank:  # receiver: ring + full flags
-                base = self.L.xgmi_alloc(self.nslot * self.cap + flag_bytes)
-                self._owned.append(base)
-                mine[i] = ("ring", self.L.xgmi_get_handle(base), base)
-            elif s == self.rank:  # sender: free (ack) flags
-                base = self.L.xgmi_alloc(flag_bytes)
-                self._owned.append(base)
-                mine[i] = ("free", self.L.xgmi_get_handle(base), base)
+        # Construction is collective and any step can fail on ONE rank only (allocation,
+        # handle export, and above all hipIpcOpenMemHandle of a peer's buffer across GPUs).
+        # Every failure is caught locally and exchanged through the two all_gather_object
+        # calls every rank makes, so all ranks raise together and a caller can fall back to
+        # the process-group transport (task4) instead of one rank waiting in a later
+        # collective until the PG timeout.
+        err = None
+        try:
+            from dmlab.ops._native import lib
+
+            self.L = lib()
+            for i, (s, d) in enumerate(links):
+                if d == self.rank:  # receiver: ring + full flags
+                    base = self.L.xgmi_alloc(self.nslot * self.cap + flag_bytes)
+                    self._owned.append(base)
+                    mine[i] = ("ring", self.L.xgmi_get_handle(base), base)
+                elif s == self.rank:  # sender: free (ack) flags
+                    base = self.L.xgmi_alloc(flag_bytes)
+                    self._owned.append(base)
+                    mine[i] = ("free", self.L.xgmi_get_handle(base), base)
+        except Exception as e:
+            err = f"rank {self.rank} alloc: {type(e).__name__}: {e}"
         allh = [None] * dist.get_world_size(group)
-        dist.all_gather_object(allh, {i: (k, h) for i, (k, h, _) in mine.items()}, group=group)
+        dist.all_gather_object(allh, ({i: (k, h) for i, (k, h, _) in mine.items()}, err),
+                               group=group)
+        errs = [e for _, e in allh if e]
         # inline: run the channel kernels on the CURRENT stream instead of per-channel streams
         # (a captured pipeline step is then one linear chain in program order; see
         # PipelineStage.capture)
         self.inline = False
         self.chan = {}
-        for i, (s, d) in enumerate(links):
-            if self.rank not in (s, d):
-                continue
-            peer = d if s == self.rank else s
-            kind, h = allh[peer][i]
-            remote = self.L.xgmi_open_handle(h)
-            self._opened.append(remote)
-            if d == self.rank:
-                ring, free_ = mine[i][2], remote
-            else:
-                ring, free_ = remote, mine[i][2]
-            self.chan[(s, d)] = dict(
-                ring=ring, full=ring + self.nslot * self.cap, free=free_,
-                state=torch.zeros(4, dtype=torch.int32, device=self.device),
-                stream=torch.cuda.Stream(device=self.device))
+        if not errs:
+            try:
+                for i, (s, d) in enumerate(links):
+                    if self.rank not in (s, d):
+                        continue
+                    peer = d if s == self.rank else s
+                    kind, h = allh[peer][0][i]
+                    remote = self._open(h)
+                    self._opened.append(remote)
+                    if d == self.rank:
+                        ring, free_ = mine[i][2], remote
+                    else:
+                        ring, free_ = remote, mine[i][2]
+                    self.chan[(s, d)] = dict(
+                        ring=ring, full=ring + self.nslot * self.cap, free=free_,
+                        state=torch.zeros(4, dtype=torch.int32, device=self.device),
+                        stream=(torch.cuda.Stream(device=self.device)
+                                if self.device.type == "cuda" else None))
+            except Exception as e:
+                err = f"rank {self.rank} open: {type(e).__name__}: {e}"
+            st = [None] * dist.get_world_size(group)
+            dist.all_gather_object(st, err, group=group)
+            errs = [e for e in st if e]
+        if errs:
+            self._release()
+            raise RuntimeError("xGMI p2p: peer memory mapping failed: " + "; ".join(errs))
         dist.barrier(group=group)
+
+    def _open(self, h):
+        return self.L.xgmi_open_handle(h)
+
+    def _release(self):
+        """Local teardown after a failed construction (no device work was queued)."""
+        for p in self._opened:
+            try:
+                self.L.xgmi_close_handle(p)
+            except Exception:
+                pass
+        self._opened = []
+        dist.barrier(group=self.group)  # every peer has closed its view of our buffers
+        for p in self._owned:
+            try:
+                self.L.xgmi_free(p)
+            except Exception:
+                pass
+        self._owned = []
+        self.chan = {}
 
     def known(self, key):
         return key in self.hdr.shapes

@@ -78,6 +78,7 @@ class PipelineStage:
         self.history = []  # (start, end, compute events) of every timed step
         self._linear = False  # no receive posted ahead (captured steps)
         self._graph = None
+        self._time_replays = False
 
     def selfcheck(self, corrupt=None) -> dict:
         """One ping-pong per adjacent stage pair over this stage's transport, payloads checked
@@ -94,7 +95,6 @@ class PipelineStage:
             if r["p2p_selfcheck"] != "pass":
                 res = "FAIL"
         return {"p2p_selfcheck": res}
-        self._time_replays = False
 
     # -------------------------------------------------------------- pieces
     def _post_recv(self, tag, m, src, ahead=False):
@@ -252,6 +252,8 @@ class PipelineStage:
         """One captured step on new data (first stage: ``x``/``y``; others: nothing).  With
         ``timing`` the step is bracketed by events (no per-compute events inside a graph:
         :meth:`step_stats` then reports the step time only)."""
+        if self._graph is None:
+            raise RuntimeError("PipelineStage.replay: no captured step; call capture() first")
         if self.first:
             self._sx.copy_(x, non_blocking=True)
             self._sy.copy_(y, non_blocking=True)

@@ -119,7 +119,20 @@ def p2p_selfcheck(p2p, rank: int, peer, device, first: bool, numel: int = 32 * 4
     on the gradient key; the other side checks x and replies.  Every rank of the default
     group must call it (the verdict is agreed over ``group``); a rank outside the pair passes
     ``peer=None``."""
-    x, _ = _coded(numel, 0, device)
+    # Readiness first: a side that cannot even start (no channel to its peer, a payload it
+    # cannot build) must not leave its peer blocked in a receive until the process-group
+    # timeout, so every rank agrees before any message is posted.  Past this point both sides
+    # post the same messages; a transfer that then fails is bounded by the transport itself
+    # (the xGMI channel's flag wait times out; RCCL/gloo by the PG timeout, 120 s in task4).
+    ready = True
+    try:
+        x, _ = _coded(numel, 0, device)
+        if peer is not None and hasattr(p2p, "chan"):
+            ready = (rank, peer) in p2p.chan and (peer, rank) in p2p.chan
+    except Exception:
+        ready = False
+    if not agree(ready, device, group):
+        return {"p2p_selfcheck": "FAIL"}
     ok = True
     try:
         if peer is None:

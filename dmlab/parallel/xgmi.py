@@ -39,6 +39,8 @@ def _device_key(device) -> str:
     reports them; host + index otherwise)."""
     import socket
 
+    if torch.device(device).type != "cuda":
+        return f"{socket.gethostname()}:{device}"
     p = torch.cuda.get_device_properties(device)
     uuid = getattr(p, "uuid", None)
     if uuid:
@@ -62,15 +64,24 @@ class XGMIAllReduce:
         if algo not in ("auto", *_ALGOS):
             raise ValueError("algo: 'auto' | 'one_shot' | 'two_shot'")
         self.algo = algo
-        L = lib()
-        self._base = L.xgmi_alloc(8 * self.cap + _FLAG_BYTES)
-        handle = L.xgmi_get_handle(self._base)
+        # every step below can fail on one rank only; failures are exchanged in the two
+        # all_gather_object calls every rank makes, so all ranks raise together
+        L, self._base, handle, err = None, 0, None, None
+        try:
+            L = lib()
+            self._base = L.xgmi_alloc(8 * self.cap + _FLAG_BYTES)
+            handle = L.xgmi_get_handle(self._base)
+        except Exception as e:
+            err = f"rank {self.rank} alloc: {type(e).__name__}: {e}"
         handles = [None] * self.world
-        dist.all_gather_object(handles, handle, group=group)
+        dist.all_gather_object(handles, (handle, err), group=group)
+        errs0 = [e for _, e in handles if e]
+        handles = [h for h, _ in handles]
         self._opened = []
         bases = []
-        err = None
         try:
+            if errs0:
+                raise RuntimeError("; ".join(errs0))
             for q, h in enumerate(handles):
                 if q == self.rank:
                     bases.append(self._base)
@@ -97,7 +108,8 @@ class XGMIAllReduce:
                 L.xgmi_close_handle(p)
             self._opened = []
             dist.barrier(group=group)
-            L.xgmi_free(self._base)
+            if self._base:
+                L.xgmi_free(self._base)
             self._base = 0
             raise RuntimeError("xGMI all-reduce: peer memory mapping failed: " + "; ".join(errs))
         keys = [k for k, _ in keys]

@@ -56,6 +56,8 @@ def parse_args(argv=None):
     p.add_argument("--cu-partition", action="store_true",
                    help="pipeline on one shared GPU: every stage runs on its own equal CU "
                         "partition (a CU-masked stream), emulating one device per stage")
+    p.add_argument("--pg-timeout", type=float, default=120.0,
+                   help="process-group timeout in seconds (pipeline / tp modes)")
     p.add_argument("--batch-size", type=int, default=32)
     p.add_argument("--epochs", type=int, default=2)
     p.add_argument("--lr", type=float, default=0.01)
@@ -139,7 +141,10 @@ _WALL_FROM = 6  # pipeline bench: wall-clock step time measured from this step o
 
 
 def run_pipeline(a):
-    dev = env.init(a.n_devices, a.rank, a.master_addr, a.master_port, device_type=a.device)
+    # a 120 s process-group timeout (env.init's default is 600 s): a transport hang fails the
+    # run within two minutes, as bench.py does
+    dev = env.init(a.n_devices, a.rank, a.master_addr, a.master_port, device_type=a.device,
+                   timeout_s=a.pg_timeout)
     rank, ws = env.get_rank(), env.get_world_size()
     assert ws == 2, "the LeNet pipeline has 2 stages"
     if a.cu_partition and dev.type == "cuda":
@@ -160,21 +165,39 @@ def _run_pipeline(a, dev, rank, ws):
     # every batch one shape (drop_last): message shapes are negotiated once and cached
     # ring slots sized for the largest message: a (batch, 400) fp32 activation / gradient
     cap = max(1 << 20, a.batch_size * 400 * 4)
-    stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
-                          transport=a.transport, timing=bool(a.bench_json), cap_bytes=cap)
-    # one ping-pong per stage pair on the chosen transport before training (both directions,
-    # payload checked); the native xGMI channel falls back to torch.distributed P2P
-    checks = stage.selfcheck()
-    checks["transport_used"] = a.transport
-    if checks["p2p_selfcheck"] != "pass" and a.transport == "xgmi":
+
+    def build(transport):
+        return PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
+                             transport=transport, timing=bool(a.bench_json), cap_bytes=cap)
+
+    # The native xGMI channel is optional: its construction (peer-memory mapping, agreed on
+    # every rank by XGMITransport) and one ping-pong per stage pair (both directions, payload
+    # checked) must succeed on every rank, else every rank falls back to torch.distributed
+    # P2P together.  The default 'pg' transport gets the same ping-pong before training.
+    stage, checks, why = None, None, None
+    if a.transport == "xgmi":
         try:
-            stage.p2p.close()
-        except Exception:
-            pass
-        a.transport = "pg"
-        stage = PipelineStage(module, opt, CrossEntropyLoss(), device=dev, schedule=a.schedule,
-                              transport="pg", timing=bool(a.bench_json), cap_bytes=cap)
-        checks = dict(stage.selfcheck(), xgmi_p2p_selfcheck="FAIL", transport_used="pg")
+            stage = build("xgmi")
+        except Exception as e:
+            why = f"construction: {type(e).__name__}: {e}"[:200]
+        if stage is not None:
+            checks = stage.selfcheck()
+            if checks["p2p_selfcheck"] != "pass":
+                why = "ping-pong mismatch or timeout"
+                try:
+                    stage.p2p.close()
+                except Exception:
+                    pass
+                stage = None
+        if stage is None:
+            a.transport = "pg"
+    if stage is None:
+        stage = build(a.transport)
+        checks = stage.selfcheck()
+    checks["transport_used"] = a.transport
+    if why is not None:
+        checks["xgmi_p2p_selfcheck"] = "FAIL"
+        checks["xgmi_p2p_reason"] = why
     if checks["p2p_selfcheck"] != "pass":
         raise SystemExit(f"pipeline transport self-check failed: {checks}")
     if rank == 0:
@@ -287,7 +310,8 @@ def run_tp(a):
     from dmlab.models import Net
     from dmlab.parallel.tensor_parallel import TPLeNet
 
-    dev = env.init(a.n_devices, a.rank, a.master_addr, a.master_port, device_type=a.device)
+    dev = env.init(a.n_devices, a.rank, a.master_addr, a.master_port, device_type=a.device,
+                   timeout_s=a.pg_timeout)
     rank = env.get_rank()
     torch.manual_seed(0)
     full = Net()
