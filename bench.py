@@ -91,6 +91,10 @@ def parse():
                     help="at one rank: initialise a 1-rank RCCL group and run DDP's full "
                          "communication path anyway (reducer, bucket hooks, every bucket's "
                          "all-reduce, buffer broadcasts) -- the multi-GPU code on one GPU")
+    ap.add_argument("--init-pg", type=int, default=0,
+                    help="diagnostic: at one rank, initialise the 1-rank RCCL process group but "
+                         "train without communication (isolates the cost of RCCL's presence "
+                         "from that of the DDP communication path)")
     ap.add_argument("--buffer-sync-every", type=int, default=1,
                     help="DDP broadcast_buffers period in training forwards (1 = every step, "
                          "as torch DDP; 0 = never)")
@@ -159,9 +163,9 @@ def main():
     from dmlab.parallel import DDP, env
 
     ws_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws_env > 1 or a.force_comm:
-        dev = env.init(timeout_s=a.pg_timeout, backend="nccl" if (a.force_comm and ws_env == 1)
-                       else None)
+    if ws_env > 1 or a.force_comm or a.init_pg:
+        dev = env.init(timeout_s=a.pg_timeout,
+                       backend="nccl" if ((a.force_comm or a.init_pg) and ws_env == 1) else None)
     else:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)

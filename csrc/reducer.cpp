@@ -97,8 +97,12 @@ class Reducer {
     if (!enabled_) return;
     for (size_t b = 0; b < buckets_.size(); ++b)
       if (!launched_[b]) launch((int64_t)b);
+    // Every asynchronous collective of this process group runs on ONE communication stream
+    // in launch order, so the current stream waiting for the LAST one orders it after all of
+    // them: one cross-queue wait instead of one per bucket (each ~5-10 us of barrier-packet
+    // latency on the step's critical tail).  Sync-launched buckets are already on this stream.
     for (size_t b = 0; b < buckets_.size(); ++b) {
-      if (works_[b]) works_[b]->wait();
+      if (works_[b] && (!single_wait_ || (int64_t)b == last_async_)) works_[b]->wait();
       at::Tensor view = buf_.slice(0, buckets_[b].lo, buckets_[b].hi);
       if (comm_[b].defined()) {
         view.copy_(comm_[b]);
@@ -115,10 +119,17 @@ class Reducer {
     scaled_.assign(nb, false);
     works_.assign(nb, c10::intrusive_ptr<c10d::Work>());
     comm_.assign(nb, at::Tensor());
+    last_async_ = -1;
     for (auto& bk : buckets_) bk.pending = bk.nparams;
   }
 
+  // an asynchronous collective was issued this backward and finalize waits for the last one
+  bool has_async() const { return single_wait_ && last_async_ >= 0; }
+
   void set_enabled(bool e) { enabled_ = e; }
+  void set_sync_launch(bool e) { sync_launch_ = e; }
+  // RCCL only (one in-order communication stream; gloo's waits are per-operation)
+  void set_single_wait(bool e) { single_wait_ = e; }
   bool enabled() const { return enabled_; }
   void set_avg_scale(double s) { avg_scale_ = s; }
   int64_t launched_total() const { return launched_total_; }
@@ -166,6 +177,10 @@ class Reducer {
       t = comm_[b];
     }
     c10d::AllreduceOptions opts;
+    // sync launch: the collective runs on the caller's current stream (ProcessGroupNCCL
+    // asyncOp = false: no communication-stream hop, still no host synchronisation); used
+    // for the step's final bucket, whose result the optimizer waits for anyway
+    opts.asyncOp = !sync_launch_;
     if (use_avg_ && avg_scale_ != 1.0) {
       opts.reduceOp = c10d::ReduceOp(c10d::ReduceOp::AVG);
       scaled_[b] = true;
@@ -174,6 +189,7 @@ class Reducer {
     }
     std::vector<at::Tensor> ts{t};
     works_[b] = pg->allreduce(ts, opts);
+    if (opts.asyncOp) last_async_ = b;
   }
 
   at::Tensor buf_;
@@ -188,6 +204,9 @@ class Reducer {
   py::object small_fn_;
   at::Tensor comm_flat_;
   bool enabled_ = true;
+  bool sync_launch_ = false;
+  bool single_wait_ = false;
+  int64_t last_async_ = -1;
   int64_t launched_total_ = 0;
   std::vector<bool> launched_, scaled_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
@@ -210,6 +229,9 @@ void register_reducer(pybind11::module_& m) {
       .def("finalize", &Reducer::finalize)
       .def("reset", &Reducer::reset)
       .def("set_enabled", &Reducer::set_enabled)
+      .def("set_sync_launch", &Reducer::set_sync_launch)
+      .def("has_async", &Reducer::has_async)
+      .def("set_single_wait", &Reducer::set_single_wait)
       .def("set_avg_scale", &Reducer::set_avg_scale)
       .def_property_readonly("enabled", &Reducer::enabled)
       .def_property_readonly("launched_total", &Reducer::launched_total)

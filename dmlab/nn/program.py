@@ -163,6 +163,7 @@ class _ProgramFn(torch.autograd.Function):
             side.wait_stream(main)  # fork (under hipGraph capture: joins the capture)
         prog._wgrad_stream = side
         pending = []  # (layer index, event after its wgrads) whose hooks have not run
+        pending_main = []  # layers whose hooks run on the main stream after the join
 
         # Hooks registered stream_ok (DDP without a communication-dtype copy) are issued on
         # the side stream once it has caught up with the main stream: the collective they
@@ -174,6 +175,14 @@ class _ProgramFn(torch.autograd.Function):
             prog._hook_stream_ok.get(h, False) for h in prog._grad_hooks)
 
         def run_side_hooks(js):
+            # a layer whose hooks enqueue nothing (no bucket completes there) runs them as
+            # host bookkeeping: no event on the main stream, no side-stream wait (each costs
+            # a few us of command-processor time between the main stream's kernels)
+            if not any(prog._hook_enqueues(h, j) for j in js for h in prog._grad_hooks):
+                for j in js:
+                    for hook in prog._grad_hooks:
+                        hook(prog, j)
+                return
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 for j in js:
@@ -198,6 +207,13 @@ class _ProgramFn(torch.autograd.Function):
                         hook(prog, i)
                     continue
                 if side_hooks:
+                    if i == 0:
+                        # the step's last layer: its hooks run on the main stream after the
+                        # side stream's join below, so the final bucket's collective is
+                        # ordered by that one join instead of main -> side -> comm -> main
+                        # (each cross-queue hop ~25 us on MI355X: profiles/forcecomm_tail_r6.txt)
+                        pending_main.append(i)
+                        continue
                     run_side_hooks([i])
                     continue
                 for j, ev in pending:
@@ -220,6 +236,16 @@ class _ProgramFn(torch.autograd.Function):
             for j, _ in pending:
                 for hook in prog._grad_hooks:
                     hook(prog, j)
+            # hooks called here run with every gradient already ordered before the current
+            # (main) stream: ``tail_hook`` tells a reducer it may issue its collective on
+            # this stream directly (no communication-stream hop)
+            prog.tail_hook = True
+            try:
+                for j in pending_main:
+                    for hook in prog._grad_hooks:
+                        hook(prog, j)
+            finally:
+                prog.tail_hook = False
         prog.flat.grad_valid = True
         for hook in prog._post_backward_hooks:
             hook(prog)
@@ -247,12 +273,16 @@ class Program(nn.Module):
         # hook -> may run on the side stream (keyed by the hook object itself, not its id: a
         # removed hook's id could be reused by an unrelated function)
         self._hook_stream_ok: dict[Callable, bool] = {}
+        # hook -> predicate(layer index): does the hook enqueue device work for that layer
+        # (absent: always assumed to)
+        self._hook_enqueues_pred: dict[Callable, Callable] = {}
         self._post_backward_hooks: list[Callable] = []
         self._anchor = torch.zeros(1, requires_grad=True)
         self._wver = None
         self._uses_side_stream = False  # set by subclasses whose layers queue wgrads aside
         self._side_streams = {}
         self._wgrad_stream = None
+        self.tail_hook = False  # True while grad hooks run on the main stream after the join
         # Events at the end of the last backward passes (two-stream programs).  Tensors one
         # stream hands to the other are freed with the caching allocator's cross-stream
         # events, which only complete when the GPU reaches them: with the host free to run
@@ -327,21 +357,29 @@ class Program(nn.Module):
         return False
 
     # ---------------------------------------------------------------- hooks
-    def register_grad_hook(self, fn, stream_ok: bool = False):
+    def _hook_enqueues(self, fn, layer_idx) -> bool:
+        pred = self._hook_enqueues_pred.get(fn)
+        return True if pred is None else bool(pred(layer_idx))
+
+    def register_grad_hook(self, fn, stream_ok: bool = False, enqueues=None):
         """fn(program, layer_index) after layer i wrote its weight gradients.
 
         stream_ok: fn only enqueues stream-ordered device work on the current stream (e.g.
         collectives over the layer's gradient buckets) and keeps no tensor it allocates past
         the call; with a two-stream backward it is then called with the weight-gradient
         stream current, once that stream has caught up with the main stream, so the main
-        stream never waits for it."""
+        stream never waits for it.  ``enqueues(layer_index) -> bool``: whether fn enqueues
+        device work for that layer (False: it runs as host bookkeeping, no stream join)."""
         self._grad_hooks.append(fn)
         self._hook_stream_ok[fn] = bool(stream_ok)
+        if enqueues is not None:
+            self._hook_enqueues_pred[fn] = enqueues
 
     def remove_grad_hook(self, fn):
         self._grad_hooks.remove(fn)
         if fn not in self._grad_hooks:
             self._hook_stream_ok.pop(fn, None)
+            self._hook_enqueues_pred.pop(fn, None)
 
     def register_post_backward_hook(self, fn):
         self._post_backward_hooks.append(fn)

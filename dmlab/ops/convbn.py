@@ -100,6 +100,9 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 # the high-priority step stream in round 4: 160-1024 blocks and CU-masked weight-gradient
 # streams all lose to 512 (profiles/wgrad_blocks_sidemask_ab_r4m.txt)
 _WGRAD_BLOCKS = 512
+# layers 3-4 (>= 256 output channels): their weight gradients hold every CU while the main
+# stream's memory-bound BN-backward applies need wave slots (experiment knob, 0 = as above)
+_WGRAD_BLOCKS_WIDE = int(os.environ.get("DMLAB_WGRAD_BLOCKS_WIDE", "0"))
 _CUS = {}
 
 
@@ -162,7 +165,10 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # have one or two output tiles, so the m-split is their only parallelism
         max_split = max(1, M // 512)
     # (2x / 4x more splits for cfg 7 measured -0.4 / -1.0 %: profiles/wgrad_s2_splits_ab_r4ap.txt)
-    S = max(1, min(max_split, math.ceil(_WGRAD_BLOCKS / tiles)))
+    budget = _WGRAD_BLOCKS
+    if cout >= 256 and _WGRAD_BLOCKS_WIDE:
+        budget = _WGRAD_BLOCKS_WIDE
+    S = max(1, min(max_split, math.ceil(budget / tiles)))
     return cfg, S
 
 

@@ -123,6 +123,14 @@ class DistributedDataParallel(nn.Module):
             e = os.environ.get("DMLAB_DDP_SIDE_HOOKS")
             side_stream_hooks = (e != "0") if e is not None else small_allreduce != "xgmi"
         self.side_stream_hooks = bool(side_stream_hooks)
+        # final-layer buckets issued on the main stream (asyncOp=False) -- RCCL only: gloo's
+        # synchronous collective would block the host (DMLAB_DDP_TAIL_SYNC=0 disables)
+        import os as _os
+
+        self._tail_sync = (_os.environ.get("DMLAB_DDP_TAIL_SYNC", "1") != "0"
+                           and dist.is_initialized()
+                           and dist.get_backend(process_group) == "nccl")
+        self._py_tail = False
         self.broadcast_buffers = bool(broadcast_buffers)
         self.buffer_sync_every = max(1, int(buffer_sync_every))
         self._fwd_count = 0
@@ -198,6 +206,9 @@ class DistributedDataParallel(nn.Module):
                                   code[self.comm_dtype],
                                   self._xgmi.cap if self._xgmi is not None else 0, small_fn,
                                   self._comm_flat)
+        # RCCL: every asynchronous collective of the group runs in order on one stream, so
+        # the end of backward waits for the last one only (gloo waits per operation)
+        self._native.set_single_wait(self._tail_sync)
 
     @property
     def buckets_launched(self):
@@ -262,7 +273,21 @@ class DistributedDataParallel(nn.Module):
         if self.comm_active:  # one rank: nothing to launch per layer (finalize still runs)
             # stream_ok: the bucket launches only enqueue collectives (or the xGMI kernel), and
             # the bf16 cast into the persistent communication buffer, on the current stream
-            prog.register_grad_hook(self._on_layer_done, stream_ok=self.side_stream_hooks)
+            # layers whose hook completes a bucket (the only ones that enqueue a collective;
+            # the first hook also issues the buffer broadcast, ordered on the main stream)
+            done = set()
+            left = {id(b): len(b.params) for b in self.buckets}
+            for li in range(len(self._layer_params) - 1, -1, -1):
+                for i in self._layer_params[li]:
+                    b = self._bucket_of_index.get(i)
+                    if b is not None:
+                        left[id(b)] -= 1
+                        if left[id(b)] == 0:
+                            done.add(li)
+            self._launch_layers = done
+            prog.register_grad_hook(self._on_layer_done, stream_ok=self.side_stream_hooks,
+                                    enqueues=lambda li: li in self._launch_layers
+                                    or self._xgmi is not None or self._comm_flat is not None)
         prog.register_post_backward_hook(lambda _p: self._finalize())
 
     def _setup_generic(self, cap_mb, first_mb):
@@ -344,7 +369,12 @@ class DistributedDataParallel(nn.Module):
             op = dist.ReduceOp.AVG
         else:
             op = dist.ReduceOp.SUM
-        b.work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
+        if getattr(self, "_py_tail", False):
+            # on the current stream, no host synchronisation (ProcessGroupNCCL asyncOp=False)
+            dist.all_reduce(t, op=op, group=self.pg, async_op=False)
+            b.work = True
+        else:
+            b.work = dist.all_reduce(t, op=op, group=self.pg, async_op=True)
         self.buckets_launched += 1
 
     def _mark_ready(self, i):
@@ -363,18 +393,38 @@ class DistributedDataParallel(nn.Module):
     def _on_layer_done(self, prog, layer_idx):
         if self._buf_state == "due":
             self._launch_buffer_sync()
+        # the Program runs the final layer's hooks on the main stream after joining the
+        # weight-gradient stream: the buckets they complete are issued on that stream itself
+        # (no hop through the communication stream on the step's critical tail)
+        tail = bool(getattr(prog, "tail_hook", False)) and self._tail_sync
         if self._native is not None:
             if self._sync_enabled:
-                self._native.mark_layer(layer_idx)
+                if tail:
+                    self._native.set_sync_launch(True)
+                try:
+                    self._native.mark_layer(layer_idx)
+                finally:
+                    if tail:
+                        self._native.set_sync_launch(False)
             return
-        for i in self._layer_params[layer_idx]:
-            self._mark_ready(i)
+        self._py_tail = tail
+        try:
+            for i in self._layer_params[layer_idx]:
+                self._mark_ready(i)
+        finally:
+            self._py_tail = False
 
     def _finalize(self):
         if self.on_compute_done is not None:
             self.on_compute_done()
         if self._buf_state is not None or self._buf_work is not None:
-            self._wait_buffer_sync()
+            if (self._buf_state is None and self._native is not None and self._sync_enabled
+                    and self._native.has_async()):
+                # the broadcast went first on the process group's communication stream; the
+                # reducer's wait for its last bucket, later on that stream, covers it
+                self._buf_work = None
+            else:
+                self._wait_buffer_sync()
         if not self._sync_enabled:
             if self.program is None:
                 self._final_queued = False

@@ -109,7 +109,8 @@ def init(world_size: int | None = None, rank: int | None = None, master_addr: st
                 # runs at high priority (dmlab.utils.streams), and the bucket all-reduces must
                 # keep progressing next to it rather than queue behind the weight gradients
                 opts = getattr(dist, "ProcessGroupNCCL", None)
-                if opts is not None and hasattr(opts, "Options"):
+                if (opts is not None and hasattr(opts, "Options")
+                        and os.environ.get("DMLAB_PG_HIGH_PRIORITY", "1") != "0"):
                     o = opts.Options()
                     o.is_high_priority_stream = True
                     kw["pg_options"] = o
