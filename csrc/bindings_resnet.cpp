@@ -104,6 +104,18 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
 
 // statistics rows a forward conv of this cfg writes (one per row tile, or per workgroup of the
 // persistent cfg 80); ncols is unused
+// part rows of a stride-2 data gradient with the reduction epilogue (conv_dgrad red_part)
+int64_t dgrad_s2_red_rows(int64_t N, int64_t H, int64_t W, int64_t cfg) {
+  dm::ConvGeomSet set{};
+  int ng = 0;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      auto& g = set.g[ng++];
+      g.M = N * ((H - a + 1) / 2) * ((W - b + 1) / 2);
+    }
+  return dm::igemm_multi_rows(set, ng, (int)cfg);
+}
+
 int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols) {
   if (cfg == 80) return dm::res64_grid(M);
   const int bm = dm::igemm_fwd_rowtile(cfg);
@@ -117,7 +129,11 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
                 c10::optional<at::Tensor> add_mask, c10::optional<at::Tensor> red_y,
                 c10::optional<at::Tensor> red_scale, c10::optional<at::Tensor> red_shift,
                 c10::optional<at::Tensor> red_mean, c10::optional<at::Tensor> red_invstd,
-                c10::optional<at::Tensor> red_part, c10::optional<at::Tensor> red_mask) {
+                c10::optional<at::Tensor> red_part, c10::optional<at::Tensor> red_mask,
+                c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> wd2) {
+  // dy2 / wd2 (optional, stride 2): a 1x1/s2/p0 projection's output gradient and packed data-
+  // gradient weights [Cin][1][1][C2]; its data gradient is merged into this launch (parity
+  // class (0,0) gets a second K segment), so dx is written once, complete
   // red_* (optional, cfg 80 only): the backward reduction of the BatchNorm + ReLU whose
   // output gradient dx is (its input red_y, forward scale/shift, mean/invstd) runs in this
   // dgrad's epilogue -> red_part [res64_grid(M)][2][Cin] (bn_backward's pre_slab)
@@ -196,7 +212,6 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
     return;
   }
-  TORCH_CHECK(!red_y.has_value(), "red_*: stride-1 data gradients only");
   // parity classes write disjoint output pixels; a class with no taps (e.g. the odd
   // pixels of a 1x1/s2 conv) is exactly zero, so zero-fill once up front when needed
   bool any_empty = false;
@@ -225,6 +240,63 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       dm::geom_finalize(g);
       set.g[ng++] = g;
     }
+  const bool multi_igemm = cfg == 11 || cfg == 12 || cfg == 13 || cfg == 14 || cfg == 15 ||
+                           cfg == 16 || cfg == 17;
+  dm::DgradSeg2 seg2{};
+  const bool merged = dy2.has_value();
+  if (merged) {
+    TORCH_CHECK(multi_igemm && !accumulate && ng == 4 && pad == 1 && KH == 3 && KW == 3,
+                "dy2: a 3x3/s2/p1 data gradient on an igemm tile (cfg 11-17), no add");
+    need_bf16_nhwc(*dy2, "dy2");
+    TORCH_CHECK(dy2->size(0) == N && dy2->size(1) == OH && dy2->size(2) == OW && dy2->size(3) % 64 == 0,
+                "dy2: [N, OH, OW, C2] with dy's grid, C2 % 64 == 0");
+    TORCH_CHECK(wd2.has_value() && wd2->scalar_type() == at::kBFloat16 && wd2->is_contiguous() &&
+                    wd2->numel() == (int64_t)Cin * dy2->size(3),
+                "wd2 must be bf16 [Cin][1][1][C2]");
+    // class (a, b) = (0, 0) is geometry 0 (the a-major loop above): rows (y, x) are the output
+    // pixels (2y, 2x), read dY at (y, x) through the centre tap -- the 1x1/s2/p0 map
+    TORCH_CHECK(set.g[0].oy0 == 0 && set.g[0].ox0 == 0 && set.g[0].Hg == OH && set.g[0].Wg == OW,
+                "dy2: parity class (0,0) must cover dy's grid");
+    seg2.X2 = dy2->data_ptr();
+    seg2.W2 = wd2->data_ptr();
+    seg2.x2bytes = (unsigned)(dy2->numel() * 2);
+    seg2.w2bytes = (unsigned)(wd2->numel() * 2);
+    seg2.C2 = (int)dy2->size(3);
+    seg2.z = 0;
+  }
+  if (red_y.has_value()) {
+    TORCH_CHECK(multi_igemm && !accumulate && !any_empty && ng == 4,
+                "red_* with stride 2: a complete data gradient (all 4 parity classes, no add) on "
+                "an igemm tile (cfg 11-17)");
+    need_bf16_nhwc(*red_y, "red_y");
+    TORCH_CHECK(red_y->sizes() == dx.sizes(), "red_y: dx's shape");
+    TORCH_CHECK(red_scale && red_shift && red_mean && red_invstd && red_part,
+                "red_*: scale, shift, mean, invstd and part are all required");
+    need_f32(*red_scale, "red_scale", Cin);
+    need_f32(*red_shift, "red_shift", Cin);
+    need_f32(*red_mean, "red_mean", Cin);
+    need_f32(*red_invstd, "red_invstd", Cin);
+    need_f32(*red_part, "red_part", dm::igemm_multi_rows(set, ng, (int)cfg) * 2 * Cin);
+    const unsigned char* rmask = nullptr;
+    if (red_mask.has_value()) {
+      TORCH_CHECK(red_mask->is_cuda() && red_mask->scalar_type() == at::kByte &&
+                      red_mask->is_contiguous() && red_mask->numel() * 8 >= dx.numel(),
+                  "red_mask: uint8 [numel/8] on the device");
+      rmask = red_mask->data_ptr<uint8_t>();
+    }
+    const dm::BnBwdRed red{bp(*red_y), rmask, fp(*red_scale), fp(*red_shift), fp(*red_mean),
+                           fp(*red_invstd), fp(*red_part)};
+    TORCH_CHECK(dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), nullptr, nullptr, set, ng, (int)cfg, st,
+                                    merged ? &seg2 : nullptr, &red),
+                "stride-2 dgrad with reduction: unsupported cfg");
+    return;
+  }
+  if (merged) {
+    TORCH_CHECK(dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), nullptr, nullptr, set, ng, (int)cfg, st,
+                                    &seg2, nullptr),
+                "merged stride-2 dgrad: unsupported cfg");
+    return;
+  }
   // pipelined tiles: all parity classes in one launch (blockIdx.y = class)
   if (cfg >= 90 && cfg <= 93 && ng > 0 &&
       dm::conv_pipe_multi(bp(dy), bp(wd), bp(dx), accumulate ? bp(dx) : nullptr, set, ng, (int)cfg, st))
@@ -787,7 +859,10 @@ void register_resnet(pybind11::module_& m) {
         py::arg("red_y") = py::none(), py::arg("red_scale") = py::none(),
         py::arg("red_shift") = py::none(), py::arg("red_mean") = py::none(),
         py::arg("red_invstd") = py::none(), py::arg("red_part") = py::none(),
-        py::arg("red_mask") = py::none());
+        py::arg("red_mask") = py::none(), py::arg("dy2") = py::none(),
+        py::arg("wd2") = py::none());
+  m.def("dgrad_s2_red_rows", &dgrad_s2_red_rows, py::arg("N"), py::arg("H"), py::arg("W"),
+        py::arg("cfg"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),

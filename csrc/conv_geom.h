@@ -38,6 +38,19 @@ struct ConvGeomSet {
   }
 };
 
+// A second K segment appended to one geometry of a ConvGeomSet launch: after the geometry's
+// own taps, the block accumulates X2[pixel] . W2 over C2 more channels at the SAME GEMM row
+// pixel (tap offset 0).  The stride-2 block's 1x1/s2/p0 projection has exactly the pixel map
+// of the 3x3/s2/p1 conv's parity class (0,0) centre tap, so its data gradient joins that
+// class's K loop and the block output gradient is written once (no accumulate pass).
+struct DgradSeg2 {
+  const void* X2;      // bf16 [N][H][W][C2] (the geometry's input grid)
+  const void* W2;      // bf16 [Ncols][C2]
+  unsigned x2bytes, w2bytes;
+  int C2;              // channels of X2 (multiple of 64)
+  int z;               // geometry index (blockIdx.z) that takes the segment
+};
+
 inline void fastdiv_init(unsigned d, unsigned& mul, unsigned& shr) {
   unsigned l = 0;
   while ((1u << l) < d) ++l;

@@ -48,14 +48,21 @@ namespace dm {
 //   * MF32 = true: v_mfma_f32_32x32x16_bf16 (half the MFMA issues of 16x16x32 for the
 //     same 64x64 wave tile; same LDS bytes per FLOP; the chunk swizzle stays
 //     conflict-free for its 32-row fragment reads).
-template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
+template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH, bool SEG2 = false, bool RED = false>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd3_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
-    float* __restrict__ stats, ConvGeomSet gs, unsigned xbytes, unsigned wbytes) {
+    float* __restrict__ stats, ConvGeomSet gs, unsigned xbytes, unsigned wbytes, DgradSeg2 s2,
+    BnBwdRed red) {
   // blockIdx.z selects the geometry: the parity classes of a stride-2 dgrad (disjoint
   // output pixels, 1..4 taps each) run as ONE launch instead of four small serial ones
   const ConvGeom g = gs.g[blockIdx.z];
-  if ((long long)blockIdx.x * BM >= g.M) return;  // classes with fewer rows (odd sizes)
+  if ((long long)blockIdx.x * BM >= g.M) {  // classes with fewer rows (odd sizes)
+    if constexpr (RED) {  // every part row is summed by the consumer: write this one's zeros
+      const long long row = (long long)blockIdx.z * gridDim.x + blockIdx.x;
+      for (int c = threadIdx.x; c < 2 * g.Ncols; c += blockDim.x) red.part[row * 2 * g.Ncols + c] = 0.f;
+    }
+    return;
+  }
   constexpr int BK = 64;
   constexpr int TM = BM / WM, TN = BN / WN;
   constexpr int FM = MF32 ? 32 : 16;                 // MFMA block edge
@@ -118,10 +125,44 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
   }
   __syncthreads();
   uint4 ra[DEPTH > 1 ? 2 : 1][AR], rb[DEPTH > 1 ? 2 : 1][BR];
-  const int nk = (g.K + BK - 1) / BK;
+  const int nk1 = (g.K + BK - 1) / BK;
+  int nk = nk1;
   const unsigned C2 = (unsigned)g.C * 2u;
+  // SEG2: K tiles nk1.. of geometry s2.z read X2 at the row's own pixel and W2 (block-uniform)
+  unsigned b_off2[SEG2 ? BR : 1];
+  const auto rsx2 = __builtin_amdgcn_make_buffer_rsrc((void*)(SEG2 ? s2.X2 : (const void*)X), (short)0,
+                                                      (int)(SEG2 ? s2.x2bytes : 0u), 0x00020000);
+  const auto rsw2 = __builtin_amdgcn_make_buffer_rsrc((void*)(SEG2 ? s2.W2 : (const void*)Wp), (short)0,
+                                                      (int)(SEG2 ? s2.w2bytes : 0u), 0x00020000);
+  if constexpr (SEG2) {
+    if ((int)blockIdx.z == s2.z) nk += s2.C2 / BK;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + (tid >> 3) + RPP * i;
+      b_off2[i] = n < g.Ncols ? (unsigned)n * (unsigned)s2.C2 * 2u : OOB;
+    }
+  }
 
   auto load = [&](int kt, auto S) {
+    if constexpr (SEG2) {
+      if (kt >= nk1) {
+        const unsigned c0b = (unsigned)(((kt - nk1) * (BK / 8) + chunk) * 16);
+        const unsigned P2 = (unsigned)s2.C2 * 2u;
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          const unsigned off = a_y[i] >= 0 ? a_pix[i] * P2 + c0b : OOB;
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx2, off, 0, 0);
+          ra[S][i] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < BR; ++i) {
+          const unsigned off = b_off2[i] != OOB ? b_off2[i] + c0b : OOB;
+          const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsw2, off, 0, 0);
+          rb[S][i] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        return;
+      }
+    }
     const int kc = kt * (BK / 8) + chunk;
     const int tap = kc >> g.lgC8;
     const unsigned c0b = (unsigned)((kc & ((1 << g.lgC8) - 1)) * 16);  // byte offset in pixel
@@ -256,8 +297,8 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN > 4 ? 1 : 2)) igemm_fwd
     }
   }
 
-  mfma_tile_epilogue<BM, BN, WM, WN, MF32>(acc, smem, m0, n0, blockIdx.z * gridDim.x + blockIdx.x,
-                                           stats, g, Y, ADD);
+  mfma_tile_epilogue<BM, BN, WM, WN, MF32, 1, RED>(acc, smem, m0, n0, blockIdx.z * gridDim.x + blockIdx.x,
+                                                    stats, g, Y, ADD, red);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -703,9 +744,10 @@ static size_t fwd_smem(int BM, int BN) {
   return main > epi ? main : epi;
 }
 
-template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
+template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH, bool SEG2 = false, bool RED = false>
 static void launch_fwd3_set(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                            float* stats, const ConvGeomSet& gs, int ng, hipStream_t st) {
+                            float* stats, const ConvGeomSet& gs, int ng, hipStream_t st,
+                            const DgradSeg2* seg2 = nullptr, const BnBwdRed* red = nullptr) {
   const ConvGeom& g = gs.g[0];
   long long mmax = 0;
   for (int i = 0; i < ng; ++i) mmax = gs.g[i].M > mmax ? gs.g[i].M : mmax;
@@ -713,9 +755,26 @@ static void launch_fwd3_set(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const 
   dim3 grid((unsigned)((mmax + BM - 1) / BM), (g.Ncols + BN - 1) / BN, ng);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = igemm_fwd3_kernel<BM, BN, WM, WN, MF32, DEPTH>;
+  const DgradSeg2 s2 = seg2 ? *seg2 : DgradSeg2{};
+  const BnBwdRed rd = red ? *red : BnBwdRed{};
+  auto k = igemm_fwd3_kernel<BM, BN, WM, WN, MF32, DEPTH, SEG2, RED>;
   set_smem_attr(k, sm);
-  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb);
+  k<<<grid, WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, s2, rd);
+}
+
+// the multi-geometry launch with the optional merged segment / reduction epilogue variants
+template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
+static void launch_fwd3_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                              float* stats, const ConvGeomSet& gs, int ng, hipStream_t st,
+                              const DgradSeg2* seg2, const BnBwdRed* red) {
+  if (seg2 && red)
+    launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH, true, true>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red);
+  else if (seg2)
+    launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH, true, false>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red);
+  else if (red)
+    launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH, false, true>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red);
+  else
+    launch_fwd3_set<BM, BN, WM, WN, MF32, DEPTH>(X, Wp, Y, ADD, stats, gs, ng, st);
 }
 
 template <int BM, int BN, int WM, int WN, bool MF32, int DEPTH>
@@ -728,14 +787,31 @@ static void launch_fwd3(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16
 // up to four geometries sharing X / W / Y (the parity classes of a stride-2 dgrad) in one
 // launch on the v3 128x128 mf32 tile (no statistics: the classes' row tiles would collide)
 bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st) {
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st, const DgradSeg2* seg2,
+                     const BnBwdRed* red) {
+  if (seg2 && (seg2->C2 % 64 != 0 || seg2->z < 0 || seg2->z >= ng))
+    throw std::runtime_error("igemm_fwd_multi: seg2 needs C2 % 64 == 0 and a valid geometry");
   switch (cfg) {  // the v3 mf32 tiles of igemm_fwd (12/13: one tile of prefetch, 15/16: two)
-    case 12: launch_fwd3_set<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
-    case 13: launch_fwd3_set<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
-    case 15: launch_fwd3_set<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
-    case 16: launch_fwd3_set<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, gs, ng, st); return true;
+    case 12: launch_fwd3_multi<128, 128, 2, 2, true, 1>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red); return true;
+    case 13: launch_fwd3_multi<128, 64, 2, 2, true, 1>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red); return true;
+    case 15: launch_fwd3_multi<128, 128, 2, 2, true, 2>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red); return true;
+    case 16: launch_fwd3_multi<128, 64, 2, 2, true, 2>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red); return true;
+    // the 64x64 16x16x32 tiles (small grids: few images per GPU)
+    case 11: case 14: launch_fwd3_multi<64, 64, 2, 2, false, 1>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red); return true;
+    case 17: launch_fwd3_multi<64, 64, 2, 2, false, 2>(X, Wp, Y, ADD, stats, gs, ng, st, seg2, red); return true;
     default: return false;
   }
+}
+
+// part rows of a multi-geometry launch with the BN-backward reduction epilogue (blockIdx.z
+// major, blockIdx.x minor; every block writes its row)
+long long igemm_multi_rows(const ConvGeomSet& gs, int ng, int cfg) {
+  long long mmax = 0;
+  for (int i = 0; i < ng; ++i) mmax = gs.g[i].M > mmax ? gs.g[i].M : mmax;
+  const int bm = (cfg == 12 || cfg == 13 || cfg == 15 || cfg == 16) ? 128
+                 : (cfg == 11 || cfg == 14 || cfg == 17) ? 64 : 0;
+  if (!bm) return 0;
+  return (long long)ng * ((mmax + bm - 1) / bm);
 }
 
 // halo-kernel configs (conv_halo.hip): 42 = 128-pixel tile of 2 x 2 waves, BN 128, with

@@ -78,8 +78,15 @@ void p2p_xgmi_recv(void* dst, long long bytes, const void* ring, const void* ful
 // conv_igemm.hip
 struct ConvGeom;
 struct ConvGeomSet;
+struct DgradSeg2;
+struct BnBwdRed;
+// seg2 (optional): a second K segment of geometry seg2->z (a 1x1/s2 projection's data
+// gradient merged into the stride-2 dgrad's parity class (0,0)); red (optional): the consumer
+// BatchNorm's backward sums in the epilogue (one part row per block: igemm_multi_rows)
 bool igemm_fwd_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st,
+                     const DgradSeg2* seg2 = nullptr, const BnBwdRed* red = nullptr);
+long long igemm_multi_rows(const ConvGeomSet& gs, int ng, int cfg);
 void igemm_fwd(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st);
 // conv_stem.hip: s2d stem (16 channels, 16 taps, 64 outputs) with resident weights (cfg 60)

@@ -8,6 +8,7 @@ models; the native path packs its own bf16 layouts from the fp32 master.
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import os
@@ -161,11 +162,12 @@ class ConvBN(Layer):
         return CB.convbn_fwd(self, x, ctx, train, residual, raw=raw, pre=pre)
 
     def native_bwd(self, dy, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
-                   red_for=None, phase=0):
+                   red_for=None, phase=0, shortcut=None):
         from dmlab.ops import convbn as CB
 
         return CB.convbn_bwd(self, dy, ctx, need_dx, dx_add=dx_add, dx_into=dx_into,
-                             fused_skip=fused_skip, red_for=red_for, phase=phase)
+                             fused_skip=fused_skip, red_for=red_for, phase=phase,
+                             shortcut=shortcut)
 
 
 class ConvBNPool(ConvBN):
@@ -245,35 +247,55 @@ class BasicBlock(Layer):
         # epilogue where the kernel supports it (layer1: csrc/conv_res64.hip RED)
         dy1, dres = self.c2.native_bwd(dy, ctx["c2"], True, fused_skip=need_dx,
                                        red_for=(self.c1, ctx["c1"]))
+        # this block's input gradient is the previous block's output gradient: its c2
+        # BN-backward sums reduce in the epilogue of the dgrad that produces it (Program sets
+        # _bwd_next to the preceding layer)
+        nxt = getattr(self, "_bwd_next", None)
+        red_for = None
+        if nxt is not None and isinstance(nxt[0], BasicBlock):
+            red_for = (nxt[0].c2, nxt[1]["c2"])
+        elif nxt is not None and isinstance(nxt[0], ConvBN):  # the stem
+            red_for = nxt
         if self.down is None:
-            # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass), and
-            # that dgrad's output is the previous block's output gradient: its c2 BN-backward
-            # sums reduce there too (Program sets _bwd_next to the preceding layer)
-            nxt = getattr(self, "_bwd_next", None)
-            red_for = None
-            if nxt is not None and isinstance(nxt[0], BasicBlock):
-                red_for = (nxt[0].c2, nxt[1]["c2"])
-            elif nxt is not None and isinstance(nxt[0], ConvBN):  # the stem
-                red_for = nxt
+            # identity skip: its gradient is added in c1's dgrad epilogue (no extra pass)
             return self.c1.native_bwd(dy1, ctx["c1"], need_dx, dx_add=dres if need_dx else None,
                                       red_for=red_for)
         aux = self._bn_stream() if need_dx else None
-        if aux is not None:
+        cd = ctx["cd"]
+        if need_dx:
             # the shortcut's BN backward (reduce + apply: memory-bound passes over the block's
-            # output gradient) only needs dres: it runs on a second high-priority stream next
-            # to c1's BN backward and stride-2 data gradient instead of after them
+            # output gradient) only needs dres: with an aux stream it runs on that second
+            # high-priority stream next to c1's BN backward instead of after it
             main = torch.cuda.current_stream()
-            aux.wait_stream(main)
-            with torch.cuda.stream(aux):
-                self.down.native_bwd(dres, ctx["cd"], need_dx, phase=1)
-            dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
-            main.wait_stream(aux)
-            self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx, phase=2)
+            if aux is not None:
+                aux.wait_stream(main)
+            with torch.cuda.stream(aux) if aux is not None else contextlib.nullcontext():
+                self.down.native_bwd(dres, cd, need_dx, phase=1)
+
+            def join():
+                if aux is not None:
+                    main.wait_stream(aux)
+                dy2 = cd["_bn_out"][0]
+                dy2.record_stream(main)
+                from dmlab.ops.convbn import packed_weights
+
+                return dy2, packed_weights(self.down, need_wd=True)[1]
+
+            # c1's stride-2 data gradient takes the shortcut's 1x1/s2 data gradient as a second
+            # K segment of its parity class (0,0): dx is written once, complete, and the
+            # previous block's BN-backward sums reduce in the same epilogue
+            sc = {"join": join, "merged": False}
+            dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx, shortcut=sc, red_for=red_for)
+            if sc["merged"]:
+                self.down.native_bwd(dres, cd, False, phase=2)  # its weight gradient only
+                return dx
+            if aux is not None:
+                main.wait_stream(aux)
+            self.down.native_bwd(dres, cd, need_dx, dx_into=dx, phase=2)
             return dx
-        dx = self.c1.native_bwd(dy1, ctx["c1"], need_dx)
-        # projection skip: its dgrad (one parity class of the 1x1/s2 conv) accumulates in place
-        self.down.native_bwd(dres, ctx["cd"], need_dx, dx_into=dx)
-        return dx
+        self.c1.native_bwd(dy1, ctx["c1"], need_dx)
+        self.down.native_bwd(dres, cd, need_dx)
+        return None
 
     def _bn_stream(self):
         prog = getattr(self, "_prog", None)

@@ -498,7 +498,12 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
     return out
 
 
-def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
+# the v3 igemm tiles whose multi-geometry launch (a stride-2 data gradient's 4 parity classes)
+# takes the merged projection segment and the BN-backward reduction epilogue
+_MULTI_IGEMM = (11, 12, 13, 14, 15, 16, 17)
+
+
+def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False, complete_s2=False):
     """conv_dgrad kwargs that reduce the consumer BN's backward sums in the dgrad epilogue
     (see convbn_bwd ``red_for``); {} when the kernel or the layer does not qualify.
 
@@ -508,10 +513,13 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
     dgrad + skip).  The stem (BN + ReLU + max-pool) reduces over the pooled grid: y is its
     value at each window's argmax (ctx["yarg"]), as bn_bwd_reduce_masked does."""
     rl, rctx = red_for
-    kernel_ok = cfg == 80 or 90 <= cfg <= 93 or cfg == 42
+    # stride 2: only a data gradient that writes dx complete in one launch (the projection's
+    # 1x1/s2 segment merged in, ``complete_s2``) can reduce its consumer's sums
+    s2_ok = stride == 2 and complete_s2 and cfg in _MULTI_IGEMM
+    kernel_ok = (stride == 1 and (cfg == 80 or 90 <= cfg <= 93 or cfg == 42)) or s2_ok
     pool = getattr(rl, "pool_k", 0)
     y = rctx.get("yarg") if pool else rctx.get("y")
-    if (stride != 1 or not kernel_ok or not rl.relu or y is None
+    if (not kernel_ok or not rl.relu or y is None
             or rctx.get("mean") is None or rctx.get("pre_sums") is not None
             or tuple(y.shape) != tuple(dx.shape)):
         return {}
@@ -530,7 +538,8 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
             and os.environ.get("DMLAB_RES64_RED_ADD", "0") != "1"):
         return {}
     N, H, W, C = dx.shape
-    rows = L.conv_stats_rows(N * H * W, cfg, C)
+    rows = (L.dgrad_s2_red_rows(N, H, W, cfg) if stride == 2
+            else L.conv_stats_rows(N * H * W, cfg, C))
     part = torch.empty(rows * 2 * C, device=dx.device, dtype=torch.float32)
     rctx["pre_sums"] = dict(pre_slab=part, pre_rows=rows)
     kw = dict(red_y=y, red_scale=rctx["scale"], red_shift=rctx["shift"],
@@ -541,7 +550,7 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False):
 
 
 def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=False,
-               red_for=None, phase=0):
+               red_for=None, phase=0, shortcut=None):
     """Returns dx (or (dx, dres) when the forward had a residual input).
 
     ``dx_add``  : tensor added to dx in the dgrad epilogue (identity skip gradient), or
@@ -557,7 +566,13 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
                   own backward skips the pass that re-reads dx and y
     ``phase``    : 0 = the whole backward; 1 = only the BatchNorm backward (dy kept in ctx),
                   on the caller's current stream; 2 = the weight and data gradients from
-                  phase 1's dy (the caller has made the current stream wait for phase 1)"""
+                  phase 1's dy (the caller has made the current stream wait for phase 1)
+    ``shortcut`` : {"join": fn} of the block's 1x1/s2 projection (a stride-2 3x3 conv only):
+                  fn() orders the current stream after the projection's BatchNorm backward and
+                  returns (its dy, its packed data-gradient weights); when the dgrad tile can
+                  merge it, the projection's data gradient becomes a second K segment of parity
+                  class (0,0) in THIS launch (dx written once, complete, so ``red_for`` applies
+                  too) and shortcut["merged"] is set -- the caller then skips its dgrad"""
     if ctx.get("fused_stem"):
         return _stem_fused_bwd(layer, dout, ctx)
     L = lib()
@@ -677,11 +692,20 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             L.conv_dgrad(dy, wd, dx_into, k, k, s, p, dx_into, cfg)
         else:
             dx = empty_nhwc(N_, H, W, Cin, x)
-            red_kw = _dgrad_red(L, red_for, cfg, s, dx) if red_for is not None else {}
+            merge_kw = {}
+            if (shortcut is not None and s == 2 and k == 3 and p == 1 and dx_add is None
+                    and cfg in _MULTI_IGEMM and H % 2 == 0 and W % 2 == 0
+                    and os.environ.get("DMLAB_MERGE_SHORTCUT", "1") != "0"):
+                dy2, wd2 = shortcut["join"]()
+                if dy2.shape[:3] == dy.shape[:3] and dy2.shape[3] % 64 == 0:
+                    merge_kw = dict(dy2=dy2, wd2=wd2)
+                    shortcut["merged"] = True
+            red_kw = (_dgrad_red(L, red_for, cfg, s, dx, complete_s2=bool(merge_kw))
+                      if red_for is not None else {})
             if isinstance(dx_add, tuple):
                 L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2], **red_kw)
             else:
-                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **red_kw)
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **red_kw, **merge_kw)
     if ctx["has_res"]:
         return dx, (("masked", dout, ctx["mask"]) if masked_res else dres)
     return dx
