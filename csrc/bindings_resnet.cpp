@@ -56,6 +56,36 @@ dm::ConvGeom fwd_geom(const at::Tensor& x, int Cout, int KH, int KW, int stride,
 
 int64_t conv_stats_rows(int64_t M, int64_t cfg, int64_t ncols);
 
+// The folded BatchNorm-backward operand (kernels.h BnBwdIn) of a data / weight gradient whose
+// dY argument is that BN's OUTPUT gradient dz: y (its input, dz's shape), coef [3][C] (bn_backward
+// with dy None), scale/shift (ReLU mask from y) or the 1-bit mask, neither: no ReLU
+dm::BnBwdIn bwd_in(const at::Tensor& dz, const at::Tensor& y, const at::Tensor& coef,
+                   const c10::optional<at::Tensor>& sc, const c10::optional<at::Tensor>& sh,
+                   const c10::optional<at::Tensor>& mask) {
+  need_bf16_nhwc(y, "bwd_y");
+  TORCH_CHECK(y.sizes() == dz.sizes(), "bwd_y: the gradient's shape");
+  const int C = dz.size(3);
+  need_f32(coef, "bwd_coef", 3 * C);
+  // unused scale/shift alias coef: the kernels load them unconditionally (kernels.h BnBwdIn)
+  dm::BnBwdIn b{bp(y), nullptr, fp(coef), fp(coef), fp(coef), C, 0};
+  TORCH_CHECK(!(mask.has_value() && sc.has_value()), "bwd: mask or scale/shift, not both");
+  if (sc.has_value()) {
+    TORCH_CHECK(sh.has_value(), "bwd_scale needs bwd_shift");
+    need_f32(*sc, "bwd_scale", C);
+    need_f32(*sh, "bwd_shift", C);
+    b.sc = fp(*sc);
+    b.sh = fp(*sh);
+    b.mode = 2;
+  }
+  if (mask.has_value()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() * 8 == dz.numel(), "bwd_mask: uint8 [numel/8]");
+    b.mask = mask->data_ptr<uint8_t>();
+    b.mode = 4;
+  }
+  return b;
+}
+
 // y = conv(x, w)  (+add) ; stats [T][2][Cout] optional
 void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Tensor> stats,
               c10::optional<at::Tensor> add, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
@@ -104,6 +134,29 @@ void conv_fwd(at::Tensor x, at::Tensor wpack, at::Tensor y, c10::optional<at::Te
 
 // statistics rows a forward conv of this cfg writes (one per row tile, or per workgroup of the
 // persistent cfg 80); ncols is unused
+// The BN-backward apply of a 3x3/s1/p1 conv's BatchNorm can fold into both consumers: the data
+// gradient on the cfg 42 halo tile and the 9-tap halo weight gradient (conv_dgrad / conv_wgrad
+// bwd_*).  x: the conv's input [N,H,W,Cin]; Cout its output channels.
+bool bn_fold_supported(int64_t N, int64_t H, int64_t W, int64_t Cin, int64_t Cout) {
+  if (Cin % 64 || Cout % 64 || ((Cout / 8) & (Cout / 8 - 1)) || ((Cin / 8) & (Cin / 8 - 1)))
+    return false;
+  dm::ConvGeom d{};  // data gradient (conv_dgrad stride 1)
+  d.N = N; d.H = H; d.W = W; d.C = Cout; d.lgC8 = ilog2(Cout / 8);
+  d.OH = H; d.OW = W; d.OC = Cin; d.KW = 3; d.Ncols = Cin; d.wK = 9 * Cout;
+  d.Hg = H; d.Wg = W; d.isy = 1; d.isx = 1; d.osy = 1; d.osx = 1; d.oy0 = 0; d.ox0 = 0;
+  d.nth = 3; d.ntw = 3; d.dy0 = 1; d.dys = -1; d.dx0 = 1; d.dxs = -1;
+  d.kh0 = 0; d.khs = 1; d.kw0 = 0; d.kws = 1; d.M = N * H * W; d.K = 9 * Cout;
+  dm::geom_finalize(d);
+  dm::ConvGeom w{};  // weight gradient (fwd_geom of the conv)
+  w.N = N; w.H = H; w.W = W; w.C = Cin; w.lgC8 = ilog2(Cin / 8);
+  w.Hg = H; w.Wg = W; w.isy = 1; w.isx = 1; w.OH = H; w.OW = W; w.OC = Cout;
+  w.osy = 1; w.osx = 1; w.oy0 = 0; w.ox0 = 0; w.nth = 3; w.ntw = 3; w.dy0 = -1; w.dys = 1;
+  w.dx0 = -1; w.dxs = 1; w.kh0 = 0; w.khs = 1; w.kw0 = 0; w.kws = 1; w.KW = 3;
+  w.Ncols = Cout; w.wK = 9 * Cin; w.M = N * H * W; w.K = 9 * Cin;
+  dm::geom_finalize(w);
+  return dm::conv_halo_supported(d) && dm::wgrad_halo_supported(w);
+}
+
 // part rows of a stride-2 data gradient with the reduction epilogue (conv_dgrad red_part)
 int64_t dgrad_s2_red_rows(int64_t N, int64_t H, int64_t W, int64_t cfg) {
   dm::ConvGeomSet set{};
@@ -113,6 +166,7 @@ int64_t dgrad_s2_red_rows(int64_t N, int64_t H, int64_t W, int64_t cfg) {
       auto& g = set.g[ng++];
       g.M = N * ((H - a + 1) / 2) * ((W - b + 1) / 2);
     }
+  if (cfg >= 90 && cfg <= 93) return dm::pipe_multi_rows(set, ng);
   return dm::igemm_multi_rows(set, ng, (int)cfg);
 }
 
@@ -130,7 +184,12 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
                 c10::optional<at::Tensor> red_scale, c10::optional<at::Tensor> red_shift,
                 c10::optional<at::Tensor> red_mean, c10::optional<at::Tensor> red_invstd,
                 c10::optional<at::Tensor> red_part, c10::optional<at::Tensor> red_mask,
-                c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> wd2) {
+                c10::optional<at::Tensor> dy2, c10::optional<at::Tensor> wd2,
+                c10::optional<at::Tensor> bwd_y, c10::optional<at::Tensor> bwd_coef,
+                c10::optional<at::Tensor> bwd_scale, c10::optional<at::Tensor> bwd_shift,
+                c10::optional<at::Tensor> bwd_mask) {
+  // bwd_* (optional, stride 1, cfg 42): dy is a BatchNorm's OUTPUT gradient; the kernel stages
+  // that BN's backward a*dz' + b*y + c itself (bwd_in)
   // dy2 / wd2 (optional, stride 2): a 1x1/s2/p0 projection's output gradient and packed data-
   // gradient weights [Cin][1][1][C2]; its data gradient is merged into this launch (parity
   // class (0,0) gets a second K segment), so dx is written once, complete
@@ -169,6 +228,13 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
                 "add_mask: uint8 [numel/8] on the device");
     addm = add_mask->data_ptr<uint8_t>();
   }
+  dm::BnBwdIn bwd{};
+  const bool has_bwd = bwd_y.has_value();
+  if (has_bwd) {
+    TORCH_CHECK(stride == 1 && cfg == 42 && bwd_coef.has_value(),
+                "bwd_*: a stride-1 cfg 42 (halo) data gradient with bwd_coef");
+    bwd = bwd_in(dy, *bwd_y, *bwd_coef, bwd_scale, bwd_shift, bwd_mask);
+  }
   if (stride == 1) {
     auto g = base;
     g.addm = addm;
@@ -177,6 +243,11 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     g.kh0 = 0; g.khs = 1; g.kw0 = 0; g.kws = 1;
     g.M = (long long)N * H * W; g.K = KH * KW * Cout;
     dm::geom_finalize(g);
+    if (has_bwd) {
+      int hbn = 0, hwv = 0;
+      TORCH_CHECK(dm::halo_cfg((int)cfg, hbn, hwv) && dm::conv_halo_supported(g),
+                  "bwd_*: the geometry must suit the halo kernel");
+    }
     if (red_y.has_value()) {
       const bool pipe = cfg >= 90 && cfg <= 93 && dm::conv_pipe_supported(g, (int)cfg);
       int hbn = 0, hwv = 0;
@@ -204,14 +275,23 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
       if (pipe)
         dm::conv_pipe(bp(dy), bp(wd), bp(dx), addp, nullptr, g, (int)cfg, st, &red);
       else if (halo)
-        dm::conv_halo(bp(dy), bp(wd), bp(dx), addp, nullptr, g, hbn, hwv, st, nullptr, nullptr, &red);
+        dm::conv_halo(bp(dy), bp(wd), bp(dx), addp, nullptr, g, hbn, hwv, st, nullptr, nullptr, &red,
+                      has_bwd ? &bwd : nullptr);
       else
         dm::conv_res64(bp(dy), bp(wd), bp(dx), addp, nullptr, g, st, nullptr, nullptr, &red);
+      return;
+    }
+    if (has_bwd) {
+      int hbn = 0, hwv = 0;
+      dm::halo_cfg((int)cfg, hbn, hwv);
+      dm::conv_halo(bp(dy), bp(wd), bp(dx), addp, nullptr, g, hbn, hwv, st, nullptr, nullptr, nullptr,
+                    &bwd);
       return;
     }
     dm::igemm_fwd(bp(dy), bp(wd), bp(dx), addp, nullptr, g, cfg, st);
     return;
   }
+  TORCH_CHECK(!has_bwd, "bwd_*: stride-1 data gradients only");
   // parity classes write disjoint output pixels; a class with no taps (e.g. the odd
   // pixels of a 1x1/s2 conv) is exactly zero, so zero-fill once up front when needed
   bool any_empty = false;
@@ -242,11 +322,15 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     }
   const bool multi_igemm = cfg == 11 || cfg == 12 || cfg == 13 || cfg == 14 || cfg == 15 ||
                            cfg == 16 || cfg == 17;
+  // the pipelined tiles merge a projection of dy's own channel count (ResNet: always)
+  const bool multi_pipe = cfg >= 90 && cfg <= 93;
   dm::DgradSeg2 seg2{};
   const bool merged = dy2.has_value();
   if (merged) {
-    TORCH_CHECK(multi_igemm && !accumulate && ng == 4 && pad == 1 && KH == 3 && KW == 3,
-                "dy2: a 3x3/s2/p1 data gradient on an igemm tile (cfg 11-17), no add");
+    TORCH_CHECK((multi_igemm || (multi_pipe && dy2->size(3) == Cout)) && !accumulate && ng == 4 &&
+                    pad == 1 && KH == 3 && KW == 3,
+                "dy2: a 3x3/s2/p1 data gradient on an igemm tile (cfg 11-17) or a pipelined tile "
+                "(cfg 90-93, projection channels == dy's), no add");
     need_bf16_nhwc(*dy2, "dy2");
     TORCH_CHECK(dy2->size(0) == N && dy2->size(1) == OH && dy2->size(2) == OW && dy2->size(3) % 64 == 0,
                 "dy2: [N, OH, OW, C2] with dy's grid, C2 % 64 == 0");
@@ -265,9 +349,9 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     seg2.z = 0;
   }
   if (red_y.has_value()) {
-    TORCH_CHECK(multi_igemm && !accumulate && !any_empty && ng == 4,
+    TORCH_CHECK((multi_igemm || multi_pipe) && !accumulate && !any_empty && ng == 4,
                 "red_* with stride 2: a complete data gradient (all 4 parity classes, no add) on "
-                "an igemm tile (cfg 11-17)");
+                "an igemm (cfg 11-17) or pipelined (cfg 90-93) tile");
     need_bf16_nhwc(*red_y, "red_y");
     TORCH_CHECK(red_y->sizes() == dx.sizes(), "red_y: dx's shape");
     TORCH_CHECK(red_scale && red_shift && red_mean && red_invstd && red_part,
@@ -276,7 +360,9 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     need_f32(*red_shift, "red_shift", Cin);
     need_f32(*red_mean, "red_mean", Cin);
     need_f32(*red_invstd, "red_invstd", Cin);
-    need_f32(*red_part, "red_part", dm::igemm_multi_rows(set, ng, (int)cfg) * 2 * Cin);
+    need_f32(*red_part, "red_part",
+             (multi_pipe ? dm::pipe_multi_rows(set, ng) : dm::igemm_multi_rows(set, ng, (int)cfg)) *
+                 2 * Cin);
     const unsigned char* rmask = nullptr;
     if (red_mask.has_value()) {
       TORCH_CHECK(red_mask->is_cuda() && red_mask->scalar_type() == at::kByte &&
@@ -286,15 +372,20 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
     }
     const dm::BnBwdRed red{bp(*red_y), rmask, fp(*red_scale), fp(*red_shift), fp(*red_mean),
                            fp(*red_invstd), fp(*red_part)};
-    TORCH_CHECK(dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), nullptr, nullptr, set, ng, (int)cfg, st,
-                                    merged ? &seg2 : nullptr, &red),
-                "stride-2 dgrad with reduction: unsupported cfg");
+    const bool ok = multi_pipe
+        ? dm::conv_pipe_multi(bp(dy), bp(wd), bp(dx), nullptr, set, ng, (int)cfg, st,
+                              merged ? &seg2 : nullptr, &red)
+        : dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), nullptr, nullptr, set, ng, (int)cfg, st,
+                              merged ? &seg2 : nullptr, &red);
+    TORCH_CHECK(ok, "stride-2 dgrad with reduction: unsupported cfg / geometry");
     return;
   }
   if (merged) {
-    TORCH_CHECK(dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), nullptr, nullptr, set, ng, (int)cfg, st,
-                                    &seg2, nullptr),
-                "merged stride-2 dgrad: unsupported cfg");
+    const bool ok = multi_pipe
+        ? dm::conv_pipe_multi(bp(dy), bp(wd), bp(dx), nullptr, set, ng, (int)cfg, st, &seg2, nullptr)
+        : dm::igemm_fwd_multi(bp(dy), bp(wd), bp(dx), nullptr, nullptr, set, ng, (int)cfg, st, &seg2,
+                              nullptr);
+    TORCH_CHECK(ok, "merged stride-2 dgrad: unsupported cfg / geometry");
     return;
   }
   // pipelined tiles: all parity classes in one launch (blockIdx.y = class)
@@ -313,9 +404,13 @@ void conv_dgrad(at::Tensor dy, at::Tensor wd, at::Tensor dx, int64_t KH, int64_t
 void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int64_t Cin,
                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, double beta, int64_t S,
                 int64_t cfg, bool s2d, c10::optional<at::Tensor> pre_scale,
-                c10::optional<at::Tensor> pre_shift) {
+                c10::optional<at::Tensor> pre_shift, c10::optional<at::Tensor> bwd_y,
+                c10::optional<at::Tensor> bwd_coef, c10::optional<at::Tensor> bwd_scale,
+                c10::optional<at::Tensor> bwd_shift, c10::optional<at::Tensor> bwd_mask) {
   // s2d: x/dy are the space-to-depth stem operands (4x4/s1 conv over 4*Cin channels);
   // dw is the original [Cout][Cin][7][7] gradient
+  // bwd_* (optional, cfg 4): dy is a BatchNorm's OUTPUT gradient; the halo weight gradient
+  // stages that BN's backward a*dz' + b*y + c itself (bwd_in)
   need_bf16_nhwc(x, "x");
   need_bf16_nhwc(dy, "dy");
   const int Cout = dy.size(3);
@@ -327,7 +422,20 @@ void conv_wgrad(at::Tensor x, at::Tensor dy, at::Tensor dw, at::Tensor slab, int
   const long long mchunk = ((steps + S - 1) / S) * 64;  // multiple of both kernels' row step
   const DeviceGuard guard(x.device());
   auto st = cur_stream();
-  if (pre_scale.has_value()) {
+  if (bwd_y.has_value()) {
+    TORCH_CHECK(cfg == 4 && !s2d && bwd_coef.has_value() && dm::wgrad_halo_supported(g),
+                "bwd_*: the 9-tap halo weight gradient (cfg 4), a 3x3/s1/p1 geometry, bwd_coef");
+    const dm::BnBwdIn bwd = bwd_in(dy, *bwd_y, *bwd_coef, bwd_scale, bwd_shift, bwd_mask);
+    const float *psc = nullptr, *psh = nullptr;
+    if (pre_scale.has_value()) {
+      TORCH_CHECK(pre_shift.has_value(), "pre_scale needs pre_shift");
+      need_f32(*pre_scale, "pre_scale", x.size(3));
+      need_f32(*pre_shift, "pre_shift", x.size(3));
+      psc = fp(*pre_scale);
+      psh = fp(*pre_shift);
+    }
+    dm::wgrad_halo(bp(x), bp(dy), fp(slab), g, (int)S, mchunk, 3, st, psc, psh, &bwd);
+  } else if (pre_scale.has_value()) {
     // x = previous conv's raw output, operand relu(x*sc + sh)
     TORCH_CHECK(pre_shift.has_value() && !s2d, "pre_scale needs pre_shift (not with s2d)");
     need_f32(*pre_scale, "pre_scale", x.size(3));
@@ -860,13 +968,19 @@ void register_resnet(pybind11::module_& m) {
         py::arg("red_shift") = py::none(), py::arg("red_mean") = py::none(),
         py::arg("red_invstd") = py::none(), py::arg("red_part") = py::none(),
         py::arg("red_mask") = py::none(), py::arg("dy2") = py::none(),
-        py::arg("wd2") = py::none());
+        py::arg("wd2") = py::none(), py::arg("bwd_y") = py::none(),
+        py::arg("bwd_coef") = py::none(), py::arg("bwd_scale") = py::none(),
+        py::arg("bwd_shift") = py::none(), py::arg("bwd_mask") = py::none());
+  m.def("bn_fold_supported", &bn_fold_supported);
   m.def("dgrad_s2_red_rows", &dgrad_s2_red_rows, py::arg("N"), py::arg("H"), py::arg("W"),
         py::arg("cfg"));
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("dw"), py::arg("slab"),
         py::arg("Cin"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
         py::arg("beta"), py::arg("S"), py::arg("cfg"), py::arg("s2d"),
-        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none());
+        py::arg("pre_scale") = py::none(), py::arg("pre_shift") = py::none(),
+        py::arg("bwd_y") = py::none(), py::arg("bwd_coef") = py::none(),
+        py::arg("bwd_scale") = py::none(), py::arg("bwd_shift") = py::none(),
+        py::arg("bwd_mask") = py::none());
   m.def("pack_weights", &pack_weights);
   m.def("pack_weights_multi", &pack_weights_multi);
   m.def("pack_weights_tiled", &pack_weights_tiled);

@@ -51,12 +51,16 @@ constexpr unsigned OOB = 0x80000000u;
 #endif
 // RED: the data gradient's epilogue also reduces the consumer BatchNorm's backward sums
 // (mfma_tile_epilogue RED)
-template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF, bool RED = false>
+// BWD (data gradients): X is a BatchNorm's OUTPUT gradient dz and the operand is that BN's
+// backward dy = a*dz' + b*y + c (kernels.h BnBwdIn), computed while staging: the BN-backward
+// apply pass and its dy tensor do not exist
+template <int BN, int HR, int WM, int WN, int BMH, bool PRE, int PF, bool RED = false, bool BWD = false>
 __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_HALO39_MINB : 2) conv_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeom g, unsigned xbytes, unsigned wbytes,
     const float* __restrict__ pre_sc, const float* __restrict__ pre_sh,
-    int xcd, int mtiles, BnBwdRed red) {
+    int xcd, int mtiles, BnBwdRed red, BnBwdIn bwd) {
+  static_assert(!(PRE && BWD), "one operand transform");
   // pre_sc/pre_sh (optional): X is a conv's raw output y; the operand is relu(y*sc + sh)
   // (BatchNorm-apply + ReLU of the previous layer fused into the halo staging).  Out-of-
   // image taps still read the zero row, i.e. the padding stays zero AFTER the BN.
@@ -70,6 +74,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
   bf16_t* Hs = reinterpret_cast<bf16_t*>(smem);      // [HP_MAX + 1][64], last row = zeros
   bf16_t* Bs = Hs + (HP_MAX + 1) * HBK;              // [2][BN][64]
   int4* taps = reinterpret_cast<int4*>(Bs + 2 * BN * HBK);
+  float* btab = reinterpret_cast<float*>(taps + MAXTAPS);  // BWD: [5][C] coefficients
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
@@ -96,6 +101,7 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
                           dy * g.W + dx);
   }
   if (tid < 8) *reinterpret_cast<uint4*>(Hs + HP_MAX * HBK + tid * 8) = make_uint4(0, 0, 0, 0);
+  if constexpr (BWD) bwd_tab_fill(btab, bwd, 0, g.C, tid, WM * WN * 64);
 
   // halo extent (flattened rows r0-1 .. r1+1)
   const int r0 = (int)fdiv((unsigned)m0, g.wg_mul, g.wg_shr);
@@ -128,7 +134,12 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
   __syncthreads();
 
   uint4 rh[HR], rb[BR];
-  auto load_halo = [&](int cc) {
+  // BWD: the BN input y of the same chunks and their mask bytes, loaded with rh
+  uint4 ry[BWD ? HR : 1];
+  unsigned rmk[BWD ? HR : 1];
+  const auto rsy = __builtin_amdgcn_make_buffer_rsrc((void*)(BWD ? (const void*)bwd.y : (const void*)X),
+                                                     (short)0, (int)(BWD ? xbytes : 0u), 0x00020000);
+  auto load_halo = [&](int cc) __attribute__((always_inline)) {
     const unsigned cb = (unsigned)(cc * HBK + chunk * 8) * 2u;
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
@@ -138,9 +149,19 @@ __global__ void __launch_bounds__(WM * WN * 64, (WM * WN == 8 && BN == 64) ? DM_
       const unsigned off = ok ? (unsigned)gp * (unsigned)g.C * 2u + cb : OOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
       rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
+      if constexpr (BWD) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsy, off, 0, 0);
+        ry[j] = make_uint4(w[0], w[1], w[2], w[3]);
+        rmk[j] = bwd_mask_byte(bwd, off, xbytes >> 4);  // off is OOB (reads 0) past the tensor
+      }
     }
   };
-  auto store_halo = [&](int cc) {
+  auto store_halo = [&](int cc) __attribute__((always_inline)) {
+    if constexpr (BWD) {
+      // rows outside the tensor become garbage here: no valid tap reads them (zero row)
+#pragma unroll
+      for (int j = 0; j < HR; ++j) rh[j] = bwd_apply(btab, g.C, cc * HBK + chunk * 8, rh[j], ry[j], rmk[j]);
+    }
 #pragma unroll
     for (int j = 0; j < HR; ++j) {
       const int hh = (tid >> 3) + RPP * j;
@@ -308,21 +329,23 @@ int halo_rows_needed(const ConvGeom& g, int bm = HBM) {
   return ((g.W - 1 + bm - 1) / g.W + 3) * g.W;
 }
 
-template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1, bool RED = false>
+template <int BN, int HR, int WM, int WN, int BMH = HBM, int PF = 1, bool RED = false, bool BWD = false>
 void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                  const ConvGeom& g, const float* pre_sc, const float* pre_sh, hipStream_t st,
-                 const BnBwdRed* red = nullptr) {
+                 const BnBwdRed* red = nullptr, const BnBwdIn* bwd = nullptr) {
   constexpr int RPP = WM * WN * 8;
-  const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16;
+  const size_t main = (size_t)(RPP * HR + 1) * HBK * 2 + (size_t)2 * BN * HBK * 2 + MAXTAPS * 16 +
+                      (BWD ? (size_t)5 * g.C * 4 : 0);
   const size_t epi = (size_t)128 * (BN + 4) * 4;  // staged in 128-row bands
   const size_t sm = main > epi ? main : epi;
   const unsigned mt = (unsigned)((g.M + BMH - 1) / BMH), nt = (g.Ncols + BN - 1) / BN;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  auto k = RED ? conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF, RED>
+  auto k = (RED || BWD) ? conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF, RED, BWD>
          : pre_sc ? conv_halo_kernel<BN, HR, WM, WN, BMH, true, PF>
                   : conv_halo_kernel<BN, HR, WM, WN, BMH, false, PF>;
   const BnBwdRed rarg = red ? *red : BnBwdRed{};
+  const BnBwdIn barg = bwd ? *bwd : BnBwdIn{};
   set_smem_attr(k, sm);
   // XCD-aware 1-D grid over the M tiles (padded to a multiple of 8) x N tiles: the N tiles of
   // one M tile share an XCD's L2.  Measured (tools/bench_conv.py, batch 512): layer3 fwd
@@ -330,11 +353,11 @@ void launch_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   if (nt > 1) {
     const unsigned mt8 = (mt + 7) / 8 * 8;
     k<<<dim3(mt8 * nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
-                                                (int)nt, (int)mt, rarg);
+                                                (int)nt, (int)mt, rarg, barg);
     return;
   }
   k<<<dim3(mt, nt), WM * WN * 64, sm, st>>>(X, Wp, Y, ADD, stats, g, xb, wb, pre_sc, pre_sh,
-                                            0, (int)mt, rarg);
+                                            0, (int)mt, rarg, barg);
 }
 }  // namespace
 
@@ -353,18 +376,30 @@ bool conv_halo_supported(const ConvGeom& g) {
 // tiles (igemm_fwd's halo cfgs): waves 4 | 0x100 = 128 px as 2 x 2 waves of 64 x 64 with two
 // weight tiles of register prefetch (cfg 42); 16 = 256 px as 4 x 2 waves of 64 x 32 (cfg 39);
 // 32 = 256 px as 4 x 1 waves of 64 x 64 (cfg 41)
+template <bool RED, bool BWD>
+static void launch_halo42(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
+                          float* stats, const ConvGeom& g, int hp, hipStream_t st,
+                          const BnBwdRed* red, const BnBwdIn* bwd) {
+  const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
+  if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2, RED, BWD>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red, bwd);
+  else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2, RED, BWD>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red, bwd);
+  else launch_halo<128, 12, 2, 2, HBM, 2, RED, BWD>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red, bwd);
+}
+
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st, const float* pre_sc,
-               const float* pre_sh, const BnBwdRed* red) {
+               const float* pre_sh, const BnBwdRed* red, const BnBwdIn* bwd) {
   const int hp = halo_rows_needed(g), hp2 = halo_rows_needed(g, 256);
-  if (red) {
-    // the BN-backward reduction epilogue is built for the cfg 42 tile (layer2's data gradient)
+  if (red || bwd) {
+    // the BN-backward reduction epilogue and the folded BN-backward operand are built for the
+    // cfg 42 tile (layer2's data gradient)
     if (waves != (4 | 0x100) || bn != 128 || pre_sc)
-      throw std::runtime_error("conv_halo: BN-backward reduction needs cfg 42, no PRE input");
-    const int hr = hp <= 192 ? 6 : hp <= 256 ? 8 : 12;
-    if (hr == 6) launch_halo<128, 6, 2, 2, HBM, 2, true>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red);
-    else if (hr == 8) launch_halo<128, 8, 2, 2, HBM, 2, true>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red);
-    else launch_halo<128, 12, 2, 2, HBM, 2, true>(X, Wp, Y, ADD, stats, g, nullptr, nullptr, st, red);
+      throw std::runtime_error("conv_halo: BN-backward reduction / operand needs cfg 42, no PRE input");
+    if (bwd && (!bwd->y || !bwd->coef || bwd->C != g.C))
+      throw std::runtime_error("conv_halo: BN-backward operand needs y, coef and C == input channels");
+    if (red && bwd) launch_halo42<true, true>(X, Wp, Y, ADD, stats, g, hp, st, red, bwd);
+    else if (red) launch_halo42<true, false>(X, Wp, Y, ADD, stats, g, hp, st, red, bwd);
+    else launch_halo42<false, true>(X, Wp, Y, ADD, stats, g, hp, st, red, bwd);
     DM_CHECK(hipGetLastError());
     return;
   }

@@ -53,11 +53,14 @@ typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
 // RED (data gradients): the backward reduction of the BatchNorm whose output gradient Y is
 // (kernels.h BnBwdRed) runs in the store loop -- each lane's 8 channels of the stored bf16
 // value against that BN's input y -- and leaves one [2][Ncols] row per M tile in red.part
-template <int BN, int WM, int WN, int MINW, bool RED = false>
+// SEG2 (stride-2 data gradients): geometry s2.z (parity class (0,0)) runs C2/64 more K steps
+// over X2 / W2 at the row's own pixel -- the block's 1x1/s2 projection (conv_geom.h DgradSeg2;
+// here X2 has X's channel count, so the row's pixel base is shared)
+template <int BN, int WM, int WN, int MINW, bool RED = false, bool SEG2 = false>
 __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wp, bf16_t* Y, const bf16_t* ADD,
     float* __restrict__ stats, ConvGeomSet gs, unsigned xbytes, unsigned wbytes, int ntN,
-    int mtiles_max, int xcd, BnBwdRed red) {
+    int mtiles_max, int xcd, BnBwdRed red, DgradSeg2 s2) {
   // blockIdx.y selects one of up to four geometries sharing X / W / Y (the parity classes of a
   // stride-2 data gradient, which write disjoint output pixels); one geometry otherwise
   const ConvGeom g = gs.g[blockIdx.y];
@@ -86,15 +89,26 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
     bx = blockIdx.x % mtiles_max;
     by = blockIdx.x / mtiles_max;
   }
-  if (bx >= mtiles) return;  // padding of the grid, or a smaller parity class
+  // part row of this block (RED): parity classes of a multi-geometry launch stack their M tiles
+  const long long prow = (long long)blockIdx.y * mtiles_max + bx;
+  if (bx >= mtiles) {  // padding of the grid, or a smaller parity class
+    if constexpr (RED) {  // every part row is summed by the consumer
+      if (bx < mtiles_max && by == 0)
+        for (int c = threadIdx.x; c < 2 * g.Ncols; c += blockDim.x) red.part[prow * 2 * g.Ncols + c] = 0.f;
+    }
+    return;
+  }
   const int m0 = bx * PBM;
   const int n0 = by * BN;
   const int ntaps = g.nth * g.ntw;
   const int nchunk = g.C / PBK;
-  const int S = ntaps * nchunk;
+  const int S1 = ntaps * nchunk;
+  const int S = S1 + ((SEG2 && (int)blockIdx.y == s2.z) ? s2.C2 / PBK : 0);
 
   const pi32x4 rsx = prsrc(X, xbytes);
   const pi32x4 rsw = prsrc(Wp, wbytes);
+  const pi32x4 rsx2 = prsrc(SEG2 ? s2.X2 : (const void*)X, SEG2 ? s2.x2bytes : 0u);
+  const pi32x4 rsw2 = prsrc(SEG2 ? s2.W2 : (const void*)Wp, SEG2 ? s2.w2bytes : 0u);
   const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) void*)smem;
 
   // ---- DMA lane geometry: instruction j of wave w fills tile rows 8 NW j + 8w + lane/8 ----
@@ -125,11 +139,12 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
     abase[j] = base;
     amask[j] = mk;
   }
-  unsigned bbase[BI];
+  unsigned bbase[BI], bbase2[SEG2 ? BI : 1];
 #pragma unroll
   for (int j = 0; j < BI; ++j) {
     const int n = n0 + 8 * NW * j + drow;
     bbase[j] = n < g.Ncols ? (unsigned)n * (unsigned)g.wK * 2u + choff : POOB;
+    if constexpr (SEG2) bbase2[j] = n < g.Ncols ? (unsigned)n * (unsigned)s2.C2 * 2u + choff : POOB;
   }
 
   // DMA of the next K step (chunk icc, tap ith/itw): prep() computes this thread's source
@@ -137,7 +152,23 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   constexpr int ND = AI + BI;
   int icc = 0, ith = 0, itw = 0;
   unsigned doff[ND];
+  bool dseg = false;  // the prepared step reads the second segment
   auto prep = [&]() __attribute__((always_inline)) {
+    if constexpr (SEG2) {
+      // after the geometry's own steps (icc == nchunk), C2/64 steps of the projection: one
+      // 64-channel chunk each, the row's own pixel (abase: X2 has X's channel count)
+      const int c2 = icc - nchunk;
+      dseg = c2 >= 0 && c2 * PBK < s2.C2 && (int)blockIdx.y == s2.z;
+      if (dseg) {
+        ++icc;
+        const unsigned co = (unsigned)(c2 * PBK * 2);
+#pragma unroll
+        for (int j = 0; j < AI; ++j) doff[j] = amask[j] ? abase[j] + co : POOB;
+#pragma unroll
+        for (int j = 0; j < BI; ++j) doff[AI + j] = bbase2[j] != POOB ? bbase2[j] + co : POOB;
+        return;
+      }
+    }
     const int cc = icc, th = ith, tw = itw;
     const int t = th * g.ntw + tw;
     if (++itw == g.ntw) {
@@ -160,9 +191,10 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   const unsigned ldsw = lds0 + (unsigned)wid * 1024u;
   auto one = [&](int q, int st) __attribute__((always_inline)) {
     if (q < AI)
-      pdma16(rsx, ldsw + (unsigned)st * STG + (unsigned)q * (NW * 1024u), doff[q]);
+      pdma16(SEG2 && dseg ? rsx2 : rsx, ldsw + (unsigned)st * STG + (unsigned)q * (NW * 1024u), doff[q]);
     else
-      pdma16(rsw, ldsw + (unsigned)st * STG + ABYTES + (unsigned)(q - AI) * (NW * 1024u), doff[q]);
+      pdma16(SEG2 && dseg ? rsw2 : rsw, ldsw + (unsigned)st * STG + ABYTES + (unsigned)(q - AI) * (NW * 1024u),
+             doff[q]);
   };
 
   // ---- fragment reads: A rows wm*TM + i*32 + (lane&31), B rows wn*TN + j*32 + (lane&31) ----
@@ -453,8 +485,8 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
           a += rr2[(w * BN + c) * 2 + 0];
           b += rr2[(w * BN + c) * 2 + 1];
         }
-        red.part[((long long)bx * 2 + 0) * g.Ncols + n0 + c] = a;
-        red.part[((long long)bx * 2 + 1) * g.Ncols + n0 + c] = b * red.is[n0 + c];
+        red.part[(prow * 2 + 0) * g.Ncols + n0 + c] = a;
+        red.part[(prow * 2 + 1) * g.Ncols + n0 + c] = b * red.is[n0 + c];
       }
     }
   }
@@ -462,7 +494,8 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
 
 template <int BN, int WM, int WN, int MINW>
 void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
-                 const ConvGeomSet& gs, int ng, hipStream_t st, const BnBwdRed* red = nullptr) {
+                 const ConvGeomSet& gs, int ng, hipStream_t st, const BnBwdRed* red = nullptr,
+                 const DgradSeg2* seg2 = nullptr) {
   const ConvGeom& g = gs.g[0];
   constexpr size_t STG = (size_t)PBM * PBK * 2 + (size_t)BN * PBK * 2;
   const size_t sm_main = 2 * STG;
@@ -474,18 +507,23 @@ void launch_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD
   const int ntN = (g.Ncols + BN - 1) / BN;
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned wb = (unsigned)((long long)g.Ncols * g.wK * 2);
-  if (red && ng != 1)
-    throw std::runtime_error("conv_pipe: BN-backward reduction is for one-geometry data gradients");
-  auto k = red ? conv_pipe_kernel<BN, WM, WN, MINW, true> : conv_pipe_kernel<BN, WM, WN, MINW, false>;
+  if (seg2 && (seg2->C2 != g.C || seg2->z < 0 || seg2->z >= ng))
+    throw std::runtime_error("conv_pipe: the merged segment needs X's channel count");
+  auto k = red ? (seg2 ? conv_pipe_kernel<BN, WM, WN, MINW, true, true>
+                       : conv_pipe_kernel<BN, WM, WN, MINW, true, false>)
+               : (seg2 ? conv_pipe_kernel<BN, WM, WN, MINW, false, true>
+                       : conv_pipe_kernel<BN, WM, WN, MINW, false, false>);
   const BnBwdRed rarg = red ? *red : BnBwdRed{};
+  const DgradSeg2 sarg = seg2 ? *seg2 : DgradSeg2{};
   constexpr int NT = WM * WN * 64;
   set_smem_attr(k, sm);
   if (ntN > 1) {
     const unsigned mt8 = (unsigned)((mtiles + 7) / 8 * 8);
-    k<<<dim3(mt8 * ntN, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, ntN, mtiles, 1, rarg);
+    k<<<dim3(mt8 * ntN, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, ntN, mtiles, 1, rarg,
+                                            sarg);
   } else {
     k<<<dim3((unsigned)mtiles, ng), NT, sm, st>>>(X, Wp, Y, ADD, stats, gs, xb, wb, 1, mtiles, 0,
-                                                  rarg);
+                                                  rarg, sarg);
   }
   DM_CHECK(hipGetLastError());
 }
@@ -521,15 +559,24 @@ void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, 
 
 // the parity classes of a stride-2 data gradient (no statistics) in one launch
 bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st) {
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st, const DgradSeg2* seg2,
+                     const BnBwdRed* red) {
   if (ng < 1 || ng > 4) return false;
   for (int i = 0; i < ng; ++i)
     if (!conv_pipe_supported(gs.g[i], cfg)) return false;
-  if (cfg == 90) launch_pipe<256, 2, 4, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st);
-  else if (cfg == 91) launch_pipe<128, 4, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st);
-  else if (cfg == 92) launch_pipe<128, 2, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st);
-  else launch_pipe<64, 4, 1, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st);
+  if (seg2 && seg2->C2 != gs.g[0].C) return false;
+  if (cfg == 90) launch_pipe<256, 2, 4, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st, red, seg2);
+  else if (cfg == 91) launch_pipe<128, 4, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st, red, seg2);
+  else if (cfg == 92) launch_pipe<128, 2, 2, 1>(X, Wp, Y, ADD, nullptr, gs, ng, st, red, seg2);
+  else launch_pipe<64, 4, 1, 2>(X, Wp, Y, ADD, nullptr, gs, ng, st, red, seg2);
   return true;
+}
+
+// part rows of a multi-geometry pipelined launch with the reduction epilogue
+long long pipe_multi_rows(const ConvGeomSet& gs, int ng) {
+  long long mmax = 0;
+  for (int i = 0; i < ng; ++i) mmax = gs.g[i].M > mmax ? gs.g[i].M : mmax;
+  return (long long)ng * ((mmax + PBM - 1) / PBM);
 }
 
 }  // namespace dm

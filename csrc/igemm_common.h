@@ -79,6 +79,78 @@ struct PreBN {
   }
 };
 
+// BatchNorm backward of a staged 16-B chunk of that BN's output gradient (8 bf16 channels,
+// kernels.h BnBwdIn): dy = a*dz' + b*y + c, the arithmetic of bn_bwd_apply_kernel.  The
+// coefficients live in an LDS table [5][n] (a, b, c, sc, sh of n channels, bwd_tab_fill) and
+// are read per chunk through an opaque address, so they occupy no registers across the
+// consumer's MFMA loop (held in VGPRs they spilled both halo kernels: 76 / 220 spills).
+__device__ __forceinline__ unsigned opq_u(unsigned v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+__device__ __forceinline__ void bwd_tab_fill(float* tab, const BnBwdIn& in, int cbase, int n,
+                                             int tid, int nt) {
+  for (int i = tid; i < 5 * n; i += nt) {
+    const int k = i / n, c = cbase + i % n;
+    float v;
+    if (k < 3) v = in.coef[k * in.C + c];
+    else if (in.mode == 2) v = (k == 3 ? in.sc : in.sh)[c];
+    else v = k == 3 ? 0.f : 1.f;  // no ReLU from y: y*0 + 1 > 0, every element passes
+    tab[i] = v;
+  }
+}
+
+// tab: the table, n its channel count, ci the chunk's first channel (relative to the table);
+// mb: the chunk's mask byte (mode 4) or 0xff.  Two halves of 4 channels, so at most 20
+// coefficients are live at a time.
+// SB: a scheduling barrier after each half (keeps the halves' coefficients from being loaded
+// together; helps the data-gradient tile, hurts the weight-gradient one)
+template <bool SB = true>
+__device__ __forceinline__ uint4 bwd_apply(const float* tab, int n, int ci, uint4 dz, uint4 y,
+                                           unsigned mb) {
+  const uint32_t dw[4] = {dz.x, dz.y, dz.z, dz.w};
+  const uint32_t yw[4] = {y.x, y.y, y.z, y.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float* t = tab + opq_u((unsigned)(ci + 4 * h));
+    const float4 va = *reinterpret_cast<const float4*>(t);
+    const float4 vb = *reinterpret_cast<const float4*>(t + n);
+    const float4 vc = *reinterpret_cast<const float4*>(t + 2 * n);
+    const float4 vs = *reinterpret_cast<const float4*>(t + 3 * n);
+    const float4 vh = *reinterpret_cast<const float4*>(t + 4 * n);
+    const float a[4] = {va.x, va.y, va.z, va.w}, b[4] = {vb.x, vb.y, vb.z, vb.w};
+    const float c[4] = {vc.x, vc.y, vc.z, vc.w}, sc[4] = {vs.x, vs.y, vs.z, vs.w};
+    const float sh[4] = {vh.x, vh.y, vh.z, vh.w};
+#pragma unroll
+    for (int q2 = 0; q2 < 2; ++q2) {
+      const int q = 2 * h + q2;
+      float r[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int jj = 2 * q2 + hh, j = 2 * q + hh;
+        const float d = __uint_as_float(hh ? (dw[q] & 0xffff0000u) : (dw[q] << 16));
+        const float yv = __uint_as_float(hh ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
+        const bool pass = ((mb >> j) & 1u) && (yv * sc[jj] + sh[jj]) > 0.f;
+        r[hh] = a[jj] * (pass ? d : 0.f) + b[jj] * yv + c[jj];
+      }
+      o[q] = pack_bf2(r[0], r[1]);
+    }
+    if constexpr (SB) __builtin_amdgcn_sched_barrier(0);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// the mask byte of the 16-B chunk at byte offset `off` of an NHWC bf16 tensor (mode 4), or 0xff:
+// a range-checked buffer load (0-byte resource when there is no mask), never a branch
+__device__ __forceinline__ unsigned bwd_mask_byte(const BnBwdIn& in, unsigned off, unsigned mbytes) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)(in.mask ? in.mask : (const uint8_t*)in.coef),
+                                                    (short)0, (int)(in.mask ? mbytes : 0u), 0x00020000);
+  const unsigned v = __builtin_amdgcn_raw_buffer_load_b8(rs, off >> 4, 0, 0);
+  return in.mode == 4 ? v : 0xffu;
+}
+
 template <bool MF32>
 using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 

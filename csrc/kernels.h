@@ -133,10 +133,29 @@ struct BnBwdRed {
   const float* is;
   float* part;
 };
+// The BatchNorm backward apply folded into a consumer's operand staging (the data and weight
+// gradients of the conv that produced that BN's input): the staged operand is the BN's OUTPUT
+// gradient dz, and the kernel stages dy = a*dz' + b*y + c (dz' = dz where the ReLU passed:
+// y*sc + sh > 0 when sc is set, bit j of the 1-bit mask when mask is set, everywhere when
+// neither) instead of reading a materialised dy.  coef: [3][C] a, b, c (bn_backward, dy None).
+// Every pointer is valid (sc / sh alias coef when unused) and `mode` says which mask applies
+// (0: none, 2: y*sc + sh > 0, 4: the 1-bit mask), so the kernels load unconditionally: a load
+// under a branch leaves a phi that makes the compiler drain every prefetch in flight.
+struct BnBwdIn {
+  const bf16_t* y;
+  const uint8_t* mask;  // null unless mode 4 (read through a range-checked buffer resource)
+  const float* coef;
+  const float* sc;
+  const float* sh;
+  int C;
+  int mode;
+};
 // conv_pipe.hip: pipelined LDS-DMA implicit-GEMM conv (cfg 90-93: 256-pixel tiles)
 bool conv_pipe_supported(const ConvGeom& g, int cfg);
 bool conv_pipe_multi(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD,
-                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st);
+                     const ConvGeomSet& gs, int ng, int cfg, hipStream_t st,
+                     const DgradSeg2* seg2 = nullptr, const BnBwdRed* red = nullptr);
+long long pipe_multi_rows(const ConvGeomSet& gs, int ng);
 void conv_pipe(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int cfg, hipStream_t st, const BnBwdRed* red = nullptr);
 // conv_res64.hip: persistent register-resident-weight 3x3 conv, 64 -> 64 channels (cfg 80);
@@ -151,7 +170,7 @@ bool halo_cfg(int cfg, int& bn, int& waves);
 void conv_halo(const bf16_t* X, const bf16_t* Wp, bf16_t* Y, const bf16_t* ADD, float* stats,
                const ConvGeom& g, int bn, int waves, hipStream_t st,
                const float* pre_sc = nullptr, const float* pre_sh = nullptr,
-               const BnBwdRed* red = nullptr);
+               const BnBwdRed* red = nullptr, const BnBwdIn* bwd = nullptr);
 bool wgrad_halo_supported(const ConvGeom& g);
 // stride-2 3x3 weight gradient over the four input parity planes (wgrad cfg 7)
 bool wgrad_s2_supported(const ConvGeom& g);
@@ -163,7 +182,7 @@ void wgrad_res64(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom&
                  hipStream_t st, const float* pre_sc = nullptr, const float* pre_sh = nullptr);
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc = nullptr,
-                const float* pre_sh = nullptr);
+                const float* pre_sh = nullptr, const BnBwdIn* bwd = nullptr);
 void pack_weights_multi(const long long* desc, const long long* prefix, int nl, long long total,
                         hipStream_t st);
 void pack_weights_tiled(const long long* desc, const int* tprefix, int nl, int ntiles,

@@ -179,8 +179,12 @@ class Reducer {
     c10d::AllreduceOptions opts;
     // sync launch: the collective runs on the caller's current stream (ProcessGroupNCCL
     // asyncOp = false: no communication-stream hop, still no host synchronisation); used
-    // for the step's final bucket, whose result the optimizer waits for anyway
+    // for the step's final bucket, whose result the optimizer waits for anyway.  Collectives
+    // of one communicator must not run concurrently on two streams (RCCL would interleave
+    // them): the current stream first waits for the last asynchronous one still in flight on
+    // the communication stream (every earlier one precedes it there).
     opts.asyncOp = !sync_launch_;
+    if (sync_launch_ && last_async_ >= 0 && works_[last_async_]) works_[last_async_]->wait();
     if (use_avg_ && avg_scale_ != 1.0) {
       opts.reduceOp = c10d::ReduceOp(c10d::ReduceOp::AVG);
       scaled_[b] = true;

@@ -28,6 +28,8 @@
 #include "igemm_common.h"
 #include "kernels.h"
 
+#include <stdexcept>
+
 namespace dm {
 
 namespace {
@@ -45,11 +47,14 @@ __device__ __forceinline__ s4 tr_read(const bf16_t* p) {
 
 // NTY = kernel rows (dy values) per block: 3 = all 9 taps share the dY fragments; 1 = one
 // row of 3 taps (smaller halo, 3x more output tiles -> 3x fewer m-splits and slab bytes)
-template <int HRN, int NTY, bool PRE>
+// BWD: DY is a BatchNorm's OUTPUT gradient dz; the dY operand is that BN's backward
+// dy = a*dz' + b*y + c (kernels.h BnBwdIn), computed while staging (no dy tensor)
+template <int HRN, int NTY, bool PRE, bool BWD = false>
 __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ DY, float* __restrict__ slab,
     ConvGeom g, long long mchunk, unsigned xbytes, unsigned dybytes,
-    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int xy, int gx, int nz) {
+    const float* __restrict__ pre_sc, const float* __restrict__ pre_sh, int xy, int gx, int nz,
+    BnBwdIn bwd) {
   // pre_sc/pre_sh (optional): X is the previous conv's raw output; the operand is
   // relu(x*sc + sh) applied while staging (out-of-image taps read the zero row)
   constexpr int HROWS_MAX = HRN * 32;  // halo rows a buffer holds (8 chunks per row)
@@ -57,6 +62,7 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);            // [2][64][WPITCH] dY
   bf16_t* Hs = As + 2 * WBK * WPITCH;                       // [2][HROWS_MAX][WPITCH] input
   bf16_t* Zr = Hs + 2 * HROWS_MAX * WPITCH;                 // one zero row
+  float* btab = reinterpret_cast<float*>(Zr + WPITCH);      // BWD: [5][64] coefficients
 
   constexpr int NT = 3 * NTY;  // taps per block
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -80,19 +86,27 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
   const int hrows = WBK + 2 + (NTY - 1) * W;  // pixels m0 + dy_lo*W - 1 ... m0 + (dy_hi)*W + 64
   const int NHW = g.N * H * W;
   if (tid < WPITCH / 8) *reinterpret_cast<uint4*>(Zr + tid * 8) = make_uint4(0, 0, 0, 0);
+  if constexpr (BWD) {
+    bwd_tab_fill(btab, bwd, co0, WBM, tid, 256);
+    __syncthreads();  // the first store below reads it
+  }
 
   const auto rsx = __builtin_amdgcn_make_buffer_rsrc((void*)X, (short)0, (int)xbytes, 0x00020000);
   const auto rsd = __builtin_amdgcn_make_buffer_rsrc((void*)DY, (short)0, (int)dybytes, 0x00020000);
   const int chunk = tid & 7, row0 = tid >> 3;  // staging: 32 rows x 8 chunks per pass
 
   uint4 ra[2], rh[HRN];
-  auto load = [&](long long m0) {
+  unsigned raoff[BWD ? 2 : 1];  // BWD: the dY chunks' byte offsets (y and mask read at store)
+  const auto rsy = __builtin_amdgcn_make_buffer_rsrc((void*)(BWD ? (const void*)bwd.y : (const void*)DY),
+                                                     (short)0, (int)(BWD ? dybytes : 0u), 0x00020000);
+  auto load = [&](long long m0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const long long m = m0 + row0 + 32 * i;
       const unsigned off = m < me ? (unsigned)((m * g.Ncols + co0 + chunk * 8) * 2) : WOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsd, off, 0, 0);
       ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      if constexpr (BWD) raoff[i] = off;
     }
     const long long hb = m0 + dy_lo * W - 1;
 #pragma unroll
@@ -105,11 +119,30 @@ __global__ void __launch_bounds__(256, 2) wgrad_halo_kernel(
       rh[j] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
-  auto store = [&](int buf, long long m0) {
-    PreBN pbn;  // PRE: loaded per store (L1 hits) instead of 16 registers live all kernel
-    if constexpr (PRE) pbn.load(pre_sc, pre_sh, cc0 + chunk * 8);
+  auto store = [&](int buf, long long m0) __attribute__((always_inline)) {
     bf16_t* as = As + buf * WBK * WPITCH;
     bf16_t* hs = Hs + buf * HROWS_MAX * WPITCH;
+    if constexpr (BWD) {
+      // rows past the m-slice keep their zero dY (the conv's reduction must not see them).
+      // y and the mask are read here, not with the dY prefetch: held across the MFMA loop
+      // they pushed the kernel (144 accumulator registers) into spills
+      uint4 ry[2];
+      unsigned rmk[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(rsy, raoff[i], 0, 0);
+        ry[i] = make_uint4(w[0], w[1], w[2], w[3]);
+        rmk[i] = bwd_mask_byte(bwd, raoff[i], dybytes >> 4);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint4 v = bwd_apply<false>(btab, WBM, chunk * 8, ra[i], ry[i], rmk[i]);
+        if (m0 + row0 + 32 * i < me) ra[i] = v;
+      }
+      __builtin_amdgcn_sched_barrier(0);  // its coefficients are dead before PreBN's load
+    }
+    PreBN pbn;  // PRE: loaded per store (L1 hits) instead of 16 registers live all kernel
+    if constexpr (PRE) pbn.load(pre_sc, pre_sh, cc0 + chunk * 8);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       *reinterpret_cast<uint4*>(as + (row0 + 32 * i) * WPITCH + chunk * 8) = ra[i];
@@ -382,15 +415,17 @@ void launch_wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvG
   k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, 0, (int)grid.x, S);
 }
 
-template <int HRN, int NTY>
+template <int HRN, int NTY, bool BWD = false>
 void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                        long long mchunk, hipStream_t st, const float* pre_sc,
-                       const float* pre_sh) {
-  const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2;
+                       const float* pre_sh, const BnBwdIn* bwd = nullptr) {
+  const size_t sm = ((size_t)2 * WBK * WPITCH + (size_t)2 * HRN * 32 * WPITCH + WPITCH) * 2 +
+                    (BWD ? (size_t)5 * WBM * 4 : 0);
   dim3 grid((g.Ncols + WBM - 1) / WBM, (g.C / WBC) * (3 / NTY), S);
   const unsigned xb = (unsigned)((long long)g.N * g.H * g.W * g.C * 2);
   const unsigned db = (unsigned)(g.M * g.Ncols * 2);
-  auto k = pre_sc ? wgrad_halo_kernel<HRN, NTY, true> : wgrad_halo_kernel<HRN, NTY, false>;
+  const BnBwdIn barg = bwd ? *bwd : BnBwdIn{};
+  auto k = pre_sc ? wgrad_halo_kernel<HRN, NTY, true, BWD> : wgrad_halo_kernel<HRN, NTY, false, BWD>;
   set_smem_attr(k, sm);
   // XCD-grouped order for the 9-tap tiles.  Measured (tools/bench_conv.py, one call): 9-tap
   // layer2 +2-4 %, layer3/4 within 1 %, step 11.55 vs 11.57 ms; the 3-tap tiles lose (layer1
@@ -399,10 +434,10 @@ void launch_wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const Con
   if (NTY == 3 && xy > 1 && S > 1) {
     const unsigned z8 = (unsigned)((S + 7) / 8 * 8);
     k<<<dim3(z8 * xy), 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, xy,
-                                       (int)grid.x, S);
+                                       (int)grid.x, S, barg);
     return;
   }
-  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, 0, (int)grid.x, S);
+  k<<<grid, 256, sm, st>>>(X, DY, slab, g, mchunk, xb, db, pre_sc, pre_sh, 0, (int)grid.x, S, barg);
 }
 }  // namespace
 
@@ -441,7 +476,18 @@ void wgrad_s2(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g,
 
 void wgrad_halo(const bf16_t* X, const bf16_t* DY, float* slab, const ConvGeom& g, int S,
                 long long mchunk, int nty, hipStream_t st, const float* pre_sc,
-                const float* pre_sh) {
+                const float* pre_sh, const BnBwdIn* bwd) {
+  if (bwd) {  // the folded BN-backward dY operand: the 9-tap tiles (wgrad cfg 4)
+    if (nty != 3 || !bwd->y || !bwd->coef || bwd->C != g.Ncols)
+      throw std::runtime_error("wgrad_halo: BN-backward operand needs the 9-tap tile, y, coef, "
+                               "C == output channels");
+    const int rows = WBK + 2 * g.W + 2;
+    if (rows <= 96) launch_wgrad_halo<3, 3, true>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, bwd);
+    else if (rows <= 128) launch_wgrad_halo<4, 3, true>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, bwd);
+    else launch_wgrad_halo<6, 3, true>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh, bwd);
+    DM_CHECK(hipGetLastError());
+    return;
+  }
   if (nty == 1) {
     launch_wgrad_halo<3, 1>(X, DY, slab, g, S, mchunk, st, pre_sc, pre_sh);  // 66 rows
   } else {

@@ -501,6 +501,11 @@ def convbn_fwd(layer, x, ctx, train, residual=None, raw=False, pre=None):
 # the v3 igemm tiles whose multi-geometry launch (a stride-2 data gradient's 4 parity classes)
 # takes the merged projection segment and the BN-backward reduction epilogue
 _MULTI_IGEMM = (11, 12, 13, 14, 15, 16, 17)
+# ... and the pipelined tiles (layer 4), whose merged segment needs the projection's channel
+# count equal to dy's (true of every ResNet projection)
+_MULTI_PIPE = (90, 91, 92, 93)
+# the layer-2 BN-backward apply folded into its halo consumers (DMLAB_BN_FOLD=1/0)
+_BN_FOLD_DEFAULT = "0"
 
 
 def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False, complete_s2=False):
@@ -515,7 +520,7 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False, complete_s2=F
     rl, rctx = red_for
     # stride 2: only a data gradient that writes dx complete in one launch (the projection's
     # 1x1/s2 segment merged in, ``complete_s2``) can reduce its consumer's sums
-    s2_ok = stride == 2 and complete_s2 and cfg in _MULTI_IGEMM
+    s2_ok = stride == 2 and complete_s2 and (cfg in _MULTI_IGEMM or cfg in _MULTI_PIPE)
     kernel_ok = (stride == 1 and (cfg == 80 or 90 <= cfg <= 93 or cfg == 42)) or s2_ok
     pool = getattr(rl, "pool_k", 0)
     y = rctx.get("yarg") if pool else rctx.get("y")
@@ -638,7 +643,32 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     wcfg, S = _wgrad_plan(M, cout, K, k, s, C, W=OW if same else 0, rows=N * OH if same else 0,
                           tail=tail, even=even)
     masked_res = fused_skip and ctx["has_res"] and mode == 4
-    if phase == 2:
+    # The BN-backward apply folded into both consumers (layer 2's halo data gradient, cfg 42,
+    # and the 9-tap halo weight gradient, cfg 4): they stage dy = a*dz' + b*y + c themselves
+    # from dout and y, so the apply pass and its dy tensor do not exist
+    # (DMLAB_BN_FOLD=0: the separate apply pass)
+    fold = False
+    if (phase == 0 and not pool and mode in (0, 2, 4) and need_dx and not ctx["first"]
+            and dx_into is None and not (ctx["has_res"] and not masked_res)
+            and s == 1 and k == 3 and p == 1 and wcfg == 4
+            and os.environ.get("DMLAB_BN_FOLD", _BN_FOLD_DEFAULT) != "0"):
+        Nx, Hx, Wx, Cx = x.shape
+        fold = (dgrad_cfg(Nx * Hx * Wx, Cx, k, s, cout, Hx, Wx) == 42
+                and L.bn_fold_supported(Nx, Hx, Wx, Cx, cout))
+    bwd_kw = {}
+    if fold:
+        L.bn_backward(dout, None, y, ctx["mean"], ctx["invstd"], layer.bn_weight.detach(),
+                      layer.grad_slot("bn_weight"), layer.grad_slot("bn_bias"), acc, mode,
+                      ctx["scale"], ctx["shift"], None, None, 3, 2, 1, None, None, work,
+                      mask=in_mask if in_mask is not None else ctx.get("mask"), **pre_sums)
+        off = L.bn_bwd_coef_offset(M, cout, bool(pre_sums))
+        bwd_kw = dict(bwd_y=y, bwd_coef=work[off:off + 3 * cout])
+        if mode == 2:
+            bwd_kw.update(bwd_scale=ctx["scale"], bwd_shift=ctx["shift"])
+        elif mode == 4:
+            bwd_kw["bwd_mask"] = in_mask if in_mask is not None else ctx["mask"]
+        dy, dres = dout, None  # the consumers' dY operand is the BN's output gradient
+    elif phase == 2:
         dy, dres = ctx.pop("_bn_out")
         # allocated on the phase-1 stream, read here and on the weight-gradient stream
         dy.record_stream(torch.cuda.current_stream())
@@ -667,7 +697,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
     def launch_wgrad():
         if side is not None:
             side.wait_stream(torch.cuda.current_stream())
-            for t in (x, dy) + (tuple(pre) if pre is not None else ()):
+            for t in (x, dy) + (tuple(pre) if pre is not None else ()) + tuple(bwd_kw.values()):
                 t.record_stream(side)
         with torch.cuda.stream(side) if side is not None else contextlib.nullcontext():
             slab = torch.empty(S * cout * K, device=y.device, dtype=torch.float32)
@@ -679,7 +709,7 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
                 else:
                     xw = _materialise(x, pre)
             L.conv_wgrad(xw, dy, layer.grad_slot("weight"), slab, layer.cin, k, k, s, p, acc, S,
-                         wcfg, s2d, **pre_kw)
+                         wcfg, s2d, **pre_kw, **bwd_kw)
 
     launch_wgrad()
     dx = None
@@ -694,18 +724,20 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             dx = empty_nhwc(N_, H, W, Cin, x)
             merge_kw = {}
             if (shortcut is not None and s == 2 and k == 3 and p == 1 and dx_add is None
-                    and cfg in _MULTI_IGEMM and H % 2 == 0 and W % 2 == 0
+                    and (cfg in _MULTI_IGEMM or cfg in _MULTI_PIPE) and H % 2 == 0 and W % 2 == 0
                     and os.environ.get("DMLAB_MERGE_SHORTCUT", "1") != "0"):
                 dy2, wd2 = shortcut["join"]()
-                if dy2.shape[:3] == dy.shape[:3] and dy2.shape[3] % 64 == 0:
+                if (dy2.shape[:3] == dy.shape[:3] and dy2.shape[3] % 64 == 0
+                        and (cfg in _MULTI_IGEMM or dy2.shape[3] == dy.shape[3])):
                     merge_kw = dict(dy2=dy2, wd2=wd2)
                     shortcut["merged"] = True
             red_kw = (_dgrad_red(L, red_for, cfg, s, dx, complete_s2=bool(merge_kw))
                       if red_for is not None else {})
             if isinstance(dx_add, tuple):
-                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2], **red_kw)
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add[1], cfg, add_mask=dx_add[2], **red_kw,
+                             **bwd_kw)
             else:
-                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **red_kw, **merge_kw)
+                L.conv_dgrad(dy, wd, dx, k, k, s, p, dx_add, cfg, **red_kw, **merge_kw, **bwd_kw)
     if ctx["has_res"]:
         return dx, (("masked", dout, ctx["mask"]) if masked_res else dres)
     return dx

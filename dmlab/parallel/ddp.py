@@ -370,7 +370,16 @@ class DistributedDataParallel(nn.Module):
         else:
             op = dist.ReduceOp.SUM
         if getattr(self, "_py_tail", False):
-            # on the current stream, no host synchronisation (ProcessGroupNCCL asyncOp=False)
+            # on the current stream, no host synchronisation (ProcessGroupNCCL asyncOp=False);
+            # ordered after the collectives still in flight on the communication stream (one
+            # communicator must not run two at once on different streams)
+            for ob in self.buckets:
+                if ob.work is not None and ob.work is not True:
+                    ob.work.wait()
+                    ob.work = True
+            if self._buf_work is not None:
+                self._buf_work.wait()
+                self._buf_work = None
             dist.all_reduce(t, op=op, group=self.pg, async_op=False)
             b.work = True
         else:
@@ -400,6 +409,12 @@ class DistributedDataParallel(nn.Module):
         if self._native is not None:
             if self._sync_enabled:
                 if tail:
+                    # the broadcast is the only collective that may still run on the
+                    # communication stream when no bucket went there (the reducer orders a sync
+                    # launch after its own last asynchronous bucket)
+                    if self._buf_work is not None and not self._native.has_async():
+                        self._buf_work.wait()
+                        self._buf_work = None
                     self._native.set_sync_launch(True)
                 try:
                     self._native.mark_layer(layer_idx)

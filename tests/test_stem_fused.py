@@ -122,16 +122,21 @@ def test_stem_pool_apply_and_masked_codes(dev):
     assert torch.equal(out2, out)
 
 
-@pytest.mark.parametrize("dtype,H", [(torch.uint8, 224), (torch.float32, 64), (torch.bfloat16, 32)])
-def test_stem_fused_backward_matches_autograd(dev, dtype, H):
+@pytest.mark.parametrize("dtype,H,B,acc", [(torch.uint8, 224, 3, 0.0), (torch.float32, 64, 3, 0.0),
+                                             (torch.bfloat16, 32, 3, 0.0),
+                                             (torch.uint8, 32, 600, 1.0)])
+def test_stem_fused_backward_matches_autograd(dev, dtype, H, B, acc):
     """stem = maxpool(relu(BN_train(conv(x)))): the native forward + backward (pooled-domain
     BN sums, (a dz + cc) weight gradient, + b*H) against float64 autograd of the same
-    function on the same bf16-rounded input and weights."""
+    function on the same bf16-rounded input and weights.  The B = 600 case (> 2 workgroups per
+    CU of images) makes every workgroup of the one-per-CU grid walk several images and runs the
+    full fixed-order slab reduce, and accumulates (beta = 1, called twice) into dW / dgamma /
+    dbeta (acc = 1, the grad slots' beta), as gradient accumulation does."""
     L = lib()
     torch.manual_seed(1)
-    B = 3
     img = _inputs(dev, dtype, B + 1, H, 5)
-    idx = torch.tensor([3, 1, 0], device=dev, dtype=torch.long)
+    idx = (torch.tensor([3, 1, 0], device=dev, dtype=torch.long) if B == 3
+           else torch.randperm(B + 1, device=dev)[:B])
     w = torch.randn(64, 3, 7, 7, device=dev) * 0.08
     gamma = torch.randn(64, device=dev)
     beta = torch.randn(64, device=dev) * 0.2
@@ -153,8 +158,11 @@ def test_stem_fused_backward_matches_autograd(dev, dtype, H):
     work = torch.empty(L.bn_bwd_work(M, 64), **f)
     dslab = torch.empty(L.stem_bwd_slab_len(L.stem_fused_grid(B)), **f)
     sc, bi = input_affine(img.dtype)
-    L.stem_bwd_fused2(img, idx, sc, bi, wk, g, code4, mean, invstd, gamma, dgamma, dbeta, 0.0,
-                      part, rows, dw, 0.0, work, dslab, L.stem_fused_grid(B))
+    for _ in range(2 if acc else 1):  # acc = 1: the second call adds the same gradient again
+        L.stem_bwd_fused2(img, idx, sc, bi, wk, g, code4, mean, invstd, gamma, dgamma, dbeta, acc,
+                          part, rows, dw, acc, work, dslab, L.stem_fused_grid(B))
+    if acc:
+        dgamma, dbeta, dw = dgamma / 2, dbeta / 2, dw / 2
     # float64 reference, routed through the KERNEL's window codes (a near-tie may select
     # another pixel than float64 argmax would; the random-sign pooled gradients make such a
     # re-routing a visible dW difference, which is not what this test checks)
