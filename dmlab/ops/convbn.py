@@ -724,7 +724,9 @@ def convbn_bwd(layer, dout, ctx, need_dx, dx_add=None, dx_into=None, fused_skip=
             dx = empty_nhwc(N_, H, W, Cin, x)
             merge_kw = {}
             if (shortcut is not None and s == 2 and k == 3 and p == 1 and dx_add is None
-                    and (cfg in _MULTI_IGEMM or cfg in _MULTI_PIPE) and H % 2 == 0 and W % 2 == 0
+                    and (cfg in _MULTI_IGEMM
+                         or (cfg in _MULTI_PIPE and os.environ.get("DMLAB_MERGE_PIPE", "1") != "0"))
+                    and H % 2 == 0 and W % 2 == 0
                     and os.environ.get("DMLAB_MERGE_SHORTCUT", "1") != "0"):
                 dy2, wd2 = shortcut["join"]()
                 if (dy2.shape[:3] == dy.shape[:3] and dy2.shape[3] % 64 == 0
