@@ -269,7 +269,8 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
     // epilogue: statistics, then 32-row bands through this wave's LDS region to 16-B stores
     // RED: this lane's channel (its MFMA output column) is fixed; its BN constants are
     // re-read per tile through a laundered address (kept out of the register budget)
-    float rsc = 0.f, rsh = 0.f, rmu = 0.f, rs = 0.f, rq = 0.f;
+    float rsc = 0.f, rsh = 0.f, rmu = 0.f;
+    red_f2 rs2 = {0.f, 0.f}, rq2 = {0.f, 0.f};
     const unsigned char* ybase = smem;
     const unsigned char* mbase = smem;
     if constexpr (RED) {
@@ -323,31 +324,45 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
       if constexpr (RED) {
         // dz = the stored (bf16) gradient where the reduced BN's ReLU passed, read back from
         // the band in the MFMA layout (this lane's channel is its column)
+        // (rows r, r + 1 as a packed pair: one bf16 rounding for both, packed fp32 FMA/add)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * hsel;
-          const int pr = i * 32 + (r & 3) + 8 * (r >> 2);  // + wm*64 + 4*hsel in ybase
-          const float v = cs[row * R_LDC + l32];
-          const float yj = __uint_as_float(
-              (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
-          const float gj = __uint_as_float(pack_bf2(v, 0.f) << 16);
-          bool pass;
-          if (red.mask)
-            pass = (mbase[pr * 8] >> (l32 & 7)) & 1u;
-          else
-            pass = yj * rsc + rsh > 0.f;
-          const float dz = pass ? gj : 0.f;
-          rs += dz;
-          rq += dz * (yj - rmu);
+        for (int r = 0; r < 16; r += 2) {
+          red_f2 v2, y2, g2;
+          unsigned mk[2];
+          float vv[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int rh = r + h;
+            const int row = (rh & 3) + 8 * (rh >> 2) + 4 * hsel;
+            const int pr = i * 32 + (rh & 3) + 8 * (rh >> 2);  // + wm*64 + 4*hsel in ybase
+            vv[h] = cs[row * R_LDC + l32];
+            y2[h] = __uint_as_float(
+                (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
+            // bit -> all-ones / zero (mask mode), then AND
+            mk[h] = red.mask ? (unsigned)((int)((unsigned)mbase[pr * 8] << (31 - (l32 & 7))) >> 31)
+                             : 0xffffffffu;
+          }
+          const unsigned pk = pack_bf2(vv[0], vv[1]);  // the stored values
+          v2.x = __uint_as_float((pk << 16) & mk[0]);
+          v2.y = __uint_as_float(pk & 0xffff0000u & mk[1]);
+          if (red.mask) {
+            g2 = v2;
+          } else {
+            const red_f2 t = y2 * red_f2{rsc, rsc} + red_f2{rsh, rsh};
+            g2.x = t.x > 0.f ? v2.x : 0.f;
+            g2.y = t.y > 0.f ? v2.y : 0.f;
+          }
+          rs2 += g2;
+          rq2 += g2 * (y2 - red_f2{rmu, rmu});
           // bound the LDS reads in flight (the scheduler would hoist all of them)
-          if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+          if ((r & 3) == 2) __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
     if constexpr (RED) {
       float2* ra = reinterpret_cast<float2*>(smem + R_RACC) + tid;
       const float2 o = *ra;
-      *ra = make_float2(o.x + rs, o.y + rq);
+      *ra = make_float2(o.x + (rs2.x + rs2.y), o.y + (rq2.x + rq2.y));
     }
     if (more) {
       // the DMA is older than the 4 stores above: vmcnt(4) retires it, not them

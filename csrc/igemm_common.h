@@ -164,6 +164,35 @@ using mfma_acc_t = typename std::conditional<MF32, f32x16, f32x4>::type;
 // RED (data gradients, kernels.h BnBwdRed): the backward reduction of the BatchNorm whose
 // output gradient Y is, from the stored bf16 values and that BN's input y (prefetched with
 // the ADD chunks): one [2][Ncols] row per stat_row in red.part.
+typedef float red_f2 __attribute__((ext_vector_type(2)));
+// RED epilogue, one output row of 8 channels: dz = the stored (bf16) gradient o where the
+// consumer's ReLU passed (bit j of the 1-bit mask, or y*sc + sh > 0), rs += dz,
+// rq += dz (y - mu), channel pairs packed (the sums are those of the values the unfused
+// reduction would re-read)
+template <bool MASK>
+__device__ __forceinline__ void red_acc8(const uint4& ov, const uint4& yv, unsigned ym,
+                                         red_f2 (&rs)[4], red_f2 (&rq)[4], const red_f2 (&sc)[4],
+                                         const red_f2 (&sh)[4], const red_f2 (&mu)[4]) {
+  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w}, ow[4] = {ov.x, ov.y, ov.z, ov.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red_f2 y2, g2;
+    y2.x = __uint_as_float(yw[q] << 16);
+    y2.y = __uint_as_float(yw[q] & 0xffff0000u);
+    if constexpr (MASK) {
+      // bit -> all-ones / zero (one signed bit-field extract), then AND: no compare, no select
+      g2.x = __uint_as_float((ow[q] << 16) & (unsigned)((int)(ym << (31 - 2 * q)) >> 31));
+      g2.y = __uint_as_float(ow[q] & 0xffff0000u & (unsigned)((int)(ym << (30 - 2 * q)) >> 31));
+    } else {
+      const red_f2 t = y2 * sc[q] + sh[q];
+      g2.x = t.x > 0.f ? __uint_as_float(ow[q] << 16) : 0.f;
+      g2.y = t.y > 0.f ? __uint_as_float(ow[q] & 0xffff0000u) : 0.f;
+    }
+    rs[q] += g2;
+    rq[q] += g2 * (y2 - mu[q]);
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool MF32, int PASSES = 1, bool RED = false>
 __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / WM / (MF32 ? 32 : 16)][BN / WN / (MF32 ? 32 : 16)],
                                                    unsigned char* smem, long long m0, int n0,
@@ -298,15 +327,18 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       }
     }
     // RED: this thread's 8 channels are fixed (col); Σdz, Σdz (y - mu) accumulate in registers
-    float rs[8], rq[8], rsc[8], rsh[8], rmu[8];
+    // as channel pairs (packed fp32 FMA/add: half the VALU issues of the scalar form)
+    float rs[8], rq[8];
+    red_f2 rs2[4], rq2[4], rsc[4], rsh[4], rmu[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      rs[j] = rq[j] = 0.f;
+    for (int q = 0; q < 4; ++q) {
+      rs2[q] = rq2[q] = red_f2{0.f, 0.f};
       if constexpr (RED) {
-        const int c = col + j < g.Ncols ? col + j : 0;
-        rsc[j] = red.mask ? 0.f : red.sc[c];
-        rsh[j] = red.mask ? 0.f : red.sh[c];
-        rmu[j] = red.mu[c];
+        const int c0 = col + 2 * q < g.Ncols ? col + 2 * q : 0;
+        const int c1 = col + 2 * q + 1 < g.Ncols ? col + 2 * q + 1 : 0;
+        rsc[q] = red.mask ? red_f2{0.f, 0.f} : red_f2{red.sc[c0], red.sc[c1]};
+        rsh[q] = red.mask ? red_f2{0.f, 0.f} : red_f2{red.sh[c0], red.sh[c1]};
+        rmu[q] = red_f2{red.mu[c0], red.mu[c1]};
       }
     }
 #pragma unroll
@@ -327,18 +359,31 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
           __builtin_nontemporal_store(v, reinterpret_cast<u32x4_nt*>(Y + o[k]));
         }
         if constexpr (RED) {
-          const uint32_t yw[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+          const uint4 ov = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          if constexpr (BM * BN >= 128 * 64) {
+            if (red.mask) red_acc8<true>(ov, yv[k], ym[k], rs2, rq2, rsc, rsh, rmu);
+            else red_acc8<false>(ov, yv[k], ym[k], rs2, rq2, rsc, rsh, rmu);
+          } else {  // 64x64 tiles: the pair alignment would cost an occupancy step (78 -> 82 VGPRs)
+            const uint32_t yw[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float yj = __uint_as_float((j & 1) ? (yw[j >> 1] & 0xffff0000u) : (yw[j >> 1] << 16));
-            const float gj = __uint_as_float((j & 1) ? (ow[j >> 1] & 0xffff0000u) : (ow[j >> 1] << 16));
-            const bool pass = red.mask ? ((ym[k] >> j) & 1u) != 0u : yj * rsc[j] + rsh[j] > 0.f;
-            const float dz = pass ? gj : 0.f;
-            rs[j] += dz;
-            rq[j] += dz * (yj - rmu[j]);
+            for (int j = 0; j < 8; ++j) {
+              const int q = j >> 1;
+              const float yj = __uint_as_float((j & 1) ? (yw[q] & 0xffff0000u) : (yw[q] << 16));
+              const float gj = __uint_as_float((j & 1) ? (ow[q] & 0xffff0000u) : (ow[q] << 16));
+              const bool pass = red.mask ? ((ym[k] >> j) & 1u) != 0u
+                                         : yj * rsc[q][j & 1] + rsh[q][j & 1] > 0.f;
+              const float dz = pass ? gj : 0.f;
+              rs2[q][j & 1] += dz;
+              rq2[q][j & 1] += dz * (yj - rmu[q][j & 1]);
+            }
           }
         }
       }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      rs[2 * q] = rs2[q].x; rs[2 * q + 1] = rs2[q].y;
+      rq[2 * q] = rq2[q].x; rq[2 * q + 1] = rq2[q].y;
     }
     if constexpr (RED) {
       // threads of one channel group (tid % CPR) add up: lanes by shuffle, waves in LDS
