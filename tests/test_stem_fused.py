@@ -208,9 +208,13 @@ def test_resnet18_fused_stem_matches_s2d_stem(dev, monkeypatch):
     ill-conditioned: BatchNorm over a few elements per channel in the deep layers amplifies
     bf16-level differences (measured: a 2^-8 relative input perturbation moves the layer-1
     weight gradient by ~50 % on the s2d path itself).  So the check is relative to that
-    sensitivity: the fused-vs-s2d difference of every downstream gradient stays within
-    twice what the s2d path shows between the batch and a 2^-8-perturbed copy, and the loss
-    agrees to 1 %.  (The stem's own gradients are compared against float64 above.)"""
+    sensitivity: the fused-vs-s2d difference of every downstream gradient stays within what
+    the s2d path shows between the batch and a 2^-8-perturbed copy (+0.01 absolute), the
+    median difference over parameters within 0.7x the median sensitivity, and the loss agrees
+    to 1 %.  Measured (tools/stem_cond.py, this seed, batch 8 / 32 / 64 at 64^2): the
+    difference is 0.49x the sensitivity at the median and at most 0.87x for any parameter --
+    what bf16 rounding differences of half the perturbation produce.  (The stem's own
+    gradients are compared against float64 above.)"""
     from dmlab.models import ResNet18
     from dmlab.nn import cross_entropy
 
@@ -234,11 +238,16 @@ def test_resnet18_fused_stem_matches_s2d_stem(dev, monkeypatch):
     def rel(u, v):
         return ((u - v).norm() / (v.norm() + 1e-12)).item()
 
+    es, bs = [], []
     for n in ga:
         if n.startswith("stem."):
             continue
         e, base = rel(ga[n], gb[n]), rel(gp[n], gb[n])
-        assert e < 2 * base + 0.02, (n, e, base)
+        assert e < base + 0.01, (n, e, base)
+        es.append(e)
+        bs.append(base)
+    es, bs = sorted(es), sorted(bs)
+    assert es[len(es) // 2] < 0.7 * bs[len(bs) // 2], (es[len(es) // 2], bs[len(bs) // 2])
 
 
 def test_resnet18_u8_gathered_batch(dev, monkeypatch):
