@@ -315,8 +315,8 @@ def test_folded_bn_backward_wgrad(dev, geom, mode, pre):
 
 @pytest.mark.parametrize("fold", ["1", "0"])
 def test_resnet18_step_bn_fold(dev, fold, monkeypatch):
-    """Whole native ResNet-18 step with the layer-2 BN-backward applies folded (default) and
-    not: held to the bf16-autocast error envelope of the fp32 step per parameter, and the folded
+    """Whole native ResNet-18 step with the layer-2 BN-backward applies folded (opt-in,
+    DMLAB_BN_FOLD=1) and not: held to the bf16-autocast error envelope of the fp32 step per parameter, and the folded
     consumers are really used at 56x56 input scale (layer 2 at 28x28 halo tiles)."""
     import copy
 
@@ -371,3 +371,4 @@ def test_resnet18_step_bn_fold(dev, fold, monkeypatch):
         assert len(folded) >= 2, calls  # dgrad + wgrad of at least one BN
     else:
         assert not folded, calls
+
