@@ -234,7 +234,7 @@ class BasicBlock(Layer):
 
     def _down_stream(self):
         prog = getattr(self, "_prog", None)
-        if prog is None:
+        if prog is None or os.environ.get("DMLAB_DOWN_FWD_STREAM", "1") == "0":
             return None
         return prog._side_stream() if prog._native_active else None
 

@@ -506,6 +506,8 @@ _MULTI_IGEMM = (11, 12, 13, 14, 15, 16, 17)
 _MULTI_PIPE = (90, 91, 92, 93)
 # the layer-2 BN-backward apply folded into its halo consumers (DMLAB_BN_FOLD=1/0)
 _BN_FOLD_DEFAULT = "0"
+# DMLAB_RES64_RED_ADD default: layer-1 identity-block dgrads reduce the previous block's BN
+_RES64_RED_ADD_DEFAULT = "1"
 
 
 def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False, complete_s2=False):
@@ -534,13 +536,15 @@ def _dgrad_red(L, red_for, cfg, stride, dx, allow_res64_add=False, complete_s2=F
         if mask is None:
             return {}
     # layer1's identity-block dgrads (res64 with the fused skip add, reducing the previous
-    # block's BN): correct (tests) but 0.3% slower per step -- the add/mask epilogue costs
-    # the kernel ~100 us, more than the contended pass it saves (profiles/
-    # dgrad_bn_reduce_ab_r3s3.txt, red9); ``allow_res64_add`` (tests) opts in.  The STEM's
-    # pooled-grid sums in the last layer-1 dgrad do pay: +0.5 % (the separate pooled reduce ran
-    # next to the full-CU tail weight gradient at ~2 TB/s; profiles/side_stream_sweep_r4f.txt)
+    # block's BN): round 3 measured them 0.3% slower per step (the add/mask epilogue cost the
+    # kernel ~100 us, more than the contended pass it saved: profiles/
+    # dgrad_bn_reduce_ab_r3s3.txt, red9); with the round-6 packed/bit-extract reduction they
+    # gain +0.26 % (profiles/res64_red_add_ab_r6.txt), default on; DMLAB_RES64_RED_ADD=0 opts
+    # out (``allow_res64_add``: tests).  The STEM's pooled-grid sums in the last layer-1 dgrad
+    # pay too: +0.5 % (the separate pooled reduce ran next to the full-CU tail weight gradient
+    # at ~2 TB/s; profiles/side_stream_sweep_r4f.txt)
     if (cfg == 80 and mask is not None and not pool and not allow_res64_add
-            and os.environ.get("DMLAB_RES64_RED_ADD", "0") != "1"):
+            and os.environ.get("DMLAB_RES64_RED_ADD", _RES64_RED_ADD_DEFAULT) != "1"):
         return {}
     N, H, W, C = dx.shape
     rows = (L.dgrad_s2_red_rows(N, H, W, cfg) if stride == 2
