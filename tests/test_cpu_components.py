@@ -362,7 +362,7 @@ def test_wgrad_s2_plan():
     assert _wgrad_plan(1024 * 28 * 28, 128, 288, 3, 2, 32, even=28)[0] != 7  # channels
 
 
-def test_dgrad_red_selection():
+def test_dgrad_red_selection(monkeypatch):
     """Which data gradients reduce the consumer BN's backward sums in their epilogue
     (ops/convbn.py _dgrad_red): cfg 80 / 90-93 / 42, stride 1, a ReLU consumer of dx's shape;
     the residual block's 1-bit mask rides along; layer1's masked case (cfg 80 + mask, or the
@@ -397,7 +397,11 @@ def test_dgrad_red_selection():
     assert CB._dgrad_red(L, (relu, ctx(has_res=True)), 90, 1, dx) == {}   # no 1-bit mask
     c = ctx(has_res=True, mask=True)
     assert CB._dgrad_red(L, (relu, c), 42, 1, dx)["red_mask"] is c["mask"]
+    # res64 with the fused skip add: on by default (round 6), DMLAB_RES64_RED_ADD=0 opts out
+    assert CB._dgrad_red(L, (relu, ctx(has_res=True, mask=True)), 80, 1, dx)["red_mask"] is not None
+    monkeypatch.setenv("DMLAB_RES64_RED_ADD", "0")
     assert CB._dgrad_red(L, (relu, ctx(has_res=True, mask=True)), 80, 1, dx) == {}
+    monkeypatch.delenv("DMLAB_RES64_RED_ADD")
     c = ctx(pool=True)  # the stem's pooled-grid sums: reduced in the last layer-1 dgrad
     assert CB._dgrad_red(L, (stem, c), 80, 1, dx)["red_y"] is c["yarg"]
     c = ctx(has_res=True, mask=True)
