@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--cfgs", default="11,12,13,14,15,16,17,90,91,92,93")
+    ap.add_argument("--variants", action="store_true", help="default tile: plain / merged / +RED")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     L = lib()
@@ -63,6 +64,19 @@ def main():
         vec = [torch.rand(Cin, device=dev, generator=g) + 0.5 for _ in range(4)]
         cfgs = [int(c) for c in a.cfgs.split(",") if Cin % WIDTH.get(int(c), 64) == 0]
         fns = {}
+        if a.variants:  # the default tile alone: plain / + merged projection / + reduction
+            cfg = dgrad_cfg(N * H * H, Cin, 3, 2, Cout, H, H)
+            rows = L.dgrad_s2_red_rows(N, H, H, cfg)
+            part = torch.empty(rows * 2 * Cin, device=dev)
+            red = dict(red_y=yb, red_scale=vec[0], red_shift=vec[1], red_mean=vec[2],
+                       red_invstd=vec[3], red_part=part, red_mask=mask)
+            fns = {
+                "plain": lambda: L.conv_dgrad(dy1, wd1, dx, 3, 3, 2, 1, None, cfg),
+                "merged": lambda: L.conv_dgrad(dy1, wd1, dx, 3, 3, 2, 1, None, cfg, dy2=dy2, wd2=wd2),
+                "merged_red": lambda: L.conv_dgrad(dy1, wd1, dx, 3, 3, 2, 1, None, cfg, dy2=dy2,
+                                                   wd2=wd2, **red),
+            }
+            cfgs = []
         for cfg in cfgs:
             rows = L.dgrad_s2_red_rows(N, H, H, cfg)
             part = torch.empty(rows * 2 * Cin, device=dev)
@@ -83,6 +97,10 @@ def main():
                 t[c].append(timeit(f, a.iters))
         flops = 2.0 * N * OH * OH * Cout * Cin * 10  # 9 taps + the 1x1
         res = {c: round(min(v), 1) for c, v in t.items()}
+        if a.variants:
+            print(json.dumps({"shape": name, "cfg": dgrad_cfg(N * H * H, Cin, 3, 2, Cout, H, H),
+                              "us": res}), flush=True)
+            continue
         print(json.dumps({"shape": name, "default_cfg": dgrad_cfg(N * H * H, Cin, 3, 2, Cout, H, H),
                           "us": res, "tflops": {c: round(flops / v / 1e6, 1) for c, v in res.items()}}),
               flush=True)
