@@ -386,30 +386,32 @@ __device__ __forceinline__ void mfma_tile_epilogue(mfma_acc_t<MF32> (&acc)[BM / 
       rq[2 * q] = rq2[q].x; rq[2 * q + 1] = rq2[q].y;
     }
     if constexpr (RED) {
-      // threads of one channel group (tid % CPR) add up: lanes by shuffle, waves in LDS
-#pragma unroll
-      for (int sft = CPR; sft < 64; sft <<= 1)
+      // threads of one channel group (tid % CPR) add up: with CPR 8 the two lanes of a
+      // 16-lane row by a DPP rotate (row_ror:8 == lane ^ 8; the bpermute shuffles cost 3 VALU
+      // + 1 LDS op each), then every row's partials in LDS
+      static_assert(CPR == 8 || CPR == 16, "RED epilogue: 64- or 128-column tiles");
+      if constexpr (CPR == 8) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          rs[j] += __shfl_xor(rs[j], sft, 64);
-          rq[j] += __shfl_xor(rq[j], sft, 64);
+          rs[j] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(rs[j]), 0x128, 0xf, 0xf, false));
+          rq[j] += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(rq[j]), 0x128, 0xf, 0xf, false));
         }
+      }
+      constexpr int NRW = NT / 16;  // 16-lane rows of the block
       __syncthreads();  // staging reads done: the LDS is reused below
-      float* rr2 = reinterpret_cast<float*>(smem);  // [NT/64][BN][2]
-      if (lane < CPR)
+      float2* rr2 = reinterpret_cast<float2*>(smem);  // [NRW][BN]
+      if ((lane & 15) < CPR)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          rr2[(wid * BN + cc * 8 + j) * 2 + 0] = rs[j];
-          rr2[(wid * BN + cc * 8 + j) * 2 + 1] = rq[j];
-        }
+        for (int j = 0; j < 8; ++j) rr2[(tid >> 4) * BN + cc * 8 + j] = make_float2(rs[j], rq[j]);
       __syncthreads();
       for (int c = tid; c < BN; c += NT) {
         if (n0 + c < g.Ncols) {
           float a = 0.f, b = 0.f;
 #pragma unroll
-          for (int w = 0; w < NT / 64; ++w) {
-            a += rr2[(w * BN + c) * 2 + 0];
-            b += rr2[(w * BN + c) * 2 + 1];
+          for (int w = 0; w < NRW; ++w) {
+            const float2 v = rr2[w * BN + c];
+            a += v.x;
+            b += v.y;
           }
           red.part[((long long)stat_row * 2 + 0) * g.Ncols + n0 + c] = a;
           red.part[((long long)stat_row * 2 + 1) * g.Ncols + n0 + c] = b * red.is[n0 + c];
