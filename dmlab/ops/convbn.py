@@ -98,11 +98,10 @@ def pick_cfg(M, ncols, k=0, stride=0, cin=0, W=0):
 # 256 43.6/43.7k, 768 43.4k, 1024 43.4/43.5k; at 1024 images per GPU 512 -> 46.6k,
 # 768 45.5-45.8k, 1024 46.0-46.2k (profiles/wgrad_blocks_b1024_r2c.jsonl); re-measured under
 # the high-priority step stream in round 4: 160-1024 blocks and CU-masked weight-gradient
-# streams all lose to 512 (profiles/wgrad_blocks_sidemask_ab_r4m.txt)
+# streams all lose to 512 (profiles/wgrad_blocks_sidemask_ab_r4m.txt); round 6, a larger
+# budget for layers 3-4 only (>= 256 output channels): 768 -1.5 %, 1024 -0.4 %
+# (profiles/merged_shortcut_ab_r6.txt, "wide768" / "wide1024")
 _WGRAD_BLOCKS = 512
-# layers 3-4 (>= 256 output channels): their weight gradients hold every CU while the main
-# stream's memory-bound BN-backward applies need wave slots (experiment knob, 0 = as above)
-_WGRAD_BLOCKS_WIDE = int(os.environ.get("DMLAB_WGRAD_BLOCKS_WIDE", "0"))
 _CUS = {}
 
 
@@ -165,10 +164,7 @@ def _wgrad_plan(M, cout, K, k=0, stride=0, cin=0, force=None, W=0, rows=0, tail=
         # have one or two output tiles, so the m-split is their only parallelism
         max_split = max(1, M // 512)
     # (2x / 4x more splits for cfg 7 measured -0.4 / -1.0 %: profiles/wgrad_s2_splits_ab_r4ap.txt)
-    budget = _WGRAD_BLOCKS
-    if cout >= 256 and _WGRAD_BLOCKS_WIDE:
-        budget = _WGRAD_BLOCKS_WIDE
-    S = max(1, min(max_split, math.ceil(budget / tiles)))
+    S = max(1, min(max_split, math.ceil(_WGRAD_BLOCKS / tiles)))
     return cfg, S
 
 
