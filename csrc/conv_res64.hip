@@ -324,39 +324,46 @@ __global__ void __launch_bounds__(RNT, 2) conv_res64_kernel(
       if constexpr (RED) {
         // dz = the stored (bf16) gradient where the reduced BN's ReLU passed, read back from
         // the band in the MFMA layout (this lane's channel is its column)
-        // (rows r, r + 1 as a packed pair: one bf16 rounding for both, packed fp32 FMA/add)
+        // (rows r, r + 1 as a packed pair: one bf16 rounding for both, packed fp32 FMA/add;
+        // the mask / ReLU-condition choice is made once, outside the row loop: a per-element
+        // uniform branch split the loop into blocks and kept the LDS reads unpaired)
+        auto rows = [&](auto mtag) __attribute__((always_inline)) {
+          constexpr bool MK = decltype(mtag)::value;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          red_f2 v2, y2, g2;
-          unsigned mk[2];
-          float vv[2];
+          for (int r = 0; r < 16; r += 2) {
+            red_f2 v2, y2, g2;
+            unsigned mk[2];
+            float vv[2];
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int rh = r + h;
-            const int row = (rh & 3) + 8 * (rh >> 2) + 4 * hsel;
-            const int pr = i * 32 + (rh & 3) + 8 * (rh >> 2);  // + wm*64 + 4*hsel in ybase
-            vv[h] = cs[row * R_LDC + l32];
-            y2[h] = __uint_as_float(
-                (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
-            // bit -> all-ones / zero (mask mode), then AND
-            mk[h] = red.mask ? (unsigned)((int)((unsigned)mbase[pr * 8] << (31 - (l32 & 7))) >> 31)
-                             : 0xffffffffu;
+            for (int h = 0; h < 2; ++h) {
+              const int rh = r + h;
+              const int row = (rh & 3) + 8 * (rh >> 2) + 4 * hsel;
+              const int pr = i * 32 + (rh & 3) + 8 * (rh >> 2);  // + wm*64 + 4*hsel in ybase
+              vv[h] = cs[row * R_LDC + l32];
+              y2[h] = __uint_as_float(
+                  (unsigned)*reinterpret_cast<const unsigned short*>(ybase + pr * 64) << 16);
+              // bit -> all-ones / zero (mask mode), then AND
+              mk[h] = MK ? (unsigned)((int)((unsigned)mbase[pr * 8] << (31 - (l32 & 7))) >> 31)
+                         : 0xffffffffu;
+            }
+            const unsigned pk = pack_bf2(vv[0], vv[1]);  // the stored values
+            v2.x = __uint_as_float((pk << 16) & mk[0]);
+            v2.y = __uint_as_float(pk & 0xffff0000u & mk[1]);
+            if constexpr (MK) {
+              g2 = v2;
+            } else {
+              const red_f2 t = y2 * red_f2{rsc, rsc} + red_f2{rsh, rsh};
+              g2.x = t.x > 0.f ? v2.x : 0.f;
+              g2.y = t.y > 0.f ? v2.y : 0.f;
+            }
+            rs2 += g2;
+            rq2 += g2 * (y2 - red_f2{rmu, rmu});
+            // bound the LDS reads in flight (the scheduler would hoist all of them)
+            if ((r & 3) == 2) __builtin_amdgcn_sched_barrier(0);
           }
-          const unsigned pk = pack_bf2(vv[0], vv[1]);  // the stored values
-          v2.x = __uint_as_float((pk << 16) & mk[0]);
-          v2.y = __uint_as_float(pk & 0xffff0000u & mk[1]);
-          if (red.mask) {
-            g2 = v2;
-          } else {
-            const red_f2 t = y2 * red_f2{rsc, rsc} + red_f2{rsh, rsh};
-            g2.x = t.x > 0.f ? v2.x : 0.f;
-            g2.y = t.y > 0.f ? v2.y : 0.f;
-          }
-          rs2 += g2;
-          rq2 += g2 * (y2 - red_f2{rmu, rmu});
-          // bound the LDS reads in flight (the scheduler would hoist all of them)
-          if ((r & 3) == 2) __builtin_amdgcn_sched_barrier(0);
-        }
+        };
+        if (red.mask) rows(std::true_type{});
+        else rows(std::false_type{});
       }
     }
     if constexpr (RED) {
