@@ -371,4 +371,3 @@ def test_resnet18_step_bn_fold(dev, fold, monkeypatch):
         assert len(folded) >= 2, calls  # dgrad + wgrad of at least one BN
     else:
         assert not folded, calls
-
