@@ -344,14 +344,30 @@ __global__ void __launch_bounds__(WM * WN * 64, MINW) conv_pipe_kernel(
   const int fcol = lane & 31;
   float rsc[8], rsh[8], rmu[8], rs[8], rq[8];
   if constexpr (RED) {
+    // 8 consecutive channels' constants as 16-byte loads when aligned (profiles/
+    // red_const_loads_ab_r6.txt); Ncols % 8 == 0, a group past the edge reads channel 0's
+    const int cb = col + 8 <= g.Ncols ? col : 0;
+    auto ld8 = [&](const float* p, float (&v)[8]) __attribute__((always_inline)) {
+      if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+        const float4 a = *reinterpret_cast<const float4*>(p + cb);
+        const float4 b = *reinterpret_cast<const float4*>(p + cb + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = col + j < g.Ncols ? col + j : 0;
-      rsc[j] = red.mask ? 0.f : red.sc[c];
-      rsh[j] = red.mask ? 0.f : red.sh[c];
-      rmu[j] = red.mu[c];
-      rs[j] = rq[j] = 0.f;
+        for (int j = 0; j < 8; ++j) v[j] = p[cb + j];
+      }
+    };
+    ld8(red.mu, rmu);
+    if (red.mask) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) rsc[j] = rsh[j] = 0.f;
+    } else {
+      ld8(red.sc, rsc);
+      ld8(red.sh, rsh);
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) rs[j] = rq[j] = 0.f;
   }
   // RED: the y chunks (and 1-bit masks) of row block i + 1 are loaded while block i is
   // staged and stored (a load per chunk in the store loop left its latency exposed: layer4's
